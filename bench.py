@@ -1,0 +1,225 @@
+#!/usr/bin/env python3
+"""bench.py -- BASELINE.json config 2 on MI355X.
+
+Workload ("step" = one pass of the hot path over one batch): 65,536
+modular exponentiations x^N mod N^2 (4096-bit modulus, shared 2048-bit
+exponent y = N -- the r^N / s^N / beta^N shape of Paillier Encrypt and the
+MtA proofs), bases uniform-ish below N^2 from a seeded generator, the node
+key N from tests/golden/paillier_key_2048.json. Inputs are resident in HBM
+before the timed region; one step = one libmpcx kernel launch over the batch.
+
+Multi-GPU (torchrun, one process per GPU): every rank runs its own 65,536
+operands (independent sessions shard with no exchange step -> weak scaling,
+no collective on the data path); `value` = all ranks' modexps / max time.
+
+Prints ONE JSON line on rank 0 (contract in the task statement), with
+`roofline` (INT32 VALU bound, algorithmic work of Go's 4-bit-window
+Montgomery ladder) and `cpu_baseline` (the C restatement of Go
+expNNMontgomery timed on this host's cores, rank 0, N=1 only).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "4096-bit modexp/s per GPU & node; 2-of-3 ECDSA sigs/s over 10k wallets"
+PEAK_INT32_NOMINAL = 256 * 64 * 2.4e9  # 39.3 T 32x32->64 MAC/s: v_mad_u64_u32 is half rate on gfx950
+PEAK_MAD_MEASURED = 33.8e12            # tools/microbench/valu_rates.hip, 8 waves/SIMD (profiles/r01_valu_rates.txt)
+
+
+def alg_macs(mod_bits: int, exp_bits: int) -> float:
+    """W = (E + ceil(E/4)) * 2 L^2 32-bit MACs, L = 32-bit limbs."""
+    L = math.ceil(mod_bits / 32)
+    return (exp_bits + math.ceil(exp_bits / 4)) * 2 * L * L
+
+
+def load_key():
+    with open(os.path.join(ROOT, "tests", "golden", "paillier_key_2048.json")) as f:
+        k = json.load(f)
+    return int(k["N"], 16)
+
+
+def synth_bases(N2: int, count: int, seed: int, words: int) -> np.ndarray:
+    """count x words little-endian uint32, each value < N^2 (top word clamped)."""
+    rng = np.random.default_rng(seed)
+    x = rng.integers(0, 1 << 32, size=(count, words), dtype=np.uint64).astype(np.uint32)
+    top = (N2 >> (32 * (words - 1))) & 0xFFFFFFFF
+    x[:, words - 1] = x[:, words - 1] % max(top, 1)
+    return x
+
+
+def cpu_baseline(N: int, seconds: float, threads: int):
+    """C restatement of Go expNNMontgomery (oracle/libgomodexp.so) on host cores."""
+    import ctypes
+    from oracle import crosscheck as cc  # test infrastructure: cpu_baseline leg only
+    lib = cc.load_c_oracle()
+    if lib is None:
+        return None
+    N2 = N * N
+    nw = (N2.bit_length() + 31) // 32
+    ew = (N.bit_length() + 31) // 32
+    mw = cc._words(N2, nw)
+    yw = cc._words(N, ew)
+    done = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(t):
+        rng = np.random.default_rng(7 + t)
+        out = (ctypes.c_uint32 * nw)()
+        xs = rng.integers(0, 1 << 32, size=nw, dtype=np.uint64).astype(np.uint32)
+        xs[-1] = xs[-1] % max((N2 >> (32 * (nw - 1))), 1)
+        xw = (ctypes.c_uint32 * nw)(*[int(v) for v in xs])
+        while time.perf_counter() < stop:
+            lib.gomodexp_montgomery(out, xw, nw, yw, ew, mw, nw)
+            done[t] += 1
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    n = sum(done)
+    return {"value": n / el, "unit": "modexp/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x (x^N mod N^2, 4096-bit modulus, 2048-bit exponent) in {el:.1f} s on {threads} "
+                      f"host threads; C restatement of Go expNNMontgomery (oracle/gomodexp.c, 32-bit words, "
+                      f"4-bit window); Go/tss-lib absent from the image"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--count", type=int, default=65536, help="operands per GPU per step")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--verify", type=int, default=16, help="results checked against CPython pow (untimed)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local)
+
+    from mpcium_amd import build, mpcx
+    if rank == 0 and not os.path.exists(os.path.join(ROOT, "mpcium_amd", "libmpcx.so")):
+        build.build()
+    if world > 1:
+        dist.barrier()
+    mpcx.init(local)
+
+    N = load_key()
+    N2 = N * N
+    mod = mpcx.Modulus(N2)
+    words = mod.class_words  # 128 for the 4096-bit class
+    count = args.count
+    bases = synth_bases(N2, count, 0x6D706332 + rank, words)
+    exp = mpcx.int_to_words(N, mpcx.nwords(N))
+    dev = torch.device("cuda", local)
+    d_bases = torch.from_numpy(bases.view(np.int32)).to(dev)
+    d_exp = torch.from_numpy(exp.view(np.int32)).to(dev)
+    d_out = torch.zeros((count, words), dtype=torch.int32, device=dev)
+    stream = torch.cuda.current_stream(dev)
+    L = mpcx.lib()
+
+    def step():
+        rc = L.mpcx_modexp_batch_device(mod.handle, count, d_bases.data_ptr(), words, d_exp.data_ptr(),
+                                        len(exp), 1, N.bit_length(), d_out.data_ptr(), words,
+                                        stream.cuda_stream)
+        if rc != 0:
+            raise mpcx.MpcxError(rc, L.mpcx_last_error().decode())
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+
+    # untimed correctness sample
+    if args.verify:
+        out = d_out.cpu().numpy().view(np.uint32)
+        idx = np.linspace(0, count - 1, args.verify).astype(int)
+        xs = mpcx.words_to_ints(bases[idx])
+        zs = mpcx.words_to_ints(out[idx])
+        bad = [int(i) for i, x, z in zip(idx, xs, zs) if pow(x, N, N2) != z]
+        if bad:
+            raise SystemExit(f"rank {rank}: GPU results differ from pow() at operands {bad[:5]}")
+
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step on `stream`
+
+    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, kernel_ms = float(t[0]), float(t[1])
+
+    total = count * world * args.steps
+    value = total / elapsed
+    ms_per_step = elapsed / args.steps * 1e3
+    W = alg_macs(4096, N.bit_length())
+    achieved = W * count / (kernel_ms * 1e-3)  # per GPU, per launch
+    result = {
+        "metric": METRIC,
+        "value": value,
+        "unit": "modexp/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": ms_per_step,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u32",
+        "data": "synthetic: bases from numpy default_rng(0x6d706332+rank) clamped below N^2; N = product of two "
+                "seeded 1024-bit safe primes (tests/golden/paillier_key_2048.json)",
+        "config": {"workload": "config2: x^N mod N^2, 4096-bit modulus, shared 2048-bit exponent y=N",
+                   "operands_per_gpu": count, "modulus_bits": N2.bit_length(), "exp_bits": N.bit_length(),
+                   "parallelism": f"shard{world} (independent operands, no collective)",
+                   "kernel_geometry": {"L": mod.L, "P": mod.P, "K": mod.K, "G": mod.G}},
+        "roofline": {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_INT32_NOMINAL / 1e12,
+                     "unit": "TOP/s", "frac": achieved / PEAK_INT32_NOMINAL, "traffic": None,
+                     "peak_measured_mad": PEAK_MAD_MEASURED / 1e12,
+                     "frac_of_measured_mad": achieved / PEAK_MAD_MEASURED,
+                     "alg_ops_per_modexp": W, "kernel_ms": kernel_ms},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, thr)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,140 @@
+/*
+ * mpcx.h -- C-ABI of libmpcx.so, the MI355X (gfx950) batched modular
+ * exponentiation engine behind mpcium's tss-lib hot path.
+ *
+ * This is the drop-in boundary: plain pointers and sizes, no C++ or torch
+ * types, no exceptions across the ABI. Every entry point returns an int
+ * status (MPCX_OK == 0); mpcx_last_error() gives the thread's last message.
+ *
+ * Integers cross the boundary as little-endian arrays of 32-bit words
+ * (Go: big.Int.Bits() on a 32-bit-word view, i.e. the natural layout a cgo
+ * shim builds from big.Int.Bytes()); batches are operand-major (operand i
+ * occupies words [i*stride, (i+1)*stride)). Results are the canonical
+ * residue in [0, m), bit-identical to Go math/big (*Int).Exp for the same
+ * non-negative inputs.
+ *
+ * Which reference interface each entry point replaces (the reference's
+ * arithmetic lives in tss-lib v2.0.2, pinned at /root/reference/go.mod:10,
+ * and Go math/big; "up:" = github.com/bnb-chain/tss-lib/v2, absent from the
+ * image -- see SURVEY.md section 0):
+ *   mpcx_modulus_register      -- the per-call setup inside math/big
+ *                                 nat.expNNMontgomery (k0, RR), hoisted to
+ *                                 once per node modulus (N^2, N~, N, p, q),
+ *                                 which mpcium keeps for the process
+ *                                 lifetime (/root/reference/pkg/mpc/node.go:69,109,170).
+ *   mpcx_modexp_batch          -- up:common/int.go  (*modInt).Exp(x, y)
+ *                                 = new(big.Int).Exp(x, y, m), for a batch of
+ *                                 x with one shared y (e.g. y = N for r^N,
+ *                                 y = lambda for c^lambda) or per-operand y
+ *                                 (e.g. HomoMult c1^m), coalesced across the
+ *                                 sessions /root/reference/pkg/mpc/session.go:199
+ *                                 drives through party.UpdateFromBytes.
+ *   mpcx_modexp_batch_device   -- same, device-resident buffers + stream
+ *                                 (pipelines that keep operands in HBM).
+ *   mpcx_fermat2_batch         -- up:common/safe_prime.go
+ *                                 isPocklingtonCriterionSatisfied(p):
+ *                                 2^(p-1) mod p == 1 for a batch of
+ *                                 candidate moduli (keygen.GeneratePreParams,
+ *                                 /root/reference/pkg/mpc/node.go:69).
+ */
+#ifndef MPCX_H_
+#define MPCX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPCX_OK 0
+#define MPCX_EINVAL 1   /* bad argument (null pointer, even/zero modulus, size out of range) */
+#define MPCX_ENODEV 2   /* no HIP device, or mpcx_init not called */
+#define MPCX_EHIP 3     /* HIP runtime error or failed device self-test */
+#define MPCX_ENOMEM 4   /* device or host allocation failed */
+
+#define MPCX_MAX_MODULUS_BITS 4096 /* largest odd modulus a kernel class accepts */
+
+typedef struct mpcx_modulus_s* mpcx_mod_t;
+
+/* Library version (major*10000 + minor*100 + patch). */
+int mpcx_version(void);
+
+/* Text of the calling thread's last error ("" if none). */
+const char* mpcx_last_error(void);
+
+/* Number of visible HIP devices (0 without a GPU; never initialises one). */
+int mpcx_device_count(int* out_count);
+
+/* Bind this process to HIP device `device` (one process per GPU) and run the
+ * device self-test. Idempotent for the same device. */
+int mpcx_init(int device);
+
+/* Release all device resources (registered moduli become invalid). */
+int mpcx_shutdown(void);
+
+/* Register an odd modulus m (m_words little-endian 32-bit words, leading zero
+ * words allowed) with 1 <= m < 2^MPCX_MAX_MODULUS_BITS. Precomputes the
+ * Montgomery constants and uploads them. *out stays valid until
+ * mpcx_modulus_release / mpcx_shutdown. Even m returns MPCX_EINVAL: math/big
+ * takes a different (CRT/windowed) path for even moduli, which the hot path
+ * never uses; callers keep those on the host. */
+int mpcx_modulus_register(const uint32_t* m_words, uint32_t m_len, mpcx_mod_t* out);
+int mpcx_modulus_release(mpcx_mod_t mod);
+
+/* Bits of the registered modulus, and the operand width (words) of the kernel
+ * class serving it: bases may have up to that many words. */
+int mpcx_modulus_info(mpcx_mod_t mod, uint32_t* out_bits, uint32_t* out_class_words);
+
+/* out[i] = bases[i] ^ e_i mod m for i < count, host buffers.
+ *   bases:    count x base_words words, base_words <= class words
+ *             (mpcx_modulus_info); any value below 2^(32*class words),
+ *             including values >= m, is accepted (math/big likewise accepts
+ *             len(x) == len(m) without reducing first)
+ *   exps:     exp_shared != 0: ONE exponent of exp_words words (e_i = exps)
+ *             exp_shared == 0: count x exp_words words (e_i = exps[i*exp_words ...])
+ *             exponents are non-negative (Go's y < 0 inverse path is the
+ *             caller's); exp_words may be 0 (y = 0)
+ *   out:      count x out_words words, out_words >= words(m); zero-padded.
+ * Synchronous: returns after the results are in `out`. */
+int mpcx_modexp_batch(mpcx_mod_t mod, uint32_t count,
+                      const uint32_t* bases, uint32_t base_words,
+                      const uint32_t* exps, uint32_t exp_words, int exp_shared,
+                      uint32_t* out, uint32_t out_words);
+
+/* Same contract with device pointers (d_*) on HIP stream `stream` (a
+ * hipStream_t, NULL = default stream). Asynchronous: the results are valid
+ * after the stream is synchronised. exp_bits is the bit length of the
+ * largest exponent (any value >= it and <= 32*exp_words is correct; the
+ * kernel processes ceil(exp_bits/4) 4-bit windows). The first call with a
+ * larger batch than before grows the kernel workspace (hipMalloc). */
+int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count,
+                             const uint32_t* d_bases, uint32_t base_words,
+                             const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
+                             uint32_t exp_bits,
+                             uint32_t* d_out, uint32_t out_words, void* stream);
+
+/* Pocklington/Fermat check for safe-prime candidates: ok[i] = (2^(p_i - 1)
+ * mod p_i == 1) for count odd candidates p_i of p_words words each
+ * (5 <= p_i < 2^1024, p_words <= 32). Each candidate is its own modulus. */
+int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint8_t* ok);
+
+/* Device memory helpers for callers without their own HIP allocator. */
+int mpcx_dev_alloc(size_t bytes, void** out_ptr);
+int mpcx_dev_free(void* ptr);
+int mpcx_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes);
+int mpcx_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes);
+int mpcx_stream_create(void** out_stream);
+int mpcx_stream_destroy(void* stream);
+int mpcx_stream_sync(void* stream);
+
+/* Kernel-class geometry of a modulus (for benchmarks and roofline math):
+ * digits L (radix 2^28), lanes per operand P, digits per lane K, operands per
+ * 64-lane wavefront G. */
+int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K, uint32_t* G);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MPCX_H_ */

@@ -1,0 +1,455 @@
+// mpcx_api.cpp -- C-ABI host side of libmpcx.so (see include/mpcx.h).
+//
+// Owns device selection, the per-modulus Montgomery constants (what Go's
+// nat.expNNMontgomery recomputes on every call: k0 and RR,
+// go:src/math/big/nat.go), the kernel workspace and the staging buffers, and
+// launches the gfx950 kernels of mpcx_kernels.hip. No CPU compute fallback:
+// every modexp runs on the GPU or the call fails with an error code.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/mpcx.h"
+#include "mpcx_internal.h"
+
+extern "C" {
+hipError_t mpcx_launch_modexp(int cls, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
+}
+
+struct mpcx_modulus_s {
+  int cls;
+  uint32_t bits;
+  uint32_t words;  // normalized length of m in 32-bit words
+  uint32_t L;
+  uint32_t n0inv;
+  uint32_t* d_const;  // 3*L digits: N, R mod N, R^2 mod N
+  std::vector<uint32_t> m;
+};
+
+namespace {
+
+constexpr int kDigitBits = 28;
+constexpr uint32_t kM28 = (1u << kDigitBits) - 1u;
+
+thread_local std::string g_err;
+std::mutex g_mu;
+int g_device = -1;
+uint32_t* g_ws = nullptr;  // exponentiation table workspace
+size_t g_ws_bytes = 0;
+struct Staging {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+};
+Staging g_stage[4];  // bases, exps, out, misc
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(MPCX_EHIP, "%s: %s", what, hipGetErrorString(e));
+}
+
+int class_for_bits(uint32_t bits) {
+  for (int c = 0; c < MPCX_NUM_CLASSES; ++c)
+    if ((int)bits <= MPCX_CLASS_MAXBITS(c)) return c;
+  return -1;
+}
+
+uint32_t bit_length(const std::vector<uint32_t>& x) {
+  for (int i = (int)x.size() - 1; i >= 0; --i)
+    if (x[i]) return (uint32_t)(32 * i + (32 - __builtin_clz(x[i])));
+  return 0;
+}
+
+uint32_t bit_length_words(const uint32_t* x, uint32_t n) {
+  for (int i = (int)n - 1; i >= 0; --i)
+    if (x[i]) return (uint32_t)(32 * i + (32 - __builtin_clz(x[i])));
+  return 0;
+}
+
+// x >= m (same length)
+bool geq(const std::vector<uint32_t>& x, const std::vector<uint32_t>& m) {
+  for (int i = (int)x.size() - 1; i >= 0; --i)
+    if (x[i] != m[i]) return x[i] > m[i];
+  return true;
+}
+
+// 2^k mod m by doubling with conditional subtraction (once per registration).
+std::vector<uint32_t> pow2_mod(uint32_t k, const std::vector<uint32_t>& m) {
+  const size_t n = m.size();
+  std::vector<uint32_t> x(n + 1, 0), mm(m);
+  mm.push_back(0);
+  x[0] = 1;
+  if (n == 1 && m[0] == 1) return std::vector<uint32_t>(n, 0);
+  for (uint32_t i = 0; i < k; ++i) {
+    uint32_t c = 0;
+    for (size_t j = 0; j <= n; ++j) {
+      const uint32_t nc = x[j] >> 31;
+      x[j] = (x[j] << 1) | c;
+      c = nc;
+    }
+    if (geq(x, mm)) {
+      uint64_t br = 0;
+      for (size_t j = 0; j <= n; ++j) {
+        const uint64_t d = (uint64_t)x[j] - mm[j] - br;
+        x[j] = (uint32_t)d;
+        br = (d >> 63) & 1;
+      }
+    }
+  }
+  x.resize(n);
+  return x;
+}
+
+std::vector<uint32_t> to_digits(const std::vector<uint32_t>& w, uint32_t L) {
+  std::vector<uint32_t> d(L, 0);
+  for (uint32_t i = 0; i < L; ++i) {
+    const uint32_t bit = i * kDigitBits, wi = bit >> 5, s = bit & 31;
+    uint64_t v = 0;
+    if (wi < w.size()) v = w[wi];
+    if (wi + 1 < w.size()) v |= (uint64_t)w[wi + 1] << 32;
+    d[i] = (uint32_t)(v >> s) & kM28;
+  }
+  return d;
+}
+
+int ensure_device() {
+  if (g_device < 0) return fail(MPCX_ENODEV, "mpcx_init() has not been called");
+  return MPCX_OK;
+}
+
+int ensure_buffer(Staging& s, size_t bytes) {
+  if (s.bytes >= bytes && s.ptr) return MPCX_OK;
+  if (s.ptr) (void)hipFree(s.ptr);
+  s.ptr = nullptr;
+  s.bytes = 0;
+  size_t want = std::max<size_t>(bytes, 1 << 20);
+  hipError_t e = hipMalloc(&s.ptr, want);
+  if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
+  s.bytes = want;
+  return MPCX_OK;
+}
+
+int ensure_workspace(size_t bytes) {
+  if (g_ws_bytes >= bytes) return MPCX_OK;
+  if (g_ws) (void)hipFree(g_ws);
+  g_ws = nullptr;
+  g_ws_bytes = 0;
+  hipError_t e = hipMalloc((void**)&g_ws, bytes);
+  if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(workspace %zu): %s", bytes, hipGetErrorString(e));
+  g_ws_bytes = bytes;
+  return MPCX_OK;
+}
+
+int run_selftest() {
+  uint32_t* d = nullptr;
+  hipError_t e = hipMalloc((void**)&d, 256 * sizeof(uint32_t));
+  if (e != hipSuccess) return hip_fail(e, "selftest alloc");
+  e = mpcx_launch_selftest(d, nullptr);
+  std::vector<uint32_t> h(256);
+  if (e == hipSuccess) e = hipMemcpy(h.data(), d, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  (void)hipFree(d);
+  if (e != hipSuccess) return hip_fail(e, "selftest");
+  for (uint32_t l = 0; l < 64; ++l) {
+    const uint32_t nxt = l < 63 ? 1000 + l + 1 : 0;
+    const uint32_t prv = l > 0 ? 1000 + l - 1 : 0;
+    const uint32_t bp = 2000 + (l / 7) * 7;
+    const uint64_t acc = (uint64_t)(0xFFFFFFF0u + l) * (0xFFFFFFF7u - l) + 0xFFFFFFFFFFFFull;
+    if (h[l] != nxt || h[64 + l] != prv || h[128 + l] != bp || h[192 + l] != (uint32_t)(acc >> 32))
+      return fail(MPCX_EHIP,
+                  "device self-test failed at lane %u (dpp next %u/%u prev %u/%u bpermute %u/%u mad %u/%u)", l,
+                  h[l], nxt, h[64 + l], prv, h[128 + l], bp, h[192 + l], (uint32_t)(acc >> 32));
+  }
+  return MPCX_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpcx_version(void) { return 100; }
+
+const char* mpcx_last_error(void) { return g_err.c_str(); }
+
+int mpcx_device_count(int* out_count) {
+  if (!out_count) return fail(MPCX_EINVAL, "null out_count");
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) n = 0;
+  *out_count = n;
+  return MPCX_OK;
+}
+
+int mpcx_init(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_device >= 0) {
+    if (g_device == device) return MPCX_OK;
+    return fail(MPCX_EINVAL, "already bound to device %d (one process per GPU)", g_device);
+  }
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess || n <= 0) return fail(MPCX_ENODEV, "no HIP device visible");
+  if (device < 0 || device >= n) return fail(MPCX_EINVAL, "device %d out of range [0,%d)", device, n);
+  e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, device);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(MPCX_ENODEV, "device %d is %s; libmpcx is built for gfx950 only", device, prop.gcnArchName);
+  g_device = device;
+  int rc = run_selftest();
+  if (rc != MPCX_OK) g_device = -1;
+  return rc;
+}
+
+int mpcx_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (g_ws) (void)hipFree(g_ws);
+  g_ws = nullptr;
+  g_ws_bytes = 0;
+  for (auto& s : g_stage) {
+    if (s.ptr) (void)hipFree(s.ptr);
+    s = Staging{};
+  }
+  g_device = -1;
+  return MPCX_OK;
+}
+
+int mpcx_modulus_register(const uint32_t* m_words, uint32_t m_len, mpcx_mod_t* out) {
+  if (!m_words || !out || m_len == 0) return fail(MPCX_EINVAL, "null modulus or output");
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  std::vector<uint32_t> m(m_words, m_words + m_len);
+  while (m.size() > 1 && m.back() == 0) m.pop_back();
+  const uint32_t bits = bit_length(m);
+  if (bits == 0) return fail(MPCX_EINVAL, "modulus is zero");
+  if ((m[0] & 1u) == 0) return fail(MPCX_EINVAL, "modulus is even (math/big uses a non-Montgomery path; keep it on the host)");
+  const int cls = class_for_bits(bits);
+  if (cls < 0) return fail(MPCX_EINVAL, "modulus has %u bits > %d", bits, MPCX_MAX_MODULUS_BITS);
+  const uint32_t L = (uint32_t)MPCX_CLASS_L(cls);
+  auto* mod = new mpcx_modulus_s();
+  mod->cls = cls;
+  mod->bits = bits;
+  mod->words = (uint32_t)m.size();
+  mod->L = L;
+  mod->m = m;
+  uint32_t inv = m[0];
+  for (int i = 0; i < 5; ++i) inv *= 2u - m[0] * inv;
+  mod->n0inv = (0u - inv) & kM28;
+  std::vector<uint32_t> host(3 * L);
+  auto nd = to_digits(m, L);
+  auto r1 = to_digits(pow2_mod(kDigitBits * L, m), L);
+  auto r2 = to_digits(pow2_mod(2 * kDigitBits * L, m), L);
+  std::copy(nd.begin(), nd.end(), host.begin());
+  std::copy(r1.begin(), r1.end(), host.begin() + L);
+  std::copy(r2.begin(), r2.end(), host.begin() + 2 * L);
+  hipError_t e = hipMalloc((void**)&mod->d_const, host.size() * sizeof(uint32_t));
+  if (e != hipSuccess) {
+    delete mod;
+    return fail(MPCX_ENOMEM, "hipMalloc(modulus): %s", hipGetErrorString(e));
+  }
+  e = hipMemcpy(mod->d_const, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(mod->d_const);
+    delete mod;
+    return hip_fail(e, "upload modulus");
+  }
+  *out = mod;
+  return MPCX_OK;
+}
+
+int mpcx_modulus_release(mpcx_mod_t mod) {
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (mod->d_const) (void)hipFree(mod->d_const);
+  delete mod;
+  return MPCX_OK;
+}
+
+int mpcx_modulus_info(mpcx_mod_t mod, uint32_t* out_bits, uint32_t* out_class_words) {
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  if (out_bits) *out_bits = mod->bits;
+  if (out_class_words) *out_class_words = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
+  return MPCX_OK;
+}
+
+int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K, uint32_t* G) {
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  if (L) *L = (uint32_t)MPCX_CLASS_L(mod->cls);
+  if (P) *P = (uint32_t)MPCX_CLASS_P(mod->cls);
+  if (K) *K = (uint32_t)MPCX_CLASS_K(mod->cls);
+  if (G) *G = (uint32_t)MPCX_CLASS_G(mod->cls);
+  return MPCX_OK;
+}
+
+static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
+                                const uint32_t* d_exps, uint32_t exp_words, int exp_shared, uint32_t exp_bits,
+                                uint32_t* d_out, uint32_t out_words, hipStream_t st) {
+  const uint32_t class_words = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
+  if (base_words > class_words)
+    return fail(MPCX_EINVAL, "base_words %u exceeds the class width %u (reduce mod m first)", base_words, class_words);
+  if (out_words < mod->words) return fail(MPCX_EINVAL, "out_words %u < modulus words %u", out_words, mod->words);
+  if (exp_bits > 32u * exp_words) return fail(MPCX_EINVAL, "exp_bits %u > 32*exp_words", exp_bits);
+  if (count == 0) return MPCX_OK;
+  if (!d_bases || !d_out || (exp_words && !d_exps)) return fail(MPCX_EINVAL, "null buffer");
+  const uint32_t G = (uint32_t)MPCX_CLASS_G(mod->cls), K = (uint32_t)MPCX_CLASS_K(mod->cls);
+  const uint32_t waves = (count + G - 1) / G;
+  int rc = ensure_workspace((size_t)waves * 16u * K * 64u * sizeof(uint32_t));
+  if (rc) return rc;
+  mpcx::ModexpArgs a;
+  a.nd = mod->d_const;
+  a.r1d = mod->d_const + mod->L;
+  a.r2d = mod->d_const + 2 * mod->L;
+  a.base = d_bases;
+  a.exps = d_exps;
+  a.out = d_out;
+  a.table = g_ws;
+  a.count = count;
+  a.base_words = base_words;
+  a.exp_words = exp_words;
+  a.exp_bits = exp_words ? exp_bits : 0;
+  a.out_words = out_words;
+  a.n0inv = mod->n0inv;
+  a.exp_shared = exp_shared ? 1 : 0;
+  hipError_t e = mpcx_launch_modexp(mod->cls, &a, waves, st);
+  if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
+  return MPCX_OK;
+}
+
+int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
+                             const uint32_t* d_exps, uint32_t exp_words, int exp_shared, uint32_t exp_bits,
+                             uint32_t* d_out, uint32_t out_words, void* stream) {
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  return modexp_device_locked(mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits, d_out,
+                              out_words, (hipStream_t)stream);
+}
+
+int mpcx_modexp_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
+                      const uint32_t* exps, uint32_t exp_words, int exp_shared, uint32_t* out,
+                      uint32_t out_words) {
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  if (count == 0) return MPCX_OK;
+  if (!bases || !out || (exp_words && !exps)) return fail(MPCX_EINVAL, "null buffer");
+  if (base_words == 0) return fail(MPCX_EINVAL, "base_words == 0");
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  uint32_t exp_bits = 0;
+  const size_t n_exp_words = exp_shared ? exp_words : (size_t)count * exp_words;
+  if (exp_shared) {
+    exp_bits = bit_length_words(exps, exp_words);
+  } else {
+    for (uint32_t i = 0; i < count; ++i)
+      exp_bits = std::max(exp_bits, bit_length_words(exps + (size_t)i * exp_words, exp_words));
+  }
+  const size_t bb = (size_t)count * base_words * 4, eb = std::max<size_t>(n_exp_words * 4, 4),
+               ob = (size_t)count * out_words * 4;
+  if ((rc = ensure_buffer(g_stage[0], bb)) || (rc = ensure_buffer(g_stage[1], eb)) ||
+      (rc = ensure_buffer(g_stage[2], ob)))
+    return rc;
+  hipError_t e = hipMemcpy(g_stage[0].ptr, bases, bb, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n_exp_words) e = hipMemcpy(g_stage[1].ptr, exps, n_exp_words * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "copy inputs");
+  rc = modexp_device_locked(mod, count, (const uint32_t*)g_stage[0].ptr, base_words,
+                            (const uint32_t*)g_stage[1].ptr, exp_words, exp_shared, exp_bits,
+                            (uint32_t*)g_stage[2].ptr, out_words, nullptr);
+  if (rc) return rc;
+  e = hipMemcpy(out, g_stage[2].ptr, ob, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "copy results");
+  return MPCX_OK;
+}
+
+int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint8_t* ok) {
+  if (count == 0) return MPCX_OK;
+  if (!p || !ok || p_words == 0) return fail(MPCX_EINVAL, "null buffer");
+  if (p_words > (uint32_t)MPCX_CLASS_WORDS(0))
+    return fail(MPCX_EINVAL, "p_words %u > %d", p_words, MPCX_CLASS_WORDS(0));
+  for (uint32_t i = 0; i < count; ++i) {
+    const uint32_t* pi = p + (size_t)i * p_words;
+    const uint32_t bits = bit_length_words(pi, p_words);
+    if (bits > (uint32_t)MPCX_CLASS_MAXBITS(0))
+      return fail(MPCX_EINVAL, "candidate %u has %u bits > %d", i, bits, MPCX_CLASS_MAXBITS(0));
+    if (bits < 3 || (pi[0] & 1u) == 0) return fail(MPCX_EINVAL, "candidate %u is not an odd integer >= 5", i);
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  const size_t pb = (size_t)count * p_words * 4;
+  if ((rc = ensure_buffer(g_stage[0], pb)) || (rc = ensure_buffer(g_stage[3], count))) return rc;
+  hipError_t e = hipMemcpy(g_stage[0].ptr, p, pb, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "copy candidates");
+  mpcx::FermatArgs a;
+  a.p = (const uint32_t*)g_stage[0].ptr;
+  a.ok = (uint8_t*)g_stage[3].ptr;
+  a.count = count;
+  a.p_words = p_words;
+  e = mpcx_launch_fermat2(&a, (count + 63) / 64, nullptr);
+  if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
+  e = hipMemcpy(ok, g_stage[3].ptr, count, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "copy results");
+  return MPCX_OK;
+}
+
+int mpcx_dev_alloc(size_t bytes, void** out_ptr) {
+  if (!out_ptr) return fail(MPCX_EINVAL, "null out_ptr");
+  if (int rc = ensure_device()) return rc;
+  hipError_t e = hipMalloc(out_ptr, bytes);
+  if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  return MPCX_OK;
+}
+
+int mpcx_dev_free(void* ptr) {
+  hipError_t e = hipFree(ptr);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipFree");
+}
+
+int mpcx_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes) {
+  hipError_t e = hipMemcpy(d_dst, h_src, bytes, hipMemcpyHostToDevice);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipMemcpy H2D");
+}
+
+int mpcx_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes) {
+  hipError_t e = hipMemcpy(h_dst, d_src, bytes, hipMemcpyDeviceToHost);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipMemcpy D2H");
+}
+
+int mpcx_stream_create(void** out_stream) {
+  if (!out_stream) return fail(MPCX_EINVAL, "null out_stream");
+  hipStream_t s;
+  hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
+  if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
+  *out_stream = (void*)s;
+  return MPCX_OK;
+}
+
+int mpcx_stream_destroy(void* stream) {
+  hipError_t e = hipStreamDestroy((hipStream_t)stream);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipStreamDestroy");
+}
+
+int mpcx_stream_sync(void* stream) {
+  hipError_t e = hipStreamSynchronize((hipStream_t)stream);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipStreamSynchronize");
+}
+
+}  // extern "C"

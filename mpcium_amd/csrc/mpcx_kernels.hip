@@ -1,0 +1,508 @@
+// mpcx_kernels.hip -- gfx950 (MI355X, CDNA4) batched modular exponentiation.
+//
+// Replaces the arithmetic of Go math/big (*Int).Exp -> nat.expNNMontgomery
+// (go1.23.5, go:src/math/big/nat.go) as reached through tss-lib v2.0.2
+// common.ModInt(m).Exp (up:common/int.go) on mpcium's hot path
+// (/root/reference/pkg/mpc/session.go:199 -> party.UpdateFromBytes -> Paillier /
+// MtA proofs; /root/reference/pkg/mpc/node.go:69 -> GeneratePreParams).
+//
+// Design (DESIGN.md section "Kernels"):
+//  * Radix 2^28 digits held in 64-bit lazy accumulators. A 28x28-bit product
+//    is < 2^56, so an accumulator absorbs > 100 products before it can
+//    overflow: every multiply-accumulate is ONE v_mad_u64_u32 (half rate on
+//    gfx950, measured ~33.8 T/s/GPU), with no per-MAC carry instruction --
+//    the carry-writing v_add_co/v_addc are half rate as well, so a 32-bit-limb
+//    carry chain would cost >= 2 half-rate ops per MAC.
+//  * Wavefront-cooperative operands: one 64-lane wavefront holds G operands;
+//    operand g is spread over P lanes, each lane holding K consecutive digits
+//    (L = P*K digits, R = 2^(28L) > 4m so no conditional subtraction is ever
+//    needed inside the exponentiation: almost-Montgomery, results < 2m).
+//  * Row-wise (CIOS) Montgomery: per digit b_i of the multiplier, every lane
+//    does K mads for a*b_i, the group's lane 0 derives m_i, one ds_bpermute
+//    broadcasts it, K more mads for m_i*N, then the accumulator window shifts
+//    one digit: within a lane by register renaming (the K-iteration block is
+//    unrolled), across lanes by ONE DPP wave_shl of a 28-bit value (the slot's
+//    high part is folded into the next slot first).
+//  * Fixed 4-bit window exponentiation like Go (16-entry table per operand in
+//    a global workspace, lane-coalesced layout); b operands are staged in LDS
+//    and read as group-broadcast ds_read_b32.
+//  * MFMA is not used: this is not a dense contraction.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <type_traits>
+
+#include "mpcx_internal.h"
+
+#ifndef MPCX_WAVES_PER_EU_C0
+#define MPCX_WAVES_PER_EU_C0 2
+#endif
+#ifndef MPCX_WAVES_PER_EU_C1
+#define MPCX_WAVES_PER_EU_C1 2
+#endif
+#ifndef MPCX_WAVES_PER_EU_C2
+#define MPCX_WAVES_PER_EU_C2 2
+#endif
+
+namespace mpcx {
+
+// Compile-time loop: f(std::integral_constant<int, i>) for i in [B, E).
+// Guarantees constant register-array indices (a partially unrolled loop
+// would demote the accumulators to scratch memory).
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+  if constexpr (B < E) {
+    f(std::integral_constant<int, B>{});
+    static_for<B + 1, E>(f);
+  }
+}
+
+constexpr int DB = 28;
+constexpr uint32_t M28 = (1u << DB) - 1u;
+
+// lane l receives lane l+1's value; lane 63 receives 0 (DPP wave_shl:1, bound_ctrl zero).
+__device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x130, 0xF, 0xF, true);
+}
+// lane l receives lane l-1's value; lane 0 receives 0 (DPP wave_shr:1).
+__device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// One carry pass over 64-bit redundant digits: digit k keeps its low 28 bits
+// and receives the high part of digit k-1 (across lanes via DPP). The carry
+// out of a group's top digit is provably zero (value < R), so group
+// boundaries need no masking.
+template <int P, int K>
+__device__ __forceinline__ void carry_pass64(uint64_t (&acc)[K]) {
+  uint64_t c[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    c[k] = acc[k] >> DB;
+    acc[k] &= M28;
+  }
+#pragma unroll
+  for (int k = 1; k < K; ++k) acc[k] += c[k - 1];
+  if constexpr (P > 1) {
+    const uint32_t clo = from_prev_lane((uint32_t)c[K - 1]);
+    const uint32_t chi = from_prev_lane((uint32_t)(c[K - 1] >> 32));
+    acc[0] += ((uint64_t)chi << 32) | clo;
+  }
+}
+
+template <int P, int K>
+__device__ __forceinline__ void carry_pass32(uint32_t (&d)[K]) {
+  uint32_t c[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    c[k] = d[k] >> DB;
+    d[k] &= M28;
+  }
+#pragma unroll
+  for (int k = 1; k < K; ++k) d[k] += c[k - 1];
+  if constexpr (P > 1) d[0] += from_prev_lane(c[K - 1]);
+}
+
+// A <- A * B * R^-1 (almost Montgomery, result < 2N given A, B < 2N), with
+// B's L digits in LDS at bl[0..L). Result digits are <= 2^28 + 2^10
+// (two carry passes), which keeps every product below 2^56.01.
+template <int P, int K>
+__device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, const uint32_t (&Nd)[K],
+                                        uint32_t n0inv, int m_src_addr) {
+  uint64_t acc[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) acc[k] = 0;
+  for (int o = 0; o < P; ++o) {
+    const uint32_t* bo = bl + o * K;
+    static_for<0, K>([&](auto uc) {
+      constexpr int u = decltype(uc)::value;
+      const uint32_t bi = bo[u];
+      static_for<0, K>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        acc[(k + u) % K] += (uint64_t)A[k] * bi;
+      });
+      uint32_t m = ((uint32_t)acc[u] * n0inv) & M28;
+      if constexpr (P > 1) m = (uint32_t)__builtin_amdgcn_ds_bpermute(m_src_addr, (int)m);
+      static_for<0, K>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        acc[(k + u) % K] += (uint64_t)m * Nd[k];
+      });
+      const uint64_t a0 = acc[u];
+      acc[(u + 1) % K] += a0 >> DB;
+      if constexpr (P > 1) {
+        acc[u] = from_next_lane((uint32_t)a0 & M28);
+      } else {
+        acc[u] = 0;
+      }
+    });
+    // Keep every accumulator below 2^64: at most ~P/2*K + K more iterations of
+    // two < 2^56.01 products follow this pass (<= 127 for every class).
+    if (o == P / 2 - 1) carry_pass64<P, K>(acc);
+  }
+  carry_pass64<P, K>(acc);
+  // digits are now < 2^28 + 2^37: one more pass brings them to <= 2^28 + 2^10
+  uint32_t c[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    c[k] = (uint32_t)(acc[k] >> DB);
+    A[k] = (uint32_t)acc[k] & M28;
+  }
+#pragma unroll
+  for (int k = 1; k < K; ++k) A[k] += c[k - 1];
+  if constexpr (P > 1) A[0] += from_prev_lane(c[K - 1]);
+}
+
+// Canonical digits (< 2^28): repeat carry passes until no digit overflows.
+template <int P, int K>
+__device__ __forceinline__ void canonicalize(uint32_t (&A)[K]) {
+  for (int it = 0; it < P * K + 2; ++it) {
+    bool over = false;
+#pragma unroll
+    for (int k = 0; k < K; ++k) over |= A[k] > M28;
+    if (!__any(over)) break;
+    carry_pass32<P, K>(A);
+  }
+}
+
+template <int K>
+__device__ __forceinline__ void lds_store_digits(uint32_t* bl, int p, const uint32_t (&A)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) bl[p * K + k] = A[k];
+}
+
+__device__ __forceinline__ uint32_t window_of(const uint32_t* e, uint32_t j) {
+  return (e[(4u * j) >> 5] >> ((4u * j) & 31u)) & 15u;
+}
+
+// Batched x_i^e_i mod m for one registered odd modulus m.
+template <int P, int K, int G, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp(const ModexpArgs a) {
+  constexpr int L = P * K;
+  __shared__ uint32_t lds[(G + 1) * L];
+  const int lane = threadIdx.x;
+  const int g_raw = lane / P;
+  const bool idle = g_raw >= G;  // lanes beyond G*P carry zeros
+  const int g = idle ? G : g_raw;
+  const int p = lane - g_raw * P;
+  const uint32_t op = blockIdx.x * G + (idle ? 0 : g_raw);
+  const bool active = !idle && op < a.count;
+  uint32_t* bl = lds + g * L;
+  const int m_src_addr = (idle ? lane : g_raw * P) * 4;
+
+  uint32_t Nd[K], A[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) Nd[k] = idle ? 0u : a.nd[p * K + k];
+
+  // base words -> radix-2^28 digits (inactive operands compute on zero)
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t d = (uint32_t)(p * K + k);
+    const uint32_t bit = d * DB;
+    const uint32_t w = bit >> 5, s = bit & 31u;
+    uint64_t v = 0;
+    if (active) {
+      const uint32_t* x = a.base + (size_t)op * a.base_words;
+      const uint32_t lo = w < a.base_words ? x[w] : 0u;
+      const uint32_t hi = (w + 1) < a.base_words ? x[w + 1] : 0u;
+      v = ((uint64_t)hi << 32) | lo;
+    }
+    A[k] = (uint32_t)(v >> s) & M28;
+  }
+
+  const uint32_t nw = (a.exp_bits + 3u) / 4u;
+  const uint32_t* ex = a.exp_shared ? a.exps : a.exps + (size_t)(active ? op : 0) * a.exp_words;
+  uint32_t* tbl = a.table + (size_t)blockIdx.x * 16u * K * 64u;
+  auto tbl_at = [&](uint32_t e, int k) -> uint32_t* { return tbl + ((size_t)e * K + k) * 64u + lane; };
+
+  // table[0] = R mod m (Montgomery one)
+#pragma unroll
+  for (int k = 0; k < K; ++k) *tbl_at(0, k) = idle ? 0u : a.r1d[p * K + k];
+  // step 0: p1 = x * R^2 * R^-1
+  {
+    uint32_t r2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) r2[k] = idle ? 0u : a.r2d[p * K + k];
+    lds_store_digits<K>(bl, p, r2);
+  }
+  wave_lds_fence();
+
+  // Step schedule: 15 table steps (s = 0..14 produce p1..p15), then for each
+  // window below the top one 4 squarings + 1 multiply, then the final
+  // multiply by 1 that leaves the Montgomery domain.
+  const uint32_t nexp = nw > 0 ? 5u * (nw - 1u) : 0u;
+  const uint32_t S = 15u + nexp + 1u;
+  for (uint32_t s = 0; s < S; ++s) {
+    montmul<P, K>(A, bl, Nd, a.n0inv, m_src_addr);
+    wave_lds_fence();
+    if (s < 15u) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) *tbl_at(s + 1, k) = A[k];
+      if (s == 0) {
+        lds_store_digits<K>(bl, p, A);  // B = p1 for the remaining table steps
+      }
+      if (s == 14) {
+        // z = table[top window] (or Montgomery one for a zero exponent)
+        const uint32_t wt = nw > 0 ? window_of(ex, nw - 1u) : 0u;
+        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+#pragma unroll
+        for (int k = 0; k < K; ++k) A[k] = *tbl_at(wt, k);
+        if (nexp == 0) {
+          uint32_t one[K];
+#pragma unroll
+          for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
+          lds_store_digits<K>(bl, p, one);
+        } else {
+          lds_store_digits<K>(bl, p, A);
+        }
+      }
+    } else if (s + 1u < S) {
+      // just finished exponent step t = s - 15; prepare step t + 1
+      const uint32_t t = s - 15u + 1u;
+      if (t == nexp) {
+        uint32_t one[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
+        lds_store_digits<K>(bl, p, one);
+      } else {
+        const uint32_t sub = t % 5u;
+        if (sub < 4u) {
+          lds_store_digits<K>(bl, p, A);
+        } else {
+          const uint32_t j = nw - 2u - t / 5u;
+          const uint32_t w = window_of(ex, j);
+          if (a.exp_shared && w == 0u) {
+            // multiplying by Montgomery one is the identity mod m: skip it
+            // (uniform across the wavefront), go straight to the next squaring
+            ++s;
+            if (t + 1u == nexp) {
+              uint32_t one[K];
+#pragma unroll
+              for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
+              lds_store_digits<K>(bl, p, one);
+            } else {
+              lds_store_digits<K>(bl, p, A);
+            }
+          } else {
+            uint32_t tv[K];
+#pragma unroll
+            for (int k = 0; k < K; ++k) tv[k] = *tbl_at(w, k);
+            lds_store_digits<K>(bl, p, tv);
+          }
+        }
+      }
+    }
+    wave_lds_fence();
+  }
+
+  // A < 2m after the first-domain exit is <= m; make digits canonical, map m -> 0.
+  canonicalize<P, K>(A);
+  bool eq = true;
+#pragma unroll
+  for (int k = 0; k < K; ++k) eq &= (A[k] == Nd[k]);
+  const uint64_t bal = __ballot(eq || idle);
+  const uint64_t gmask = (P == 64 ? ~0ull : (((1ull << P) - 1ull) << (g_raw * P)));
+  if (!idle && (bal & gmask) == gmask) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) A[k] = 0;
+  }
+  // digits -> words through LDS
+  wave_lds_fence();
+  lds_store_digits<K>(bl, p, A);
+  wave_lds_fence();
+  if (active) {
+    uint32_t* o = a.out + (size_t)op * a.out_words;
+    for (uint32_t w = (uint32_t)p; w < a.out_words; w += P) {
+      const uint32_t bit = w * 32u;
+      const uint32_t d0 = bit / DB, s0 = bit % DB;
+      uint32_t v = 0;
+      if (d0 < (uint32_t)L) {
+        // s0 = 32w mod 28 <= 24, so bits [s0, s0+32) lie in two digits
+        const uint64_t lo = bl[d0];
+        const uint64_t hi = (d0 + 1 < (uint32_t)L) ? bl[d0 + 1] : 0u;
+        v = (uint32_t)((lo | (hi << DB)) >> s0);
+      }
+      o[w] = v;
+    }
+  }
+}
+
+// ---------------------------------------------------------------- Fermat(2)
+// ok[i] = 2^(p_i - 1) mod p_i == 1, one candidate per lane (P = 1, thread per
+// operand, per-lane modulus). Square-and-double: squarings are Montgomery
+// squarings, the "multiply by 2" is a digit doubling with no reduction (values
+// stay < 4p << R/4, which the almost-Montgomery bound absorbs).
+template <int K>
+__device__ __forceinline__ bool ge_digits(const uint32_t (&x)[K], const uint32_t (&y)[K]) {
+  // branch-free lexicographic compare from the top digit
+  int r = 0;  // 0 = equal so far, 1 = x > y, -1 = x < y
+#pragma unroll
+  for (int k = K - 1; k >= 0; --k) {
+    const int c = (x[k] > y[k]) - (x[k] < y[k]);
+    r = r != 0 ? r : c;
+  }
+  return r >= 0;
+}
+template <int K>
+__device__ __forceinline__ void sub_digits(uint32_t (&x)[K], const uint32_t (&y)[K]) {
+  uint32_t br = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t t = x[k] - y[k] - br;
+    br = (t >> 31) & 1u;  // digits < 2^28: a borrow shows as the sign bit
+    x[k] = t & M28;
+  }
+}
+template <int K>
+__device__ __forceinline__ void norm_serial(uint32_t (&x)[K]) {
+  uint32_t c = 0;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t t = x[k] + c;
+    x[k] = t & M28;
+    c = t >> DB;
+  }
+}
+
+template <int K, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fermat2(const FermatArgs a) {
+  constexpr int L = K;
+  __shared__ uint32_t lds[65 * L];
+  const int lane = threadIdx.x;
+  const uint32_t op = blockIdx.x * 64u + lane;
+  const bool active = op < a.count;
+  uint32_t* bl = lds + lane * L;
+  uint32_t Nd[K], A[K];
+  const uint32_t* pw = a.p + (size_t)(active ? op : 0) * a.p_words;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t bit = (uint32_t)k * DB;
+    const uint32_t w = bit >> 5, s = bit & 31u;
+    uint64_t v = 0;
+    if (active) {
+      const uint32_t lo = w < a.p_words ? pw[w] : 0u;
+      const uint32_t hi = (w + 1) < a.p_words ? pw[w + 1] : 0u;
+      v = ((uint64_t)hi << 32) | lo;
+    }
+    Nd[k] = (uint32_t)(v >> s) & M28;
+  }
+  if (!active) Nd[0] = 1;  // dummy odd modulus
+  // n0inv = -p^-1 mod 2^28 (Newton on 32 bits)
+  uint32_t inv = Nd[0];
+  for (int i = 0; i < 5; ++i) inv *= 2u - Nd[0] * inv;
+  const uint32_t n0inv = (0u - inv) & M28;
+  // bit length of p (unrolled: no dynamic register indexing)
+  int pbits = 1;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (Nd[k] != 0u) pbits = k * DB + (32 - __builtin_clz(Nd[k]));
+  // R mod p, R = 2^(28K): t = 2^pbits - p (< p), then (28K - pbits) doublings mod p
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] = 0;
+  {
+    // two's complement of p within pbits bits
+    uint32_t c = 1;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int lo = k * DB;
+      uint32_t maskk = 0;
+      if (pbits >= lo + DB) maskk = M28;
+      else if (pbits > lo) maskk = (1u << (pbits - lo)) - 1u;
+      const uint32_t t = ((~Nd[k]) & maskk) + c;
+      c = t >> DB;
+      A[k] = t & maskk;
+    }
+  }
+  for (int i = pbits; i < DB * K; ++i) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) A[k] <<= 1;
+    norm_serial<K>(A);
+    if (ge_digits<K>(A, Nd)) sub_digits<K>(A, Nd);
+  }
+  // A = R mod p = Montgomery form of 1. The top bit of e = p - 1 is set, so
+  // start from 2 (Montgomery form 2R, left unreduced: < 2p).
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] <<= 1;
+  norm_serial<K>(A);
+  const int m_src_addr = lane * 4;
+  for (int i = pbits - 2; i >= 0; --i) {
+    // A <- A^2 / R
+    lds_store_digits<K>(bl, 0, A);
+    wave_lds_fence();
+    montmul<1, K>(A, bl, Nd, n0inv, m_src_addr);
+    wave_lds_fence();
+    uint32_t ebit = active ? (pw[i >> 5] >> (i & 31)) & 1u : 0u;
+    if (i == 0) ebit = 0;  // e = p - 1
+    if (ebit) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) A[k] <<= 1;
+      norm_serial<K>(A);
+    }
+  }
+  // leave the Montgomery domain: A * 1 / R, then canonical compare with 1
+  {
+    uint32_t one[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) one[k] = (k == 0) ? 1u : 0u;
+    lds_store_digits<K>(bl, 0, one);
+    wave_lds_fence();
+    montmul<1, K>(A, bl, Nd, n0inv, m_src_addr);
+  }
+  norm_serial<K>(A);
+  while (ge_digits<K>(A, Nd)) sub_digits<K>(A, Nd);
+  bool is_one = A[0] == 1u;
+#pragma unroll
+  for (int k = 1; k < K; ++k) is_one &= A[k] == 0u;
+  if (active) a.ok[op] = is_one ? 1 : 0;
+}
+
+// Device self-test of the cross-lane primitives the kernels rely on.
+__global__ void k_selftest(uint32_t* out) {
+  const int lane = threadIdx.x;
+  out[lane] = from_next_lane(1000u + lane);
+  out[64 + lane] = from_prev_lane(1000u + lane);
+  out[128 + lane] = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane / 7) * 7) * 4, (int)(2000 + lane));
+  const uint64_t acc = (uint64_t)(0xFFFFFFF0u + lane) * (0xFFFFFFF7u - lane) + 0xFFFFFFFFFFFFull;
+  out[192 + lane] = (uint32_t)(acc >> 32);
+}
+
+}  // namespace mpcx
+
+// ------------------------------------------------------------ launchers
+#define MPCX_WPE(c) ((c) == 0 ? MPCX_WAVES_PER_EU_C0 : (c) == 1 ? MPCX_WAVES_PER_EU_C1 : MPCX_WAVES_PER_EU_C2)
+
+extern "C" {
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_modexp(int cls, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st) {
+  switch (cls) {
+#define MPCX_CASE(C)                                                                                        \
+  case C:                                                                                                   \
+    hipLaunchKernelGGL((mpcx::k_modexp<MPCX_CLASS_P(C), MPCX_CLASS_K(C), MPCX_CLASS_G(C), MPCX_WPE(C)>),   \
+                       dim3(waves),                                                                         \
+                       dim3(64), 0, st, *a);                                                                \
+    return hipGetLastError();
+    MPCX_CASE(0)
+    MPCX_CASE(1)
+    MPCX_CASE(2)
+#undef MPCX_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks,
+                                                                    hipStream_t st) {
+  hipLaunchKernelGGL((mpcx::k_fermat2<MPCX_CLASS_K(0), MPCX_WAVES_PER_EU_C0>), dim3(blocks), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st) {
+  hipLaunchKernelGGL(mpcx::k_selftest, dim3(1), dim3(64), 0, st, d_out);
+  return hipGetLastError();
+}
+
+}  // extern "C"

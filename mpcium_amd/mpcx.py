@@ -1,0 +1,197 @@
+"""ctypes binding of libmpcx.so (include/mpcx.h).
+
+Integers cross the boundary as little-endian 32-bit words, operand-major.
+No fallback: if libmpcx.so is missing or the GPU call fails, an exception is
+raised.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Iterable, List, Optional, Sequence, Union
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libmpcx.so")
+
+MPCX_OK, MPCX_EINVAL, MPCX_ENODEV, MPCX_EHIP, MPCX_ENOMEM = 0, 1, 2, 3, 4
+
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+_vp = ctypes.c_void_p
+
+# (name, restype, argtypes) -- must match include/mpcx.h
+SIGNATURES = [
+    ("mpcx_version", ctypes.c_int, []),
+    ("mpcx_last_error", ctypes.c_char_p, []),
+    ("mpcx_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
+    ("mpcx_init", ctypes.c_int, [ctypes.c_int]),
+    ("mpcx_shutdown", ctypes.c_int, []),
+    ("mpcx_modulus_register", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    ("mpcx_modulus_release", ctypes.c_int, [_vp]),
+    ("mpcx_modulus_info", ctypes.c_int, [_vp, _u32p, _u32p]),
+    ("mpcx_modulus_geometry", ctypes.c_int, [_vp, _u32p, _u32p, _u32p, _u32p]),
+    ("mpcx_modexp_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
+                                         ctypes.c_int, _vp, ctypes.c_uint32]),
+    ("mpcx_modexp_batch_device", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
+                                                ctypes.c_int, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    ("mpcx_fermat2_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    ("mpcx_dev_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
+    ("mpcx_dev_free", ctypes.c_int, [_vp]),
+    ("mpcx_memcpy_h2d", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    ("mpcx_memcpy_d2h", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
+    ("mpcx_stream_create", ctypes.c_int, [ctypes.POINTER(_vp)]),
+    ("mpcx_stream_destroy", ctypes.c_int, [_vp]),
+    ("mpcx_stream_sync", ctypes.c_int, [_vp]),
+]
+
+
+class MpcxError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"mpcx error {code}: {msg}")
+        self.code = code
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libmpcx.so (raises if it has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise MpcxError(MPCX_ENODEV, f"{_LIB_PATH} not built: run `python -m mpcium_amd.build`")
+        l = ctypes.CDLL(_LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def _check(rc: int):
+    if rc != MPCX_OK:
+        raise MpcxError(rc, lib().mpcx_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(lib().mpcx_device_count(ctypes.byref(n)))
+    return n.value
+
+
+def init(device: int = 0):
+    _check(lib().mpcx_init(device))
+
+
+def shutdown():
+    _check(lib().mpcx_shutdown())
+
+
+# ----------------------------------------------------------- int <-> words
+def int_to_words(v: int, n: int) -> np.ndarray:
+    if v < 0:
+        raise ValueError("negative integers do not cross the C-ABI")
+    return np.frombuffer(v.to_bytes(4 * n, "little"), dtype="<u4").copy()
+
+
+def ints_to_words(vals: Sequence[int], n: int) -> np.ndarray:
+    buf = b"".join(int(v).to_bytes(4 * n, "little") for v in vals)
+    return np.frombuffer(buf, dtype="<u4").reshape(len(vals), n).copy()
+
+
+def words_to_ints(arr: np.ndarray) -> List[int]:
+    arr = np.ascontiguousarray(arr, dtype="<u4")
+    n = arr.shape[1]
+    raw = arr.tobytes()
+    return [int.from_bytes(raw[i * 4 * n:(i + 1) * 4 * n], "little") for i in range(arr.shape[0])]
+
+
+def nwords(v: int) -> int:
+    return max(1, (v.bit_length() + 31) // 32)
+
+
+class Modulus:
+    """A registered odd modulus (mpcx_modulus_register)."""
+
+    def __init__(self, m: int):
+        if m <= 0:
+            raise ValueError("modulus must be positive")
+        self.m = m
+        w = int_to_words(m, nwords(m))
+        h = _vp()
+        _check(lib().mpcx_modulus_register(w.ctypes.data, len(w), ctypes.byref(h)))
+        self._h = h
+        bits, cw = ctypes.c_uint32(), ctypes.c_uint32()
+        _check(lib().mpcx_modulus_info(h, ctypes.byref(bits), ctypes.byref(cw)))
+        self.bits, self.class_words = bits.value, cw.value
+        g = [ctypes.c_uint32() for _ in range(4)]
+        _check(lib().mpcx_modulus_geometry(h, *[ctypes.byref(x) for x in g]))
+        self.L, self.P, self.K, self.G = (x.value for x in g)
+        self.words = nwords(m)
+
+    @property
+    def handle(self):
+        return self._h
+
+    def release(self):
+        if self._h:
+            _check(lib().mpcx_modulus_release(self._h))
+            self._h = None
+
+    def exp_words(self, bases: np.ndarray, exps: np.ndarray, shared: bool, out_words: Optional[int] = None) -> np.ndarray:
+        """Raw word-level batch: bases (count, bw) uint32, exps (ew,) or (count, ew)."""
+        bases = np.ascontiguousarray(bases, dtype="<u4")
+        exps = np.ascontiguousarray(exps, dtype="<u4")
+        count, bw = bases.shape
+        ew = exps.shape[-1] if exps.size else 0
+        ow = out_words or self.words
+        out = np.zeros((count, ow), dtype="<u4")
+        _check(lib().mpcx_modexp_batch(self._h, count, bases.ctypes.data, bw,
+                                       exps.ctypes.data if exps.size else None, ew, 1 if shared else 0,
+                                       out.ctypes.data, ow))
+        return out
+
+    def exp(self, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> List[int]:
+        """[b^e mod m] for non-negative ints; `exps` is one shared int or one per base."""
+        if len(bases) == 0:
+            return []
+        bw = self.class_words
+        lim = 1 << (32 * bw)
+        if any(b < 0 or b >= lim for b in bases):
+            raise ValueError("bases must be in [0, 2^(32*class_words)); reduce mod m first")
+        B = ints_to_words(bases, bw)
+        if isinstance(exps, int):
+            if exps < 0:
+                raise ValueError("negative exponent")
+            E = int_to_words(exps, nwords(exps)) if exps else np.zeros(0, dtype="<u4")
+            shared = True
+        else:
+            if len(exps) != len(bases):
+                raise ValueError("one exponent per base")
+            if any(e < 0 for e in exps):
+                raise ValueError("negative exponent")
+            ew = max(nwords(e) for e in exps)
+            E = ints_to_words(exps, ew)
+            shared = False
+        return words_to_ints(self.exp_words(B, E, shared))
+
+
+def exp_batch(m: int, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> List[int]:
+    mod = Modulus(m)
+    try:
+        return mod.exp(bases, exps)
+    finally:
+        mod.release()
+
+
+def fermat2_batch(cands: Sequence[int]) -> List[bool]:
+    """[2^(p-1) mod p == 1] for odd candidates p (5 <= p < 2^1024)."""
+    if len(cands) == 0:
+        return []
+    pw = max(nwords(p) for p in cands)
+    P = ints_to_words(cands, pw)
+    ok = np.zeros(len(cands), dtype=np.uint8)
+    _check(lib().mpcx_fermat2_batch(len(cands), P.ctypes.data, pw, ok.ctypes.data))
+    return [bool(x) for x in ok]

@@ -1,0 +1,104 @@
+"""GPU parity tests: every result through libmpcx.so (C-ABI) must equal the
+oracle bit for bit (integer arithmetic, no tolerance)."""
+import random
+
+import numpy as np
+import pytest
+
+from conftest import H
+from oracle import gomath as gm
+
+pytestmark = pytest.mark.gpu
+
+
+def by_modulus(vectors):
+    groups = {}
+    for v in vectors:
+        groups.setdefault(H(v["m"]), []).append(v)
+    return groups
+
+
+def test_golden_vectors_gpu(gpu, golden_modexp):
+    for m, vs in by_modulus(golden_modexp).items():
+        if m % 2 == 0:
+            continue
+        mod = gpu.Modulus(m)
+        # per-operand exponents in one batch
+        xs = [H(v["x"]) for v in vs]
+        ys = [H(v["y"]) for v in vs]
+        lim = 1 << (32 * mod.class_words)
+        xs_in = [x if x < lim else x % m for x in xs]
+        got = mod.exp(xs_in, ys)
+        for v, g in zip(vs, got):
+            assert g == H(v["z"]), v["name"]
+        # and each one with a shared exponent
+        for v, x in zip(vs, xs_in):
+            assert mod.exp([x], H(v["y"]))[0] == H(v["z"]), v["name"] + " shared"
+        mod.release()
+
+
+@pytest.mark.parametrize("bits", [64, 1024, 2048, 4096])
+def test_ragged_batches_shared_exponent(gpu, bits):
+    rng = random.Random(bits)
+    m = rng.getrandbits(bits) | 1 | (1 << (bits - 1))
+    mod = gpu.Modulus(m)
+    e = rng.getrandbits(bits // 2) | 1
+    for count in (1, mod.G - 1, mod.G, mod.G + 1, 3 * mod.G + 5):
+        xs = [rng.randrange(m) for _ in range(count)]
+        assert mod.exp(xs, e) == [pow(x, e, m) for x in xs], count
+    mod.release()
+
+
+def test_empty_batch(gpu):
+    mod = gpu.Modulus((1 << 127) - 1)
+    assert mod.exp([], 5) == []
+
+
+def test_zero_and_small_exponents(gpu, paillier_key):
+    N2 = paillier_key["N"] ** 2
+    mod = gpu.Modulus(N2)
+    rng = random.Random(3)
+    xs = [rng.randrange(N2) for _ in range(20)] + [0, 1, N2 - 1]
+    for e in (0, 1, 2, 3, 15, 16, 17, (1 << 64) - 1, 1 << 64):
+        assert mod.exp(xs, e) == [gm.go_exp(x, e, N2) for x in xs], e
+
+
+def test_shared_exponent_N_config2_sample(gpu, paillier_key):
+    """Config-2 shape (x^N mod N^2) at a reduced count; full size runs in bench.py."""
+    N = paillier_key["N"]
+    N2 = N * N
+    mod = gpu.Modulus(N2)
+    rng = gm.CounterDRBG(0x6D706332)
+    xs = [rng.randbelow(N2) for _ in range(2 * mod.G * 7 + 3)]
+    got = mod.exp(xs, N)
+    for x, g in zip(xs, got):
+        assert g == pow(x, N, N2)
+
+
+def test_per_operand_exponents_mixed_lengths(gpu, paillier_key):
+    N = paillier_key["N"]
+    N2 = N * N
+    mod = gpu.Modulus(N2)
+    rng = random.Random(11)
+    xs = [rng.randrange(N2) for _ in range(40)]
+    ys = [rng.getrandbits(rng.choice([0, 1, 5, 256, 768, 2048, 4096])) for _ in xs]
+    assert mod.exp(xs, ys) == [pow(x, y, N2) for x, y in zip(xs, ys)]
+
+
+def test_fermat2_batch(gpu, paillier_key):
+    rng = random.Random(5)
+    P, Q = paillier_key["P"], paillier_key["Q"]
+    cands = [P, Q, (P - 1) // 2 * 2 + 1]
+    cands += [rng.getrandbits(1024) | 1 | (1 << 1023) for _ in range(100)]
+    cands += [rng.getrandbits(b) | 1 | (1 << (b - 1)) for b in (8, 64, 300, 512, 1000) for _ in range(3)]
+    cands += [101, 65537, 561, 1105]  # primes and Carmichael numbers (which pass base 2)
+    got = gpu.fermat2_batch(cands)
+    assert got == [pow(2, p - 1, p) == 1 for p in cands]
+    assert got[0] and got[1]
+
+
+def test_rejects_even_and_oversized_modulus(gpu):
+    with pytest.raises(gpu.MpcxError):
+        gpu.Modulus(1 << 100)
+    with pytest.raises(gpu.MpcxError):
+        gpu.Modulus((1 << 4097) + 1)
