@@ -114,6 +114,30 @@ int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count,
                              uint32_t exp_bits,
                              uint32_t* d_out, uint32_t out_words, void* stream);
 
+/* Fused variant: out[i] = muls[i] * bases[i]^e_i mod m (muls: count x
+ * mul_words words, mul_words <= class words). Replaces the
+ * "Exp then ModInt.Mul" pairs of the reference: Paillier Encrypt
+ * c = (1 + m*N) * r^N mod N^2 (up:crypto/paillier/paillier.go
+ * EncryptAndReturnRandomness) and the MtA proof terms. */
+int mpcx_modexp_mul_batch(mpcx_mod_t mod, uint32_t count,
+                          const uint32_t* bases, uint32_t base_words,
+                          const uint32_t* exps, uint32_t exp_words, int exp_shared,
+                          const uint32_t* muls, uint32_t mul_words,
+                          uint32_t* out, uint32_t out_words);
+int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count,
+                                 const uint32_t* d_bases, uint32_t base_words,
+                                 const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
+                                 uint32_t exp_bits,
+                                 const uint32_t* d_muls, uint32_t mul_words,
+                                 uint32_t* d_out, uint32_t out_words, void* stream);
+
+/* out[i] = a[i] * b[i] mod m -- up:common/int.go (*modInt).Mul and
+ * paillier.(*PublicKey).HomoAdd (c1*c2 mod N^2), batched. */
+int mpcx_mulmod_batch(mpcx_mod_t mod, uint32_t count,
+                      const uint32_t* a, uint32_t a_words,
+                      const uint32_t* b, uint32_t b_words,
+                      uint32_t* out, uint32_t out_words);
+
 /* Pocklington/Fermat check for safe-prime candidates: ok[i] = (2^(p_i - 1)
  * mod p_i == 1) for count odd candidates p_i of p_words words each
  * (5 <= p_i < 2^1024, p_words <= 32). Each candidate is its own modulus. */

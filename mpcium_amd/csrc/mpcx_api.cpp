@@ -301,35 +301,79 @@ int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K,
 
 static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
                                 const uint32_t* d_exps, uint32_t exp_words, int exp_shared, uint32_t exp_bits,
-                                uint32_t* d_out, uint32_t out_words, hipStream_t st) {
+                                const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out, uint32_t out_words,
+                                hipStream_t st) {
   const uint32_t class_words = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
-  if (base_words > class_words)
-    return fail(MPCX_EINVAL, "base_words %u exceeds the class width %u (reduce mod m first)", base_words, class_words);
+  if (base_words == 0 || base_words > class_words)
+    return fail(MPCX_EINVAL, "base_words %u outside [1, %u] (reduce mod m first)", base_words, class_words);
+  if (d_muls && (mul_words == 0 || mul_words > class_words))
+    return fail(MPCX_EINVAL, "mul_words %u outside [1, %u]", mul_words, class_words);
   if (out_words < mod->words) return fail(MPCX_EINVAL, "out_words %u < modulus words %u", out_words, mod->words);
   if (exp_bits > 32u * exp_words) return fail(MPCX_EINVAL, "exp_bits %u > 32*exp_words", exp_bits);
   if (count == 0) return MPCX_OK;
   if (!d_bases || !d_out || (exp_words && !d_exps)) return fail(MPCX_EINVAL, "null buffer");
   const uint32_t G = (uint32_t)MPCX_CLASS_G(mod->cls), K = (uint32_t)MPCX_CLASS_K(mod->cls);
   const uint32_t waves = (count + G - 1) / G;
-  int rc = ensure_workspace((size_t)waves * 16u * K * 64u * sizeof(uint32_t));
+  int rc = ensure_workspace((size_t)waves * MPCX_TABLE_ENTRIES * K * 64u * sizeof(uint32_t));
   if (rc) return rc;
-  mpcx::ModexpArgs a;
+  mpcx::ModexpArgs a{};
   a.nd = mod->d_const;
   a.r1d = mod->d_const + mod->L;
   a.r2d = mod->d_const + 2 * mod->L;
   a.base = d_bases;
   a.exps = d_exps;
+  a.mul = d_muls;
   a.out = d_out;
   a.table = g_ws;
   a.count = count;
   a.base_words = base_words;
   a.exp_words = exp_words;
+  a.mul_words = d_muls ? mul_words : 0;
   a.exp_bits = exp_words ? exp_bits : 0;
   a.out_words = out_words;
   a.n0inv = mod->n0inv;
   a.exp_shared = exp_shared ? 1 : 0;
   hipError_t e = mpcx_launch_modexp(mod->cls, &a, waves, st);
   if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
+  return MPCX_OK;
+}
+
+static uint32_t max_exp_bits(const uint32_t* exps, uint32_t exp_words, int exp_shared, uint32_t count) {
+  uint32_t bits = 0;
+  if (!exp_words) return 0;
+  if (exp_shared) return bit_length_words(exps, exp_words);
+  for (uint32_t i = 0; i < count; ++i) bits = std::max(bits, bit_length_words(exps + (size_t)i * exp_words, exp_words));
+  return bits;
+}
+
+// host-buffer path: stage inputs, launch, copy back (synchronous)
+static int modexp_host(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
+                       const uint32_t* exps, uint32_t exp_words, int exp_shared, const uint32_t* muls,
+                       uint32_t mul_words, uint32_t* out, uint32_t out_words) {
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  if (count == 0) return MPCX_OK;
+  if (!bases || !out || (exp_words && !exps)) return fail(MPCX_EINVAL, "null buffer");
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  const uint32_t exp_bits = max_exp_bits(exps, exp_words, exp_shared, count);
+  const size_t n_exp_words = exp_shared ? exp_words : (size_t)count * exp_words;
+  const size_t bb = (size_t)count * base_words * 4, eb = std::max<size_t>(n_exp_words * 4, 4),
+               ob = (size_t)count * out_words * 4, mb = muls ? (size_t)count * mul_words * 4 : 0;
+  if ((rc = ensure_buffer(g_stage[0], bb)) || (rc = ensure_buffer(g_stage[1], eb)) ||
+      (rc = ensure_buffer(g_stage[2], ob)) || (muls && (rc = ensure_buffer(g_stage[3], mb))))
+    return rc;
+  hipError_t e = hipMemcpy(g_stage[0].ptr, bases, bb, hipMemcpyHostToDevice);
+  if (e == hipSuccess && n_exp_words) e = hipMemcpy(g_stage[1].ptr, exps, n_exp_words * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess && muls) e = hipMemcpy(g_stage[3].ptr, muls, mb, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "copy inputs");
+  rc = modexp_device_locked(mod, count, (const uint32_t*)g_stage[0].ptr, base_words,
+                            (const uint32_t*)g_stage[1].ptr, exp_words, exp_shared, exp_bits,
+                            muls ? (const uint32_t*)g_stage[3].ptr : nullptr, mul_words, (uint32_t*)g_stage[2].ptr,
+                            out_words, nullptr);
+  if (rc) return rc;
+  e = hipMemcpy(out, g_stage[2].ptr, ob, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "copy results");
   return MPCX_OK;
 }
 
@@ -340,43 +384,41 @@ int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_b
   std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
-  return modexp_device_locked(mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits, d_out,
-                              out_words, (hipStream_t)stream);
+  return modexp_device_locked(mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits, nullptr, 0,
+                              d_out, out_words, (hipStream_t)stream);
+}
+
+int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
+                                 const uint32_t* d_exps, uint32_t exp_words, int exp_shared, uint32_t exp_bits,
+                                 const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out, uint32_t out_words,
+                                 void* stream) {
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  if (!d_muls) return fail(MPCX_EINVAL, "null multipliers");
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  return modexp_device_locked(mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits, d_muls,
+                              mul_words, d_out, out_words, (hipStream_t)stream);
 }
 
 int mpcx_modexp_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
                       const uint32_t* exps, uint32_t exp_words, int exp_shared, uint32_t* out,
                       uint32_t out_words) {
-  if (!mod) return fail(MPCX_EINVAL, "null modulus");
-  if (count == 0) return MPCX_OK;
-  if (!bases || !out || (exp_words && !exps)) return fail(MPCX_EINVAL, "null buffer");
-  if (base_words == 0) return fail(MPCX_EINVAL, "base_words == 0");
-  std::lock_guard<std::mutex> lk(g_mu);
-  int rc = ensure_device();
-  if (rc) return rc;
-  uint32_t exp_bits = 0;
-  const size_t n_exp_words = exp_shared ? exp_words : (size_t)count * exp_words;
-  if (exp_shared) {
-    exp_bits = bit_length_words(exps, exp_words);
-  } else {
-    for (uint32_t i = 0; i < count; ++i)
-      exp_bits = std::max(exp_bits, bit_length_words(exps + (size_t)i * exp_words, exp_words));
-  }
-  const size_t bb = (size_t)count * base_words * 4, eb = std::max<size_t>(n_exp_words * 4, 4),
-               ob = (size_t)count * out_words * 4;
-  if ((rc = ensure_buffer(g_stage[0], bb)) || (rc = ensure_buffer(g_stage[1], eb)) ||
-      (rc = ensure_buffer(g_stage[2], ob)))
-    return rc;
-  hipError_t e = hipMemcpy(g_stage[0].ptr, bases, bb, hipMemcpyHostToDevice);
-  if (e == hipSuccess && n_exp_words) e = hipMemcpy(g_stage[1].ptr, exps, n_exp_words * 4, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "copy inputs");
-  rc = modexp_device_locked(mod, count, (const uint32_t*)g_stage[0].ptr, base_words,
-                            (const uint32_t*)g_stage[1].ptr, exp_words, exp_shared, exp_bits,
-                            (uint32_t*)g_stage[2].ptr, out_words, nullptr);
-  if (rc) return rc;
-  e = hipMemcpy(out, g_stage[2].ptr, ob, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail(e, "copy results");
-  return MPCX_OK;
+  return modexp_host(mod, count, bases, base_words, exps, exp_words, exp_shared, nullptr, 0, out, out_words);
+}
+
+int mpcx_modexp_mul_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
+                          const uint32_t* exps, uint32_t exp_words, int exp_shared, const uint32_t* muls,
+                          uint32_t mul_words, uint32_t* out, uint32_t out_words) {
+  if (!muls) return fail(MPCX_EINVAL, "null multipliers");
+  return modexp_host(mod, count, bases, base_words, exps, exp_words, exp_shared, muls, mul_words, out, out_words);
+}
+
+int mpcx_mulmod_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* a, uint32_t a_words, const uint32_t* b,
+                      uint32_t b_words, uint32_t* out, uint32_t out_words) {
+  if (!a || !b) return fail(MPCX_EINVAL, "null operands");
+  const uint32_t one = 1;
+  return modexp_host(mod, count, a, a_words, &one, 1, 1, b, b_words, out, out_words);
 }
 
 int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint8_t* ok) {

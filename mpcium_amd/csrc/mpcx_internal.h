@@ -31,6 +31,10 @@
 #define MPCX_CLASS_WORDS(c) ((28 * MPCX_CLASS_L(c)) / 32)
 #define MPCX_CLASS_MAXBITS(c) (32 * MPCX_CLASS_WORDS(c))
 
+// table entries per wavefront in the workspace: powers p_0..p_15 + the
+// Montgomery form of the optional multiplier (entry 16)
+#define MPCX_TABLE_ENTRIES 17
+
 namespace mpcx {
 
 struct ModexpArgs {
@@ -39,11 +43,13 @@ struct ModexpArgs {
   const uint32_t* r2d;  // L digits of R^2 mod m
   const uint32_t* base; // count x base_words
   const uint32_t* exps; // 1 or count x exp_words
+  const uint32_t* mul;  // optional count x mul_words multipliers (nullptr: none)
   uint32_t* out;        // count x out_words
-  uint32_t* table;      // workspace: waves x 16 x K x 64 words
+  uint32_t* table;      // workspace: waves x MPCX_TABLE_ENTRIES x K x 64 words
   uint32_t count;
   uint32_t base_words;
   uint32_t exp_words;
+  uint32_t mul_words;
   uint32_t exp_bits;    // windows processed = ceil(exp_bits / 4)
   uint32_t out_words;
   uint32_t n0inv;       // -m^-1 mod 2^28

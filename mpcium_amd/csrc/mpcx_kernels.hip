@@ -34,6 +34,13 @@
 
 #include "mpcx_internal.h"
 
+#ifndef MPCX_SCHED_BARRIER
+#define MPCX_SCHED_BARRIER 0
+#endif
+#ifndef MPCX_PREFETCH_B
+#define MPCX_PREFETCH_B 1
+#endif
+// occupancy targets (waves per SIMD) -> register budgets 256 / 256 / 168
 #ifndef MPCX_WAVES_PER_EU_C0
 #define MPCX_WAVES_PER_EU_C0 2
 #endif
@@ -41,7 +48,10 @@
 #define MPCX_WAVES_PER_EU_C1 2
 #endif
 #ifndef MPCX_WAVES_PER_EU_C2
-#define MPCX_WAVES_PER_EU_C2 2
+#define MPCX_WAVES_PER_EU_C2 3
+#endif
+#ifndef MPCX_WAVES_PER_EU_FERMAT
+#define MPCX_WAVES_PER_EU_FERMAT 2
 #endif
 
 namespace mpcx {
@@ -69,6 +79,13 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
 }
 
+// acc += a * b (32x32 -> 64 plus 64-bit addend): hipcc lowers this to ONE
+// v_mad_u64_u32. (Inline asm would force ~20 s_nop hazard pads per digit
+// iteration around its SGPR carry-out.)
+__device__ __forceinline__ void mad64(uint64_t& acc, uint32_t a, uint32_t b) {
+  acc += (uint64_t)a * b;
+}
+
 __device__ __forceinline__ void wave_lds_fence() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -80,32 +97,25 @@ __device__ __forceinline__ void wave_lds_fence() {
 // boundaries need no masking.
 template <int P, int K>
 __device__ __forceinline__ void carry_pass64(uint64_t (&acc)[K]) {
-  uint64_t c[K];
+  // in place, top slot first, so only one carry is live at a time
+  const uint64_t ctop = acc[K - 1] >> DB;
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    c[k] = acc[k] >> DB;
-    acc[k] &= M28;
-  }
-#pragma unroll
-  for (int k = 1; k < K; ++k) acc[k] += c[k - 1];
+  for (int k = K - 1; k >= 1; --k) acc[k] = (acc[k] & M28) + (acc[k - 1] >> DB);
+  acc[0] &= M28;
   if constexpr (P > 1) {
-    const uint32_t clo = from_prev_lane((uint32_t)c[K - 1]);
-    const uint32_t chi = from_prev_lane((uint32_t)(c[K - 1] >> 32));
+    const uint32_t clo = from_prev_lane((uint32_t)ctop);
+    const uint32_t chi = from_prev_lane((uint32_t)(ctop >> 32));
     acc[0] += ((uint64_t)chi << 32) | clo;
   }
 }
 
 template <int P, int K>
 __device__ __forceinline__ void carry_pass32(uint32_t (&d)[K]) {
-  uint32_t c[K];
+  const uint32_t ctop = d[K - 1] >> DB;
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    c[k] = d[k] >> DB;
-    d[k] &= M28;
-  }
-#pragma unroll
-  for (int k = 1; k < K; ++k) d[k] += c[k - 1];
-  if constexpr (P > 1) d[0] += from_prev_lane(c[K - 1]);
+  for (int k = K - 1; k >= 1; --k) d[k] = (d[k] & M28) + (d[k - 1] >> DB);
+  d[0] &= M28;
+  if constexpr (P > 1) d[0] += from_prev_lane(ctop);
 }
 
 // A <- A * B * R^-1 (almost Montgomery, result < 2N given A, B < 2N), with
@@ -117,20 +127,31 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
   uint64_t acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
+  uint32_t bnext = bl[0];
   for (int o = 0; o < P; ++o) {
     const uint32_t* bo = bl + o * K;
     static_for<0, K>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
-      const uint32_t bi = bo[u];
-      static_for<0, K>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        acc[(k + u) % K] += (uint64_t)A[k] * bi;
-      });
+      const uint32_t bi = bnext;
+      // slot 0 first: it feeds m_i, the only serial dependency of the iteration
+      mad64(acc[u], A[0], bi);
       uint32_t m = ((uint32_t)acc[u] * n0inv) & M28;
       if constexpr (P > 1) m = (uint32_t)__builtin_amdgcn_ds_bpermute(m_src_addr, (int)m);
+#if MPCX_PREFETCH_B
+      // next digit of b, in flight behind the bpermute and the a*b_i mads
+      // (the last read of the last block touches the neighbour row: unused)
+      bnext = bo[u + 1];
+#endif
+      static_for<1, K>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        mad64(acc[(k + u) % K], A[k], bi);
+      });
+#if !MPCX_PREFETCH_B
+      bnext = bo[u + 1];
+#endif
       static_for<0, K>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
-        acc[(k + u) % K] += (uint64_t)m * Nd[k];
+        mad64(acc[(k + u) % K], m, Nd[k]);
       });
       const uint64_t a0 = acc[u];
       acc[(u + 1) % K] += a0 >> DB;
@@ -139,6 +160,12 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
       } else {
         acc[u] = 0;
       }
+#if MPCX_SCHED_BARRIER
+      // keep iterations from being interleaved by the machine scheduler: it
+      // otherwise hoists b loads and mads across iterations and blows the
+      // register budget (occupancy) for no issue-rate gain
+      __builtin_amdgcn_sched_barrier(0);
+#endif
     });
     // Keep every accumulator below 2^64: at most ~P/2*K + K more iterations of
     // two < 2^56.01 products follow this pass (<= 127 for every class).
@@ -146,15 +173,11 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
   }
   carry_pass64<P, K>(acc);
   // digits are now < 2^28 + 2^37: one more pass brings them to <= 2^28 + 2^10
-  uint32_t c[K];
+  const uint32_t ctop = (uint32_t)(acc[K - 1] >> DB);
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    c[k] = (uint32_t)(acc[k] >> DB);
-    A[k] = (uint32_t)acc[k] & M28;
-  }
-#pragma unroll
-  for (int k = 1; k < K; ++k) A[k] += c[k - 1];
-  if constexpr (P > 1) A[0] += from_prev_lane(c[K - 1]);
+  for (int k = K - 1; k >= 1; --k) A[k] = ((uint32_t)acc[k] & M28) + (uint32_t)(acc[k - 1] >> DB);
+  A[0] = (uint32_t)acc[0] & M28;
+  if constexpr (P > 1) A[0] += from_prev_lane(ctop);
 }
 
 // Canonical digits (< 2^28): repeat carry passes until no digit overflows.
@@ -183,7 +206,7 @@ __device__ __forceinline__ uint32_t window_of(const uint32_t* e, uint32_t j) {
 template <int P, int K, int G, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp(const ModexpArgs a) {
   constexpr int L = P * K;
-  __shared__ uint32_t lds[(G + 1) * L];
+  __shared__ uint32_t lds[(G + 1) * L + 1];  // +1: the b prefetch reads one past a row
   const int lane = threadIdx.x;
   const int g_raw = lane / P;
   const bool idle = g_raw >= G;  // lanes beyond G*P carry zeros
@@ -198,103 +221,163 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 #pragma unroll
   for (int k = 0; k < K; ++k) Nd[k] = idle ? 0u : a.nd[p * K + k];
 
-  // base words -> radix-2^28 digits (inactive operands compute on zero)
+  // operand words -> radix-2^28 digits (inactive operands compute on zero)
+  auto load_digits = [&] __attribute__((always_inline))(const uint32_t* src, uint32_t words) {
+    // opaque pointer and lane index: keeps the per-digit address/shift math
+    // from being hoisted out of the step loop and held live across every
+    // montmul (it cost ~3K registers and forced spills)
+    asm volatile("" : "+s"(src));
+    int pp = p;
+    asm volatile("" : "+v"(pp));
 #pragma unroll
-  for (int k = 0; k < K; ++k) {
-    const uint32_t d = (uint32_t)(p * K + k);
-    const uint32_t bit = d * DB;
-    const uint32_t w = bit >> 5, s = bit & 31u;
-    uint64_t v = 0;
-    if (active) {
-      const uint32_t* x = a.base + (size_t)op * a.base_words;
-      const uint32_t lo = w < a.base_words ? x[w] : 0u;
-      const uint32_t hi = (w + 1) < a.base_words ? x[w + 1] : 0u;
-      v = ((uint64_t)hi << 32) | lo;
+    for (int k = 0; k < K; ++k) {
+      const uint32_t bit = (uint32_t)(pp * K + k) * DB;
+      const uint32_t w = bit >> 5, sh = bit & 31u;
+      uint64_t v = 0;
+      if (active) {
+        const uint32_t* x = src + (size_t)op * words;
+        const uint32_t lo = w < words ? x[w] : 0u;
+        const uint32_t hi = (w + 1) < words ? x[w + 1] : 0u;
+        v = ((uint64_t)hi << 32) | lo;
+      }
+      A[k] = (uint32_t)(v >> sh) & M28;
     }
-    A[k] = (uint32_t)(v >> s) & M28;
-  }
+  };
 
   const uint32_t nw = (a.exp_bits + 3u) / 4u;
   const uint32_t* ex = a.exp_shared ? a.exps : a.exps + (size_t)(active ? op : 0) * a.exp_words;
-  uint32_t* tbl = a.table + (size_t)blockIdx.x * 16u * K * 64u;
-  auto tbl_at = [&](uint32_t e, int k) -> uint32_t* { return tbl + ((size_t)e * K + k) * 64u + lane; };
-
-  // table[0] = R mod m (Montgomery one)
+  // Per-wavefront table of MPCX_TABLE_ENTRIES entries x K digit-slots x 64 lanes, accessed
+  // through a buffer descriptor: lane offset in one VGPR, entry/slot offset
+  // in an SGPR (no per-slot address registers live across the montmuls).
+  uint32_t* tbl = a.table + (size_t)blockIdx.x * MPCX_TABLE_ENTRIES * K * 64u;
+  const auto tbl_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc(tbl, (short)0, (int)(MPCX_TABLE_ENTRIES * K * 64u * 4u), 0x00020000);
+  const int tbl_lane_off = lane * 4;
+  // entry offset (possibly per-lane) in voffset, slot offset k*256 as a constant soffset
+  auto tbl_store = [&](uint32_t e, const uint32_t (&v)[K]) __attribute__((always_inline)) {
+    const int voff = tbl_lane_off + (int)(e * K * 256u);
 #pragma unroll
-  for (int k = 0; k < K; ++k) *tbl_at(0, k) = idle ? 0u : a.r1d[p * K + k];
-  // step 0: p1 = x * R^2 * R^-1
+    for (int k = 0; k < K; ++k) __builtin_amdgcn_raw_buffer_store_b32(v[k], tbl_rsrc, voff, k * 256, 0);
+  };
+  auto tbl_load = [&](uint32_t e, uint32_t (&v)[K]) __attribute__((always_inline)) {
+    const int voff = tbl_lane_off + (int)(e * K * 256u);
+#pragma unroll
+    for (int k = 0; k < K; ++k) v[k] = __builtin_amdgcn_raw_buffer_load_b32(tbl_rsrc, voff, k * 256, 0);
+  };
+  auto lds_from_table = [&] __attribute__((always_inline))(uint32_t e) {
+    uint32_t tv[K];
+    tbl_load(e, tv);
+    lds_store_digits<K>(bl, p, tv);
+  };
+  auto lds_one = [&] __attribute__((always_inline))() {
+    uint32_t one[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
+    lds_store_digits<K>(bl, p, one);
+  };
+
+  // table[0] = R mod m (Montgomery one); LDS <- R^2 mod m for the conversions
+  {
+    uint32_t r1[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) r1[k] = idle ? 0u : a.r1d[p * K + k];
+    tbl_store(0, r1);
+  }
   {
     uint32_t r2[K];
 #pragma unroll
     for (int k = 0; k < K; ++k) r2[k] = idle ? 0u : a.r2d[p * K + k];
     lds_store_digits<K>(bl, p, r2);
   }
+  const bool has_mul = a.mul != nullptr;
+  // top window and the table entries actually needed: a shared exponent of at
+  // most one window (e.g. the multiply-only call, e = 1) needs p_1..p_wt only
+  // Control state must stay provably wave-uniform (SGPRs): a shared exponent
+  // is read through readfirstlane, so the compiler keeps the step machine,
+  // the table offsets and the zero-window skip off the VGPR file.
+  const bool shared = a.exp_shared != 0;
+  const uint32_t wt = nw > 0 ? window_of(ex, nw - 1u) : 0u;
+  const uint32_t wt_u = __builtin_amdgcn_readfirstlane(wt);
+  const uint32_t T = (shared && nw <= 1u) ? (wt_u > 1u ? wt_u : 1u) : 15u;
+  const uint32_t nexp = nw > 0 ? 5u * (nw - 1u) : 0u;
+
+  // Montgomery-step state machine (ONE montmul call site keeps the code small):
+  //   PRE : mul*R   = mont(mul, R^2)           -> table[16]   (only with a multiplier)
+  //   TAB : p_i     = mont(x, R^2), mont(p_{i-1}, p_1)  i = 1..T -> table[i]
+  //   EXP : per window below the top one: 4 squarings, then mont(z, p_w)
+  //         (a zero window of a shared exponent is skipped: uniform branch)
+  //   MULF: z*mul*R = mont(z*R, mul*R)                          (only with a multiplier)
+  //   FIN : z       = mont(z*R, 1) <= m
+  enum { ST_PRE, ST_TAB, ST_EXP, ST_MULF, ST_FIN };
+  int st;
+  uint32_t idx = 1;
+  if (has_mul) {
+    load_digits(a.mul, a.mul_words);
+    st = ST_PRE;
+  } else {
+    load_digits(a.base, a.base_words);
+    st = ST_TAB;
+  }
   wave_lds_fence();
 
-  // Step schedule: 15 table steps (s = 0..14 produce p1..p15), then for each
-  // window below the top one 4 squarings + 1 multiply, then the final
-  // multiply by 1 that leaves the Montgomery domain.
-  const uint32_t nexp = nw > 0 ? 5u * (nw - 1u) : 0u;
-  const uint32_t S = 15u + nexp + 1u;
-  for (uint32_t s = 0; s < S; ++s) {
+  // prepares LDS (and state) for exponent step idx, skipping zero windows
+  auto prepare_exp = [&] __attribute__((always_inline))() {
+    for (;;) {
+      if (idx == nexp) {
+        if (has_mul) {
+          st = ST_MULF;
+          lds_from_table(16);
+        } else {
+          st = ST_FIN;
+          lds_one();
+        }
+        return;
+      }
+      if (idx % 5u < 4u) {
+        lds_store_digits<K>(bl, p, A);
+        return;
+      }
+      if (shared) {
+        const uint32_t w = __builtin_amdgcn_readfirstlane(window_of(a.exps, nw - 2u - idx / 5u));
+        if (w == 0u) {
+          ++idx;  // multiplying by Montgomery one is the identity mod m
+          continue;
+        }
+        lds_from_table(w);
+      } else {
+        lds_from_table(window_of(ex, nw - 2u - idx / 5u));
+      }
+      return;
+    }
+  };
+
+  for (;;) {
     montmul<P, K>(A, bl, Nd, a.n0inv, m_src_addr);
     wave_lds_fence();
-    if (s < 15u) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) *tbl_at(s + 1, k) = A[k];
-      if (s == 0) {
-        lds_store_digits<K>(bl, p, A);  // B = p1 for the remaining table steps
-      }
-      if (s == 14) {
-        // z = table[top window] (or Montgomery one for a zero exponent)
-        const uint32_t wt = nw > 0 ? window_of(ex, nw - 1u) : 0u;
-        __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
-#pragma unroll
-        for (int k = 0; k < K; ++k) A[k] = *tbl_at(wt, k);
-        if (nexp == 0) {
-          uint32_t one[K];
-#pragma unroll
-          for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
-          lds_store_digits<K>(bl, p, one);
-        } else {
-          lds_store_digits<K>(bl, p, A);
-        }
-      }
-    } else if (s + 1u < S) {
-      // just finished exponent step t = s - 15; prepare step t + 1
-      const uint32_t t = s - 15u + 1u;
-      if (t == nexp) {
-        uint32_t one[K];
-#pragma unroll
-        for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
-        lds_store_digits<K>(bl, p, one);
+    if (st == ST_PRE) {
+      tbl_store(16, A);
+      load_digits(a.base, a.base_words);  // LDS still holds R^2
+      st = ST_TAB;
+      idx = 1;
+    } else if (st == ST_TAB) {
+      tbl_store(idx, A);
+      if (idx == 1) lds_store_digits<K>(bl, p, A);  // B = p_1 for the remaining table steps
+      if (idx < T) {
+        ++idx;
       } else {
-        const uint32_t sub = t % 5u;
-        if (sub < 4u) {
-          lds_store_digits<K>(bl, p, A);
-        } else {
-          const uint32_t j = nw - 2u - t / 5u;
-          const uint32_t w = window_of(ex, j);
-          if (a.exp_shared && w == 0u) {
-            // multiplying by Montgomery one is the identity mod m: skip it
-            // (uniform across the wavefront), go straight to the next squaring
-            ++s;
-            if (t + 1u == nexp) {
-              uint32_t one[K];
-#pragma unroll
-              for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
-              lds_store_digits<K>(bl, p, one);
-            } else {
-              lds_store_digits<K>(bl, p, A);
-            }
-          } else {
-            uint32_t tv[K];
-#pragma unroll
-            for (int k = 0; k < K; ++k) tv[k] = *tbl_at(w, k);
-            lds_store_digits<K>(bl, p, tv);
-          }
-        }
+        tbl_load(shared ? wt_u : wt, A);  // z = p_top (Montgomery one if e = 0)
+        st = ST_EXP;
+        idx = 0;
+        prepare_exp();
       }
+    } else if (st == ST_EXP) {
+      ++idx;
+      prepare_exp();
+    } else if (st == ST_MULF) {
+      st = ST_FIN;
+      lds_one();
+    } else {
+      break;  // ST_FIN done
     }
     wave_lds_fence();
   }
@@ -371,7 +454,7 @@ __device__ __forceinline__ void norm_serial(uint32_t (&x)[K]) {
 template <int K, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fermat2(const FermatArgs a) {
   constexpr int L = K;
-  __shared__ uint32_t lds[65 * L];
+  __shared__ uint32_t lds[65 * L + 1];
   const int lane = threadIdx.x;
   const uint32_t op = blockIdx.x * 64u + lane;
   const bool active = op < a.count;
@@ -496,7 +579,7 @@ __attribute__((visibility("hidden"))) hipError_t mpcx_launch_modexp(int cls, con
 
 __attribute__((visibility("hidden"))) hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks,
                                                                     hipStream_t st) {
-  hipLaunchKernelGGL((mpcx::k_fermat2<MPCX_CLASS_K(0), MPCX_WAVES_PER_EU_C0>), dim3(blocks), dim3(64), 0, st, *a);
+  hipLaunchKernelGGL((mpcx::k_fermat2<MPCX_CLASS_K(0), MPCX_WAVES_PER_EU_FERMAT>), dim3(blocks), dim3(64), 0, st, *a);
   return hipGetLastError();
 }
 

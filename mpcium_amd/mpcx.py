@@ -35,6 +35,13 @@ SIGNATURES = [
                                          ctypes.c_int, _vp, ctypes.c_uint32]),
     ("mpcx_modexp_batch_device", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
                                                 ctypes.c_int, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    ("mpcx_modexp_mul_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
+                                             ctypes.c_int, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32]),
+    ("mpcx_modexp_mul_batch_device", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp,
+                                                    ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, _vp,
+                                                    ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    ("mpcx_mulmod_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp,
+                                         ctypes.c_uint32]),
     ("mpcx_fermat2_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
     ("mpcx_dev_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
     ("mpcx_dev_free", ctypes.c_int, [_vp]),
@@ -153,28 +160,60 @@ class Modulus:
                                        out.ctypes.data, ow))
         return out
 
+    def _operands(self, vals: Sequence[int], what: str) -> np.ndarray:
+        bw = self.class_words
+        lim = 1 << (32 * bw)
+        if any(v < 0 or v >= lim for v in vals):
+            raise ValueError(f"{what} must be in [0, 2^(32*class_words)); reduce mod m first")
+        return ints_to_words(vals, bw)
+
+    def mulmod(self, a: Sequence[int], b: Sequence[int]) -> List[int]:
+        """[a_i * b_i mod m] (mpcx_mulmod_batch)."""
+        if len(a) != len(b):
+            raise ValueError("length mismatch")
+        if len(a) == 0:
+            return []
+        A, B = self._operands(a, "a"), self._operands(b, "b")
+        out = np.zeros((len(a), self.words), dtype="<u4")
+        _check(lib().mpcx_mulmod_batch(self._h, len(a), A.ctypes.data, A.shape[1], B.ctypes.data, B.shape[1],
+                                       out.ctypes.data, self.words))
+        return words_to_ints(out)
+
+    def exp_mul(self, bases: Sequence[int], exps: Union[int, Sequence[int]], muls: Sequence[int]) -> List[int]:
+        """[mul_i * b_i^e_i mod m] (mpcx_modexp_mul_batch)."""
+        if len(muls) != len(bases):
+            raise ValueError("one multiplier per base")
+        if len(bases) == 0:
+            return []
+        B = self._operands(bases, "bases")
+        Mu = self._operands(muls, "muls")
+        E, shared = self._exps(exps, len(bases))
+        out = np.zeros((len(bases), self.words), dtype="<u4")
+        _check(lib().mpcx_modexp_mul_batch(self._h, len(bases), B.ctypes.data, B.shape[1],
+                                           E.ctypes.data if E.size else None, E.shape[-1] if E.size else 0,
+                                           1 if shared else 0, Mu.ctypes.data, Mu.shape[1], out.ctypes.data,
+                                           self.words))
+        return words_to_ints(out)
+
+    @staticmethod
+    def _exps(exps, count):
+        if isinstance(exps, int):
+            if exps < 0:
+                raise ValueError("negative exponent")
+            return (int_to_words(exps, nwords(exps)) if exps else np.zeros(0, dtype="<u4")), True
+        if len(exps) != count:
+            raise ValueError("one exponent per base")
+        if any(e < 0 for e in exps):
+            raise ValueError("negative exponent")
+        ew = max(nwords(e) for e in exps)
+        return ints_to_words(exps, ew), False
+
     def exp(self, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> List[int]:
         """[b^e mod m] for non-negative ints; `exps` is one shared int or one per base."""
         if len(bases) == 0:
             return []
-        bw = self.class_words
-        lim = 1 << (32 * bw)
-        if any(b < 0 or b >= lim for b in bases):
-            raise ValueError("bases must be in [0, 2^(32*class_words)); reduce mod m first")
-        B = ints_to_words(bases, bw)
-        if isinstance(exps, int):
-            if exps < 0:
-                raise ValueError("negative exponent")
-            E = int_to_words(exps, nwords(exps)) if exps else np.zeros(0, dtype="<u4")
-            shared = True
-        else:
-            if len(exps) != len(bases):
-                raise ValueError("one exponent per base")
-            if any(e < 0 for e in exps):
-                raise ValueError("negative exponent")
-            ew = max(nwords(e) for e in exps)
-            E = ints_to_words(exps, ew)
-            shared = False
+        B = self._operands(bases, "bases")
+        E, shared = self._exps(exps, len(bases))
         return words_to_ints(self.exp_words(B, E, shared))
 
 

@@ -102,3 +102,20 @@ def test_rejects_even_and_oversized_modulus(gpu):
         gpu.Modulus(1 << 100)
     with pytest.raises(gpu.MpcxError):
         gpu.Modulus((1 << 4097) + 1)
+
+
+def test_exp_mul_and_mulmod(gpu, paillier_key):
+    N = paillier_key["N"]
+    N2 = N * N
+    rng = random.Random(21)
+    for m in (N2, N, paillier_key["P"]):
+        mod = gpu.Modulus(m)
+        n = mod.G + 3
+        xs = [rng.randrange(m) for _ in range(n)]
+        cs = [rng.randrange(m) for _ in range(n)]
+        assert mod.mulmod(xs, cs) == [x * c % m for x, c in zip(xs, cs)]
+        assert mod.exp_mul(xs, N, cs) == [c * pow(x, N, m) % m for x, c in zip(xs, cs)]
+        es = [rng.getrandbits(rng.choice([0, 3, 256, 2048])) for _ in xs]
+        assert mod.exp_mul(xs, es, cs) == [c * pow(x, e, m) % m for x, e, c in zip(xs, es, cs)]
+        assert mod.exp_mul(xs, 0, cs) == [c % m for c in cs]
+        mod.release()
