@@ -143,6 +143,13 @@ int mpcx_mulmod_batch(mpcx_mod_t mod, uint32_t count,
  * (5 <= p_i < 2^1024, p_words <= 32). Each candidate is its own modulus. */
 int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint8_t* ok);
 
+/* Miller-Rabin: ok[i] = n_i is a strong probable prime to base bases[i]
+ * (5 <= n_i < 2^1024 odd, bases[i] < 2^(32*n_words); a base that is 0 mod
+ * n_i reports "composite"). Each candidate is its own modulus. Serves
+ * q.ProbablyPrime(20) of up:common/safe_prime.go (Go: math/big
+ * probablyPrimeMillerRabin, go:src/math/big/prime.go). */
+int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* bases, uint8_t* ok);
+
 /* Device memory helpers for callers without their own HIP allocator. */
 int mpcx_dev_alloc(size_t bytes, void** out_ptr);
 int mpcx_dev_free(void* ptr);

@@ -12,6 +12,7 @@ from .mpcx import (  # noqa: F401
     device_count,
     exp_batch,
     fermat2_batch,
+    mr_batch,
     init,
     lib,
     shutdown,

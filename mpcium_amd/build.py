@@ -17,7 +17,8 @@ HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
 KERNEL_SRCS = ["mpcx_kernels.hip", "mpcx_api.cpp"]
-HOST_SRCS = ["host/bignum.cpp", "host/modint.cpp", "host/paillier.cpp", "host/safeprime.cpp", "host/capi.cpp"]
+HOST_SRCS = ["host/bignum.cpp", "host/engine.cpp", "host/modint.cpp", "host/paillier.cpp", "host/safeprime.cpp",
+             "host/capi.cpp"]
 
 
 def _newer(target: str, deps) -> bool:
@@ -45,7 +46,8 @@ def build(force: bool = False, verbose: bool = True) -> dict:
     host_srcs = [os.path.join(CSRC, s) for s in HOST_SRCS if os.path.exists(os.path.join(CSRC, s))]
     if host_srcs:
         hlib = os.path.join(HERE, "libmpcx_host.so")
-        hdeps = host_srcs + [os.path.join(CSRC, "host", h) for h in os.listdir(os.path.join(CSRC, "host")) if h.endswith(".hpp")]
+        hdeps = host_srcs + [os.path.join(CSRC, "host", h) for h in os.listdir(os.path.join(CSRC, "host"))
+                             if h.endswith(".hpp")] + [os.path.join(ROOT, "include", "mpcx_host.h")]
         if force or _newer(hlib, hdeps + [lib]):
             _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-pthread",
                   "-I", os.path.join(ROOT, "include"), "-I", os.path.join(CSRC, "host"),

@@ -1,0 +1,117 @@
+// engine.cpp -- see engine.hpp.
+#include "engine.hpp"
+
+#include <algorithm>
+
+namespace mpcx::host {
+
+void throw_last(int rc, const char* what) {
+  throw EngineError(rc, std::string(what) + ": " + mpcx_last_error());
+}
+
+Engine& Engine::get() {
+  static Engine e;
+  return e;
+}
+
+void Engine::init(int device) {
+  std::lock_guard<std::mutex> lk(mu_);
+  int rc = mpcx_init(device);
+  if (rc) throw_last(rc, "mpcx_init");
+  device_ = device;
+}
+
+Engine::Mod& Engine::modulus(const Nat& m) {
+  auto it = mods_.find(m.limbs());
+  if (it != mods_.end()) return it->second;
+  Mod md{};
+  int rc = mpcx_modulus_register(m.limbs().data(), (uint32_t)m.words(), &md.h);
+  if (rc) throw_last(rc, "mpcx_modulus_register");
+  uint32_t bits = 0;
+  mpcx_modulus_info(md.h, &bits, &md.class_words);
+  md.words = (uint32_t)m.words();
+  return mods_.emplace(m.limbs(), md).first->second;
+}
+
+static std::vector<uint32_t> pack(const std::vector<Nat>& v, uint32_t w) {
+  std::vector<uint32_t> out((size_t)v.size() * w);
+  for (size_t i = 0; i < v.size(); ++i) v[i].to_words(out.data() + i * w, w);
+  return out;
+}
+
+static std::vector<Nat> unpack(const std::vector<uint32_t>& buf, size_t count, uint32_t w) {
+  std::vector<Nat> out(count);
+  for (size_t i = 0; i < count; ++i) out[i] = Nat::from_words(buf.data() + i * w, w);
+  return out;
+}
+
+std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const std::vector<Nat>& exps,
+                             const std::vector<Nat>* muls) {
+  if (exps.size() != 1 && exps.size() != bases.size()) throw std::invalid_argument("exps: 1 or one per base");
+  if (muls && muls->size() != bases.size()) throw std::invalid_argument("muls: one per base");
+  if (bases.empty()) return {};
+  std::lock_guard<std::mutex> lk(mu_);
+  Mod& md = modulus(m);
+  // math/big reduces x mod m first when len(x) > len(m) (nat.expNNMontgomery);
+  // here: only when x does not fit the kernel class width.
+  auto fit = [&](const std::vector<Nat>& v) {
+    std::vector<Nat> r(v);
+    for (auto& x : r)
+      if (x.words() > md.class_words) x = x % m;
+    return r;
+  };
+  const std::vector<Nat> b = fit(bases);
+  const bool shared = exps.size() == 1;
+  uint32_t ew = 1;
+  for (const auto& e : exps) ew = std::max<uint32_t>(ew, (uint32_t)e.words());
+  auto B = pack(b, md.class_words);
+  auto E = pack(exps, ew);
+  std::vector<uint32_t> out((size_t)bases.size() * md.words);
+  int rc;
+  if (muls) {
+    auto M = pack(fit(*muls), md.class_words);
+    rc = mpcx_modexp_mul_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
+                               M.data(), md.class_words, out.data(), md.words);
+  } else {
+    rc = mpcx_modexp_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
+                           out.data(), md.words);
+  }
+  if (rc) throw_last(rc, "mpcx_modexp_batch");
+  return unpack(out, bases.size(), md.words);
+}
+
+std::vector<Nat> Engine::mulmod(const Nat& m, const std::vector<Nat>& a, const std::vector<Nat>& b) {
+  std::vector<Nat> one{Nat(1)};
+  return exp(m, a, one, &b);
+}
+
+std::vector<uint8_t> Engine::fermat2(const std::vector<Nat>& cands) {
+  if (cands.empty()) return {};
+  uint32_t w = 1;
+  for (const auto& c : cands) w = std::max<uint32_t>(w, (uint32_t)c.words());
+  auto P = pack(cands, w);
+  std::vector<uint8_t> ok(cands.size());
+  std::lock_guard<std::mutex> lk(mu_);
+  int rc = mpcx_fermat2_batch((uint32_t)cands.size(), P.data(), w, ok.data());
+  if (rc) throw_last(rc, "mpcx_fermat2_batch");
+  return ok;
+}
+
+std::vector<uint8_t> Engine::strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases) {
+  if (n.size() != bases.size()) throw std::invalid_argument("one base per candidate");
+  if (n.empty()) return {};
+  uint32_t w = 1;
+  for (const auto& c : n) w = std::max<uint32_t>(w, (uint32_t)c.words());
+  std::vector<Nat> b(bases);
+  for (size_t i = 0; i < b.size(); ++i)
+    if (b[i].words() > w) b[i] = b[i] % n[i];
+  auto N = pack(n, w);
+  auto A = pack(b, w);
+  std::vector<uint8_t> ok(n.size());
+  std::lock_guard<std::mutex> lk(mu_);
+  int rc = mpcx_mr_batch((uint32_t)n.size(), N.data(), w, A.data(), ok.data());
+  if (rc) throw_last(rc, "mpcx_mr_batch");
+  return ok;
+}
+
+}  // namespace mpcx::host

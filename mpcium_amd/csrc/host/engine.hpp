@@ -1,0 +1,58 @@
+// engine.hpp -- C++ host mirror of the reference's modexp-calling surfaces,
+// layered on the libmpcx.so C-ABI (include/mpcx.h). This is the code a Go
+// integration would put in its cgo package; Go is absent
+// from this image, so the mirror is C++ (compiled reference -> compiled host).
+#pragma once
+
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "bignum.hpp"
+#include "mpcx.h"
+
+namespace mpcx::host {
+
+class EngineError : public std::runtime_error {
+ public:
+  EngineError(int code, const std::string& msg) : std::runtime_error(msg), code(code) {}
+  int code;
+};
+
+// Process-wide handle on one GPU (one process per GPU) plus a cache of
+// registered moduli: a node's N^2, N, N~ are registered once and reused by
+// every session, exactly like mpcium reuses its preparams
+// (/root/reference/pkg/mpc/node.go:69,109,170).
+class Engine {
+ public:
+  static Engine& get();
+  void init(int device);
+  bool initialized() const { return device_ >= 0; }
+
+  // out[i] = (muls ? muls[i] : 1) * bases[i]^e_i mod m, m odd, 1 <= m < 2^4096.
+  // exps.size() == 1: shared exponent; else one per base. Bases of any size
+  // (reduced mod m on the host first when wider than the kernel class).
+  std::vector<Nat> exp(const Nat& m, const std::vector<Nat>& bases, const std::vector<Nat>& exps,
+                       const std::vector<Nat>* muls = nullptr);
+  std::vector<Nat> mulmod(const Nat& m, const std::vector<Nat>& a, const std::vector<Nat>& b);
+  std::vector<uint8_t> fermat2(const std::vector<Nat>& cands);
+  std::vector<uint8_t> strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases);
+
+ private:
+  struct Mod {
+    mpcx_mod_t h;
+    uint32_t class_words;
+    uint32_t words;
+  };
+  Mod& modulus(const Nat& m);
+  std::mutex mu_;
+  int device_ = -1;
+  std::map<std::vector<uint32_t>, Mod> mods_;
+};
+
+[[noreturn]] void throw_last(int rc, const char* what);
+
+}  // namespace mpcx::host

@@ -1,0 +1,329 @@
+// safeprime.cpp -- see safeprime.hpp.
+#include "safeprime.hpp"
+
+#include <algorithm>
+#include <chrono>
+#include <cstring>
+#include <thread>
+
+#include "engine.hpp"
+#include "modint.hpp"
+
+namespace mpcx::host {
+
+// ------------------------------------------------------------------ SHA-256
+namespace {
+struct Sha256 {
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  static uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+  void block(const uint8_t* p) {
+    static const uint32_t k[64] = {
+        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+        0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+        0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+        0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+        0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+        0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+        0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+        0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+    uint32_t w[64];
+    for (int i = 0; i < 16; ++i) w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
+    for (int i = 16; i < 64; ++i) {
+      const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
+      const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
+      w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+    }
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
+    for (int i = 0; i < 64; ++i) {
+      const uint32_t S1 = ror(e, 6) ^ ror(e, 11) ^ ror(e, 25);
+      const uint32_t ch = (e & f) ^ (~e & g);
+      const uint32_t t1 = hh + S1 + ch + k[i] + w[i];
+      const uint32_t S0 = ror(a, 2) ^ ror(a, 13) ^ ror(a, 22);
+      const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
+      const uint32_t t2 = S0 + mj;
+      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+    }
+    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+  // one-shot digest of a short message (< 56 bytes)
+  static void digest_short(const uint8_t* msg, size_t n, uint8_t out[32]) {
+    Sha256 s;
+    uint8_t blk[64] = {0};
+    std::memcpy(blk, msg, n);
+    blk[n] = 0x80;
+    const uint64_t bits = (uint64_t)n * 8;
+    for (int i = 0; i < 8; ++i) blk[63 - i] = (uint8_t)(bits >> (8 * i));
+    s.block(blk);
+    for (int i = 0; i < 8; ++i)
+      for (int j = 0; j < 4; ++j) out[4 * i + j] = (uint8_t)(s.h[i] >> (24 - 8 * j));
+  }
+};
+}  // namespace
+
+void CounterDRBG::read(uint8_t* out, size_t n) {
+  while (n) {
+    if (pos_ == buf_.size()) {
+      uint8_t msg[25];
+      std::memcpy(msg, "mpcx-drbg", 9);
+      for (int i = 0; i < 8; ++i) msg[9 + i] = (uint8_t)(seed_ >> (8 * i));
+      for (int i = 0; i < 8; ++i) msg[17 + i] = (uint8_t)(ctr_ >> (8 * i));
+      ++ctr_;
+      buf_.assign(32, 0);
+      Sha256::digest_short(msg, sizeof msg, buf_.data());
+      pos_ = 0;
+    }
+    const size_t take = std::min(n, buf_.size() - pos_);
+    std::memcpy(out, buf_.data() + pos_, take);
+    pos_ += take;
+    out += take;
+    n -= take;
+  }
+}
+
+// ------------------------------------------------------------ candidates
+static const uint32_t kSmallPrimes[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53};
+static const uint64_t kSmallPrimesProduct = 16294579238595022365ull;
+
+Nat CandidateFromBytes(const uint8_t* bytes_in, size_t n, int qBitLen) {
+  if (n == 0) throw std::invalid_argument("empty candidate");
+  std::vector<uint8_t> bytes(bytes_in, bytes_in + n);
+  unsigned b = (unsigned)(qBitLen % 8);
+  if (b == 0) b = 8;
+  bytes[0] &= (uint8_t)((1u << b) - 1);
+  if (b >= 2) {
+    bytes[0] |= (uint8_t)(3u << (b - 2));
+  } else {
+    bytes[0] |= 1;
+    if (bytes.size() > 1) bytes[1] |= 0x80;
+  }
+  bytes.back() |= 1;
+  Nat q = Nat::from_bytes_be(bytes.data(), bytes.size());
+  // bigMod.Mod(q, smallPrimesProduct); delta walk (Go's old crypto/rand.Prime)
+  uint64_t mod = 0;
+  for (int i = (int)q.words() - 1; i >= 0; --i)
+    mod = (uint64_t)(((unsigned __int128)mod << 32 | q.limbs()[i]) % kSmallPrimesProduct);
+  for (uint64_t delta = 0; delta < (1ull << 20); delta += 2) {
+    const uint64_t m = mod + delta;
+    bool bad = false;
+    for (uint32_t p : kSmallPrimes) {
+      if (m % p == 0 && (qBitLen > 6 || m != p)) {
+        bad = true;
+        break;
+      }
+    }
+    if (bad) continue;
+    if (delta > 0) q = q + Nat(delta);
+    break;
+  }
+  return q;
+}
+
+namespace {
+// trial-division groups: primes 59 .. 2039 packed into products < 2^32
+struct TrialGroups {
+  std::vector<uint32_t> prod;
+  std::vector<std::vector<uint32_t>> primes;
+  TrialGroups() {
+    std::vector<uint32_t> ps;
+    for (uint32_t v = 59; v < 2048; v += 2) {
+      bool pr = true;
+      for (uint32_t d = 3; d * d <= v; d += 2)
+        if (v % d == 0) {
+          pr = false;
+          break;
+        }
+      if (pr) ps.push_back(v);
+    }
+    uint64_t cur = 1;
+    std::vector<uint32_t> grp;
+    for (uint32_t p : ps) {
+      if (cur * p >= (1ull << 32)) {
+        prod.push_back((uint32_t)cur);
+        primes.push_back(grp);
+        cur = 1;
+        grp.clear();
+      }
+      cur *= p;
+      grp.push_back(p);
+    }
+    if (!grp.empty()) {
+      prod.push_back((uint32_t)cur);
+      primes.push_back(grp);
+    }
+  }
+};
+const TrialGroups& trial_groups() {
+  static TrialGroups t;
+  return t;
+}
+
+// exact: true iff neither q nor 2q+1 has a prime factor in [59, 2048)
+bool passes_trial(const Nat& q) {
+  const auto& tg = trial_groups();
+  for (size_t g = 0; g < tg.prod.size(); ++g) {
+    const uint64_t r = q.mod_u32(tg.prod[g]);
+    for (uint32_t p : tg.primes[g]) {
+      const uint64_t rq = r % p;
+      if (rq == 0 || (2 * rq + 1) % p == 0) return false;
+    }
+  }
+  return true;
+}
+
+// 20 deterministic Miller-Rabin bases in [2, q-2] for candidate q, plus base 2
+std::vector<Nat> mr_bases(const Nat& q) {
+  std::vector<Nat> out{Nat(2)};
+  CounterDRBG rng(q.low64() ^ 0x4d52u);
+  const uint32_t bits = q.bit_len();
+  const Nat lim = q - Nat(3);
+  std::vector<uint8_t> buf((bits + 7) / 8);
+  while (out.size() < 21) {
+    rng.read(buf.data(), buf.size());
+    Nat v = Nat::from_bytes_be(buf.data(), buf.size()) % lim;
+    out.push_back(v + Nat(2));
+  }
+  return out;
+}
+}  // namespace
+
+std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, const RandFn& rand,
+                                                  SafePrimeStats* stats, size_t batch, uint64_t max_candidates) {
+  if (bitLen < 6) throw std::invalid_argument("safe prime size must be at least 6 bits");
+  if (numPrimes < 1) throw std::invalid_argument("numPrimes should be > 0");
+  if (bitLen > 1024) throw std::invalid_argument("GPU candidate class holds safe primes up to 1024 bits");
+  const auto t0 = std::chrono::steady_clock::now();
+  SafePrimeStats st;
+  const int qBitLen = bitLen - 1;
+  const size_t nbytes = (size_t)(qBitLen + 7) / 8;
+  std::vector<GermainSafePrime> out;
+  std::vector<uint8_t> raw(nbytes * batch);
+  const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  uint64_t index = 0;
+  while ((int)out.size() < numPrimes && index < max_candidates) {
+    // draw a batch from the stream (sequential: stream order is the contract)
+    for (size_t i = 0; i < batch; ++i) rand(raw.data() + i * nbytes, nbytes);
+    std::vector<Nat> qs(batch);
+    std::vector<uint8_t> keep(batch, 0);
+    auto work = [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        qs[i] = CandidateFromBytes(raw.data() + i * nbytes, nbytes, qBitLen);
+        keep[i] = (qs[i].bit_len() == (uint32_t)qBitLen) && (bitLen <= 12 || passes_trial(qs[i]));
+      }
+    };
+    std::vector<std::thread> th;
+    const size_t chunk = (batch + nthreads - 1) / nthreads;
+    for (unsigned t = 0; t < nthreads; ++t) {
+      const size_t lo = t * chunk, hi = std::min(batch, lo + chunk);
+      if (lo < hi) th.emplace_back(work, lo, hi);
+    }
+    for (auto& t : th) t.join();
+    std::vector<size_t> idx;
+    std::vector<Nat> ps;
+    for (size_t i = 0; i < batch; ++i) {
+      if (!keep[i]) continue;
+      idx.push_back(i);
+      ps.push_back((qs[i] << 1) + Nat(1));
+    }
+    st.candidates += batch;
+    st.sieved_out += batch - idx.size();
+    st.fermat_tests += ps.size();
+    // GPU: Pocklington criterion 2^(p-1) == 1 mod p on every survivor
+    std::vector<uint8_t> f = bitLen >= 4 ? Engine::get().fermat2(ps) : std::vector<uint8_t>(ps.size(), 1);
+    // GPU: Miller-Rabin on q for the Fermat survivors, in stream order
+    std::vector<size_t> surv;
+    std::vector<Nat> mr_n, mr_a;
+    for (size_t j = 0; j < idx.size(); ++j) {
+      if (!f[j]) continue;
+      surv.push_back(j);
+      for (const Nat& a : mr_bases(qs[idx[j]])) {
+        mr_n.push_back(qs[idx[j]]);
+        mr_a.push_back(a);
+      }
+    }
+    st.mr_tests += mr_n.size();
+    std::vector<uint8_t> mr = Engine::get().strong_probable_prime(mr_n, mr_a);
+    for (size_t s = 0; s < surv.size() && (int)out.size() < numPrimes; ++s) {
+      bool prime = true;
+      for (size_t r = 0; r < 21; ++r) prime &= mr[s * 21 + r] != 0;
+      if (!prime) continue;
+      const size_t j = surv[s];
+      out.push_back({ps[j], qs[idx[j]], index + idx[j]});
+    }
+    index += batch;
+  }
+  st.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  if (stats) {
+    stats->candidates += st.candidates;
+    stats->sieved_out += st.sieved_out;
+    stats->fermat_tests += st.fermat_tests;
+    stats->mr_tests += st.mr_tests;
+    stats->seconds += st.seconds;
+  }
+  if ((int)out.size() < numPrimes) throw std::runtime_error("safe prime search exhausted max_candidates");
+  return out;
+}
+
+Nat MustGetRandomInt(const RandFn& rand, uint32_t bits) {
+  // crypto/rand.Int(rand, max), max = 2^bits - 1: bitLen(max-1) = bits (bits >= 2)
+  if (bits < 2) throw std::invalid_argument("MustGetRandomInt: bits must be >= 2");
+  const Nat max = (Nat(1) << bits) - Nat(1);
+  const size_t k = (bits + 7) / 8;
+  unsigned b = bits % 8;
+  if (b == 0) b = 8;
+  std::vector<uint8_t> buf(k);
+  for (;;) {
+    rand(buf.data(), k);
+    buf[0] &= (uint8_t)((1u << b) - 1);
+    Nat n = Nat::from_bytes_be(buf.data(), k);
+    if (n < max) return n;
+  }
+}
+
+Nat GetRandomPositiveRelativelyPrimeInt(const RandFn& rand, const Nat& n) {
+  for (;;) {
+    Nat t = MustGetRandomInt(rand, n.bit_len());
+    if (t < n && t >= Nat(1) && gcd(t, n) == Nat(1)) return t;
+  }
+}
+
+paillier::PrivateKey GenerateKeyPair(int modulusBitLen, const RandFn& rand, SafePrimeStats* stats) {
+  const int half = modulusBitLen / 2;
+  Nat P, Q;
+  for (;;) {
+    auto sgps = GetRandomSafePrimes(half, 2, rand, stats);
+    P = sgps[0].p;
+    Q = sgps[1].p;
+    const Nat d = P >= Q ? P - Q : Q - P;
+    if ((int)d.bit_len() >= half - 3) break;  // KS-BTL-F-03: |P-Q| must be large
+  }
+  paillier::PrivateKey sk;
+  sk.pub.N = P * Q;
+  const Nat Pm1 = P - Nat(1), Qm1 = Q - Nat(1);
+  sk.PhiN = Pm1 * Qm1;
+  sk.LambdaN = sk.PhiN / gcd(Pm1, Qm1);
+  sk.P = P;
+  sk.Q = Q;
+  return sk;
+}
+
+LocalPreParams GeneratePreParams(const RandFn& rand, SafePrimeStats* stats) {
+  LocalPreParams pp;
+  // tss-lib runs these two searches concurrently on one reader (stream
+  // interleaving is scheduling-defined); here they run in a fixed order.
+  pp.PaillierSK = GenerateKeyPair(2048, rand, stats);
+  auto sgps = GetRandomSafePrimes(1024, 2, rand, stats);
+  const Nat P = sgps[0].p, Q = sgps[1].p;
+  pp.NTildei = P * Q;
+  pp.P = sgps[0].q;
+  pp.Q = sgps[1].q;
+  const Nat pq = pp.P * pp.Q;
+  const Nat f1 = GetRandomPositiveRelativelyPrimeInt(rand, pp.NTildei);
+  pp.Alpha = GetRandomPositiveRelativelyPrimeInt(rand, pp.NTildei);
+  if (!mod_inverse(Int(pp.Alpha), pq, &pp.Beta)) throw std::runtime_error("alpha not invertible mod pq");
+  const ModInt modN(pp.NTildei);
+  pp.H1i = modN.Mul(f1, f1);
+  if (!modN.Exp(Int(pp.H1i), Int(pp.Alpha), &pp.H2i)) throw std::runtime_error("h2 = h1^alpha failed");
+  return pp;
+}
+
+}  // namespace mpcx::host

@@ -21,6 +21,7 @@
 extern "C" {
 hipError_t mpcx_launch_modexp(int cls, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 }
 
@@ -447,6 +448,39 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
   a.p_words = p_words;
   e = mpcx_launch_fermat2(&a, (count + 63) / 64, nullptr);
   if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
+  e = hipMemcpy(ok, g_stage[3].ptr, count, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "copy results");
+  return MPCX_OK;
+}
+
+int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* bases, uint8_t* ok) {
+  if (count == 0) return MPCX_OK;
+  if (!n || !bases || !ok || n_words == 0) return fail(MPCX_EINVAL, "null buffer");
+  if (n_words > (uint32_t)MPCX_CLASS_WORDS(0))
+    return fail(MPCX_EINVAL, "n_words %u > %d", n_words, MPCX_CLASS_WORDS(0));
+  for (uint32_t i = 0; i < count; ++i) {
+    const uint32_t* ni = n + (size_t)i * n_words;
+    if (bit_length_words(ni, n_words) < 3 || (ni[0] & 1u) == 0)
+      return fail(MPCX_EINVAL, "candidate %u is not an odd integer >= 5", i);
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  const size_t nb = (size_t)count * n_words * 4;
+  if ((rc = ensure_buffer(g_stage[0], nb)) || (rc = ensure_buffer(g_stage[1], nb)) ||
+      (rc = ensure_buffer(g_stage[3], count)))
+    return rc;
+  hipError_t e = hipMemcpy(g_stage[0].ptr, n, nb, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(g_stage[1].ptr, bases, nb, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "copy candidates");
+  mpcx::MrArgs a{};
+  a.n = (const uint32_t*)g_stage[0].ptr;
+  a.a = (const uint32_t*)g_stage[1].ptr;
+  a.ok = (uint8_t*)g_stage[3].ptr;
+  a.count = count;
+  a.n_words = n_words;
+  e = mpcx_launch_mr(&a, (count + 63) / 64, nullptr);
+  if (e != hipSuccess) return hip_fail(e, "launch k_mr");
   e = hipMemcpy(ok, g_stage[3].ptr, count, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return hip_fail(e, "copy results");
   return MPCX_OK;

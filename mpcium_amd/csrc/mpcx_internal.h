@@ -63,6 +63,14 @@ struct FermatArgs {
   uint32_t p_words;
 };
 
+struct MrArgs {
+  const uint32_t* n;  // count x n_words odd candidates
+  const uint32_t* a;  // count x n_words bases (< 2^(32*n_words))
+  uint8_t* ok;
+  uint32_t count;
+  uint32_t n_words;
+};
+
 }  // namespace mpcx
 
 #endif

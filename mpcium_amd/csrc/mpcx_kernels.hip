@@ -51,7 +51,10 @@
 #define MPCX_WAVES_PER_EU_C2 3
 #endif
 #ifndef MPCX_WAVES_PER_EU_FERMAT
-#define MPCX_WAVES_PER_EU_FERMAT 2
+#define MPCX_WAVES_PER_EU_FERMAT 1
+#endif
+#ifndef MPCX_WAVES_PER_EU_MR
+#define MPCX_WAVES_PER_EU_MR 1
 #endif
 
 namespace mpcx {
@@ -543,6 +546,150 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if (active) a.ok[op] = is_one ? 1 : 0;
 }
 
+// ---------------------------------------------------------- Miller-Rabin
+// ok[i] = n_i is a strong probable prime to base a_i (one candidate per lane,
+// per-lane modulus): n - 1 = 2^s d, x = a^d; pass iff x == 1 or x^(2^j) == n-1
+// for some j < s. Serves q.ProbablyPrime(20) in the safe-prime search
+// (up:common/safe_prime.go). All Montgomery constants are derived on the
+// device: R mod n by doubling, R^2 mod n = Mont(2^(28K)) by square-and-double.
+template <int K>
+__device__ __forceinline__ void canon_serial(uint32_t (&x)[K], const uint32_t (&n)[K]) {
+  norm_serial<K>(x);
+  for (int it = 0; it < 8 && ge_digits<K>(x, n); ++it) sub_digits<K>(x, n);
+}
+
+template <int K, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_mr(const MrArgs a) {
+  constexpr int L = K;
+  __shared__ uint32_t lds[2 * 65 * L + 1];
+  const int lane = threadIdx.x;
+  const uint32_t op = blockIdx.x * 64u + lane;
+  const bool active = op < a.count;
+  uint32_t* bt = lds + lane * L;             // row for the running value (squarings)
+  uint32_t* bm = lds + (65 + lane) * L;      // row for a*R (multiplies)
+  const int m_src_addr = lane * 4;
+  const uint32_t* nw = a.n + (size_t)(active ? op : 0) * a.n_words;
+  const uint32_t* aw = a.a + (size_t)(active ? op : 0) * a.n_words;
+  uint32_t Nd[K], A[K], X[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t bit = (uint32_t)k * DB, w = bit >> 5, sh = bit & 31u;
+    uint64_t v = 0, u = 0;
+    if (active) {
+      v = ((uint64_t)((w + 1) < a.n_words ? nw[w + 1] : 0u) << 32) | (w < a.n_words ? nw[w] : 0u);
+      u = ((uint64_t)((w + 1) < a.n_words ? aw[w + 1] : 0u) << 32) | (w < a.n_words ? aw[w] : 0u);
+    }
+    Nd[k] = (uint32_t)(v >> sh) & M28;
+    X[k] = (uint32_t)(u >> sh) & M28;
+  }
+  if (!active) Nd[0] = 1;
+  uint32_t inv = Nd[0];
+  for (int i = 0; i < 5; ++i) inv *= 2u - Nd[0] * inv;
+  const uint32_t n0inv = (0u - inv) & M28;
+  int nbits = 1;
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (Nd[k] != 0u) nbits = k * DB + (32 - __builtin_clz(Nd[k]));
+  // R mod n
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] = 0;
+  {
+    uint32_t c = 1;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const int lo = k * DB;
+      uint32_t maskk = 0;
+      if (nbits >= lo + DB) maskk = M28;
+      else if (nbits > lo) maskk = (1u << (nbits - lo)) - 1u;
+      const uint32_t t = ((~Nd[k]) & maskk) + c;
+      c = t >> DB;
+      A[k] = t & maskk;
+    }
+  }
+  for (int i = nbits; i < DB * K; ++i) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) A[k] <<= 1;
+    norm_serial<K>(A);
+    if (ge_digits<K>(A, Nd)) sub_digits<K>(A, Nd);
+  }
+  uint32_t R1[K];  // R mod n, canonical: Montgomery form of 1
+#pragma unroll
+  for (int k = 0; k < K; ++k) R1[k] = A[k];
+  // R^2 mod n = Mont(2^(28K)): square-and-double over the bits of E = 28K
+  constexpr int E = DB * K;
+  constexpr int ETOP = 31 - __builtin_clz((unsigned)E);
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] <<= 1;  // Mont(2) (top bit of E)
+  norm_serial<K>(A);
+  for (int i = ETOP - 1; i >= 0; --i) {
+    lds_store_digits<K>(bt, 0, A);
+    wave_lds_fence();
+    montmul<1, K>(A, bt, Nd, n0inv, m_src_addr);
+    wave_lds_fence();
+    if ((E >> i) & 1) {
+#pragma unroll
+      for (int k = 0; k < K; ++k) A[k] <<= 1;
+    }
+    norm_serial<K>(A);
+  }
+  // a*R = mont(a, R^2)
+  lds_store_digits<K>(bt, 0, A);
+  wave_lds_fence();
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] = X[k];
+  montmul<1, K>(A, bt, Nd, n0inv, m_src_addr);
+  wave_lds_fence();
+  lds_store_digits<K>(bm, 0, A);
+  // n - 1 = 2^s d (n odd, n >= 5): s = number of trailing zero bits of n-1
+  int s = 1;
+  while (s < nbits && !((nw[s >> 5] >> (s & 31)) & 1u)) ++s;
+  if (!active) s = 1;
+  const int dbits = nbits - s;  // bit length of d
+  // x = a^d, left to right binary (d's top bit is set)
+  for (int i = dbits - 2; i >= 0; --i) {
+    wave_lds_fence();
+    lds_store_digits<K>(bt, 0, A);
+    wave_lds_fence();
+    montmul<1, K>(A, bt, Nd, n0inv, m_src_addr);
+    const uint32_t bit = active ? (nw[(i + s) >> 5] >> ((i + s) & 31)) & 1u : 0u;
+    if (bit) {
+      wave_lds_fence();
+      montmul<1, K>(A, bm, Nd, n0inv, m_src_addr);
+    }
+  }
+  // compare in the Montgomery domain: 1 -> R1, n-1 -> n - R1
+  uint32_t NR1[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) NR1[k] = Nd[k];
+  {
+    uint32_t br = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t t = NR1[k] - R1[k] - br;
+      br = (t >> 31) & 1u;
+      NR1[k] = t & M28;
+    }
+  }
+  auto eq = [&](const uint32_t (&x)[K], const uint32_t (&y)[K]) __attribute__((always_inline)) {
+    bool e = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) e &= x[k] == y[k];
+    return e;
+  };
+  canon_serial<K>(A, Nd);
+  bool pass = eq(A, R1) || eq(A, NR1);
+  for (int j = 1; j < s && !pass; ++j) {
+    wave_lds_fence();
+    lds_store_digits<K>(bt, 0, A);
+    wave_lds_fence();
+    montmul<1, K>(A, bt, Nd, n0inv, m_src_addr);
+    canon_serial<K>(A, Nd);
+    if (eq(A, R1)) break;  // nontrivial square root of 1: composite
+    pass = eq(A, NR1);
+  }
+  if (active) a.ok[op] = pass ? 1 : 0;
+}
+
 // Device self-test of the cross-lane primitives the kernels rely on.
 __global__ void k_selftest(uint32_t* out) {
   const int lane = threadIdx.x;
@@ -580,6 +727,12 @@ __attribute__((visibility("hidden"))) hipError_t mpcx_launch_modexp(int cls, con
 __attribute__((visibility("hidden"))) hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks,
                                                                     hipStream_t st) {
   hipLaunchKernelGGL((mpcx::k_fermat2<MPCX_CLASS_K(0), MPCX_WAVES_PER_EU_FERMAT>), dim3(blocks), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks,
+                                                               hipStream_t st) {
+  hipLaunchKernelGGL((mpcx::k_mr<MPCX_CLASS_K(0), MPCX_WAVES_PER_EU_MR>), dim3(blocks), dim3(64), 0, st, *a);
   return hipGetLastError();
 }
 

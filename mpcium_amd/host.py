@@ -1,0 +1,184 @@
+"""ctypes binding of libmpcx_host.so (include/mpcx_host.h): the C++ mirror of
+tss-lib's ModInt.Exp, crypto/paillier and safe-prime / preparams generation.
+Same names and error behaviour as the Go API, with a batch dimension."""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .mpcx import MpcxError, ints_to_words, nwords, words_to_ints
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libmpcx_host.so")
+_vp, _u32, _u64, _i = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+
+RAND_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t)
+
+SIGNATURES = [
+    ("mpcxh_last_error", ctypes.c_char_p, []),
+    ("mpcxh_init", _i, [_i]),
+    ("mpcxh_modint_exp_batch", _i, [_vp, _u32, _u32, _vp, _u32, _vp, _vp, _u32, _vp, _i, _vp, _u32, _vp]),
+    ("mpcxh_paillier_encrypt_batch", _i, [_vp, _u32, _u32, _vp, _u32, _vp, _vp, _u32, _vp, _u32, _vp]),
+    ("mpcxh_paillier_homomult_batch", _i, [_vp, _u32, _u32, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
+    ("mpcxh_paillier_homoadd_batch", _i, [_vp, _u32, _u32, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
+    ("mpcxh_paillier_decrypt_batch", _i, [_vp, _u32, _vp, _u32, _vp, _u32, _vp, _u32, _u32, _vp, _u32, _vp, _vp,
+                                          _u32, _vp]),
+    ("mpcxh_safe_primes", _i, [_i, _i, _u64, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
+    ("mpcxh_generate_preparams", _i, [_u64, _vp, _vp, _vp, _vp]),
+    ("mpcxh_candidate_from_bytes", _i, [_vp, ctypes.c_size_t, _i, _vp, _u32]),
+    ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
+]
+
+ERR_OK, ERR_MESSAGE_TOO_LONG, ERR_MESSAGE_MALFORMED = 0, 1, 2
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            raise MpcxError(2, f"{_LIB_PATH} not built: run `python -m mpcium_amd.build`")
+        l = ctypes.CDLL(_LIB_PATH)
+        for name, res, args in SIGNATURES:
+            f = getattr(l, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = l
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise MpcxError(rc, lib().mpcxh_last_error().decode(errors="replace"))
+
+
+def init(device: int = 0):
+    _check(lib().mpcxh_init(device))
+
+
+def _signed(vals: Sequence[int]) -> Tuple[np.ndarray, np.ndarray]:
+    w = max([nwords(abs(v)) for v in vals] + [1])
+    return ints_to_words([abs(v) for v in vals], w), np.array([1 if v < 0 else 0 for v in vals], dtype=np.uint8)
+
+
+def _w(v: int) -> np.ndarray:
+    return ints_to_words([v], nwords(v))[0]
+
+
+def modint_exp(m: int, xs: Sequence[int], ys, shared: Optional[bool] = None) -> List[Optional[int]]:
+    """Go common.ModInt(m).Exp semantics; None where Go returns nil."""
+    if isinstance(ys, int):
+        ys, shared = [ys], True
+    shared = bool(shared) if shared is not None else len(ys) == 1 and len(xs) != 1
+    X, xn = _signed(xs)
+    Y, yn = _signed(ys)
+    M = _w(m)
+    ow = len(M)
+    out = np.zeros((len(xs), ow), dtype="<u4")
+    ok = np.zeros(len(xs), dtype=np.uint8)
+    _check(lib().mpcxh_modint_exp_batch(M.ctypes.data, len(M), len(xs), X.ctypes.data, X.shape[1], xn.ctypes.data,
+                                        Y.ctypes.data, Y.shape[1], yn.ctypes.data, 1 if shared else 0,
+                                        out.ctypes.data, ow, ok.ctypes.data))
+    return [z if k else None for z, k in zip(words_to_ints(out), ok)]
+
+
+class PublicKey:
+    """crypto/paillier.PublicKey (batched)."""
+
+    def __init__(self, N: int):
+        self.N = N
+        self._Nw = _w(N)
+
+    def _out(self, n, words):
+        return np.zeros((n, words), dtype="<u4"), np.zeros(n, dtype=np.uint8)
+
+    def encrypt(self, ms: Sequence[int], rs: Sequence[int]):
+        """EncryptAndReturnRandomness with supplied r: ([c or None], [err])."""
+        Mw, mn = _signed(ms)
+        R = ints_to_words(rs, max(nwords(r) for r in rs))
+        cw = 2 * len(self._Nw)
+        c, err = self._out(len(ms), cw)
+        _check(lib().mpcxh_paillier_encrypt_batch(self._Nw.ctypes.data, len(self._Nw), len(ms), Mw.ctypes.data,
+                                                  Mw.shape[1], mn.ctypes.data, R.ctypes.data, R.shape[1],
+                                                  c.ctypes.data, cw, err.ctypes.data))
+        return words_to_ints(c), [int(e) for e in err]
+
+    def homo_mult(self, ms: Sequence[int], c1s: Sequence[int]):
+        Mw, mn = _signed(ms)
+        C, cn = _signed(c1s)
+        ow = 2 * len(self._Nw)
+        o, err = self._out(len(ms), ow)
+        _check(lib().mpcxh_paillier_homomult_batch(self._Nw.ctypes.data, len(self._Nw), len(ms), Mw.ctypes.data,
+                                                   Mw.shape[1], mn.ctypes.data, C.ctypes.data, C.shape[1],
+                                                   cn.ctypes.data, o.ctypes.data, ow, err.ctypes.data))
+        return words_to_ints(o), [int(e) for e in err]
+
+    def homo_add(self, c1s: Sequence[int], c2s: Sequence[int]):
+        A, an = _signed(c1s)
+        B, bn = _signed(c2s)
+        ow = 2 * len(self._Nw)
+        o, err = self._out(len(c1s), ow)
+        _check(lib().mpcxh_paillier_homoadd_batch(self._Nw.ctypes.data, len(self._Nw), len(c1s), A.ctypes.data,
+                                                  A.shape[1], an.ctypes.data, B.ctypes.data, B.shape[1],
+                                                  bn.ctypes.data, o.ctypes.data, ow, err.ctypes.data))
+        return words_to_ints(o), [int(e) for e in err]
+
+
+class PrivateKey(PublicKey):
+    def __init__(self, N: int, lambda_n: int, P: int, Q: int):
+        super().__init__(N)
+        self.LambdaN, self.P, self.Q = lambda_n, P, Q
+
+    def decrypt(self, cs: Sequence[int]):
+        C, cn = _signed(cs)
+        lw, pw, qw = _w(self.LambdaN), _w(self.P), _w(self.Q)
+        mw = len(self._Nw)
+        m, err = self._out(len(cs), mw)
+        _check(lib().mpcxh_paillier_decrypt_batch(self._Nw.ctypes.data, len(self._Nw), lw.ctypes.data, len(lw),
+                                                  pw.ctypes.data, len(pw), qw.ctypes.data, len(qw), len(cs),
+                                                  C.ctypes.data, C.shape[1], cn.ctypes.data, m.ctypes.data, mw,
+                                                  err.ctypes.data))
+        return words_to_ints(m), [int(e) for e in err]
+
+
+def safe_primes(bit_len: int, num: int, seed: int = 0, rand_fn=None):
+    """[(p, q, index)] in candidate-stream order + stats dict."""
+    words = (bit_len + 31) // 32
+    P = np.zeros((num, words), dtype="<u4")
+    Q = np.zeros((num, words), dtype="<u4")
+    idx = np.zeros(num, dtype=np.uint64)
+    st = np.zeros(5, dtype=np.uint64)
+    cb = RAND_FN(rand_fn) if rand_fn else None
+    _check(lib().mpcxh_safe_primes(bit_len, num, seed, ctypes.cast(cb, _vp) if cb else None, None, P.ctypes.data,
+                                   Q.ctypes.data, words, idx.ctypes.data, st.ctypes.data))
+    stats = dict(zip(["candidates", "sieved_out", "fermat_tests", "mr_tests", "usec"], (int(x) for x in st)))
+    return list(zip(words_to_ints(P), words_to_ints(Q), (int(i) for i in idx))), stats
+
+
+PREPARAM_FIELDS = ["N", "LambdaN", "PhiN", "P", "Q", "NTildei", "H1i", "H2i", "Alpha", "Beta", "p", "q"]
+
+
+def generate_preparams(seed: int = 0):
+    out = np.zeros((len(PREPARAM_FIELDS), 64), dtype="<u4")
+    st = np.zeros(5, dtype=np.uint64)
+    _check(lib().mpcxh_generate_preparams(seed, None, None, out.ctypes.data, st.ctypes.data))
+    vals = dict(zip(PREPARAM_FIELDS, words_to_ints(out)))
+    stats = dict(zip(["candidates", "sieved_out", "fermat_tests", "mr_tests", "usec"], (int(x) for x in st)))
+    return vals, stats
+
+
+def candidate_from_bytes(raw: bytes, q_bit_len: int) -> int:
+    words = (q_bit_len + 31) // 32 + 1
+    out = np.zeros(words, dtype="<u4")
+    buf = (ctypes.c_uint8 * len(raw)).from_buffer_copy(raw)
+    _check(lib().mpcxh_candidate_from_bytes(buf, len(raw), q_bit_len, out.ctypes.data, words))
+    return words_to_ints(out[None, :])[0]
+
+
+def drbg_read(seed: int, n: int) -> bytes:
+    buf = (ctypes.c_uint8 * n)()
+    _check(lib().mpcxh_drbg_read(seed, buf, n))
+    return bytes(buf)

@@ -43,6 +43,7 @@ SIGNATURES = [
     ("mpcx_mulmod_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp,
                                          ctypes.c_uint32]),
     ("mpcx_fermat2_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    ("mpcx_mr_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
     ("mpcx_dev_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
     ("mpcx_dev_free", ctypes.c_int, [_vp]),
     ("mpcx_memcpy_h2d", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
@@ -233,4 +234,18 @@ def fermat2_batch(cands: Sequence[int]) -> List[bool]:
     P = ints_to_words(cands, pw)
     ok = np.zeros(len(cands), dtype=np.uint8)
     _check(lib().mpcx_fermat2_batch(len(cands), P.ctypes.data, pw, ok.ctypes.data))
+    return [bool(x) for x in ok]
+
+
+def mr_batch(ns: Sequence[int], bases: Sequence[int]) -> List[bool]:
+    """[n is a strong probable prime to base a] for odd n (5 <= n < 2^1024)."""
+    if len(ns) != len(bases):
+        raise ValueError("one base per candidate")
+    if len(ns) == 0:
+        return []
+    w = max(nwords(n) for n in ns)
+    Nw = ints_to_words(ns, w)
+    A = ints_to_words([b % n if b.bit_length() > 32 * w else b for b, n in zip(bases, ns)], w)
+    ok = np.zeros(len(ns), dtype=np.uint8)
+    _check(lib().mpcx_mr_batch(len(ns), Nw.ctypes.data, w, A.ctypes.data, ok.ctypes.data))
     return [bool(x) for x in ok]

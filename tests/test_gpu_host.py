@@ -1,0 +1,121 @@
+"""GPU parity tests of the C++ host mirror (ModInt.Exp, crypto/paillier,
+safe primes, GeneratePreParams) against the oracle and golden fixtures."""
+import math
+import random
+
+import pytest
+
+from conftest import H, load_golden
+from oracle import gomath as gm
+from oracle import safeprime_ref as sp
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def host(gpu):
+    from mpcium_amd import host as h
+    h.init(0)
+    return h
+
+
+def test_modint_go_semantics_golden(host):
+    for c in load_golden("go_exp_semantics.json")["cases"]:
+        x, y, m = H(c["x"]), H(c["y"]), H(c["m"])
+        if m % 2 == 0:
+            continue  # math/big's even-modulus path stays with the caller
+        assert host.modint_exp(m, [x], [y], shared=False)[0] == H(c["z"]), c
+
+
+def test_modint_go_semantics_random(host, paillier_key):
+    N = paillier_key["N"]
+    rng = random.Random(8)
+    for m in (N * N, N, 65537, 3, 1):
+        xs = [rng.randrange(-m * 3, m * 3) for _ in range(30)] + [0, 1, -1, m, -m]
+        ys = [rng.randrange(-2 ** 300, 2 ** 300) for _ in xs]
+        got = host.modint_exp(m, xs, ys, shared=False)
+        assert got == [gm.go_exp(x, y, m) for x, y in zip(xs, ys)], m
+        got = host.modint_exp(m, xs, -5)
+        assert got == [gm.go_exp(x, -5, m) for x in xs]
+
+
+def test_modint_rejects_even_modulus(host):
+    from mpcium_amd.mpcx import MpcxError
+    with pytest.raises(MpcxError):
+        host.modint_exp(1 << 64, [3], 5)
+
+
+def test_paillier_golden(host, paillier_key):
+    N, lam, P, Q = paillier_key["N"], paillier_key["LambdaN"], paillier_key["P"], paillier_key["Q"]
+    sk = host.PrivateKey(N, lam, P, Q)
+    ops = load_golden("paillier_vectors.json")["ops"]
+    ms = [H(o["m"]) for o in ops]
+    rs = [H(o["r"]) for o in ops]
+    cs, err = sk.encrypt(ms, rs)
+    assert err == [0] * len(ops) and cs == [H(o["c"]) for o in ops]
+    hm, err = sk.homo_mult([H(o["b"]) for o in ops], cs)
+    assert err == [0] * len(ops) and hm == [H(o["homo_mult"]) for o in ops]
+    ha, err = sk.homo_add(cs, [H(o["c2"]) for o in ops])
+    assert err == [0] * len(ops) and ha == [H(o["homo_add"]) for o in ops]
+    dm, err = sk.decrypt(cs + hm + ha)
+    assert err == [0] * (3 * len(ops))
+    assert dm == ms + [m * H(o["b"]) % N for m, o in zip(ms, ops)] + [(m + H(o["m2"])) % N for m, o in zip(ms, ops)]
+
+
+def test_paillier_errors(host, paillier_key):
+    N, lam, P, Q = paillier_key["N"], paillier_key["LambdaN"], paillier_key["P"], paillier_key["Q"]
+    sk = host.PrivateKey(N, lam, P, Q)
+    N2 = N * N
+    _, err = sk.encrypt([N, -1, 5], [3, 3, 3])
+    assert err == [host.ERR_MESSAGE_TOO_LONG, host.ERR_MESSAGE_TOO_LONG, 0]
+    _, err = sk.homo_mult([5, N, 5], [N2, 7, -1])
+    assert err == [1, 1, 1]
+    _, err = sk.homo_add([N2, 5], [5, N2 + 1])
+    assert err == [1, 1]
+    _, err = sk.decrypt([N2, -3, P * 5, Q, 0, 12345])
+    assert err == [1, 1, 2, 2, 2, 0]
+
+
+def test_paillier_random_roundtrip(host, paillier_key):
+    N, lam, P, Q = paillier_key["N"], paillier_key["LambdaN"], paillier_key["P"], paillier_key["Q"]
+    sk = host.PrivateKey(N, lam, P, Q)
+    rng = gm.CounterDRBG(1234)
+    n = 200
+    ms = [rng.randbelow(N) for _ in range(n)]
+    rs = [rng.rand_coprime(N) for _ in range(n)]
+    cs, _ = sk.encrypt(ms, rs)
+    assert cs == [gm.paillier_encrypt(N, m, r) for m, r in zip(ms, rs)]
+    dm, _ = sk.decrypt(cs)
+    assert dm == ms
+
+
+def test_safe_primes_match_oracle_stream(host):
+    for v in load_golden("safeprime_vectors.json")["primes"]:
+        got, stats = host.safe_primes(v["bits"], 1, seed=v["seed"])
+        p, q, idx = got[0]
+        assert (p, q, idx) == (H(v["p"]), H(v["q"]), v["index"]), v["bits"]
+        assert stats["fermat_tests"] > 0
+
+
+def test_safe_primes_small_multi(host):
+    got, _ = host.safe_primes(128, 3, seed=77)
+    want = sp.first_safe_primes(77, 128, 3)
+    assert [(p, q, i) for p, q, i in got] == [(p, q, i) for i, p, q in want]
+
+
+def test_generate_preparams_relations(host):
+    pp, stats = host.generate_preparams(seed=0x6D706333)
+    N, P, Q = pp["N"], pp["P"], pp["Q"]
+    assert N == P * Q and N.bit_length() == 2048
+    assert abs(P - Q).bit_length() >= 1024 - 3
+    assert pp["PhiN"] == (P - 1) * (Q - 1)
+    assert pp["LambdaN"] == pp["PhiN"] // math.gcd(P - 1, Q - 1)
+    p, q = pp["p"], pp["q"]
+    assert pp["NTildei"] == (2 * p + 1) * (2 * q + 1)
+    for sp_ in (P, Q, 2 * p + 1, 2 * q + 1):
+        assert pow(2, sp_ - 1, sp_) == 1 and sp.miller_rabin((sp_ - 1) // 2, 4)
+    Nt = pp["NTildei"]
+    assert pp["H2i"] == pow(pp["H1i"], pp["Alpha"], Nt)
+    assert pp["Alpha"] * pp["Beta"] % (p * q) == 1
+    assert math.gcd(pp["H1i"], Nt) == 1
+    assert stats["candidates"] > 0

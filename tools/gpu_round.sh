@@ -1,9 +1,10 @@
-mkdir -p gpurun_out/prof_r01 && export TMPDIR=/tmp
-timeout -k 10 300 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu3.txt 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -5 gpurun_out/pytest_gpu3.txt
+# one GPU session: parity tests, then a batch-size sweep of bench.py
+set -o pipefail
+mkdir -p gpurun_out && export TMPDIR=/tmp
+timeout -k 10 600 python -m pytest tests -m gpu -x -q > gpurun_out/pytest_gpu.txt 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -15 gpurun_out/pytest_gpu.txt
 if [ $rc -ne 0 ]; then exit 1; fi
-timeout -k 10 400 python tools/ab_variants.py run 3 > gpurun_out/ab.txt 2>&1
-rc=$?; echo "ab rc=$rc"; cat gpurun_out/ab.txt
-if [ $rc -ne 0 ]; then exit 1; fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_r01 -o r01 -- python3 bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof_r01/bench.txt 2>&1
-echo "prof rc=$?"; tail -2 gpurun_out/prof_r01/bench.txt; find gpurun_out/prof_r01 -name "*stats*" -exec cat {} \; 
+for c in 27648 55296 65536 82944; do
+  timeout -k 10 120 python bench.py --steps 2 --warmup 1 --no-cpu-baseline --count $c > gpurun_out/bench_c$c.txt 2>&1 || exit 1
+  python -c "import json,sys; d=json.loads(open('gpurun_out/bench_c$c.txt').read().strip().splitlines()[-1]); print($c, round(d['value']), round(d['roofline']['kernel_ms'],2))"
+done
