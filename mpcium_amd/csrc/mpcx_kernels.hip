@@ -37,6 +37,9 @@
 #ifndef MPCX_SCHED_BARRIER
 #define MPCX_SCHED_BARRIER 0
 #endif
+#ifndef MPCX_SQR_OPT
+#define MPCX_SQR_OPT 1  // half-product squarings (montmul<..., true>)
+#endif
 #ifndef MPCX_PREFETCH_B
 #define MPCX_PREFETCH_B 1
 #endif
@@ -122,22 +125,53 @@ __device__ __forceinline__ void carry_pass32(uint32_t (&d)[K]) {
 }
 
 // A <- A * B * R^-1 (almost Montgomery, result < 2N given A, B < 2N), with
-// B's L digits in LDS at bl[0..L). Result digits are <= 2^28 + 2^10
-// (two carry passes), which keeps every product below 2^56.01.
-template <int P, int K>
+// B's L digits in LDS at bl[0..L) (p = this lane's index in its group).
+// Result digits are <= 2^28 + 2^10 (two carry passes), which keeps every
+// product below 2^56.01 (2^57.01 for the doubled squaring products: a
+// position then takes <= L/2+1 of those plus one m*N per iteration, < 2^63.8
+// over the longest 84-iteration segment between carry passes).
+//
+// SQR (B == A, squaring): each unordered digit pair {i, j} needs ONE product
+// 2*a_i*a_j (plus a_i^2 on the diagonal). In iteration t the product of
+// multiplicand register k (digit s = p*K + k) is needed iff d = (k - t) mod K
+// lies in [1, (K-1)/2] (doubled), or d == 0 with a per-lane factor
+// (2 above the diagonal lane, 1 on it, 0 below); every other register is
+// skipped for ALL lanes -- a compile-time decision, since t mod K is the
+// unrolled index. Each pair lands in its column before that column is
+// reduced (both orientations use an iteration <= i + j). K must be odd.
+// Saves (K-1)/2 of the K a*b mads of every squaring iteration.
+template <int P, int K, bool SQR>
 __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, const uint32_t (&Nd)[K],
-                                        uint32_t n0inv, int m_src_addr) {
+                                        uint32_t n0inv, int m_src_addr, int p) {
+  static_assert(!SQR || (K % 2) == 1, "squaring schedule needs an odd digit count per lane");
   uint64_t acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
   uint32_t bnext = bl[0];
   for (int o = 0; o < P; ++o) {
     const uint32_t* bo = bl + o * K;
+    // diagonal-register factor of this lane for the whole block
+    const uint32_t fdiag = p > o ? 2u : (p == o ? 1u : 0u);
     static_for<0, K>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
       const uint32_t bi = bnext;
+      const uint32_t b2 = bi << 1;
+      const uint32_t bd = bi * fdiag;
+      auto ab = [&](auto kc) __attribute__((always_inline)) {
+        constexpr int k = decltype(kc)::value;
+        if constexpr (!SQR) {
+          mad64(acc[(k + u) % K], A[k], bi);
+        } else {
+          constexpr int d = ((k - u) % K + K) % K;
+          if constexpr (d == 0) {
+            mad64(acc[(k + u) % K], A[k], bd);
+          } else if constexpr (d <= (K - 1) / 2) {
+            mad64(acc[(k + u) % K], A[k], b2);
+          }
+        }
+      };
       // slot 0 first: it feeds m_i, the only serial dependency of the iteration
-      mad64(acc[u], A[0], bi);
+      ab(std::integral_constant<int, 0>{});
       uint32_t m = ((uint32_t)acc[u] * n0inv) & M28;
       if constexpr (P > 1) m = (uint32_t)__builtin_amdgcn_ds_bpermute(m_src_addr, (int)m);
 #if MPCX_PREFETCH_B
@@ -145,10 +179,7 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
       // (the last read of the last block touches the neighbour row: unused)
       bnext = bo[u + 1];
 #endif
-      static_for<1, K>([&](auto kc) {
-        constexpr int k = decltype(kc)::value;
-        mad64(acc[(k + u) % K], A[k], bi);
-      });
+      static_for<1, K>(ab);
 #if !MPCX_PREFETCH_B
       bnext = bo[u + 1];
 #endif
@@ -314,6 +345,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   enum { ST_PRE, ST_TAB, ST_EXP, ST_MULF, ST_FIN };
   int st;
   uint32_t idx = 1;
+  bool sqr = false;  // next montmul is a squaring (B == A)
   if (has_mul) {
     load_digits(a.mul, a.mul_words);
     st = ST_PRE;
@@ -338,6 +370,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
       if (idx % 5u < 4u) {
         lds_store_digits<K>(bl, p, A);
+        sqr = true;
         return;
       }
       if (shared) {
@@ -355,7 +388,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   };
 
   for (;;) {
-    montmul<P, K>(A, bl, Nd, a.n0inv, m_src_addr);
+    if (MPCX_SQR_OPT && sqr) {
+      montmul<P, K, true>(A, bl, Nd, a.n0inv, m_src_addr, p);
+    } else {
+      montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
+    }
+    sqr = false;
     wave_lds_fence();
     if (st == ST_PRE) {
       tbl_store(16, A);
@@ -519,7 +557,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     // A <- A^2 / R
     lds_store_digits<K>(bl, 0, A);
     wave_lds_fence();
-    montmul<1, K>(A, bl, Nd, n0inv, m_src_addr);
+    montmul<1, K, true>(A, bl, Nd, n0inv, m_src_addr, 0);
     wave_lds_fence();
     uint32_t ebit = active ? (pw[i >> 5] >> (i & 31)) & 1u : 0u;
     if (i == 0) ebit = 0;  // e = p - 1
@@ -536,7 +574,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     for (int k = 0; k < K; ++k) one[k] = (k == 0) ? 1u : 0u;
     lds_store_digits<K>(bl, 0, one);
     wave_lds_fence();
-    montmul<1, K>(A, bl, Nd, n0inv, m_src_addr);
+    montmul<1, K, false>(A, bl, Nd, n0inv, m_src_addr, 0);
   }
   norm_serial<K>(A);
   while (ge_digits<K>(A, Nd)) sub_digits<K>(A, Nd);
@@ -624,7 +662,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   for (int i = ETOP - 1; i >= 0; --i) {
     lds_store_digits<K>(bt, 0, A);
     wave_lds_fence();
-    montmul<1, K>(A, bt, Nd, n0inv, m_src_addr);
+    montmul<1, K, true>(A, bt, Nd, n0inv, m_src_addr, 0);
     wave_lds_fence();
     if ((E >> i) & 1) {
 #pragma unroll
@@ -637,7 +675,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   wave_lds_fence();
 #pragma unroll
   for (int k = 0; k < K; ++k) A[k] = X[k];
-  montmul<1, K>(A, bt, Nd, n0inv, m_src_addr);
+  montmul<1, K, false>(A, bt, Nd, n0inv, m_src_addr, 0);
   wave_lds_fence();
   lds_store_digits<K>(bm, 0, A);
   // n - 1 = 2^s d (n odd, n >= 5): s = number of trailing zero bits of n-1
@@ -650,11 +688,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     wave_lds_fence();
     lds_store_digits<K>(bt, 0, A);
     wave_lds_fence();
-    montmul<1, K>(A, bt, Nd, n0inv, m_src_addr);
+    montmul<1, K, true>(A, bt, Nd, n0inv, m_src_addr, 0);
     const uint32_t bit = active ? (nw[(i + s) >> 5] >> ((i + s) & 31)) & 1u : 0u;
     if (bit) {
       wave_lds_fence();
-      montmul<1, K>(A, bm, Nd, n0inv, m_src_addr);
+      montmul<1, K, false>(A, bm, Nd, n0inv, m_src_addr, 0);
     }
   }
   // compare in the Montgomery domain: 1 -> R1, n-1 -> n - R1
@@ -682,7 +720,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     wave_lds_fence();
     lds_store_digits<K>(bt, 0, A);
     wave_lds_fence();
-    montmul<1, K>(A, bt, Nd, n0inv, m_src_addr);
+    montmul<1, K, true>(A, bt, Nd, n0inv, m_src_addr, 0);
     canon_serial<K>(A, Nd);
     if (eq(A, R1)) break;  // nontrivial square root of 1: composite
     pass = eq(A, NR1);
