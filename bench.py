@@ -177,10 +177,8 @@ def main():
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step on `stream`
 
-    t = torch.tensor([elapsed, kernel_ms], dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed, kernel_ms = float(t[0]), float(t[1])
+    from mpcium_amd.shard import max_over_ranks
+    elapsed, kernel_ms = max_over_ranks([elapsed, kernel_ms], world)
 
     total = count * world * args.steps
     value = total / elapsed
