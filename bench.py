@@ -107,6 +107,7 @@ def main():
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=16, help="results checked against CPython pow (untimed)")
+    ap.add_argument("--opt", action="append", default=[], help="libmpcx tuning knob key=value (mpcx_set_option)")
     args = ap.parse_args()
 
     import torch
@@ -126,6 +127,9 @@ def main():
     if world > 1:
         dist.barrier()
     mpcx.init(local)
+    for kv in args.opt:
+        k, v = kv.split("=")
+        mpcx.set_option(k, int(v))
 
     N = load_key()
     N2 = N * N

@@ -159,6 +159,15 @@ int mpcx_stream_create(void** out_stream);
 int mpcx_stream_destroy(void* stream);
 int mpcx_stream_sync(void* stream);
 
+/* Tuning knobs (process-wide):
+ *   "split"      0 (default) / 1: run the partial last round of resident
+ *                wavefronts of a large batch in the class's narrow geometry
+ *                (more lanes per operand, shorter wavefronts). Batches under
+ *                0.15 of a round always use the narrow geometry.
+ *   "force_geom" -1 (default) or a geometry id (0..4, see mpcx_internal.h) to
+ *                run every batch of the matching class in that geometry. */
+int mpcx_set_option(const char* key, int value);
+
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):
  * digits L (radix 2^28), lanes per operand P, digits per lane K, operands per
  * 64-lane wavefront G. */

@@ -8,8 +8,10 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -19,7 +21,8 @@
 #include "mpcx_internal.h"
 
 extern "C" {
-hipError_t mpcx_launch_modexp(int cls, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st);
+hipError_t mpcx_modexp_occupancy(int geom, int* blocks_per_cu);
 hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
@@ -43,6 +46,10 @@ constexpr uint32_t kM28 = (1u << kDigitBits) - 1u;
 thread_local std::string g_err;
 std::mutex g_mu;
 int g_device = -1;
+int g_num_cus = 0;
+int g_geom_slots[MPCX_NUM_GEOMS] = {0};  // resident wavefronts per device, per geometry
+bool g_split = false;                    // narrow-geometry tail launch (measured slower: off)
+int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): one geometry for everything
 uint32_t* g_ws = nullptr;  // exponentiation table workspace
 size_t g_ws_bytes = 0;
 struct Staging {
@@ -185,6 +192,20 @@ extern "C" {
 
 int mpcx_version(void) { return 100; }
 
+int mpcx_set_option(const char* key, int value) {
+  if (!key) return fail(MPCX_EINVAL, "null option");
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (std::strcmp(key, "split") == 0) {
+    g_split = value != 0;
+  } else if (std::strcmp(key, "force_geom") == 0) {
+    if (value < -1 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "force_geom %d out of range", value);
+    g_force_geom = value;
+  } else {
+    return fail(MPCX_EINVAL, "unknown option %s", key);
+  }
+  return MPCX_OK;
+}
+
 const char* mpcx_last_error(void) { return g_err.c_str(); }
 
 int mpcx_device_count(int* out_count) {
@@ -214,6 +235,14 @@ int mpcx_init(int device) {
   if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
     return fail(MPCX_ENODEV, "device %d is %s; libmpcx is built for gfx950 only", device, prop.gcnArchName);
   g_device = device;
+  g_num_cus = prop.multiProcessorCount;
+  for (int g = 0; g < MPCX_NUM_GEOMS; ++g) {
+    int b = 0;
+    if (mpcx_modexp_occupancy(g, &b) != hipSuccess || b <= 0) b = 1;
+    g_geom_slots[g] = b * g_num_cus;
+  }
+  const char* sp = std::getenv("MPCX_SPLIT");
+  if (sp) g_split = sp[0] != '0';
   int rc = run_selftest();
   if (rc != MPCX_OK) g_device = -1;
   return rc;
@@ -313,29 +342,68 @@ static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* 
   if (exp_bits > 32u * exp_words) return fail(MPCX_EINVAL, "exp_bits %u > 32*exp_words", exp_bits);
   if (count == 0) return MPCX_OK;
   if (!d_bases || !d_out || (exp_words && !d_exps)) return fail(MPCX_EINVAL, "null buffer");
-  const uint32_t G = (uint32_t)MPCX_CLASS_G(mod->cls), K = (uint32_t)MPCX_CLASS_K(mod->cls);
-  const uint32_t waves = (count + G - 1) / G;
-  int rc = ensure_workspace((size_t)waves * MPCX_TABLE_ENTRIES * K * 64u * sizeof(uint32_t));
+  // Geometry plan: whole rounds of resident wavefronts in the main geometry,
+  // the partial last round (or a small batch) in the narrow geometry.
+  struct Part {
+    int geom;
+    uint32_t first, count;
+  } parts[2];
+  int nparts = 0;
+  const int gm = mod->cls, gn = MPCX_NARROW_GEOM(mod->cls);
+  if (g_force_geom >= 0 && (g_force_geom == gm || g_force_geom == gn)) {
+    parts[nparts++] = {g_force_geom, 0, count};
+  } else {
+    const uint32_t G = (uint32_t)MPCX_GEOM_G(gm);
+    const double waves = (double)((count + G - 1) / G);
+    const double rounds = waves / (double)std::max(1, g_geom_slots[gm]);
+    const double full = std::floor(rounds), frac = rounds - full;
+    // Measured on MI355X (profiles/r01): a lone wavefront issues v_mad_u64_u32
+    // at ~45% of SIMD peak, so tiny batches (< 0.15 of a round) finish sooner
+    // spread over the narrow geometry's 3x more wavefronts; from ~0.3 rounds up
+    // the main geometry wins, and a narrow tail launch did not pay.
+    if (gn >= 0 && rounds < 0.15) {
+      parts[nparts++] = {gn, 0, count};
+    } else if (!g_split || gn < 0 || rounds < 1.0 || frac == 0.0 || frac > 0.75) {
+      parts[nparts++] = {gm, 0, count};
+    } else {
+      const uint32_t nmain = (uint32_t)full * (uint32_t)g_geom_slots[gm] * G;
+      parts[nparts++] = {gm, 0, nmain};
+      parts[nparts++] = {gn, nmain, count - nmain};
+    }
+  }
+  size_t ws_words = 0;
+  for (int i = 0; i < nparts; ++i) {
+    const uint32_t G = (uint32_t)MPCX_GEOM_G(parts[i].geom), K = (uint32_t)MPCX_GEOM_K(parts[i].geom);
+    ws_words += (size_t)((parts[i].count + G - 1) / G) * MPCX_TABLE_ENTRIES * K * 64u;
+  }
+  int rc = ensure_workspace(ws_words * sizeof(uint32_t));
   if (rc) return rc;
-  mpcx::ModexpArgs a{};
-  a.nd = mod->d_const;
-  a.r1d = mod->d_const + mod->L;
-  a.r2d = mod->d_const + 2 * mod->L;
-  a.base = d_bases;
-  a.exps = d_exps;
-  a.mul = d_muls;
-  a.out = d_out;
-  a.table = g_ws;
-  a.count = count;
-  a.base_words = base_words;
-  a.exp_words = exp_words;
-  a.mul_words = d_muls ? mul_words : 0;
-  a.exp_bits = exp_words ? exp_bits : 0;
-  a.out_words = out_words;
-  a.n0inv = mod->n0inv;
-  a.exp_shared = exp_shared ? 1 : 0;
-  hipError_t e = mpcx_launch_modexp(mod->cls, &a, waves, st);
-  if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
+  size_t ws_off = 0;
+  for (int i = 0; i < nparts; ++i) {
+    const Part& pt = parts[i];
+    const uint32_t G = (uint32_t)MPCX_GEOM_G(pt.geom), K = (uint32_t)MPCX_GEOM_K(pt.geom);
+    const uint32_t waves = (pt.count + G - 1) / G;
+    mpcx::ModexpArgs a{};
+    a.nd = mod->d_const;
+    a.r1d = mod->d_const + mod->L;
+    a.r2d = mod->d_const + 2 * mod->L;
+    a.base = d_bases + (size_t)pt.first * base_words;
+    a.exps = exp_shared ? d_exps : (d_exps ? d_exps + (size_t)pt.first * exp_words : nullptr);
+    a.mul = d_muls ? d_muls + (size_t)pt.first * mul_words : nullptr;
+    a.out = d_out + (size_t)pt.first * out_words;
+    a.table = g_ws + ws_off;
+    a.count = pt.count;
+    a.base_words = base_words;
+    a.exp_words = exp_words;
+    a.mul_words = d_muls ? mul_words : 0;
+    a.exp_bits = exp_words ? exp_bits : 0;
+    a.out_words = out_words;
+    a.n0inv = mod->n0inv;
+    a.exp_shared = exp_shared ? 1 : 0;
+    hipError_t e = mpcx_launch_modexp(pt.geom, &a, waves, st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
+    ws_off += (size_t)waves * MPCX_TABLE_ENTRIES * K * 64u;
+  }
   return MPCX_OK;
 }
 

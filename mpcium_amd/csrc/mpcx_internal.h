@@ -27,6 +27,22 @@
 #define MPCX_CLASS_K(c) ((c) == 0 ? MPCX_C0_K : (c) == 1 ? MPCX_C1_K : MPCX_C2_K)
 #define MPCX_CLASS_G(c) ((c) == 0 ? MPCX_C0_G : (c) == 1 ? MPCX_C1_G : MPCX_C2_G)
 #define MPCX_CLASS_L(c) (MPCX_CLASS_P(c) * MPCX_CLASS_K(c))
+// Kernel geometries. Geometry c < MPCX_NUM_CLASSES is class c's main
+// (throughput) geometry; the "narrow" ones split the same L digits over more
+// lanes (fewer digits per lane -> ~3x shorter wavefronts) and serve the last
+// partial round of a batch and small, latency-bound batches.
+#define MPCX_NUM_GEOMS 5
+#define MPCX_G3_P 15  // class 1 narrow: 15 x 5 = 75 digits, 4 operands per wave
+#define MPCX_G3_K 5
+#define MPCX_G3_G 4
+#define MPCX_G4_P 21  // class 2 narrow: 21 x 7 = 147 digits, 3 operands per wave
+#define MPCX_G4_K 7
+#define MPCX_G4_G 3
+#define MPCX_GEOM_P(g) ((g) < 3 ? MPCX_CLASS_P(g) : (g) == 3 ? MPCX_G3_P : MPCX_G4_P)
+#define MPCX_GEOM_K(g) ((g) < 3 ? MPCX_CLASS_K(g) : (g) == 3 ? MPCX_G3_K : MPCX_G4_K)
+#define MPCX_GEOM_G(g) ((g) < 3 ? MPCX_CLASS_G(g) : (g) == 3 ? MPCX_G3_G : MPCX_G4_G)
+#define MPCX_NARROW_GEOM(c) ((c) == 1 ? 3 : (c) == 2 ? 4 : -1)
+
 // operand width in 32-bit words (bases and moduli)
 #define MPCX_CLASS_WORDS(c) ((28 * MPCX_CLASS_L(c)) / 32)
 #define MPCX_CLASS_MAXBITS(c) (32 * MPCX_CLASS_WORDS(c))

@@ -741,21 +741,49 @@ __global__ void k_selftest(uint32_t* out) {
 }  // namespace mpcx
 
 // ------------------------------------------------------------ launchers
-#define MPCX_WPE(c) ((c) == 0 ? MPCX_WAVES_PER_EU_C0 : (c) == 1 ? MPCX_WAVES_PER_EU_C1 : MPCX_WAVES_PER_EU_C2)
+#ifndef MPCX_WAVES_PER_EU_G3
+#define MPCX_WAVES_PER_EU_G3 8
+#endif
+#ifndef MPCX_WAVES_PER_EU_G4
+#define MPCX_WAVES_PER_EU_G4 8
+#endif
+#define MPCX_WPE(g)                                                                                       \
+  ((g) == 0 ? MPCX_WAVES_PER_EU_C0                                                                        \
+            : (g) == 1 ? MPCX_WAVES_PER_EU_C1                                                             \
+                       : (g) == 2 ? MPCX_WAVES_PER_EU_C2 : (g) == 3 ? MPCX_WAVES_PER_EU_G3 : MPCX_WAVES_PER_EU_G4)
+#define MPCX_KERNEL(g) mpcx::k_modexp<MPCX_GEOM_P(g), MPCX_GEOM_K(g), MPCX_GEOM_G(g), MPCX_WPE(g)>
 
 extern "C" {
 
-__attribute__((visibility("hidden"))) hipError_t mpcx_launch_modexp(int cls, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st) {
-  switch (cls) {
-#define MPCX_CASE(C)                                                                                        \
-  case C:                                                                                                   \
-    hipLaunchKernelGGL((mpcx::k_modexp<MPCX_CLASS_P(C), MPCX_CLASS_K(C), MPCX_CLASS_G(C), MPCX_WPE(C)>),   \
-                       dim3(waves),                                                                         \
-                       dim3(64), 0, st, *a);                                                                \
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t waves,
+                                                                   hipStream_t st) {
+  switch (geom) {
+#define MPCX_CASE(G)                                                                 \
+  case G:                                                                            \
+    hipLaunchKernelGGL((MPCX_KERNEL(G)), dim3(waves), dim3(64), 0, st, *a);          \
     return hipGetLastError();
     MPCX_CASE(0)
     MPCX_CASE(1)
     MPCX_CASE(2)
+    MPCX_CASE(3)
+    MPCX_CASE(4)
+#undef MPCX_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+// resident 64-thread blocks (= wavefronts) per CU for a geometry's kernel
+__attribute__((visibility("hidden"))) hipError_t mpcx_modexp_occupancy(int geom, int* blocks_per_cu) {
+  switch (geom) {
+#define MPCX_CASE(G) \
+  case G:            \
+    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, MPCX_KERNEL(G), 64, 0);
+    MPCX_CASE(0)
+    MPCX_CASE(1)
+    MPCX_CASE(2)
+    MPCX_CASE(3)
+    MPCX_CASE(4)
 #undef MPCX_CASE
     default:
       return hipErrorInvalidValue;

@@ -23,6 +23,7 @@ _vp = ctypes.c_void_p
 # (name, restype, argtypes) -- must match include/mpcx.h
 SIGNATURES = [
     ("mpcx_version", ctypes.c_int, []),
+    ("mpcx_set_option", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
     ("mpcx_last_error", ctypes.c_char_p, []),
     ("mpcx_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     ("mpcx_init", ctypes.c_int, [ctypes.c_int]),
@@ -91,6 +92,10 @@ def device_count() -> int:
 
 def init(device: int = 0):
     _check(lib().mpcx_init(device))
+
+
+def set_option(key: str, value: int):
+    _check(lib().mpcx_set_option(key.encode(), int(value)))
 
 
 def shutdown():

@@ -119,3 +119,42 @@ def test_exp_mul_and_mulmod(gpu, paillier_key):
         assert mod.exp_mul(xs, es, cs) == [c * pow(x, e, m) % m for x, e, c in zip(xs, es, cs)]
         assert mod.exp_mul(xs, 0, cs) == [c % m for c in cs]
         mod.release()
+
+
+@pytest.mark.parametrize("geom", [1, 2, 3, 4])
+def test_each_geometry_forced(gpu, paillier_key, geom):
+    """Main (1, 2) and narrow (3, 4) geometries of the 2048/4096-bit classes."""
+    N = paillier_key["N"]
+    m = N * N if geom in (2, 4) else N
+    rng = random.Random(geom)
+    gpu.set_option("force_geom", geom)
+    try:
+        mod = gpu.Modulus(m)
+        xs = [rng.randrange(m) for _ in range(40)]
+        es = [rng.getrandbits(rng.choice([1, 17, 256, 2048])) for _ in xs]
+        assert mod.exp(xs, N) == [pow(x, N, m) for x in xs]
+        assert mod.exp(xs, es) == [pow(x, e, m) for x, e in zip(xs, es)]
+        cs = [rng.randrange(m) for _ in xs]
+        assert mod.exp_mul(xs, es, cs) == [c * pow(x, e, m) % m for x, e, c in zip(xs, es, cs)]
+        mod.release()
+    finally:
+        gpu.set_option("force_geom", -1)
+
+
+def test_split_plan_large_batch(gpu, paillier_key):
+    """A batch that spans >1 round of resident wavefronts takes the main +
+    narrow split; spot-check results across the split point."""
+    N = paillier_key["N"]
+    N2 = N * N
+    mod = gpu.Modulus(N2)
+    count = 30000  # ~1.1 rounds of the main 4096-bit geometry on MI355X
+    rng = np.random.default_rng(3)
+    words = mod.class_words
+    B = rng.integers(0, 1 << 32, size=(count, words), dtype=np.uint64).astype(np.uint32)
+    B[:, -1] %= (N2 >> (32 * (words - 1)))
+    E = gpu.int_to_words(N, gpu.nwords(N))
+    out = mod.exp_words(B, E, True)
+    idx = list(range(0, count, 997)) + [count - 1]
+    xs = gpu.words_to_ints(B[idx])
+    zs = gpu.words_to_ints(out[idx])
+    assert zs == [pow(x, N, N2) for x in xs]
