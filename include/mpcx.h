@@ -164,8 +164,10 @@ int mpcx_stream_sync(void* stream);
  *                wavefronts of a large batch in the class's narrow geometry
  *                (more lanes per operand, shorter wavefronts). Batches under
  *                0.15 of a round always use the narrow geometry.
- *   "force_geom" -1 (default) or a geometry id (0..4, see mpcx_internal.h) to
- *                run every batch of the matching class in that geometry. */
+ *   "force_geom" -1 (default) or a geometry id (0..6, see mpcx_internal.h) to
+ *                run every batch of the matching class in that geometry.
+ *   "main_geom"  geometry id: make it the main (throughput) geometry of its
+ *                class (A/B of kernel layouts). */
 int mpcx_set_option(const char* key, int value);
 
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):

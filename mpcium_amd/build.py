@@ -16,7 +16,9 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-KERNEL_SRCS = ["mpcx_kernels.hip", "mpcx_api.cpp"]
+NUM_GEOMS = 7  # kernel geometries (mpcx_internal.h), one translation unit each
+HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
+KERNEL_HDRS = ["mpcx_device.hpp", "mpcx_internal.h"]
 HOST_SRCS = ["host/bignum.cpp", "host/engine.cpp", "host/modint.cpp", "host/paillier.cpp", "host/safeprime.cpp",
              "host/capi.cpp"]
 
@@ -33,15 +35,36 @@ def _run(cmd):
     subprocess.run(cmd, check=True)
 
 
-def build(force: bool = False, verbose: bool = True) -> dict:
+def _objects():
+    """(object, source, extra flags) of libmpcx.so: one k_modexp geometry per
+    object (compiled in parallel: the unrolled Montgomery loops make each
+    geometry ~30-60 s of hipcc), the prime kernels, and the C-ABI host code."""
+    objdir = os.path.join(HERE, "build")
+    objs = [(os.path.join(objdir, f"mpcx_geom{g}.o"), "mpcx_geom.hip", [f"-DMPCX_GEOM_ID={g}"])
+            for g in range(NUM_GEOMS)]
+    objs.append((os.path.join(objdir, "mpcx_prime.o"), "mpcx_prime.hip", []))
+    objs.append((os.path.join(objdir, "mpcx_api.o"), "mpcx_api.cpp", []))
+    return objs
+
+
+def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> dict:
+    from concurrent.futures import ThreadPoolExecutor
     out = {}
     lib = os.path.join(HERE, "libmpcx.so")
-    deps = [os.path.join(CSRC, s) for s in KERNEL_SRCS] + [
-        os.path.join(CSRC, "mpcx_internal.h"), os.path.join(ROOT, "include", "mpcx.h")]
-    if force or _newer(lib, deps):
-        _run([HIPCC, f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-shared",
-              "-Wall", "-Wno-unused-result", "-fvisibility=default",
-              "-I", os.path.join(ROOT, "include"), "-o", lib] + [os.path.join(CSRC, s) for s in KERNEL_SRCS])
+    common = [os.path.join(CSRC, h) for h in KERNEL_HDRS] + [os.path.join(ROOT, "include", "mpcx.h")]
+    objs = _objects()
+    os.makedirs(os.path.join(HERE, "build"), exist_ok=True)
+    todo = [(o, s, f) for o, s, f in objs if force or _newer(o, [os.path.join(CSRC, s)] + common)]
+    if todo:
+        def one(item):
+            o, src, flags = item
+            _run([HIPCC, f"--offload-arch={ARCH}"] + HIP_FLAGS + flags +
+                 ["-I", os.path.join(ROOT, "include"), "-c", "-o", o, os.path.join(CSRC, src)])
+        n = jobs or min(len(todo), max(1, (os.cpu_count() or 2)), 16)
+        with ThreadPoolExecutor(n) as ex:
+            list(ex.map(one, todo))
+    if force or todo or _newer(lib, [o for o, _, _ in objs]):
+        _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", lib] + [o for o, _, _ in objs])
     out["libmpcx"] = lib
     host_srcs = [os.path.join(CSRC, s) for s in HOST_SRCS if os.path.exists(os.path.join(CSRC, s))]
     if host_srcs:

@@ -20,9 +20,14 @@
 #include "../../include/mpcx.h"
 #include "mpcx_internal.h"
 
+// per-geometry kernels (mpcx_geom.hip, one translation unit per geometry id)
+#define MPCX_GEOM_DECL(g)                                                                          \
+  hipError_t mpcx_launch_modexp_g##g(const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st); \
+  hipError_t mpcx_modexp_occupancy_g##g(int* blocks_per_cu);
+#define MPCX_FOR_EACH_GEOM(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6)
+static_assert(MPCX_NUM_GEOMS == 7, "update MPCX_FOR_EACH_GEOM and build.py GEOMS");
 extern "C" {
-hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st);
-hipError_t mpcx_modexp_occupancy(int geom, int* blocks_per_cu);
+MPCX_FOR_EACH_GEOM(MPCX_GEOM_DECL)
 hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
@@ -32,9 +37,9 @@ struct mpcx_modulus_s {
   int cls;
   uint32_t bits;
   uint32_t words;  // normalized length of m in 32-bit words
-  uint32_t L;
   uint32_t n0inv;
-  uint32_t* d_const;  // 3*L digits: N, R mod N, R^2 mod N
+  uint32_t* d_const;  // per geometry of the class: 3*L_g digits N, R mod N, R^2 mod N
+  uint32_t const_off[MPCX_NUM_GEOMS];  // digit offset of geometry g's block (class members only)
   std::vector<uint32_t> m;
 };
 
@@ -50,6 +55,7 @@ int g_num_cus = 0;
 int g_geom_slots[MPCX_NUM_GEOMS] = {0};  // resident wavefronts per device, per geometry
 bool g_split = false;                    // narrow-geometry tail launch (measured slower: off)
 int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): one geometry for everything
+int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 uint32_t* g_ws = nullptr;  // exponentiation table workspace
 size_t g_ws_bytes = 0;
 struct Staging {
@@ -136,6 +142,30 @@ std::vector<uint32_t> to_digits(const std::vector<uint32_t>& w, uint32_t L) {
   return d;
 }
 
+hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st) {
+  switch (geom) {
+#define MPCX_CASE(g) \
+  case g:            \
+    return mpcx_launch_modexp_g##g(a, waves, st);
+    MPCX_FOR_EACH_GEOM(MPCX_CASE)
+#undef MPCX_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+hipError_t mpcx_modexp_occupancy(int geom, int* blocks_per_cu) {
+  switch (geom) {
+#define MPCX_CASE(g) \
+  case g:            \
+    return mpcx_modexp_occupancy_g##g(blocks_per_cu);
+    MPCX_FOR_EACH_GEOM(MPCX_CASE)
+#undef MPCX_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
 int ensure_device() {
   if (g_device < 0) return fail(MPCX_ENODEV, "mpcx_init() has not been called");
   return MPCX_OK;
@@ -200,6 +230,10 @@ int mpcx_set_option(const char* key, int value) {
   } else if (std::strcmp(key, "force_geom") == 0) {
     if (value < -1 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "force_geom %d out of range", value);
     g_force_geom = value;
+  } else if (std::strcmp(key, "main_geom") == 0) {
+    // main (throughput) geometry of the geometry's class
+    if (value < 0 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "main_geom %d out of range", value);
+    g_main_geom[MPCX_GEOM_CLASS(value)] = value;
   } else {
     return fail(MPCX_EINVAL, "unknown option %s", key);
   }
@@ -273,23 +307,27 @@ int mpcx_modulus_register(const uint32_t* m_words, uint32_t m_len, mpcx_mod_t* o
   if ((m[0] & 1u) == 0) return fail(MPCX_EINVAL, "modulus is even (math/big uses a non-Montgomery path; keep it on the host)");
   const int cls = class_for_bits(bits);
   if (cls < 0) return fail(MPCX_EINVAL, "modulus has %u bits > %d", bits, MPCX_MAX_MODULUS_BITS);
-  const uint32_t L = (uint32_t)MPCX_CLASS_L(cls);
   auto* mod = new mpcx_modulus_s();
   mod->cls = cls;
   mod->bits = bits;
   mod->words = (uint32_t)m.size();
-  mod->L = L;
   mod->m = m;
   uint32_t inv = m[0];
   for (int i = 0; i < 5; ++i) inv *= 2u - m[0] * inv;
   mod->n0inv = (0u - inv) & kM28;
-  std::vector<uint32_t> host(3 * L);
-  auto nd = to_digits(m, L);
-  auto r1 = to_digits(pow2_mod(kDigitBits * L, m), L);
-  auto r2 = to_digits(pow2_mod(2 * kDigitBits * L, m), L);
-  std::copy(nd.begin(), nd.end(), host.begin());
-  std::copy(r1.begin(), r1.end(), host.begin() + L);
-  std::copy(r2.begin(), r2.end(), host.begin() + 2 * L);
+  std::vector<uint32_t> host;
+  for (int g = 0; g < MPCX_NUM_GEOMS; ++g) {
+    mod->const_off[g] = 0;
+    if (MPCX_GEOM_CLASS(g) != cls) continue;
+    const uint32_t L = (uint32_t)MPCX_GEOM_L(g);
+    mod->const_off[g] = (uint32_t)host.size();
+    auto nd = to_digits(m, L);
+    auto r1 = to_digits(pow2_mod(kDigitBits * L, m), L);
+    auto r2 = to_digits(pow2_mod(2 * kDigitBits * L, m), L);
+    host.insert(host.end(), nd.begin(), nd.end());
+    host.insert(host.end(), r1.begin(), r1.end());
+    host.insert(host.end(), r2.begin(), r2.end());
+  }
   hipError_t e = hipMalloc((void**)&mod->d_const, host.size() * sizeof(uint32_t));
   if (e != hipSuccess) {
     delete mod;
@@ -322,10 +360,11 @@ int mpcx_modulus_info(mpcx_mod_t mod, uint32_t* out_bits, uint32_t* out_class_wo
 
 int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K, uint32_t* G) {
   if (!mod) return fail(MPCX_EINVAL, "null modulus");
-  if (L) *L = (uint32_t)MPCX_CLASS_L(mod->cls);
-  if (P) *P = (uint32_t)MPCX_CLASS_P(mod->cls);
-  if (K) *K = (uint32_t)MPCX_CLASS_K(mod->cls);
-  if (G) *G = (uint32_t)MPCX_CLASS_G(mod->cls);
+  const int g = g_main_geom[mod->cls];
+  if (L) *L = (uint32_t)MPCX_GEOM_L(g);
+  if (P) *P = (uint32_t)MPCX_GEOM_P(g);
+  if (K) *K = (uint32_t)MPCX_GEOM_K(g);
+  if (G) *G = (uint32_t)MPCX_GEOM_G(g);
   return MPCX_OK;
 }
 
@@ -349,8 +388,8 @@ static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* 
     uint32_t first, count;
   } parts[2];
   int nparts = 0;
-  const int gm = mod->cls, gn = MPCX_NARROW_GEOM(mod->cls);
-  if (g_force_geom >= 0 && (g_force_geom == gm || g_force_geom == gn)) {
+  const int gm = g_main_geom[mod->cls], gn = MPCX_NARROW_GEOM(mod->cls);
+  if (g_force_geom >= 0 && MPCX_GEOM_CLASS(g_force_geom) == mod->cls) {
     parts[nparts++] = {g_force_geom, 0, count};
   } else {
     const uint32_t G = (uint32_t)MPCX_GEOM_G(gm);
@@ -384,9 +423,10 @@ static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* 
     const uint32_t G = (uint32_t)MPCX_GEOM_G(pt.geom), K = (uint32_t)MPCX_GEOM_K(pt.geom);
     const uint32_t waves = (pt.count + G - 1) / G;
     mpcx::ModexpArgs a{};
-    a.nd = mod->d_const;
-    a.r1d = mod->d_const + mod->L;
-    a.r2d = mod->d_const + 2 * mod->L;
+    const uint32_t L = (uint32_t)MPCX_GEOM_L(pt.geom);
+    a.nd = mod->d_const + mod->const_off[pt.geom];
+    a.r1d = a.nd + L;
+    a.r2d = a.nd + 2 * L;
     a.base = d_bases + (size_t)pt.first * base_words;
     a.exps = exp_shared ? d_exps : (d_exps ? d_exps + (size_t)pt.first * exp_words : nullptr);
     a.mul = d_muls ? d_muls + (size_t)pt.first * mul_words : nullptr;

@@ -1,4 +1,6 @@
-// mpcx_kernels.hip -- gfx950 (MI355X, CDNA4) batched modular exponentiation.
+// mpcx_device.hpp -- gfx950 (MI355X, CDNA4) batched modular exponentiation:
+// device code shared by the per-geometry translation units (mpcx_geom.hip)
+// and the primality kernels (mpcx_prime.hip).
 //
 // Replaces the arithmetic of Go math/big (*Int).Exp -> nat.expNNMontgomery
 // (go1.23.5, go:src/math/big/nat.go) as reached through tss-lib v2.0.2
@@ -27,6 +29,7 @@
 //    a global workspace, lane-coalesced layout); b operands are staged in LDS
 //    and read as group-broadcast ds_read_b32.
 //  * MFMA is not used: this is not a dense contraction.
+#pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -42,16 +45,6 @@
 #endif
 #ifndef MPCX_PREFETCH_B
 #define MPCX_PREFETCH_B 1
-#endif
-// occupancy targets (waves per SIMD) -> register budgets 256 / 256 / 168
-#ifndef MPCX_WAVES_PER_EU_C0
-#define MPCX_WAVES_PER_EU_C0 2
-#endif
-#ifndef MPCX_WAVES_PER_EU_C1
-#define MPCX_WAVES_PER_EU_C1 2
-#endif
-#ifndef MPCX_WAVES_PER_EU_C2
-#define MPCX_WAVES_PER_EU_C2 3
 #endif
 #ifndef MPCX_WAVES_PER_EU_FERMAT
 #define MPCX_WAVES_PER_EU_FERMAT 1
@@ -83,6 +76,21 @@ __device__ __forceinline__ uint32_t from_next_lane(uint32_t v) {
 // lane l receives lane l-1's value; lane 0 receives 0 (DPP wave_shr:1).
 __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x138, 0xF, 0xF, true);
+}
+
+// Broadcast lane 0 of each P-lane operand group to the whole group. Quads
+// (P = 4) and pairs (P = 2) use a DPP quad_perm -- a VALU move with a few
+// cycles of latency on the per-iteration serial path; other group widths go
+// through the LDS crossbar (ds_bpermute, ~100+ cycles of latency).
+template <int P>
+__device__ __forceinline__ uint32_t group_bcast(uint32_t v, int src_addr) {
+  if constexpr (P == 4) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);  // quad_perm [0,0,0,0]
+  } else if constexpr (P == 2) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
+  } else {
+    return (uint32_t)__builtin_amdgcn_ds_bpermute(src_addr, (int)v);
+  }
 }
 
 // acc += a * b (32x32 -> 64 plus 64-bit addend): hipcc lowers this to ONE
@@ -173,7 +181,7 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
       // slot 0 first: it feeds m_i, the only serial dependency of the iteration
       ab(std::integral_constant<int, 0>{});
       uint32_t m = ((uint32_t)acc[u] * n0inv) & M28;
-      if constexpr (P > 1) m = (uint32_t)__builtin_amdgcn_ds_bpermute(m_src_addr, (int)m);
+      if constexpr (P > 1) m = group_bcast<P>(m, m_src_addr);
 #if MPCX_PREFETCH_B
       // next digit of b, in flight behind the bpermute and the a*b_i mads
       // (the last read of the last block touches the neighbour row: unused)
@@ -728,83 +736,5 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   if (active) a.ok[op] = pass ? 1 : 0;
 }
 
-// Device self-test of the cross-lane primitives the kernels rely on.
-__global__ void k_selftest(uint32_t* out) {
-  const int lane = threadIdx.x;
-  out[lane] = from_next_lane(1000u + lane);
-  out[64 + lane] = from_prev_lane(1000u + lane);
-  out[128 + lane] = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane / 7) * 7) * 4, (int)(2000 + lane));
-  const uint64_t acc = (uint64_t)(0xFFFFFFF0u + lane) * (0xFFFFFFF7u - lane) + 0xFFFFFFFFFFFFull;
-  out[192 + lane] = (uint32_t)(acc >> 32);
-}
-
 }  // namespace mpcx
 
-// ------------------------------------------------------------ launchers
-#ifndef MPCX_WAVES_PER_EU_G3
-#define MPCX_WAVES_PER_EU_G3 8
-#endif
-#ifndef MPCX_WAVES_PER_EU_G4
-#define MPCX_WAVES_PER_EU_G4 8
-#endif
-#define MPCX_WPE(g)                                                                                       \
-  ((g) == 0 ? MPCX_WAVES_PER_EU_C0                                                                        \
-            : (g) == 1 ? MPCX_WAVES_PER_EU_C1                                                             \
-                       : (g) == 2 ? MPCX_WAVES_PER_EU_C2 : (g) == 3 ? MPCX_WAVES_PER_EU_G3 : MPCX_WAVES_PER_EU_G4)
-#define MPCX_KERNEL(g) mpcx::k_modexp<MPCX_GEOM_P(g), MPCX_GEOM_K(g), MPCX_GEOM_G(g), MPCX_WPE(g)>
-
-extern "C" {
-
-__attribute__((visibility("hidden"))) hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t waves,
-                                                                   hipStream_t st) {
-  switch (geom) {
-#define MPCX_CASE(G)                                                                 \
-  case G:                                                                            \
-    hipLaunchKernelGGL((MPCX_KERNEL(G)), dim3(waves), dim3(64), 0, st, *a);          \
-    return hipGetLastError();
-    MPCX_CASE(0)
-    MPCX_CASE(1)
-    MPCX_CASE(2)
-    MPCX_CASE(3)
-    MPCX_CASE(4)
-#undef MPCX_CASE
-    default:
-      return hipErrorInvalidValue;
-  }
-}
-
-// resident 64-thread blocks (= wavefronts) per CU for a geometry's kernel
-__attribute__((visibility("hidden"))) hipError_t mpcx_modexp_occupancy(int geom, int* blocks_per_cu) {
-  switch (geom) {
-#define MPCX_CASE(G) \
-  case G:            \
-    return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, MPCX_KERNEL(G), 64, 0);
-    MPCX_CASE(0)
-    MPCX_CASE(1)
-    MPCX_CASE(2)
-    MPCX_CASE(3)
-    MPCX_CASE(4)
-#undef MPCX_CASE
-    default:
-      return hipErrorInvalidValue;
-  }
-}
-
-__attribute__((visibility("hidden"))) hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks,
-                                                                    hipStream_t st) {
-  hipLaunchKernelGGL((mpcx::k_fermat2<MPCX_CLASS_K(0), MPCX_WAVES_PER_EU_FERMAT>), dim3(blocks), dim3(64), 0, st, *a);
-  return hipGetLastError();
-}
-
-__attribute__((visibility("hidden"))) hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks,
-                                                               hipStream_t st) {
-  hipLaunchKernelGGL((mpcx::k_mr<MPCX_CLASS_K(0), MPCX_WAVES_PER_EU_MR>), dim3(blocks), dim3(64), 0, st, *a);
-  return hipGetLastError();
-}
-
-__attribute__((visibility("hidden"))) hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st) {
-  hipLaunchKernelGGL(mpcx::k_selftest, dim3(1), dim3(64), 0, st, d_out);
-  return hipGetLastError();
-}
-
-}  // extern "C"

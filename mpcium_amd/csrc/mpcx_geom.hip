@@ -1,0 +1,44 @@
+// mpcx_geom.hip -- one k_modexp geometry per translation unit (compiled once
+// per geometry id with -DMPCX_GEOM_ID=g, in parallel, by mpcium_amd/build.py).
+#include "mpcx_device.hpp"
+
+#ifndef MPCX_GEOM_ID
+#error "compile with -DMPCX_GEOM_ID=<geometry id>"
+#endif
+
+// waves per SIMD each geometry's kernel is compiled for (register budget)
+#ifndef MPCX_WPE
+#if MPCX_GEOM_ID == 0
+#define MPCX_WPE 2
+#elif MPCX_GEOM_ID == 1
+#define MPCX_WPE 3
+#elif MPCX_GEOM_ID == 2
+#define MPCX_WPE 2
+#elif MPCX_GEOM_ID == 3 || MPCX_GEOM_ID == 4
+#define MPCX_WPE 8
+#elif MPCX_GEOM_ID == 5
+#define MPCX_WPE 2
+#else
+#define MPCX_WPE 3
+#endif
+#endif
+
+#define MPCX_CAT2(a, b) a##b
+#define MPCX_CAT(a, b) MPCX_CAT2(a, b)
+#define MPCX_THIS_KERNEL \
+  mpcx::k_modexp<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID), MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>
+
+extern "C" {
+
+__attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_g, MPCX_GEOM_ID)(
+    const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st) {
+  hipLaunchKernelGGL((MPCX_THIS_KERNEL), dim3(waves), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
+// resident 64-thread blocks (= wavefronts) per CU
+__attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_modexp_occupancy_g, MPCX_GEOM_ID)(int* blocks_per_cu) {
+  return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, MPCX_THIS_KERNEL, 64, 0);
+}
+
+}  // extern "C"

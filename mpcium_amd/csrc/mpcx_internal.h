@@ -5,47 +5,38 @@
 
 #include <stdint.h>
 
-// A class serves odd moduli m with R = 2^(28L) > 4m and bases that fit in
-// floor(28L/32) words:
-//   P: lanes per operand, K: radix-2^28 digits per lane, G: operands per
-//   64-lane wavefront (G*P <= 64), L = P*K digits.
+// A class serves odd moduli m of up to MPCX_CLASS_MAXBITS(c) bits; bases fit
+// in MPCX_CLASS_WORDS(c) words. Each class is served by kernel geometries
+// (P lanes per operand, K radix-2^28 digits per lane, G operands per 64-lane
+// wavefront, L = P*K digits); every geometry of a class has R = 2^(28L) > 4m
+// for the class's largest modulus, and its own Montgomery constants (R mod m,
+// R^2 mod m depend on L), uploaded at registration.
 #define MPCX_NUM_CLASSES 3
-// class 0: moduli up to 1024 bits (1024-bit safe-prime candidates p)
-#define MPCX_C0_P 1
-#define MPCX_C0_K 37
-#define MPCX_C0_G 64
-// class 1: moduli up to 2080 bits (Paillier N, N~)
-#define MPCX_C1_P 3
-#define MPCX_C1_K 25
-#define MPCX_C1_G 21
-// class 2: moduli up to 4096 bits (Paillier N^2)
-#define MPCX_C2_P 7
-#define MPCX_C2_K 21
-#define MPCX_C2_G 9
-
-#define MPCX_CLASS_P(c) ((c) == 0 ? MPCX_C0_P : (c) == 1 ? MPCX_C1_P : MPCX_C2_P)
-#define MPCX_CLASS_K(c) ((c) == 0 ? MPCX_C0_K : (c) == 1 ? MPCX_C1_K : MPCX_C2_K)
-#define MPCX_CLASS_G(c) ((c) == 0 ? MPCX_C0_G : (c) == 1 ? MPCX_C1_G : MPCX_C2_G)
-#define MPCX_CLASS_L(c) (MPCX_CLASS_P(c) * MPCX_CLASS_K(c))
-// Kernel geometries. Geometry c < MPCX_NUM_CLASSES is class c's main
-// (throughput) geometry; the "narrow" ones split the same L digits over more
-// lanes (fewer digits per lane -> ~3x shorter wavefronts) and serve the last
-// partial round of a batch and small, latency-bound batches.
-#define MPCX_NUM_GEOMS 5
-#define MPCX_G3_P 15  // class 1 narrow: 15 x 5 = 75 digits, 4 operands per wave
-#define MPCX_G3_K 5
-#define MPCX_G3_G 4
-#define MPCX_G4_P 21  // class 2 narrow: 21 x 7 = 147 digits, 3 operands per wave
-#define MPCX_G4_K 7
-#define MPCX_G4_G 3
-#define MPCX_GEOM_P(g) ((g) < 3 ? MPCX_CLASS_P(g) : (g) == 3 ? MPCX_G3_P : MPCX_G4_P)
-#define MPCX_GEOM_K(g) ((g) < 3 ? MPCX_CLASS_K(g) : (g) == 3 ? MPCX_G3_K : MPCX_G4_K)
-#define MPCX_GEOM_G(g) ((g) < 3 ? MPCX_CLASS_G(g) : (g) == 3 ? MPCX_G3_G : MPCX_G4_G)
-#define MPCX_NARROW_GEOM(c) ((c) == 1 ? 3 : (c) == 2 ? 4 : -1)
-
+// class L_min: the smallest digit count of the class's geometries
+#define MPCX_CLASS_LMIN(c) ((c) == 0 ? 37 : (c) == 1 ? 75 : 147)
 // operand width in 32-bit words (bases and moduli)
-#define MPCX_CLASS_WORDS(c) ((28 * MPCX_CLASS_L(c)) / 32)
+#define MPCX_CLASS_WORDS(c) ((28 * MPCX_CLASS_LMIN(c)) / 32)
 #define MPCX_CLASS_MAXBITS(c) (32 * MPCX_CLASS_WORDS(c))
+
+// Geometries (id: P x K, G, class):
+//   0: 1 x 37, 64, class 0  thread per operand (1024-bit safe-prime candidates)
+//   1: 4 x 19, 16, class 1  quad per operand: m_i broadcast by DPP quad_perm (N, N~)
+//   2: 4 x 37, 16, class 2  quad per operand (Paillier N^2)
+//   3: 15 x 5,  4, class 1  narrow: small latency-bound batches
+//   4: 21 x 7,  3, class 2  narrow
+//   5: 3 x 25, 21, class 1  7-lane/3-lane groups, m_i by ds_bpermute (round-1 main)
+//   6: 7 x 21,  9, class 2  (round-1 main)
+#define MPCX_NUM_GEOMS 7
+#define MPCX_GEOM_P(g) ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 15 : (g) == 4 ? 21 : (g) == 5 ? 3 : 7)
+#define MPCX_GEOM_K(g) ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 7 : (g) == 5 ? 25 : 21)
+#define MPCX_GEOM_G(g) ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 3 : (g) == 5 ? 21 : 9)
+#define MPCX_GEOM_CLASS(g) ((g) == 0 ? 0 : ((g) == 1 || (g) == 3 || (g) == 5) ? 1 : 2)
+#define MPCX_GEOM_L(g) (MPCX_GEOM_P(g) * MPCX_GEOM_K(g))
+// default main (throughput) and narrow geometry of each class
+#define MPCX_MAIN_GEOM(c) ((c) == 0 ? 0 : (c) == 1 ? 1 : 2)
+#define MPCX_NARROW_GEOM(c) ((c) == 1 ? 3 : (c) == 2 ? 4 : -1)
+// 1024-bit class used by the Fermat / Miller-Rabin kernels (thread per operand)
+#define MPCX_C0_K 37
 
 // table entries per wavefront in the workspace: powers p_0..p_15 + the
 // Montgomery form of the optional multiplier (entry 16)

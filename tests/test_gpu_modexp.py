@@ -121,11 +121,12 @@ def test_exp_mul_and_mulmod(gpu, paillier_key):
         mod.release()
 
 
-@pytest.mark.parametrize("geom", [1, 2, 3, 4])
+@pytest.mark.parametrize("geom", [1, 2, 3, 4, 5, 6])
 def test_each_geometry_forced(gpu, paillier_key, geom):
-    """Main (1, 2) and narrow (3, 4) geometries of the 2048/4096-bit classes."""
+    """Every geometry of the 2048-bit (1, 3, 5) and 4096-bit (2, 4, 6) classes:
+    quad-per-operand main, narrow, and the 3/7-lane-group (bpermute) layouts."""
     N = paillier_key["N"]
-    m = N * N if geom in (2, 4) else N
+    m = N * N if geom in (2, 4, 6) else N
     rng = random.Random(geom)
     gpu.set_option("force_geom", geom)
     try:
