@@ -16,6 +16,9 @@
  *   mpcxh_safe_primes            up:common/safe_prime.go GetRandomSafePrimesConcurrent
  *   mpcxh_generate_preparams     up:ecdsa/keygen/prepare.go GeneratePreParams,
  *                                called at /root/reference/pkg/mpc/node.go:69
+ *   mpcxh_mta_*_batch            up:crypto/mta/{share_protocol,range_proof,proofs}.go
+ *                                (AliceInit, BobMid[WC], AliceEnd[WC], the
+ *                                 range / Bob proofs and their Verify)
  */
 #ifndef MPCX_HOST_H_
 #define MPCX_HOST_H_
@@ -74,6 +77,73 @@ int mpcxh_safe_primes(int bit_len, int num, uint64_t seed, mpcxh_rand_fn rand_fn
  * NTildei, H1i, H2i, Alpha, Beta, P, Q (Germain primes of N~). */
 int mpcxh_generate_preparams(uint64_t seed, mpcxh_rand_fn rand_fn, void* rand_ctx,
                              uint32_t* out, uint64_t* stats_out);
+
+/* ---------------------------------------------------------------- MtA
+ * Batched mirror of tss-lib v2.0.2's MtA / MtAwc (up:crypto/mta/share_protocol.go,
+ * range_proof.go, proofs.go), the Paillier work of GG18 signing that mpcium's
+ * signing sessions (/root/reference/pkg/mpc/ecdsa_signing_session.go:134-147)
+ * run through party.UpdateFromBytes (/root/reference/pkg/mpc/session.go:199).
+ * One call = a batch of independent sessions sharing key material. Every
+ * integer is `w` little-endian 32-bit words (w >= 128: N^2 fits); proofs are
+ * count x fields x w words:
+ *   RangeProofAlice (6 fields): Z, U, W, S, S1, S2
+ *   ProofBob[WC]   (12 fields): Z, ZPrm, T, V, W, S, S1, S2, T1, T2, U.x, U.y
+ *                               (U = 0, 0 for the plain ProofBob)
+ * Points (B, the MtAwc public value) are count x 16 words: x (8), y (8).
+ * Session ids are count x session_len bytes. seeds[i]: session i's io.Reader
+ * (CounterDRBG stream). err[i]: 0 ok, 1 ErrMessageTooLong, 2
+ * ErrMessageMalFormed, 3 proof verification failed. */
+typedef struct {
+  const uint32_t* N;       /* Paillier N */
+  const uint32_t* LambdaN; /* private-key fields: NULL for a peer's public key */
+  const uint32_t* P;
+  const uint32_t* Q;
+} mpcxh_paillier_t;
+
+typedef struct {
+  const uint32_t* NTilde;
+  const uint32_t* h1;
+  const uint32_t* h2;
+  const uint32_t* P; /* safe-prime factors of NTilde when the caller owns it, else NULL */
+  const uint32_t* Q;
+} mpcxh_dln_t;
+
+#define MPCXH_RANGE_PROOF_FIELDS 6
+#define MPCXH_PROOF_BOB_FIELDS 12
+
+/* mta.AliceInit(ec, pkA, a, NTildeB, h1B, h2B, rand) -> cA, RangeProofAlice */
+int mpcxh_mta_alice_init_batch(uint32_t w, const mpcxh_paillier_t* pkA, const mpcxh_dln_t* dlnB, uint32_t count,
+                               const uint32_t* a, const uint64_t* seeds, uint32_t* cA, uint32_t* pf, uint8_t* err);
+/* (*RangeProofAlice).Verify(ec, pk, NTilde, h1, h2, c) */
+int mpcxh_mta_verify_range_alice_batch(uint32_t w, const mpcxh_paillier_t* pk, const mpcxh_dln_t* dln,
+                                       uint32_t count, const uint32_t* c, const uint32_t* pf, uint8_t* ok);
+/* mta.BobMid (B == NULL) / BobMidWC(Session, ec, pkA, pf, b, cA, NTildeA, h1A, h2A,
+ * NTildeB, h1B, h2B[, B], rand) -> beta, cB, betaPrm, ProofBob[WC] */
+int mpcxh_mta_bob_mid_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* pkA,
+                            const mpcxh_dln_t* dlnA, const mpcxh_dln_t* dlnB, uint32_t count, const uint32_t* pfA,
+                            const uint32_t* b, const uint32_t* cA, const uint32_t* B, const uint64_t* seeds,
+                            uint32_t* beta, uint32_t* cB, uint32_t* betaPrm, uint32_t* pfB, uint8_t* err);
+/* (*ProofBob).Verify / (*ProofBobWC).Verify(Session, ec, pk, NTilde, h1, h2, c1, c2[, X]) */
+int mpcxh_mta_verify_bob_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* pk,
+                               const mpcxh_dln_t* dln, uint32_t count, const uint32_t* c1, const uint32_t* c2,
+                               const uint32_t* pfB, const uint32_t* X, uint8_t* ok);
+/* mta.AliceEnd (B == NULL) / AliceEndWC(Session, ec, pkA, pf, h1A, h2A, cA, cB, NTildeA[, B], sk) -> alpha */
+int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* skA,
+                              const mpcxh_dln_t* dlnA, uint32_t count, const uint32_t* pfB, const uint32_t* cA,
+                              const uint32_t* cB, const uint32_t* B, uint32_t* alpha, uint8_t* err);
+
+/* Host-side helpers of the MtA path, exported as test hooks (no GPU needed):
+ * common.SHA512_256i / SHA512_256i_TAGGED (tag == NULL: untagged) over count
+ * integers of w words -> 32-byte digest; secp256k1 k*G and k*P (k: w words,
+ * points 16 words x|y, all-zero = infinity); the first `count` draws of
+ * common.GetRandomPositiveInt(rand, lessThan) (relprime != 0:
+ * GetRandomPositiveRelativelyPrimeInt) from the CounterDRBG `seed`. */
+int mpcxh_sha512_256i(const uint8_t* tag, size_t tag_len, uint32_t count, const uint32_t* ints, uint32_t w,
+                      uint8_t* digest32);
+int mpcxh_secp_scalar_base_mult(const uint32_t* k, uint32_t w, uint32_t* out16);
+int mpcxh_secp_scalar_mult(const uint32_t* p16, const uint32_t* k, uint32_t w, uint32_t* out16);
+int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int relprime, uint32_t count,
+                       uint32_t* out);
 
 /* tss-lib candidate q from raw stream bytes (masking + delta walk; test hook). */
 int mpcxh_candidate_from_bytes(const uint8_t* bytes, size_t n, int q_bit_len, uint32_t* q_out, uint32_t words);

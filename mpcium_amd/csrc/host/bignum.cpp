@@ -308,3 +308,85 @@ bool mod_inverse(const Int& g, const Nat& n, Nat* out) {
 }
 
 }  // namespace mpcx::host
+
+namespace mpcx::host {
+namespace {
+
+using V64 = std::vector<uint64_t>;
+
+V64 to64(const Nat& a) {
+  const auto& w = a.limbs();
+  V64 r((w.size() + 1) / 2, 0);
+  for (size_t i = 0; i < w.size(); ++i) r[i / 2] |= (uint64_t)w[i] << (32 * (i % 2));
+  while (!r.empty() && r.back() == 0) r.pop_back();
+  return r;
+}
+
+int cmp64(const V64& a, const V64& b) {
+  if (a.size() != b.size()) return a.size() < b.size() ? -1 : 1;
+  for (size_t i = a.size(); i-- > 0;)
+    if (a[i] != b[i]) return a[i] < b[i] ? -1 : 1;
+  return 0;
+}
+
+// a -= b (a > b), then a >>= ctz(a), trimmed
+void sub_shift(V64& a, const V64& b) {
+  unsigned __int128 br = 0;
+  for (size_t i = 0; i < a.size(); ++i) {
+    const unsigned __int128 d = (unsigned __int128)a[i] - (i < b.size() ? b[i] : 0) - br;
+    a[i] = (uint64_t)d;
+    br = (d >> 64) & 1;
+  }
+  size_t z = 0;
+  while (z < a.size() && a[z] == 0) ++z;
+  if (z) a.erase(a.begin(), a.begin() + (long)z);
+  const int s = __builtin_ctzll(a[0]);
+  if (s) {
+    for (size_t i = 0; i + 1 < a.size(); ++i) a[i] = (a[i] >> s) | (a[i + 1] << (64 - s));
+    a.back() >>= s;
+  }
+  while (!a.empty() && a.back() == 0) a.pop_back();
+}
+
+}  // namespace
+
+bool coprime_odd(const Nat& x, const Nat& m) {
+  if (m.is_zero() || !m.is_odd()) throw std::invalid_argument("coprime_odd: modulus must be odd");
+  if (m == Nat(1)) return true;
+  const Nat a = x >= m ? x % m : x;
+  if (a.is_zero()) return false;
+  V64 u = to64(a), v = to64(m);
+  {
+    size_t z = 0;
+    while (u[z] == 0) ++z;
+    u.erase(u.begin(), u.begin() + (long)z);
+    const int s = __builtin_ctzll(u[0]);
+    if (s) {
+      for (size_t i = 0; i + 1 < u.size(); ++i) u[i] = (u[i] >> s) | (u[i + 1] << (64 - s));
+      u.back() >>= s;
+    }
+    while (!u.empty() && u.back() == 0) u.pop_back();
+  }
+  // binary GCD of odd u, v (gcd(x, m) = gcd(x / 2^k, m) for odd m)
+  for (;;) {
+    if (u.size() == 1 && v.size() == 1) {
+      uint64_t a64 = u[0], b64 = v[0];
+      while (a64 != b64) {
+        if (a64 > b64) {
+          a64 -= b64;
+          a64 >>= __builtin_ctzll(a64);
+        } else {
+          b64 -= a64;
+          b64 >>= __builtin_ctzll(b64);
+        }
+      }
+      return a64 == 1;
+    }
+    const int c = cmp64(u, v);
+    if (c == 0) return u.size() == 1 && u[0] == 1;
+    if (c > 0) sub_shift(u, v);
+    else sub_shift(v, u);
+  }
+}
+
+}  // namespace mpcx::host

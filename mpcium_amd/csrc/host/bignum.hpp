@@ -55,6 +55,9 @@ class Nat {
 };
 
 Nat gcd(Nat a, Nat b);
+// gcd(x, m) == 1 for odd m > 0 (binary GCD on 64-bit limbs; the validity
+// checks of the MtA proofs and GetRandomPositiveRelativelyPrimeInt)
+bool coprime_odd(const Nat& x, const Nat& m);
 
 // Signed integer (sign-magnitude like Go's big.Int; zero is never negative).
 struct Int {

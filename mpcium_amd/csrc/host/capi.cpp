@@ -12,6 +12,7 @@
 #include "engine.hpp"
 #include "modint.hpp"
 #include "paillier.hpp"
+#include "mta.hpp"
 #include "safeprime.hpp"
 
 using namespace mpcx::host;
@@ -52,6 +53,109 @@ RandFn rand_from(uint64_t seed, mpcxh_rand_fn fn, void* ctx, CounterDRBG* drbg) 
   if (fn) return [fn, ctx](uint8_t* b, size_t n) { fn(ctx, b, n); };
   *drbg = CounterDRBG(seed);
   return drbg->fn();
+}
+Nat nat_or0(const uint32_t* p, uint32_t w) { return p ? Nat::from_words(p, w) : Nat(); }
+
+paillier::PrivateKey paillier_from(const mpcxh_paillier_t* k, uint32_t w) {
+  if (!k || !k->N) throw std::invalid_argument("null Paillier key");
+  paillier::PrivateKey sk;
+  sk.pub.N = Nat::from_words(k->N, w);
+  sk.LambdaN = nat_or0(k->LambdaN, w);
+  sk.P = nat_or0(k->P, w);
+  sk.Q = nat_or0(k->Q, w);
+  if (!sk.P.is_zero() && !sk.Q.is_zero()) sk.PhiN = (sk.P - Nat(1)) * (sk.Q - Nat(1));
+  return sk;
+}
+
+mta::DLNParams dln_from(const mpcxh_dln_t* d, uint32_t w) {
+  if (!d || !d->NTilde || !d->h1 || !d->h2) throw std::invalid_argument("null DLN parameters");
+  mta::DLNParams p;
+  p.NTilde = Nat::from_words(d->NTilde, w);
+  p.h1 = Nat::from_words(d->h1, w);
+  p.h2 = Nat::from_words(d->h2, w);
+  p.P = nat_or0(d->P, w);
+  p.Q = nat_or0(d->Q, w);
+  return p;
+}
+
+void check_width(uint32_t w) {
+  if (w < 128) throw std::invalid_argument("MtA integer width must be >= 128 words (N^2)");
+}
+
+std::vector<RandFn> readers(const uint64_t* seeds, uint32_t count, std::vector<CounterDRBG>* drbgs) {
+  if (!seeds) throw std::invalid_argument("null seeds");
+  drbgs->clear();
+  drbgs->reserve(count);
+  std::vector<RandFn> r;
+  r.reserve(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    drbgs->emplace_back(seeds[i]);
+    r.push_back(drbgs->back().fn());
+  }
+  return r;
+}
+
+std::vector<mta::Bytes> sessions_from(const uint8_t* s, uint32_t len, uint32_t count) {
+  std::vector<mta::Bytes> v(count);
+  for (uint32_t i = 0; i < count; ++i) v[i].assign(s + (size_t)i * len, s + (size_t)(i + 1) * len);
+  return v;
+}
+
+std::vector<secp::Affine> points_from(const uint32_t* p, uint32_t count) {
+  std::vector<secp::Affine> v(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    v[i].x = secp::NatToFe(Nat::from_words(p + (size_t)i * 16, 8));
+    v[i].y = secp::NatToFe(Nat::from_words(p + (size_t)i * 16 + 8, 8));
+    v[i].inf = false;
+  }
+  return v;
+}
+
+void put(const Nat& v, uint32_t* out, uint32_t w) { v.to_words(out, w); }
+
+std::vector<mta::RangeProofAlice> range_from(const uint32_t* p, uint32_t count, uint32_t w) {
+  std::vector<mta::RangeProofAlice> v(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    const uint32_t* b = p + (size_t)i * MPCXH_RANGE_PROOF_FIELDS * w;
+    Nat* f[] = {&v[i].Z, &v[i].U, &v[i].W, &v[i].S, &v[i].S1, &v[i].S2};
+    for (int k = 0; k < MPCXH_RANGE_PROOF_FIELDS; ++k) *f[k] = Nat::from_words(b + (size_t)k * w, w);
+  }
+  return v;
+}
+
+void range_to(const std::vector<mta::RangeProofAlice>& v, uint32_t* p, uint32_t w) {
+  for (size_t i = 0; i < v.size(); ++i) {
+    uint32_t* b = p + i * MPCXH_RANGE_PROOF_FIELDS * w;
+    const Nat* f[] = {&v[i].Z, &v[i].U, &v[i].W, &v[i].S, &v[i].S1, &v[i].S2};
+    for (int k = 0; k < MPCXH_RANGE_PROOF_FIELDS; ++k) put(*f[k], b + (size_t)k * w, w);
+  }
+}
+
+std::vector<mta::ProofBob> bob_from(const uint32_t* p, uint32_t count, uint32_t w, bool wc) {
+  std::vector<mta::ProofBob> v(count);
+  for (uint32_t i = 0; i < count; ++i) {
+    const uint32_t* b = p + (size_t)i * MPCXH_PROOF_BOB_FIELDS * w;
+    Nat* f[] = {&v[i].Z, &v[i].ZPrm, &v[i].T, &v[i].V, &v[i].W, &v[i].S, &v[i].S1, &v[i].S2, &v[i].T1, &v[i].T2};
+    for (int k = 0; k < 10; ++k) *f[k] = Nat::from_words(b + (size_t)k * w, w);
+    if (wc) {
+      const Nat ux = Nat::from_words(b + (size_t)10 * w, w), uy = Nat::from_words(b + (size_t)11 * w, w);
+      v[i].U.x = secp::NatToFe(ux);
+      v[i].U.y = secp::NatToFe(uy);
+      v[i].U.inf = ux.bit_len() > 256 || uy.bit_len() > 256;  // off the field: fails IsOnCurve
+      if (v[i].U.inf) v[i].U.x = v[i].U.y = secp::Fe{};
+    }
+  }
+  return v;
+}
+
+void bob_to(const std::vector<mta::ProofBob>& v, uint32_t* p, uint32_t w) {
+  for (size_t i = 0; i < v.size(); ++i) {
+    uint32_t* b = p + i * MPCXH_PROOF_BOB_FIELDS * w;
+    const Nat* f[] = {&v[i].Z, &v[i].ZPrm, &v[i].T, &v[i].V, &v[i].W, &v[i].S, &v[i].S1, &v[i].S2, &v[i].T1, &v[i].T2};
+    for (int k = 0; k < 10; ++k) put(*f[k], b + (size_t)k * w, w);
+    put(v[i].U.inf ? Nat() : secp::FeToNat(v[i].U.x), b + (size_t)10 * w, w);
+    put(v[i].U.inf ? Nat() : secp::FeToNat(v[i].U.y), b + (size_t)11 * w, w);
+  }
 }
 }  // namespace
 
@@ -185,6 +289,140 @@ int mpcxh_drbg_read(uint64_t seed, uint8_t* out, size_t n) {
   return guard([&] {
     CounterDRBG d(seed);
     d.read(out, n);
+  });
+}
+
+// ------------------------------------------------------------------ MtA
+int mpcxh_mta_alice_init_batch(uint32_t w, const mpcxh_paillier_t* pkA, const mpcxh_dln_t* dlnB, uint32_t count,
+                               const uint32_t* a, const uint64_t* seeds, uint32_t* cA, uint32_t* pf, uint8_t* err) {
+  return guard([&] {
+    check_width(w);
+    const auto sk = paillier_from(pkA, w);
+    const auto dln = dln_from(dlnB, w);
+    std::vector<CounterDRBG> drbgs;
+    const auto rd = readers(seeds, count, &drbgs);
+    std::vector<Nat> c;
+    std::vector<mta::RangeProofAlice> p;
+    std::vector<uint8_t> e;
+    mta::AliceInitBatch(sk.pub, nats(a, w, count), dln, rd, &c, &p, &e);
+    store(c, cA, w);
+    range_to(p, pf, w);
+    std::memcpy(err, e.data(), count);
+  });
+}
+
+int mpcxh_mta_verify_range_alice_batch(uint32_t w, const mpcxh_paillier_t* pk, const mpcxh_dln_t* dln,
+                                       uint32_t count, const uint32_t* c, const uint32_t* pf, uint8_t* ok) {
+  return guard([&] {
+    check_width(w);
+    const auto sk = paillier_from(pk, w);
+    const auto ok_v = mta::VerifyRangeAliceBatch(sk.pub, dln_from(dln, w), nats(c, w, count), range_from(pf, count, w));
+    std::memcpy(ok, ok_v.data(), count);
+  });
+}
+
+int mpcxh_mta_bob_mid_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* pkA,
+                            const mpcxh_dln_t* dlnA, const mpcxh_dln_t* dlnB, uint32_t count, const uint32_t* pfA,
+                            const uint32_t* b, const uint32_t* cA, const uint32_t* B, const uint64_t* seeds,
+                            uint32_t* beta, uint32_t* cB, uint32_t* betaPrm, uint32_t* pfB, uint8_t* err) {
+  return guard([&] {
+    check_width(w);
+    const auto sk = paillier_from(pkA, w);
+    std::vector<CounterDRBG> drbgs;
+    const auto rd = readers(seeds, count, &drbgs);
+    std::vector<secp::Affine> Bv;
+    if (B) Bv = points_from(B, count);
+    std::vector<mta::BobMidResult> out;
+    std::vector<uint8_t> e;
+    mta::BobMidBatch(sessions_from(sessions, session_len, count), sk.pub, range_from(pfA, count, w), nats(b, w, count),
+                     nats(cA, w, count), dln_from(dlnA, w), dln_from(dlnB, w), B ? &Bv : nullptr, rd, &out, &e);
+    std::vector<mta::ProofBob> pfs(count);
+    for (uint32_t i = 0; i < count; ++i) {
+      put(out[i].beta, beta + (size_t)i * w, w);
+      put(out[i].cB, cB + (size_t)i * w, w);
+      put(out[i].betaPrm, betaPrm + (size_t)i * w, w);
+      pfs[i] = out[i].pf;
+    }
+    bob_to(pfs, pfB, w);
+    std::memcpy(err, e.data(), count);
+  });
+}
+
+int mpcxh_mta_verify_bob_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* pk,
+                               const mpcxh_dln_t* dln, uint32_t count, const uint32_t* c1, const uint32_t* c2,
+                               const uint32_t* pfB, const uint32_t* X, uint8_t* ok) {
+  return guard([&] {
+    check_width(w);
+    const auto sk = paillier_from(pk, w);
+    std::vector<secp::Affine> Xv;
+    if (X) Xv = points_from(X, count);
+    const bool own = !sk.P.is_zero() && !sk.Q.is_zero();
+    const auto ok_v = mta::VerifyBobBatch(sessions_from(sessions, session_len, count), sk.pub, dln_from(dln, w),
+                                          nats(c1, w, count), nats(c2, w, count), bob_from(pfB, count, w, X != nullptr),
+                                          X ? &Xv : nullptr, own ? &sk : nullptr);
+    std::memcpy(ok, ok_v.data(), count);
+  });
+}
+
+int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* skA,
+                              const mpcxh_dln_t* dlnA, uint32_t count, const uint32_t* pfB, const uint32_t* cA,
+                              const uint32_t* cB, const uint32_t* B, uint32_t* alpha, uint8_t* err) {
+  return guard([&] {
+    check_width(w);
+    const auto sk = paillier_from(skA, w);
+    if (sk.LambdaN.is_zero() || sk.P.is_zero() || sk.Q.is_zero())
+      throw std::invalid_argument("AliceEnd needs the private key (LambdaN, P, Q)");
+    std::vector<secp::Affine> Bv;
+    if (B) Bv = points_from(B, count);
+    std::vector<Nat> al;
+    std::vector<uint8_t> e;
+    mta::AliceEndBatch(sessions_from(sessions, session_len, count), sk, bob_from(pfB, count, w, B != nullptr),
+                       dln_from(dlnA, w), nats(cA, w, count), nats(cB, w, count), B ? &Bv : nullptr, &al, &e);
+    store(al, alpha, w);
+    std::memcpy(err, e.data(), count);
+  });
+}
+
+// ------------------------------------------------------------------ test hooks
+int mpcxh_sha512_256i(const uint8_t* tag, size_t tag_len, uint32_t count, const uint32_t* ints, uint32_t w,
+                      uint8_t* digest32) {
+  return guard([&] {
+    const std::vector<Nat> v = nats(ints, w, count);
+    std::vector<const Nat*> ptrs;
+    for (const auto& x : v) ptrs.push_back(&x);
+    const Nat h = tag ? SHA512_256i_TAGGED(std::vector<uint8_t>(tag, tag + tag_len), ptrs) : SHA512_256i(ptrs);
+    std::vector<uint8_t> b = h.to_bytes_be();
+    std::memset(digest32, 0, 32);
+    std::memcpy(digest32 + (32 - b.size()), b.data(), b.size());
+  });
+}
+
+static void point_out(const secp::Affine& p, uint32_t* out16) {
+  std::memset(out16, 0, 16 * sizeof(uint32_t));
+  if (p.inf) return;
+  secp::FeToNat(p.x).to_words(out16, 8);
+  secp::FeToNat(p.y).to_words(out16 + 8, 8);
+}
+
+int mpcxh_secp_scalar_base_mult(const uint32_t* k, uint32_t w, uint32_t* out16) {
+  return guard([&] { point_out(secp::ScalarBaseMult(Nat::from_words(k, w)), out16); });
+}
+
+int mpcxh_secp_scalar_mult(const uint32_t* p16, const uint32_t* k, uint32_t w, uint32_t* out16) {
+  return guard([&] {
+    const auto P = points_from(p16, 1)[0];
+    point_out(secp::ScalarMult(P, Nat::from_words(k, w)), out16);
+  });
+}
+
+int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int relprime, uint32_t count,
+                       uint32_t* out) {
+  return guard([&] {
+    CounterDRBG d(seed);
+    const RandFn r = d.fn();
+    const Nat lt = Nat::from_words(less_than, w);
+    for (uint32_t i = 0; i < count; ++i)
+      (relprime ? GetRandomPositiveRelativelyPrimeInt(r, lt) : GetRandomPositiveInt(r, lt)).to_words(out + (size_t)i * w, w);
   });
 }
 

@@ -1,0 +1,484 @@
+// mta.cpp -- see mta.hpp. Every formula below cites the tss-lib v2.0.2 step it
+// implements (restated in oracle/mta_ref.py and SURVEY.md 8(a) A8-A10).
+#include "mta.hpp"
+
+#include <algorithm>
+#include <map>
+#include <stdexcept>
+
+#include "engine.hpp"
+
+namespace mpcx::host::mta {
+namespace {
+
+// ------------------------------------------------------------------ ExpSet
+// Modexp requests against one modulus, issued as few GPU launches: requests
+// that share one exponent object (y = N, y = lambda) go to a shared-exponent
+// launch; the rest are grouped by exponent length (the kernel processes the
+// group's longest exponent, so lengths within a group differ by <= 1/8).
+// Products base^e * mul run fused (mpcx_modexp_mul_batch).
+class ExpSet {
+ public:
+  explicit ExpSet(const Nat& m) : m_(m) {}
+  void add(const Nat& base, const Nat& e, Nat* out, const Nat* mul = nullptr) {
+    reqs_.push_back({&base, &e, mul, out});
+  }
+  size_t size() const { return reqs_.size(); }
+  void run() {
+    if (reqs_.empty()) return;
+    std::map<const Nat*, std::vector<size_t>> by_e;
+    for (size_t i = 0; i < reqs_.size(); ++i) by_e[reqs_[i].e].push_back(i);
+    std::vector<size_t> rest;
+    for (auto& kv : by_e) {
+      if (kv.second.size() >= 2) {
+        launch(kv.second, true);
+      } else {
+        rest.push_back(kv.second[0]);
+      }
+    }
+    std::sort(rest.begin(), rest.end(),
+              [&](size_t a, size_t b) { return reqs_[a].e->bit_len() < reqs_[b].e->bit_len(); });
+    size_t g0 = 0;
+    while (g0 < rest.size()) {
+      const uint32_t lo = reqs_[rest[g0]].e->bit_len();
+      size_t g1 = g0 + 1;
+      while (g1 < rest.size() && reqs_[rest[g1]].e->bit_len() <= lo + lo / 8 + 32) ++g1;
+      launch(std::vector<size_t>(rest.begin() + (long)g0, rest.begin() + (long)g1), false);
+      g0 = g1;
+    }
+    reqs_.clear();
+  }
+
+ private:
+  struct Req {
+    const Nat* b;
+    const Nat* e;
+    const Nat* mul;
+    Nat* out;
+  };
+  void launch(const std::vector<size_t>& idx, bool shared) {
+    std::vector<Nat> bases, exps, muls;
+    bases.reserve(idx.size());
+    bool any_mul = false;
+    for (size_t i : idx) any_mul |= reqs_[i].mul != nullptr;
+    for (size_t i : idx) {
+      bases.push_back(*reqs_[i].b);
+      if (!shared) exps.push_back(*reqs_[i].e);
+      if (any_mul) muls.push_back(reqs_[i].mul ? *reqs_[i].mul : Nat(1));
+    }
+    if (shared) exps.push_back(*reqs_[idx[0]].e);
+    std::vector<Nat> r = Engine::get().exp(m_, bases, exps, any_mul ? &muls : nullptr);
+    for (size_t j = 0; j < idx.size(); ++j) *reqs_[idx[j]].out = std::move(r[j]);
+  }
+  const Nat m_;  // by value: callers pass temporaries (pk.NSquare())
+  std::vector<Req> reqs_;
+};
+
+const Nat& q3() {
+  static const Nat v = Q() * Q() * Q();
+  return v;
+}
+const Nat& q7() {
+  static const Nat v = q3() * q3() * Q();
+  return v;
+}
+
+// Gamma^k mod N^2 = (1 + N)^k = 1 + (k mod N) N  (binomial theorem; < N^2)
+Nat gamma_pow(const Nat& k, const Nat& N) { return Nat(1) + (k % N) * N; }
+
+// gcd(x, m) == 1 for odd m; with known factors P, Q (m = P*Q or m = P^2 Q^2 with
+// the same prime set): P !| x and Q !| x.
+bool coprime_to(const Nat& x, const Nat& m, const Nat& P, const Nat& Qf) {
+  if (!P.is_zero() && !Qf.is_zero()) return !(x % P).is_zero() && !(x % Qf).is_zero();
+  return coprime_odd(x, m);
+}
+
+Nat affine_x(const secp::Affine& p) { return secp::FeToNat(p.x); }
+Nat affine_y(const secp::Affine& p) { return secp::FeToNat(p.y); }
+
+// ---- ProveRangeAlice in stages (shared by ProveRangeAliceBatch and AliceInitBatch)
+struct RangeProveState {
+  Nat alpha, beta, gamma, rho;
+  Nat gam_alpha, t1, t2, e;
+};
+
+// steps 1-4: alpha < q^3, beta in Z*_N, gamma < q^3 N~, rho < q N~
+void range_draw(RangeProveState& s, const paillier::PublicKey& pk, const DLNParams& dln, const RandFn& rand) {
+  s.alpha = GetRandomPositiveInt(rand, q3());
+  s.beta = GetRandomPositiveRelativelyPrimeInt(rand, pk.N);
+  s.gamma = GetRandomPositiveInt(rand, q3() * dln.NTilde);
+  s.rho = GetRandomPositiveInt(rand, Q() * dln.NTilde);
+}
+
+}  // namespace
+
+const Nat& Q() { return secp::CurveN(); }
+
+// ================================================================ RangeProofAlice
+void ProveRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln, const std::vector<Nat>& c,
+                          const std::vector<Nat>& m, const std::vector<Nat>& r, const std::vector<RandFn>& rand,
+                          std::vector<RangeProofAlice>* out) {
+  const size_t n = c.size();
+  if (m.size() != n || r.size() != n || rand.size() != n) throw std::invalid_argument("ProveRangeAlice: sizes");
+  const Nat N2 = pk.NSquare();
+  std::vector<RangeProveState> st(n);
+  out->assign(n, RangeProofAlice{});
+  parallel_for(n, [&](size_t i) {
+    range_draw(st[i], pk, dln, rand[i]);
+    st[i].gam_alpha = gamma_pow(st[i].alpha, pk.N);
+  });
+  ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
+  for (size_t i = 0; i < n; ++i) {
+    auto& s = st[i];
+    auto& o = (*out)[i];
+    eN2.add(s.beta, pk.N, &o.U, &s.gam_alpha);  // 6. u = Gamma^alpha beta^N mod N^2
+    eNt.add(dln.h1, m[i], &s.t1);               // 5. h1^m
+    eNt.add(dln.h1, s.alpha, &s.t2);            // 7. h1^alpha
+  }
+  eN2.run();
+  eNt.run();
+  for (size_t i = 0; i < n; ++i) {
+    eNt.add(dln.h2, st[i].rho, &(*out)[i].Z, &st[i].t1);    // 5. z = h1^m h2^rho mod N~
+    eNt.add(dln.h2, st[i].gamma, &(*out)[i].W, &st[i].t2);  // 7. w = h1^alpha h2^gamma mod N~
+  }
+  eNt.run();
+  const Nat gamma = pk.Gamma();
+  parallel_for(n, [&](size_t i) {  // 8-9. e = RejectionSample(q, SHA512_256i(N, Gamma, c, z, u, w))
+    auto& o = (*out)[i];
+    st[i].e = RejectionSample(Q(), SHA512_256i({&pk.N, &gamma, &c[i], &o.Z, &o.U, &o.W}));
+  });
+  for (size_t i = 0; i < n; ++i) eN.add(r[i], st[i].e, &(*out)[i].S, &st[i].beta);  // s = r^e beta mod N
+  eN.run();
+  parallel_for(n, [&](size_t i) {
+    auto& o = (*out)[i];
+    o.S1 = st[i].e * m[i] + st[i].alpha;    // s1 = e m + alpha
+    o.S2 = st[i].e * st[i].rho + st[i].gamma;  // s2 = e rho + gamma
+  });
+}
+
+std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln,
+                                           const std::vector<Nat>& c, const std::vector<RangeProofAlice>& pf) {
+  const size_t n = c.size();
+  if (pf.size() != n) throw std::invalid_argument("RangeProofAlice.Verify: sizes");
+  const Nat N2 = pk.NSquare();
+  const Nat gamma = pk.Gamma();
+  std::vector<uint8_t> ok(n, 0);
+  std::vector<Nat> e(n), gs1(n), L1(n), R1(n), t(n), L2(n), R2(n);
+  parallel_for(n, [&](size_t i) {
+    const auto& p = pf[i];
+    if (!IsInInterval(p.Z, dln.NTilde) || !IsInInterval(p.U, N2) || !IsInInterval(p.W, dln.NTilde) ||
+        !IsInInterval(p.S, pk.N))
+      return;
+    if (!coprime_to(p.Z, dln.NTilde, dln.P, dln.Q) || !coprime_odd(p.U, pk.N) ||
+        !coprime_to(p.W, dln.NTilde, dln.P, dln.Q) || !coprime_odd(p.S, pk.N))
+      return;
+    if (p.S1 > q3()) return;
+    if (!(c[i] < N2) || !coprime_odd(c[i], pk.N)) return;  // c^-e defined (Go: nil -> panic)
+    e[i] = RejectionSample(Q(), SHA512_256i({&pk.N, &gamma, &c[i], &p.Z, &p.U, &p.W}));
+    gs1[i] = gamma_pow(p.S1, pk.N);
+    ok[i] = 1;
+  });
+  ExpSet eN2(N2), eNt(dln.NTilde);
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) continue;
+    const auto& p = pf[i];
+    eN2.add(c[i], e[i], &L1[i], &p.U);      // u c^e
+    eN2.add(p.S, pk.N, &R1[i], &gs1[i]);    // Gamma^s1 s^N
+    eNt.add(dln.h1, p.S1, &t[i]);           // h1^s1
+    eNt.add(p.Z, e[i], &L2[i], &p.W);       // w z^e
+  }
+  eN2.run();
+  eNt.run();
+  for (size_t i = 0; i < n; ++i)
+    if (ok[i]) eNt.add(dln.h2, pf[i].S2, &R2[i], &t[i]);  // h1^s1 h2^s2
+  eNt.run();
+  for (size_t i = 0; i < n; ++i) ok[i] = ok[i] && L1[i] == R1[i] && L2[i] == R2[i];
+  return ok;
+}
+
+// ================================================================ ProofBob[WC]
+namespace {
+struct BobProveState {
+  Nat alpha, rho, sigma, tau, rhoPrm, beta, gamma;
+  secp::Affine u;
+  Nat bg, a1, a2, a3, a4, e;
+};
+
+// steps 1-4 (+5 for WC): draw order alpha, rho, sigma, tau, rhoPrm, beta, gamma
+void bob_draw(BobProveState& s, const paillier::PublicKey& pk, const DLNParams& dln, const RandFn& rand, bool wc) {
+  const Nat qNt = Q() * dln.NTilde, q3Nt = q3() * dln.NTilde;
+  s.alpha = GetRandomPositiveInt(rand, q3());
+  s.rho = GetRandomPositiveInt(rand, qNt);
+  s.sigma = GetRandomPositiveInt(rand, qNt);
+  s.tau = GetRandomPositiveInt(rand, q3Nt);
+  s.rhoPrm = GetRandomPositiveInt(rand, q3Nt);
+  s.beta = GetRandomPositiveRelativelyPrimeInt(rand, pk.N);
+  s.gamma = GetRandomPositiveInt(rand, q7());
+  if (wc) s.u = secp::ScalarBaseMult(s.alpha);  // 5. u = alpha*G
+}
+
+// stage A of ProveBob: N^2 -> bg = Gamma^gamma beta^N ; N~ -> h1^x, h1^alpha, h1^y, h1^gamma
+void bob_stage_a(BobProveState& s, const paillier::PublicKey& pk, const DLNParams& dln, const Nat& x, const Nat& y,
+                 ExpSet& eN2, ExpSet& eNt, Nat* gam_gamma) {
+  *gam_gamma = gamma_pow(s.gamma, pk.N);
+  eN2.add(s.beta, pk.N, &s.bg, gam_gamma);
+  eNt.add(dln.h1, x, &s.a1);
+  eNt.add(dln.h1, s.alpha, &s.a2);
+  eNt.add(dln.h1, y, &s.a3);
+  eNt.add(dln.h1, s.gamma, &s.a4);
+}
+
+// stage B: v = c1^alpha Gamma^gamma beta^N (9.), z, z', t, w (6-8, 10.)
+void bob_stage_b(BobProveState& s, const DLNParams& dln, const Nat& c1, ExpSet& eN2, ExpSet& eNt, ProofBob& o) {
+  eN2.add(c1, s.alpha, &o.V, &s.bg);
+  eNt.add(dln.h2, s.rho, &o.Z, &s.a1);
+  eNt.add(dln.h2, s.rhoPrm, &o.ZPrm, &s.a2);
+  eNt.add(dln.h2, s.sigma, &o.T, &s.a3);
+  eNt.add(dln.h2, s.tau, &o.W, &s.a4);
+}
+
+// 11-12. e = RejectionSample(q, SHA512_256i_TAGGED(Session, N, Gamma, [X.x, X.y,] c1, c2, [u.x, u.y,] z, z', t, v, w))
+Nat bob_challenge(const Bytes& session, const paillier::PublicKey& pk, const Nat& gamma, const secp::Affine* X,
+                  const Nat& c1, const Nat& c2, const ProofBob& p) {
+  if (!X) return RejectionSample(Q(), SHA512_256i_TAGGED(session, {&pk.N, &gamma, &c1, &c2, &p.Z, &p.ZPrm, &p.T,
+                                                                     &p.V, &p.W}));
+  const Nat Xx = affine_x(*X), Xy = affine_y(*X), ux = affine_x(p.U), uy = affine_y(p.U);
+  return RejectionSample(Q(), SHA512_256i_TAGGED(session, {&pk.N, &gamma, &Xx, &Xy, &c1, &c2, &ux, &uy, &p.Z,
+                                                           &p.ZPrm, &p.T, &p.V, &p.W}));
+}
+
+// 13. s1 = e x + alpha, s2 = e rho + rhoPrm, t1 = e y + gamma, t2 = e sigma + tau
+void bob_responses(const BobProveState& s, const Nat& x, const Nat& y, ProofBob& o) {
+  o.S1 = s.e * x + s.alpha;
+  o.S2 = s.e * s.rho + s.rhoPrm;
+  o.T1 = s.e * y + s.gamma;
+  o.T2 = s.e * s.sigma + s.tau;
+  o.U = s.u;
+}
+}  // namespace
+
+void ProveBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pk, const DLNParams& dln,
+                   const std::vector<Nat>& c1, const std::vector<Nat>& c2, const std::vector<Nat>& x,
+                   const std::vector<Nat>& y, const std::vector<Nat>& r, const std::vector<secp::Affine>* X,
+                   const std::vector<RandFn>& rand, std::vector<ProofBob>* out) {
+  const size_t n = c1.size();
+  if (session.size() != n || c2.size() != n || x.size() != n || y.size() != n || r.size() != n ||
+      rand.size() != n || (X && X->size() != n))
+    throw std::invalid_argument("ProveBob: sizes");
+  const Nat N2 = pk.NSquare(), gamma = pk.Gamma();
+  std::vector<BobProveState> st(n);
+  std::vector<Nat> gg(n);
+  out->assign(n, ProofBob{});
+  parallel_for(n, [&](size_t i) { bob_draw(st[i], pk, dln, rand[i], X != nullptr); });
+  ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
+  for (size_t i = 0; i < n; ++i) bob_stage_a(st[i], pk, dln, x[i], y[i], eN2, eNt, &gg[i]);
+  eN2.run();
+  eNt.run();
+  for (size_t i = 0; i < n; ++i) bob_stage_b(st[i], dln, c1[i], eN2, eNt, (*out)[i]);
+  eN2.run();
+  eNt.run();
+  parallel_for(n, [&](size_t i) {
+    (*out)[i].U = st[i].u;
+    st[i].e = bob_challenge(session[i], pk, gamma, X ? &(*X)[i] : nullptr, c1[i], c2[i], (*out)[i]);
+  });
+  for (size_t i = 0; i < n; ++i) eN.add(r[i], st[i].e, &(*out)[i].S, &st[i].beta);  // s = r^e beta mod N
+  eN.run();
+  parallel_for(n, [&](size_t i) { bob_responses(st[i], x[i], y[i], (*out)[i]); });
+}
+
+std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pk,
+                                    const DLNParams& dln, const std::vector<Nat>& c1, const std::vector<Nat>& c2,
+                                    const std::vector<ProofBob>& pf, const std::vector<secp::Affine>* X,
+                                    const paillier::PrivateKey* own_sk) {
+  const size_t n = c1.size();
+  if (session.size() != n || c2.size() != n || pf.size() != n || (X && X->size() != n))
+    throw std::invalid_argument("ProofBob.Verify: sizes");
+  const Nat N2 = pk.NSquare(), gamma = pk.Gamma();
+  const Nat zero;
+  const Nat& kP = own_sk ? own_sk->P : zero;
+  const Nat& kQ = own_sk ? own_sk->Q : zero;
+  std::vector<uint8_t> ok(n, 0);
+  std::vector<Nat> e(n), gt1(n), p1(n), p2(n), r1(n), r2(n), q1(n), r3(n), l1(n), l2(n), l3(n);
+  parallel_for(n, [&](size_t i) {
+    const auto& p = pf[i];
+    if (X && !secp::IsOnCurve(p.U)) return;
+    const Nat& Nt = dln.NTilde;
+    for (const Nat* v : {&p.Z, &p.ZPrm, &p.T, &p.W})
+      if (!IsInInterval(*v, Nt) || !coprime_to(*v, Nt, dln.P, dln.Q)) return;
+    if (!IsInInterval(p.V, N2) || !coprime_to(p.V, pk.N, kP, kQ)) return;
+    if (!IsInInterval(p.S, pk.N) || !coprime_to(p.S, pk.N, kP, kQ)) return;
+    // 3. s1 <= q^3. No t1 bound: BobMid draws betaPrm < N, so an honest
+    // t1 = e betaPrm + gamma has ~2300 bits (upstream, verify).
+    if (p.S1 > q3()) return;
+    e[i] = bob_challenge(session[i], pk, gamma, X ? &(*X)[i] : nullptr, c1[i], c2[i], p);
+    if (X) {  // 4. s1*G == e*X + u
+      const secp::Affine gS1 = secp::ScalarBaseMult(p.S1 % Q());
+      const secp::Affine xEU = secp::Add(secp::ScalarMult((*X)[i], e[i]), p.U);
+      if (xEU.inf || !secp::Equal(gS1, xEU)) return;
+    }
+    gt1[i] = gamma_pow(p.T1, pk.N);
+    ok[i] = 1;
+  });
+  ExpSet eN2(N2), eNt(dln.NTilde);
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) continue;
+    const auto& p = pf[i];
+    eNt.add(dln.h1, p.S1, &p1[i]);          // 5. h1^s1
+    eNt.add(dln.h1, p.T1, &p2[i]);          // 6. h1^t1
+    eNt.add(p.Z, e[i], &r1[i], &p.ZPrm);    // 5. z^e z'
+    eNt.add(p.T, e[i], &r2[i], &p.W);       // 6. t^e w
+    eN2.add(p.S, pk.N, &q1[i], &gt1[i]);    // 7. s^N Gamma^t1
+    eN2.add(c2[i], e[i], &r3[i], &p.V);     // 7. c2^e v
+  }
+  eN2.run();
+  eNt.run();
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) continue;
+    eNt.add(dln.h2, pf[i].S2, &l1[i], &p1[i]);  // 5. h1^s1 h2^s2
+    eNt.add(dln.h2, pf[i].T2, &l2[i], &p2[i]);  // 6. h1^t1 h2^t2
+    eN2.add(c1[i], pf[i].S1, &l3[i], &q1[i]);   // 7. c1^s1 s^N Gamma^t1
+  }
+  eN2.run();
+  eNt.run();
+  for (size_t i = 0; i < n; ++i) ok[i] = ok[i] && l1[i] == r1[i] && l2[i] == r2[i] && l3[i] == r3[i];
+  return ok;
+}
+
+// ================================================================ protocol
+void AliceInitBatch(const paillier::PublicKey& pkA, const std::vector<Nat>& a, const DLNParams& dlnB,
+                    const std::vector<RandFn>& rand, std::vector<Nat>* cA, std::vector<RangeProofAlice>* pf,
+                    std::vector<uint8_t>* err) {
+  const size_t n = a.size();
+  if (rand.size() != n) throw std::invalid_argument("AliceInit: sizes");
+  cA->assign(n, Nat());
+  err->assign(n, OK);
+  // EncryptAndReturnRandomness: 0 <= a < N, then r in Z*_N
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < n; ++i) {
+    if (!(a[i] < pkA.N)) (*err)[i] = ErrMessageTooLong;
+    else idx.push_back(i);
+  }
+  const size_t k = idx.size();
+  std::vector<Nat> r(k), ga(k), c(k), m(k);
+  std::vector<RandFn> rd(k);
+  parallel_for(k, [&](size_t j) {
+    r[j] = GetRandomPositiveRelativelyPrimeInt(rand[idx[j]], pkA.N);
+    ga[j] = gamma_pow(a[idx[j]], pkA.N);
+  });
+  ExpSet eN2(pkA.NSquare());
+  for (size_t j = 0; j < k; ++j) {
+    eN2.add(r[j], pkA.N, &c[j], &ga[j]);  // c = Gamma^a r^N mod N^2
+    m[j] = a[idx[j]];
+    rd[j] = rand[idx[j]];
+  }
+  eN2.run();
+  std::vector<RangeProofAlice> p;
+  ProveRangeAliceBatch(pkA, dlnB, c, m, r, rd, &p);
+  pf->assign(n, RangeProofAlice{});
+  for (size_t j = 0; j < k; ++j) {
+    (*cA)[idx[j]] = c[j];
+    (*pf)[idx[j]] = std::move(p[j]);
+  }
+}
+
+void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pkA,
+                 const std::vector<RangeProofAlice>& pf, const std::vector<Nat>& b, const std::vector<Nat>& cA,
+                 const DLNParams& dlnA, const DLNParams& dlnB, const std::vector<secp::Affine>* B,
+                 const std::vector<RandFn>& rand, std::vector<BobMidResult>* out, std::vector<uint8_t>* err) {
+  const size_t n = cA.size();
+  if (session.size() != n || pf.size() != n || b.size() != n || rand.size() != n || (B && B->size() != n))
+    throw std::invalid_argument("BobMid: sizes");
+  const Nat N2 = pkA.NSquare(), gamma = pkA.Gamma();
+  out->assign(n, BobMidResult{});
+  err->assign(n, OK);
+  // RangeProofAlice.Verify(ec, pkA, NTildeB, h1B, h2B, cA)
+  const std::vector<uint8_t> ok = VerifyRangeAliceBatch(pkA, dlnB, cA, pf);
+  // HomoMult's range checks: cA < N^2 holds for every verified session; b < N
+  // is checked after betaPrm and the Encrypt randomness are drawn, as in Go.
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) (*err)[i] = ErrProofVerify;
+    else idx.push_back(i);
+  }
+  const size_t k = idx.size();
+  std::vector<BobProveState> st(k);
+  std::vector<Nat> cRand(k), gbp(k), cbp(k), gg(k);
+  parallel_for(k, [&](size_t j) {
+    const size_t i = idx[j];
+    auto& o = (*out)[i];
+    o.betaPrm = GetRandomPositiveInt(rand[i], pkA.N);                 // betaPrm < N
+    cRand[j] = GetRandomPositiveRelativelyPrimeInt(rand[i], pkA.N);   // Encrypt(betaPrm) randomness
+    gbp[j] = gamma_pow(o.betaPrm, pkA.N);
+    if (!(b[i] < pkA.N)) {  // HomoMult(b, cA) fails before ProveBob draws anything
+      (*err)[i] = ErrMessageTooLong;
+      return;
+    }
+    bob_draw(st[j], pkA, dlnA, rand[i], B != nullptr);                // ProveBob[WC] steps 1-5
+  });
+  ExpSet eN2(N2), eNt(dlnA.NTilde), eN(pkA.N);
+  for (size_t j = 0; j < k; ++j) {
+    const size_t i = idx[j];
+    if ((*err)[i]) continue;
+    eN2.add(cRand[j], pkA.N, &cbp[j], &gbp[j]);  // cBetaPrm = Gamma^betaPrm r^N
+    bob_stage_a(st[j], pkA, dlnA, b[i], (*out)[i].betaPrm, eN2, eNt, &gg[j]);
+  }
+  eN2.run();
+  eNt.run();
+  for (size_t j = 0; j < k; ++j) {
+    const size_t i = idx[j];
+    if ((*err)[i]) continue;
+    eN2.add(cA[i], b[i], &(*out)[i].cB, &cbp[j]);  // cB = HomoAdd(HomoMult(b, cA), cBetaPrm)
+    bob_stage_b(st[j], dlnA, cA[i], eN2, eNt, (*out)[i].pf);
+  }
+  eN2.run();
+  eNt.run();
+  parallel_for(k, [&](size_t j) {
+    const size_t i = idx[j];
+    if ((*err)[i]) return;
+    auto& o = (*out)[i];
+    o.beta = (Q() - o.betaPrm % Q()) % Q();  // beta = ModInt(q).Sub(0, betaPrm)
+    o.pf.U = st[j].u;
+    st[j].e = bob_challenge(session[i], pkA, gamma, B ? &(*B)[i] : nullptr, cA[i], o.cB, o.pf);
+  });
+  for (size_t j = 0; j < k; ++j) {
+    const size_t i = idx[j];
+    if (!(*err)[i]) eN.add(cRand[j], st[j].e, &(*out)[i].pf.S, &st[j].beta);  // s = r^e beta mod N
+  }
+  eN.run();
+  parallel_for(k, [&](size_t j) {
+    const size_t i = idx[j];
+    if (!(*err)[i]) bob_responses(st[j], b[i], (*out)[i].betaPrm, (*out)[i].pf);
+  });
+}
+
+void AliceEndBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,
+                   const std::vector<ProofBob>& pf, const DLNParams& dlnA, const std::vector<Nat>& cA,
+                   const std::vector<Nat>& cB, const std::vector<secp::Affine>* B, std::vector<Nat>* alpha,
+                   std::vector<uint8_t>* err) {
+  const size_t n = cA.size();
+  const std::vector<uint8_t> ok = VerifyBobBatch(session, skA.pub, dlnA, cA, cB, pf, B, &skA);
+  alpha->assign(n, Nat());
+  err->assign(n, OK);
+  std::vector<Int> cs;
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) {
+      (*err)[i] = ErrProofVerify;
+      continue;
+    }
+    idx.push_back(i);
+    cs.push_back(Int(cB[i]));
+  }
+  std::vector<Nat> m;
+  std::vector<uint8_t> derr;
+  skA.DecryptBatch(cs, &m, &derr);
+  for (size_t j = 0; j < idx.size(); ++j) {
+    if (derr[j]) {
+      (*err)[idx[j]] = derr[j];
+      continue;
+    }
+    (*alpha)[idx[j]] = m[j] % Q();
+  }
+}
+
+}  // namespace mpcx::host::mta

@@ -11,75 +11,6 @@
 
 namespace mpcx::host {
 
-// ------------------------------------------------------------------ SHA-256
-namespace {
-struct Sha256 {
-  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
-  static uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
-  void block(const uint8_t* p) {
-    static const uint32_t k[64] = {
-        0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
-        0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
-        0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
-        0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
-        0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
-        0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
-        0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
-        0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
-    uint32_t w[64];
-    for (int i = 0; i < 16; ++i) w[i] = (uint32_t)p[4 * i] << 24 | (uint32_t)p[4 * i + 1] << 16 | (uint32_t)p[4 * i + 2] << 8 | p[4 * i + 3];
-    for (int i = 16; i < 64; ++i) {
-      const uint32_t s0 = ror(w[i - 15], 7) ^ ror(w[i - 15], 18) ^ (w[i - 15] >> 3);
-      const uint32_t s1 = ror(w[i - 2], 17) ^ ror(w[i - 2], 19) ^ (w[i - 2] >> 10);
-      w[i] = w[i - 16] + s0 + w[i - 7] + s1;
-    }
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-    for (int i = 0; i < 64; ++i) {
-      const uint32_t S1 = ror(e, 6) ^ ror(e, 11) ^ ror(e, 25);
-      const uint32_t ch = (e & f) ^ (~e & g);
-      const uint32_t t1 = hh + S1 + ch + k[i] + w[i];
-      const uint32_t S0 = ror(a, 2) ^ ror(a, 13) ^ ror(a, 22);
-      const uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-      const uint32_t t2 = S0 + mj;
-      hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
-    }
-    h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
-  }
-  // one-shot digest of a short message (< 56 bytes)
-  static void digest_short(const uint8_t* msg, size_t n, uint8_t out[32]) {
-    Sha256 s;
-    uint8_t blk[64] = {0};
-    std::memcpy(blk, msg, n);
-    blk[n] = 0x80;
-    const uint64_t bits = (uint64_t)n * 8;
-    for (int i = 0; i < 8; ++i) blk[63 - i] = (uint8_t)(bits >> (8 * i));
-    s.block(blk);
-    for (int i = 0; i < 8; ++i)
-      for (int j = 0; j < 4; ++j) out[4 * i + j] = (uint8_t)(s.h[i] >> (24 - 8 * j));
-  }
-};
-}  // namespace
-
-void CounterDRBG::read(uint8_t* out, size_t n) {
-  while (n) {
-    if (pos_ == buf_.size()) {
-      uint8_t msg[25];
-      std::memcpy(msg, "mpcx-drbg", 9);
-      for (int i = 0; i < 8; ++i) msg[9 + i] = (uint8_t)(seed_ >> (8 * i));
-      for (int i = 0; i < 8; ++i) msg[17 + i] = (uint8_t)(ctr_ >> (8 * i));
-      ++ctr_;
-      buf_.assign(32, 0);
-      Sha256::digest_short(msg, sizeof msg, buf_.data());
-      pos_ = 0;
-    }
-    const size_t take = std::min(n, buf_.size() - pos_);
-    std::memcpy(out, buf_.data() + pos_, take);
-    pos_ += take;
-    out += take;
-    n -= take;
-  }
-}
-
 // ------------------------------------------------------------ candidates
 static const uint32_t kSmallPrimes[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53};
 static const uint64_t kSmallPrimesProduct = 16294579238595022365ull;
@@ -261,29 +192,6 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, con
   }
   if ((int)out.size() < numPrimes) throw std::runtime_error("safe prime search exhausted max_candidates");
   return out;
-}
-
-Nat MustGetRandomInt(const RandFn& rand, uint32_t bits) {
-  // crypto/rand.Int(rand, max), max = 2^bits - 1: bitLen(max-1) = bits (bits >= 2)
-  if (bits < 2) throw std::invalid_argument("MustGetRandomInt: bits must be >= 2");
-  const Nat max = (Nat(1) << bits) - Nat(1);
-  const size_t k = (bits + 7) / 8;
-  unsigned b = bits % 8;
-  if (b == 0) b = 8;
-  std::vector<uint8_t> buf(k);
-  for (;;) {
-    rand(buf.data(), k);
-    buf[0] &= (uint8_t)((1u << b) - 1);
-    Nat n = Nat::from_bytes_be(buf.data(), k);
-    if (n < max) return n;
-  }
-}
-
-Nat GetRandomPositiveRelativelyPrimeInt(const RandFn& rand, const Nat& n) {
-  for (;;) {
-    Nat t = MustGetRandomInt(rand, n.bit_len());
-    if (t < n && t >= Nat(1) && gcd(t, n) == Nat(1)) return t;
-  }
 }
 
 paillier::PrivateKey GenerateKeyPair(int modulusBitLen, const RandFn& rand, SafePrimeStats* stats) {

@@ -21,27 +21,9 @@
 
 #include "bignum.hpp"
 #include "paillier.hpp"
+#include "tsscommon.hpp"
 
 namespace mpcx::host {
-
-// io.Reader stand-in: fill buf[0..n) with random bytes.
-using RandFn = std::function<void(uint8_t* buf, size_t n)>;
-
-// Deterministic byte stream SHA-256(b"mpcx-drbg" || seed_le64 || ctr_le64),
-// identical to oracle/gomath.py CounterDRBG (tests and synthetic inputs).
-class CounterDRBG {
- public:
-  explicit CounterDRBG(uint64_t seed) : seed_(seed) {}
-  void read(uint8_t* out, size_t n);
-  RandFn fn() {
-    return [this](uint8_t* b, size_t n) { read(b, n); };
-  }
-
- private:
-  uint64_t seed_, ctr_ = 0;
-  std::vector<uint8_t> buf_;
-  size_t pos_ = 0;
-};
 
 struct GermainSafePrime {
   Nat p;  // safe prime p = 2q + 1
@@ -64,11 +46,6 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, con
 
 // Candidate q from raw bytes (steps 1-3); exposed for tests.
 Nat CandidateFromBytes(const uint8_t* bytes, size_t n, int qBitLen);
-
-// crypto/rand.Int(rand, 2^bits - 1) as used by common.MustGetRandomInt, and
-// common.GetRandomPositiveRelativelyPrimeInt(rand, n) (up:common/random.go).
-Nat MustGetRandomInt(const RandFn& rand, uint32_t bits);
-Nat GetRandomPositiveRelativelyPrimeInt(const RandFn& rand, const Nat& n);
 
 // paillier.GenerateKeyPair(ctx, rand, modulusBitLen)
 paillier::PrivateKey GenerateKeyPair(int modulusBitLen, const RandFn& rand, SafePrimeStats* stats = nullptr);

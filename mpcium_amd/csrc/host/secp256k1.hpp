@@ -1,0 +1,38 @@
+// secp256k1.hpp -- the curve arithmetic the MtAwc proofs need on the host
+// (tss.EC() = btcec/v2 S256, /root/reference/go.mod:29): u = alpha*G in
+// ProveBobWC and s1*G == e*X + u in (*ProofBobWC).Verify
+// (up:crypto/mta/proofs.go). Fixed-width 4x64-bit field arithmetic mod
+// p = 2^256 - 2^32 - 977, Jacobian coordinates, 4-bit fixed-window scalar
+// multiplication, and a precomputed 64 x 16 table for the base point.
+// ScalarBaseMult(k) = (k mod n)*G (crypto.ScalarBaseMult semantics under which
+// the MtAwc check holds for alpha < q^3).
+#pragma once
+
+#include <array>
+#include <cstdint>
+
+#include "bignum.hpp"
+
+namespace mpcx::host::secp {
+
+using Fe = std::array<uint64_t, 4>;  // little-endian limbs, value < p
+
+struct Affine {
+  Fe x{}, y{};
+  bool inf = true;  // point at infinity
+};
+
+extern const Nat& CurveN();  // group order n (= q in tss-lib)
+
+// k*G, k reduced mod n
+Affine ScalarBaseMult(const Nat& k);
+// k*P, k reduced mod n
+Affine ScalarMult(const Affine& P, const Nat& k);
+Affine Add(const Affine& P, const Affine& Q);
+bool IsOnCurve(const Affine& P);
+bool Equal(const Affine& P, const Affine& Q);
+
+Nat FeToNat(const Fe& a);
+Fe NatToFe(const Nat& a);  // requires a < 2^256 (reduced mod p)
+
+}  // namespace mpcx::host::secp

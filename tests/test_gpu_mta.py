@@ -1,0 +1,167 @@
+"""GPU parity tests of the batched MtA / MtAwc mirror (rows A8-A10) against
+the oracle's golden sessions (tests/golden/mta_vectors.json, made by
+oracle/mta_ref.py): every output field bit-exact, error codes for tampered
+proofs and bad inputs, and the MtA relations on a larger random batch."""
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN, H
+from oracle import mta_ref as M
+from oracle import tss_ref as T
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mta(gpu):
+    from mpcium_amd import host, mta
+    host.init(0)
+    return mta
+
+
+@pytest.fixture(scope="module")
+def nodes():
+    d = json.load(open(os.path.join(GOLDEN, "node_preparams.json")))
+    return [{k: int(v, 16) for k, v in n.items() if isinstance(v, str) and k != "paillier_source"} for n in d["nodes"]]
+
+
+@pytest.fixture(scope="module")
+def vec():
+    return json.load(open(os.path.join(GOLDEN, "mta_vectors.json")))["sessions"]
+
+
+def dln(n, own=False):
+    d = {"NTilde": n["NTildei"], "h1": n["H1i"], "h2": n["H2i"]}
+    if own:
+        d["P"], d["Q"] = 2 * n["p"] + 1, 2 * n["q"] + 1
+    return d
+
+
+def hx(d):
+    return {k: (H(v) if isinstance(v, str) else v) for k, v in d.items()}
+
+
+def bob_pf(d, wc):
+    p = {k: H(d[k]) for k in M.ProofBob.__dataclass_fields__ if k != "U"}
+    p["U"] = (H(d["Ux"]), H(d["Uy"])) if wc else None
+    return p
+
+
+def test_golden_sessions_bit_exact(mta, nodes, vec):
+    A, B = nodes[0], nodes[1]
+    n = len(vec)
+    a = [H(v["a"]) for v in vec]
+    cA, pfA, err = mta.alice_init(A["N"], a, dln(B), [v["seed_a"] for v in vec])
+    assert err == [0] * n
+    assert cA == [H(v["cA"]) for v in vec]
+    assert pfA == [hx(v["pfA"]) for v in vec]
+    ss = [bytes.fromhex(v["session"]) for v in vec]
+    Bpts = [(H(v["Bx"]), H(v["By"])) for v in vec]
+    for wc, key, bs, seeds in ((False, "bob", [H(v["b"]) for v in vec], [v["seed_b"] for v in vec]),
+                               (True, "bob_wc", [H(v["wB"]) for v in vec], [v["seed_bwc"] for v in vec])):
+        beta, cB, bp, pfB, err = mta.bob_mid(ss, A["N"], pfA, bs, cA, dln(A), dln(B, own=True), seeds,
+                                             B=Bpts if wc else None)
+        assert err == [0] * n, key
+        assert beta == [H(v[key]["beta"]) for v in vec], key
+        assert cB == [H(v[key]["cB"]) for v in vec], key
+        assert bp == [H(v[key]["betaPrm"]) for v in vec], key
+        assert pfB == [bob_pf(v[key]["pf"], wc) for v in vec], key
+        sk = (A["N"], A["LambdaN"], A["P"], A["Q"])
+        alpha, err = mta.alice_end(ss, sk, pfB, dln(A, own=True), cA, cB, B=Bpts if wc else None)
+        assert err == [0] * n, key
+        assert alpha == [H(v["alpha_wc" if wc else "alpha"]) for v in vec], key
+
+
+def test_range_proof_rejections(mta, nodes, vec):
+    A, B = nodes[0], nodes[1]
+    v = vec[0]
+    c, pf = H(v["cA"]), hx(v["pfA"])
+    bad = []
+    for f, delta in (("S1", 1), ("S2", 1), ("Z", 1), ("U", 1), ("W", 1), ("S", 1)):
+        p = dict(pf)
+        p[f] += delta
+        bad.append(p)
+    p = dict(pf)
+    p["S1"] = M.Q ** 3 + 1  # out of range
+    bad.append(p)
+    p = dict(pf)
+    p["Z"] = B["NTildei"]  # not in [0, N~)
+    bad.append(p)
+    p = dict(pf)
+    p["S"] = A["P"]  # gcd(S, N) != 1
+    bad.append(p)
+    cs = [c] * (len(bad) + 2) + [c + 1]
+    pfs = [pf] + bad + [pf, pf]
+    ok = mta.verify_range_alice(A["N"], dln(B), cs, pfs)
+    assert ok == [True] + [False] * len(bad) + [True, False]
+    # same decisions as the oracle
+    for cc, p, o in zip(cs, pfs, ok):
+        assert M.verify_range_alice(M.RangeProofAlice(**p), A["N"], B["NTildei"], B["H1i"], B["H2i"], cc) == o
+
+
+def test_bob_mid_rejects_bad_range_proof_and_b(mta, nodes, vec):
+    A, B = nodes[0], nodes[1]
+    v = vec[0]
+    pf = hx(v["pfA"])
+    bad = dict(pf)
+    bad["S"] = (bad["S"] + 1) % A["N"]
+    ss = [bytes.fromhex(v["session"])] * 3
+    beta, cB, bp, pfB, err = mta.bob_mid(ss, A["N"], [pf, bad, pf], [H(v["b"]), H(v["b"]), A["N"]],
+                                         [H(v["cA"])] * 3, dln(A), dln(B), [v["seed_b"]] * 3)
+    assert err == [0, mta.ERR_PROOF_VERIFY, mta.ERR_MESSAGE_TOO_LONG]
+    assert cB[0] == H(v["bob"]["cB"]) and beta[0] == H(v["bob"]["beta"])
+
+
+def test_bob_proof_rejections(mta, nodes, vec):
+    A = nodes[0]
+    v = vec[0]
+    ss = bytes.fromhex(v["session"])
+    c1, c2 = H(v["cA"]), H(v["bob_wc"]["cB"])
+    X = (H(v["Bx"]), H(v["By"]))
+    pf = bob_pf(v["bob_wc"]["pf"], True)
+    cases = [(pf, ss, X, True)]
+    for f in ("Z", "ZPrm", "T", "V", "W", "S", "S1", "S2", "T1", "T2"):
+        p = dict(pf)
+        p[f] += 1
+        cases.append((p, ss, X, False))
+    p = dict(pf)
+    p["U"] = T.ec_add(pf["U"], T.SECP_G)
+    cases.append((p, ss, X, False))                       # wrong u
+    cases.append((pf, ss[:-1] + bytes([ss[-1] ^ 1]), X, False))  # other session
+    cases.append((pf, ss, T.ec_add(X, T.SECP_G), False))  # other X
+    p = dict(pf)
+    p["S1"] = M.Q ** 3 + 1
+    cases.append((p, ss, X, False))
+    sk = (A["LambdaN"], A["P"], A["Q"])
+    for own in (None, sk):
+        ok = mta.verify_bob([c[1] for c in cases], A["N"], dln(A, own=own is not None), [c1] * len(cases),
+                            [c2] * len(cases), [c[0] for c in cases], X=[c[2] for c in cases], own_sk=own)
+        assert ok == [c[3] for c in cases]
+    # plain ProofBob: verify the non-WC golden proof, WC-only fields ignored
+    pfp = bob_pf(v["bob"]["pf"], False)
+    assert mta.verify_bob([ss], A["N"], dln(A), [c1], [H(v["bob"]["cB"])], [pfp]) == [True]
+
+
+def test_random_batch_relations(mta, nodes):
+    """64 sessions per direction for every ordered node pair, with the MtA
+    relations alpha + beta = a*b (mod q) checked on every session."""
+    q = M.Q
+    rd = T.Reader(0xBA7C4)
+    for ia, ib in ((0, 1), (1, 2), (2, 0)):
+        A, B = nodes[ia], nodes[ib]
+        n = 64
+        a = [T.get_random_positive_int(rd, q) for _ in range(n)]
+        b = [T.get_random_positive_int(rd, q) for _ in range(n)]
+        ss = [rd.read(32) for _ in range(n)]
+        seeds = [1000 * ia + 10 * ib + i for i in range(n)]
+        cA, pfA, err = mta.alice_init(A["N"], a, dln(B), seeds)
+        assert err == [0] * n
+        Bp = [T.scalar_base_mult(x) for x in b]
+        beta, cB, _, pfB, err = mta.bob_mid(ss, A["N"], pfA, b, cA, dln(A), dln(B, own=True),
+                                            [s + 7 for s in seeds], B=Bp)
+        assert err == [0] * n
+        alpha, err = mta.alice_end(ss, (A["N"], A["LambdaN"], A["P"], A["Q"]), pfB, dln(A, own=True), cA, cB, B=Bp)
+        assert err == [0] * n
+        assert [(x + y) % q for x, y in zip(alpha, beta)] == [x * y % q for x, y in zip(a, b)]

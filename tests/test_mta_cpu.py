@@ -1,0 +1,94 @@
+"""CPU tests of the MtA path (no GPU): the oracle restatement against its
+golden fixtures and its own algebra, and the host-side C++ helpers the GPU
+path relies on (SHA-512/256 framing, secp256k1, tss-lib random draws) against
+the oracle, through libmpcx_host.so test hooks."""
+import hashlib
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN, H
+from oracle import mta_ref as M
+from oracle import tss_ref as T
+
+
+def _nodes():
+    d = json.load(open(os.path.join(GOLDEN, "node_preparams.json")))
+    return [{k: int(v, 16) for k, v in n.items() if isinstance(v, str) and k != "paillier_source"} for n in d["nodes"]]
+
+
+@pytest.fixture(scope="module")
+def nodes():
+    return _nodes()
+
+
+@pytest.fixture(scope="module")
+def vectors():
+    return json.load(open(os.path.join(GOLDEN, "mta_vectors.json")))["sessions"]
+
+
+@pytest.fixture(scope="module")
+def mta():
+    from mpcium_amd import build, mta
+    build.build()
+    return mta
+
+
+def test_node_preparams_relations(nodes):
+    from oracle import safeprime_ref as sp
+    for n in nodes:
+        assert n["N"] == n["P"] * n["Q"] and n["N"].bit_length() == 2048
+        assert n["NTildei"] == (2 * n["p"] + 1) * (2 * n["q"] + 1)
+        for p in (n["P"], n["Q"], 2 * n["p"] + 1, 2 * n["q"] + 1):
+            assert sp.miller_rabin(p, 8) and sp.miller_rabin((p - 1) // 2, 8)
+        assert n["H2i"] == pow(n["H1i"], n["Alpha"], n["NTildei"])
+        assert n["Alpha"] * n["Beta"] % (n["p"] * n["q"]) == 1
+
+
+def test_oracle_reproduces_golden_alice_init(nodes, vectors):
+    A, B = nodes[0], nodes[1]
+    v = vectors[0]
+    cA, pf = M.alice_init(A["N"], H(v["a"]), B["NTildei"], B["H1i"], B["H2i"], T.Reader(v["seed_a"]))
+    assert cA == H(v["cA"])
+    assert {k: getattr(pf, k) for k in M.RangeProofAlice.__dataclass_fields__} == {k: H(x) for k, x in v["pfA"].items()}
+    assert M.verify_range_alice(pf, A["N"], B["NTildei"], B["H1i"], B["H2i"], cA)
+    # a proof for another ciphertext / a tampered response must not verify
+    assert not M.verify_range_alice(pf, A["N"], B["NTildei"], B["H1i"], B["H2i"], cA + 1)
+    pf.S1 += 1
+    assert not M.verify_range_alice(pf, A["N"], B["NTildei"], B["H1i"], B["H2i"], cA)
+
+
+def test_oracle_golden_relations(vectors):
+    q = M.Q
+    for v in vectors:
+        assert (H(v["alpha"]) + H(v["bob"]["beta"])) % q == H(v["a"]) * H(v["b"]) % q
+        assert (H(v["alpha_wc"]) + H(v["bob_wc"]["beta"])) % q == H(v["a"]) * H(v["wB"]) % q
+        assert T.scalar_base_mult(H(v["wB"])) == (H(v["Bx"]), H(v["By"]))
+
+
+def test_sha512_256_framing_matches_oracle(mta):
+    assert T.sha512_256(b"abc") == hashlib.new("sha512_256", b"\x01" + b"\0" * 7 + b"abc$").digest()
+    cases = [(1,), (0, 5, 2 ** 4095 + 7), tuple(range(1, 14)), (2 ** 2048 - 1, 0, 0)]
+    for ints in cases:
+        assert mta.sha512_256i(*ints) == T.sha512_256i(*ints), ints
+        for tag in (b"", b"session-id", bytes(range(32)) * 5):
+            assert mta.sha512_256i(*ints, tag=tag) == T.sha512_256i_tagged(tag, *ints), (ints, tag)
+
+
+def test_secp256k1_matches_oracle(mta):
+    for k in (1, 2, 3, T.SECP_N - 1, T.SECP_N, T.SECP_N + 5, 2 ** 255 + 12345, M.Q ** 3 - 1, 0xDEADBEEF ** 9):
+        assert mta.scalar_base_mult(k) == T.scalar_base_mult(k), k
+    P = T.scalar_base_mult(0x1234567)
+    for k in (1, 7, T.SECP_N - 2, 2 ** 200 + 1):
+        assert mta.scalar_mult(P, k) == T.ec_mul(k, P), k
+    assert mta.scalar_base_mult(T.SECP_N) is None
+
+
+def test_random_draws_match_oracle(mta, nodes):
+    for less_than, relprime in ((M.Q ** 3, False), (nodes[0]["N"], True), (M.Q * nodes[1]["NTildei"], False),
+                                (M.Q ** 7, False), (1000, False), (257, True)):
+        rd = T.Reader(99)
+        f = T.get_random_positive_relatively_prime_int if relprime else T.get_random_positive_int
+        want = [f(rd, less_than) for _ in range(6)]
+        assert mta.random_draws(99, less_than, 6, relprime) == want, hex(less_than)
