@@ -132,6 +132,16 @@ int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t sess
                               const mpcxh_dln_t* dlnA, uint32_t count, const uint32_t* pfB, const uint32_t* cA,
                               const uint32_t* cB, const uint32_t* B, uint32_t* alpha, uint8_t* err);
 
+/* Config-4 driver: the MtA / MtAwc work of one GG18 signature for each of
+ * `wallets` wallets, signed by the first `signers` of `n_nodes` nodes (keys:
+ * Paillier private keys + own DLN params with factors, width w). Plays every
+ * signer (rounds 1-3 of up:ecdsa/signing, see csrc/host/signing.hpp) and
+ * checks alpha + beta = k gamma and mu + nu = k w (mod q) for every session.
+ * stats_out[8]: round1_s, round2_s, round3_s, total_s, wallets, sessions,
+ * errors, relation_failures. */
+int mpcxh_bench_signing_mta(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
+                            uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out);
+
 /* Host-side helpers of the MtA path, exported as test hooks (no GPU needed):
  * common.SHA512_256i / SHA512_256i_TAGGED (tag == NULL: untagged) over count
  * integers of w words -> 32-byte digest; secp256k1 k*G and k*P (k: w words,

@@ -14,6 +14,7 @@
 #include "paillier.hpp"
 #include "mta.hpp"
 #include "safeprime.hpp"
+#include "signing.hpp"
 
 using namespace mpcx::host;
 
@@ -423,6 +424,22 @@ int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int
     const Nat lt = Nat::from_words(less_than, w);
     for (uint32_t i = 0; i < count; ++i)
       (relprime ? GetRandomPositiveRelativelyPrimeInt(r, lt) : GetRandomPositiveInt(r, lt)).to_words(out + (size_t)i * w, w);
+  });
+}
+
+int mpcxh_bench_signing_mta(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
+                            uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out) {
+  return guard([&] {
+    check_width(w);
+    std::vector<signing::NodeKeys> nodes(n_nodes);
+    for (uint32_t i = 0; i < n_nodes; ++i) {
+      nodes[i].sk = paillier_from(&sks[i], w);
+      nodes[i].dln = dln_from(&dlns[i], w);
+    }
+    const auto st = signing::RunSigningMtA(nodes, (int)signers, wallets, seed);
+    const double v[8] = {st.round1_s, st.round2_s, st.round3_s, st.total_s, (double)st.wallets, (double)st.sessions,
+                         (double)st.errors, (double)st.relation_failures};
+    std::memcpy(stats_out, v, sizeof v);
   });
 }
 

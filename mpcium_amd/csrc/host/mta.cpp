@@ -12,9 +12,9 @@ namespace mpcx::host::mta {
 namespace {
 
 // ------------------------------------------------------------------ ExpSet
-// Modexp requests against one modulus, issued as few GPU launches: requests
-// that share one exponent object (y = N, y = lambda) go to a shared-exponent
-// launch; the rest are grouped by exponent length (the kernel processes the
+// Modexp requests against one modulus, issued as few GPU launches: large
+// groups of requests that share one exponent object (y = N, y = lambda) go to
+// a shared-exponent launch; the rest are grouped by exponent length (the kernel processes the
 // group's longest exponent, so lengths within a group differ by <= 1/8).
 // Products base^e * mul run fused (mpcx_modexp_mul_batch).
 class ExpSet {
@@ -30,10 +30,12 @@ class ExpSet {
     for (size_t i = 0; i < reqs_.size(); ++i) by_e[reqs_[i].e].push_back(i);
     std::vector<size_t> rest;
     for (auto& kv : by_e) {
-      if (kv.second.size() >= 2) {
+      // a shared-exponent launch only for a large group (y = N, y = lambda);
+      // a session's own e used by two requests stays in the per-operand groups
+      if (kv.second.size() >= 64 || kv.second.size() == reqs_.size()) {
         launch(kv.second, true);
       } else {
-        rest.push_back(kv.second[0]);
+        rest.insert(rest.end(), kv.second.begin(), kv.second.end());
       }
     }
     std::sort(rest.begin(), rest.end(),

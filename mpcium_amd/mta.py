@@ -45,6 +45,7 @@ SIGNATURES = [
     ("mpcxh_secp_scalar_base_mult", _i, [_vp, _u32, _vp]),
     ("mpcxh_secp_scalar_mult", _i, [_vp, _vp, _u32, _vp]),
     ("mpcxh_random_draws", _i, [_u64, _vp, _u32, _i, _u32, _vp]),
+    ("mpcxh_bench_signing_mta", _i, [_u32, _vp, _vp, _u32, _u32, _u32, _u64, _vp]),
 ]
 
 _bound = False
@@ -259,3 +260,17 @@ def random_draws(seed: int, less_than: int, count: int, relprime: bool = False) 
     o = np.zeros((count, W), dtype="<u4")
     _check(lib().mpcxh_random_draws(seed, L.ctypes.data, W, 1 if relprime else 0, count, o.ctypes.data))
     return words_to_ints(o)
+
+
+def bench_signing_mta(nodes: Sequence[Dict[str, int]], signers: int, wallets: int, seed: int = 0x5167) -> dict:
+    """Config-4 driver (csrc/host/signing.hpp): the MtA work of one signature
+    for each of `wallets` wallets. nodes: dicts with N, LambdaN, P, Q, NTildei,
+    H1i, H2i, p, q (node_preparams.json fields)."""
+    k = _Keep()
+    sks = (PaillierKey * len(nodes))(*[_paillier(k, n["N"], n["LambdaN"], n["P"], n["Q"]) for n in nodes])
+    dlns = (DLN * len(nodes))(*[_dln(k, {"NTilde": n["NTildei"], "h1": n["H1i"], "h2": n["H2i"],
+                                         "P": 2 * n["p"] + 1, "Q": 2 * n["q"] + 1}) for n in nodes])
+    st = np.zeros(8, dtype=np.float64)
+    _check(lib().mpcxh_bench_signing_mta(W, sks, dlns, len(nodes), signers, wallets, seed, st.ctypes.data))
+    keys = ["round1_s", "round2_s", "round3_s", "total_s", "wallets", "sessions", "errors", "relation_failures"]
+    return dict(zip(keys, [float(x) for x in st]))
