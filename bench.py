@@ -97,6 +97,100 @@ def cpu_baseline(N: int, seconds: float, threads: int):
                       f"4-bit window); Go/tss-lib absent from the image"}
 
 
+def load_nodes():
+    with open(os.path.join(ROOT, "tests", "golden", "node_preparams.json")) as f:
+        d = json.load(f)
+    return [{k: int(v, 16) for k, v in n.items() if isinstance(v, str) and k != "paillier_source"}
+            for n in d["nodes"]]
+
+
+def _signing_worker(args):
+    """One process of the signing CPU baseline: 2-signer MtA/MtAwc work
+    (oracle/mta_ref.py with the C restatement of Go's expNN), ordered signer
+    pair by pair, until the deadline; returns completed pairs (2 per signature)."""
+    deadline, seed = args
+    from oracle import mta_ref as M
+    from oracle import tss_ref as T
+    M.use_go_modexp()
+    nodes = load_nodes()
+    rd = T.Reader(seed)
+    pairs = 0
+    while time.time() < deadline:
+        k, g, w = (T.get_random_positive_int(rd, M.Q) for _ in range(3))
+        ss = rd.read(32)
+        i, j = pairs % 2, 1 - pairs % 2
+        A, B = nodes[i], nodes[j]
+        cA, pf = M.alice_init(A["N"], k, B["NTildei"], B["H1i"], B["H2i"], rd)
+        Wj = T.scalar_base_mult(w)
+        _, cB, _, piB = M.bob_mid(ss, A["N"], pf, g, cA, A["NTildei"], A["H1i"], A["H2i"], B["NTildei"],
+                                  B["H1i"], B["H2i"], rd)
+        _, cBw, _, piBw = M.bob_mid(ss, A["N"], pf, w, cA, A["NTildei"], A["H1i"], A["H2i"], B["NTildei"],
+                                    B["H1i"], B["H2i"], rd, B=Wj, wc=True)
+        M.alice_end(ss, A["N"], piB, A["H1i"], A["H2i"], cA, cB, A["NTildei"], A["LambdaN"])
+        M.alice_end(ss, A["N"], piBw, A["H1i"], A["H2i"], cA, cBw, A["NTildei"], A["LambdaN"], B=Wj, wc=True)
+        if time.time() <= deadline:
+            pairs += 1
+    return pairs
+
+
+def cpu_baseline_signing(seconds: float, procs: int):
+    """2-of-3 signing's MtA work on host cores: the oracle restatement of
+    tss-lib's MtA (oracle/mta_ref.py) with exponentiations by the C
+    restatement of Go's nat.expNN, one process per core."""
+    from concurrent.futures import ProcessPoolExecutor
+    from oracle import crosscheck as cc
+    if cc.load_c_oracle() is None:
+        return None
+    t0 = time.time()
+    deadline = t0 + seconds
+    import multiprocessing as mp
+    with ProcessPoolExecutor(procs, mp_context=mp.get_context("fork")) as ex:
+        n = sum(ex.map(_signing_worker, [(deadline, 0x51C0 + i) for i in range(procs)]))
+    el = max(time.time() - t0, seconds)
+    return {"value": n / 2 / el, "unit": "sigs/s", "cores": procs, "kind": "port",
+            "sample": f"{n} ordered signer pairs = {n / 2:g} 2-signer signatures' MtA/MtAwc (per pair: AliceInit, "
+                      f"BobMid, BobMidWC, AliceEnd, AliceEndWC, all proofs verified) in {el:.1f} s on {procs} "
+                      f"processes; "
+                      f"oracle/mta_ref.py with Go expNN restated in C (oracle/gomodexp.c)"}
+
+
+def signing_line(args, world, rank):
+    """Config 4 (BASELINE.json): 2-of-3 ECDSA signing's MtA / MtAwc work with
+    range proofs, `wallets` wallets per GPU (csrc/host/signing.hpp). Each rank
+    signs its own wallets (weak scaling); value = all ranks' wallets / max time."""
+    import torch
+    import torch.distributed as dist
+    from mpcium_amd import host as mhost
+    from mpcium_amd import mta
+    from mpcium_amd.shard import max_over_ranks
+    mhost.init(int(os.environ.get("LOCAL_RANK", "0")))
+    nodes = load_nodes()
+    warm = mta.bench_signing_mta(nodes, args.signers, 256, seed=0x5167 + 7919 * rank)
+    if warm["errors"] or warm["relation_failures"]:
+        raise SystemExit(f"rank {rank}: signing warmup failed: {warm}")
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    st = mta.bench_signing_mta(nodes, args.signers, args.wallets, seed=0x5168 + 7919 * rank)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    el = time.perf_counter() - t0
+    if st["errors"] or st["relation_failures"]:
+        raise SystemExit(f"rank {rank}: signing MtA failed: {st}")
+    el, r1, r2, r3 = max_over_ranks([el, st["round1_s"], st["round2_s"], st["round3_s"]], world)
+    line = {"metric": f"{args.signers}-of-3 ECDSA sigs/s over {args.wallets * world // 1000}k wallets "
+                      f"(MtA/MtAwc + range proofs, every Paillier/DLN exponentiation on the GPU)",
+            "value": args.wallets * world / el, "unit": "sigs/s", "n_gpus": world,
+            "wallets_per_gpu": args.wallets, "signers": args.signers, "seconds": el,
+            "rounds_s": {"round1_alice_init": r1, "round2_bob_mid": r2, "round3_alice_end": r3},
+            "sessions_per_gpu": st["sessions"], "checked": "alpha+beta == k*gamma, mu+nu == k*w (mod q), every session",
+            "scope": "GG18 signing rounds 1-3 MtA/MtAwc (tss-lib up:crypto/mta); other rounds are secp256k1 work "
+                     "outside the Paillier path", "cpu_baseline": None}
+    return line
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -108,6 +202,10 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=16, help="results checked against CPython pow (untimed)")
     ap.add_argument("--opt", action="append", default=[], help="libmpcx tuning knob key=value (mpcx_set_option)")
+    ap.add_argument("--wallets", type=int, default=10000,
+                    help="config 4: wallets per GPU for the 2-of-3 signing MtA line (0: skip)")
+    ap.add_argument("--signers", type=int, default=2)
+    ap.add_argument("--cpu-sign-seconds", type=float, default=20.0)
     ap.add_argument("--modbits", type=int, default=4096, choices=(2048, 4096),
                     help="4096: x^N mod N^2 (config 2, the bench line); 2048: x^N mod N (Paillier N / N~ class)")
     args = ap.parse_args()
@@ -118,6 +216,11 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # The signing CPU baseline forks worker processes: run it before this
+    # process touches the GPU.
+    sign_cpu = None
+    if args.wallets > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sign_cpu = cpu_baseline_signing(args.cpu_sign_seconds, args.cpu_threads or min(16, os.cpu_count() or 1))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -221,6 +324,9 @@ def main():
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, thr)
+    if args.wallets > 0:
+        result["signing"] = signing_line(args, world, rank)
+        result["signing"]["cpu_baseline"] = sign_cpu
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -35,6 +35,21 @@ from . import tss_ref as T
 
 Q = T.SECP_N  # ec.Params().N for tss.EC() = secp256k1
 
+# Modular exponentiation used by the restatement: CPython pow by default;
+# use_go_modexp() switches to the C restatement of Go's nat.expNN
+# (oracle/gomodexp.c) -- the CPU baseline of bench.py's signing line.
+_pw = pow
+
+
+def use_go_modexp() -> bool:
+    global _pw
+    from .crosscheck import c_expnn, load_c_oracle
+    lib = load_c_oracle()
+    if lib is None:
+        return False
+    _pw = lambda x, y, m: c_expnn(lib, x % m, y, m)  # noqa: E731
+    return True
+
 
 class ErrMessageTooLong(ValueError):
     pass
@@ -49,8 +64,8 @@ def _exp(x: int, y: int, m: int) -> Optional[int]:
     if y < 0:
         if math.gcd(x % m, m) != 1:
             return None
-        return pow(pow(x, -1, m), -y, m)
-    return pow(x, y, m)
+        return _pw(pow(x, -1, m), -y, m)
+    return _pw(x, y, m)
 
 
 # ----------------------------------------------------------------- Paillier
@@ -60,7 +75,7 @@ def encrypt_and_return_randomness(rd: T.Reader, N: int, m: int) -> Tuple[int, in
         raise ErrMessageTooLong()
     x = T.get_random_positive_relatively_prime_int(rd, N)
     N2 = N * N
-    c = pow(N + 1, m, N2) * pow(x, N, N2) % N2
+    c = _pw(N + 1, m, N2) * _pw(x, N, N2) % N2
     return c, x
 
 
@@ -68,7 +83,7 @@ def homo_mult(N: int, m: int, c1: int) -> int:
     N2 = N * N
     if m < 0 or m >= N or c1 < 0 or c1 >= N2:
         raise ErrMessageTooLong()
-    return pow(c1, m, N2)
+    return _pw(c1, m, N2)
 
 
 def homo_add(N: int, c1: int, c2: int) -> int:
@@ -84,8 +99,8 @@ def decrypt(N: int, lam: int, c: int) -> int:
         raise ErrMessageTooLong()
     if math.gcd(c, N2) > 1:
         raise ErrMessageMalFormed()
-    lc = (pow(c, lam, N2) - 1) // N
-    lg = (pow(N + 1, lam, N2) - 1) // N
+    lc = (_pw(c, lam, N2) - 1) // N
+    lg = (_pw(N + 1, lam, N2) - 1) // N
     return lc * pow(lg, -1, N) % N
 
 
@@ -124,12 +139,12 @@ def prove_range_alice(pkN: int, c: int, NTilde: int, h1: int, h2: int, m: int, r
     beta = T.get_random_positive_relatively_prime_int(rd, pkN)
     gamma = T.get_random_positive_int(rd, q3Nt)
     rho = T.get_random_positive_int(rd, qNt)
-    z = pow(h1, m, NTilde) * pow(h2, rho, NTilde) % NTilde
+    z = _pw(h1, m, NTilde) * _pw(h2, rho, NTilde) % NTilde
     N2 = pkN * pkN
-    u = pow(pkN + 1, alpha, N2) * pow(beta, pkN, N2) % N2
-    w = pow(h1, alpha, NTilde) * pow(h2, gamma, NTilde) % NTilde
+    u = _pw(pkN + 1, alpha, N2) * _pw(beta, pkN, N2) % N2
+    w = _pw(h1, alpha, NTilde) * _pw(h2, gamma, NTilde) % NTilde
     e = T.rejection_sample(Q, T.sha512_256i(pkN, pkN + 1, c, z, u, w))
-    s = pow(r, e, pkN) * beta % pkN
+    s = _pw(r, e, pkN) * beta % pkN
     return RangeProofAlice(z, u, w, s, e * m + alpha, e * rho + gamma)
 
 
@@ -151,13 +166,13 @@ def verify_range_alice(pf: RangeProofAlice, pkN: int, NTilde: int, h1: int, h2: 
     c_me = _exp(c, -e, N2)
     if c_me is None:
         return False
-    prod = pow(pkN + 1, pf.S1, N2) * pow(pf.S, pkN, N2) % N2 * c_me % N2
+    prod = _pw(pkN + 1, pf.S1, N2) * _pw(pf.S, pkN, N2) % N2 * c_me % N2
     if pf.U != prod:
         return False
     z_me = _exp(pf.Z, -e, NTilde)
     if z_me is None:
         return False
-    prod = pow(h1, pf.S1, NTilde) * pow(h2, pf.S2, NTilde) % NTilde * z_me % NTilde
+    prod = _pw(h1, pf.S1, NTilde) * _pw(h2, pf.S2, NTilde) % NTilde * z_me % NTilde
     return pf.W == prod
 
 
@@ -176,18 +191,18 @@ def prove_bob_wc(session: bytes, pkN: int, NTilde: int, h1: int, h2: int, c1: in
     gamma = T.get_random_positive_int(rd, q7)
     u = T.scalar_base_mult(alpha) if X is not None else None
     Nt = NTilde
-    z = pow(h1, x, Nt) * pow(h2, rho, Nt) % Nt
-    z_prm = pow(h1, alpha, Nt) * pow(h2, rho_prm, Nt) % Nt
-    t = pow(h1, y, Nt) * pow(h2, sigma, Nt) % Nt
+    z = _pw(h1, x, Nt) * _pw(h2, rho, Nt) % Nt
+    z_prm = _pw(h1, alpha, Nt) * _pw(h2, rho_prm, Nt) % Nt
+    t = _pw(h1, y, Nt) * _pw(h2, sigma, Nt) % Nt
     N2 = pkN * pkN
-    v = pow(c1, alpha, N2) * pow(pkN + 1, gamma, N2) % N2 * pow(beta, pkN, N2) % N2
-    w = pow(h1, gamma, Nt) * pow(h2, tau, Nt) % Nt
+    v = _pw(c1, alpha, N2) * _pw(pkN + 1, gamma, N2) % N2 * _pw(beta, pkN, N2) % N2
+    w = _pw(h1, gamma, Nt) * _pw(h2, tau, Nt) % Nt
     if X is None:
         eh = T.sha512_256i_tagged(session, pkN, pkN + 1, c1, c2, z, z_prm, t, v, w)
     else:
         eh = T.sha512_256i_tagged(session, pkN, pkN + 1, X[0], X[1], c1, c2, u[0], u[1], z, z_prm, t, v, w)
     e = T.rejection_sample(Q, eh)
-    s = pow(r, e, pkN) * beta % pkN
+    s = _pw(r, e, pkN) * beta % pkN
     return ProofBob(z, z_prm, t, v, w, s, e * x + alpha, e * rho + rho_prm, e * y + gamma, e * sigma + tau, u)
 
 
@@ -219,14 +234,14 @@ def verify_bob_wc(pf: ProofBob, session: bytes, pkN: int, NTilde: int, h1: int, 
         xeu = T.ec_add(T.ec_mul(e, X), pf.U)
         if xeu is None or g_s1 != xeu:
             return False
-    left = pow(h1, pf.S1, Nt) * pow(h2, pf.S2, Nt) % Nt
-    if left != pow(pf.Z, e, Nt) * pf.ZPrm % Nt:
+    left = _pw(h1, pf.S1, Nt) * _pw(h2, pf.S2, Nt) % Nt
+    if left != _pw(pf.Z, e, Nt) * pf.ZPrm % Nt:
         return False
-    left = pow(h1, pf.T1, Nt) * pow(h2, pf.T2, Nt) % Nt
-    if left != pow(pf.T, e, Nt) * pf.W % Nt:
+    left = _pw(h1, pf.T1, Nt) * _pw(h2, pf.T2, Nt) % Nt
+    if left != _pw(pf.T, e, Nt) * pf.W % Nt:
         return False
-    left = pow(c1, pf.S1, N2) * pow(pf.S, pkN, N2) % N2 * pow(pkN + 1, pf.T1, N2) % N2
-    return left == pow(c2, e, N2) * pf.V % N2
+    left = _pw(c1, pf.S1, N2) * _pw(pf.S, pkN, N2) % N2 * _pw(pkN + 1, pf.T1, N2) % N2
+    return left == _pw(c2, e, N2) * pf.V % N2
 
 
 # ----------------------------------------------------------------- protocol
