@@ -16,6 +16,8 @@
  *   mpcxh_safe_primes            up:common/safe_prime.go GetRandomSafePrimesConcurrent
  *   mpcxh_generate_preparams     up:ecdsa/keygen/prepare.go GeneratePreParams,
  *                                called at /root/reference/pkg/mpc/node.go:69
+ *   mpcxh_dln_*, mpcxh_mod_*,    up:crypto/dlnproof, up:crypto/modproof,
+ *   mpcxh_fac_*_batch            up:crypto/facproof (keygen / reshare proofs)
  *   mpcxh_mta_*_batch            up:crypto/mta/{share_protocol,range_proof,proofs}.go
  *                                (AliceInit, BobMid[WC], AliceEnd[WC], the
  *                                 range / Bob proofs and their Verify)
@@ -131,6 +133,41 @@ int mpcxh_mta_verify_bob_batch(uint32_t w, const uint8_t* sessions, uint32_t ses
 int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* skA,
                               const mpcxh_dln_t* dlnA, uint32_t count, const uint32_t* pfB, const uint32_t* cA,
                               const uint32_t* cB, const uint32_t* B, uint32_t* alpha, uint8_t* err);
+
+/* ---------------------------------------------------------------- keygen proofs
+ * Batched mirror of tss-lib v2.0.2's DLN (up:crypto/dlnproof, 128 iterations),
+ * Paillier-Blum modulus (up:crypto/modproof, 80 iterations) and no-small-factor
+ * (up:crypto/facproof) proofs: keygen round 1-3 and reshare
+ * (/root/reference/pkg/mpc/ecdsa_keygen_session.go:85-92,
+ * /root/reference/pkg/mpc/ecdsa_resharing_session.go:132-143). A batch holds
+ * `count` proofs over the same public parameters; integers are `w` words
+ * (w >= 160: FacProof's v and sigma reach ~4.9 kbit), seeds[i] is proof i's
+ * io.Reader (CounterDRBG), sessions are count x session_len bytes.
+ *   DLN proof: alpha (count x 128 x w), t (count x 128 x w)
+ *   Mod proof: W (count x w), X (count x 80 x w), A, B (count x w), Z (count x 80 x w)
+ *   Fac proof: count x 11 x w fields P, Q, A, B, T, Sigma, Z1, Z2, W1, W2, |V|
+ *              and v_neg[count] (sign of V) */
+#define MPCXH_PROOF_WORDS 160
+#define MPCXH_DLN_ITERATIONS 128
+#define MPCXH_MOD_ITERATIONS 80
+#define MPCXH_FAC_FIELDS 11
+int mpcxh_dln_prove_batch(uint32_t w, const uint32_t* h1, const uint32_t* h2, const uint32_t* x, const uint32_t* p,
+                          const uint32_t* q, const uint32_t* N, uint32_t count, const uint64_t* seeds, uint32_t* alpha,
+                          uint32_t* t);
+int mpcxh_dln_verify_batch(uint32_t w, const uint32_t* h1, const uint32_t* h2, const uint32_t* N, uint32_t count,
+                           const uint32_t* alpha, const uint32_t* t, uint8_t* ok);
+int mpcxh_mod_prove_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N,
+                          const uint32_t* P, const uint32_t* Q, uint32_t count, const uint64_t* seeds, uint32_t* W,
+                          uint32_t* X, uint32_t* A, uint32_t* B, uint32_t* Z);
+int mpcxh_mod_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N,
+                           uint32_t count, const uint32_t* W, const uint32_t* X, const uint32_t* A, const uint32_t* B,
+                           const uint32_t* Z, uint8_t* ok);
+int mpcxh_fac_prove_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N0,
+                          const uint32_t* NCap, const uint32_t* s, const uint32_t* t, const uint32_t* N0p,
+                          const uint32_t* N0q, uint32_t count, const uint64_t* seeds, uint32_t* pf, uint8_t* v_neg);
+int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N0,
+                           const uint32_t* NCap, const uint32_t* s, const uint32_t* t, uint32_t count,
+                           const uint32_t* pf, const uint8_t* v_neg, uint8_t* ok);
 
 /* Config-4 driver: the MtA / MtAwc work of one GG18 signature for each of
  * `wallets` wallets, signed by the first `signers` of `n_nodes` nodes (keys:

@@ -390,3 +390,39 @@ bool coprime_odd(const Nat& x, const Nat& m) {
 }
 
 }  // namespace mpcx::host
+
+namespace mpcx::host {
+
+Nat isqrt(const Nat& n) {
+  if (n.is_zero()) return Nat();
+  // Newton from above: x0 = 2^ceil(bits/2) >= sqrt(n)
+  Nat x = Nat(1) << ((n.bit_len() + 1) / 2);
+  for (;;) {
+    Nat y = (x + n / x) >> 1;
+    if (!(y < x)) return x;
+    x = y;
+  }
+}
+
+int jacobi(const Nat& a_in, const Nat& n_in) {
+  if (!n_in.is_odd()) throw std::invalid_argument("jacobi: n must be odd");
+  Nat a = a_in % n_in, n = n_in;
+  int j = 1;
+  while (!a.is_zero()) {
+    uint32_t z = 0;
+    while (!a.bit(z)) ++z;
+    if (z) {
+      a = a >> z;
+      const uint32_t n8 = (uint32_t)(n.low64() & 7u);
+      if ((z & 1u) && (n8 == 3 || n8 == 5)) j = -j;
+    }
+    // reciprocity: swap, flip if both are 3 mod 4
+    if ((a.low64() & 3u) == 3 && (n.low64() & 3u) == 3) j = -j;
+    Nat r = n % a;
+    n = a;
+    a = r;
+  }
+  return n == Nat(1) ? j : 0;
+}
+
+}  // namespace mpcx::host

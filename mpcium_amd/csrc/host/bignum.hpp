@@ -58,6 +58,10 @@ Nat gcd(Nat a, Nat b);
 // gcd(x, m) == 1 for odd m > 0 (binary GCD on 64-bit limbs; the validity
 // checks of the MtA proofs and GetRandomPositiveRelativelyPrimeInt)
 bool coprime_odd(const Nat& x, const Nat& m);
+// floor(sqrt(n)) (Go (*Int).Sqrt)
+Nat isqrt(const Nat& n);
+// Jacobi symbol (a | n) for odd n > 0 (Go big.Jacobi)
+int jacobi(const Nat& a, const Nat& n);
 
 // Signed integer (sign-magnitude like Go's big.Int; zero is never negative).
 struct Int {

@@ -13,6 +13,7 @@
 #include "modint.hpp"
 #include "paillier.hpp"
 #include "mta.hpp"
+#include "proofs.hpp"
 #include "safeprime.hpp"
 #include "signing.hpp"
 
@@ -440,6 +441,123 @@ int mpcxh_bench_signing_mta(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh
     const double v[8] = {st.round1_s, st.round2_s, st.round3_s, st.total_s, (double)st.wallets, (double)st.sessions,
                          (double)st.errors, (double)st.relation_failures};
     std::memcpy(stats_out, v, sizeof v);
+  });
+}
+
+// ------------------------------------------------------------------ keygen proofs
+static void check_pw(uint32_t w) {
+  if (w < MPCXH_PROOF_WORDS) throw std::invalid_argument("proof integer width must be >= 160 words");
+}
+static Nat one_nat(const uint32_t* p, uint32_t w) {
+  if (!p) throw std::invalid_argument("null integer");
+  return Nat::from_words(p, w);
+}
+
+int mpcxh_dln_prove_batch(uint32_t w, const uint32_t* h1, const uint32_t* h2, const uint32_t* x, const uint32_t* p,
+                          const uint32_t* q, const uint32_t* N, uint32_t count, const uint64_t* seeds, uint32_t* alpha,
+                          uint32_t* t) {
+  return guard([&] {
+    check_pw(w);
+    std::vector<CounterDRBG> drbgs;
+    const auto rd = readers(seeds, count, &drbgs);
+    const auto pf = proofs::DLNProveBatch(one_nat(h1, w), one_nat(h2, w), one_nat(x, w), one_nat(p, w),
+                                          one_nat(q, w), one_nat(N, w), rd);
+    for (uint32_t i = 0; i < count; ++i)
+      for (int k = 0; k < proofs::kDLNIterations; ++k) {
+        const size_t off = ((size_t)i * proofs::kDLNIterations + k) * w;
+        put(pf[i].Alpha[k], alpha + off, w);
+        put(pf[i].T[k], t + off, w);
+      }
+  });
+}
+
+int mpcxh_dln_verify_batch(uint32_t w, const uint32_t* h1, const uint32_t* h2, const uint32_t* N, uint32_t count,
+                           const uint32_t* alpha, const uint32_t* t, uint8_t* ok) {
+  return guard([&] {
+    check_pw(w);
+    std::vector<proofs::DLNProof> pf(count);
+    for (uint32_t i = 0; i < count; ++i) {
+      pf[i].Alpha = nats(alpha + (size_t)i * proofs::kDLNIterations * w, w, proofs::kDLNIterations);
+      pf[i].T = nats(t + (size_t)i * proofs::kDLNIterations * w, w, proofs::kDLNIterations);
+    }
+    const auto v = proofs::DLNVerifyBatch(one_nat(h1, w), one_nat(h2, w), one_nat(N, w), pf);
+    std::memcpy(ok, v.data(), count);
+  });
+}
+
+int mpcxh_mod_prove_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N,
+                          const uint32_t* P, const uint32_t* Q, uint32_t count, const uint64_t* seeds, uint32_t* W,
+                          uint32_t* X, uint32_t* A, uint32_t* B, uint32_t* Z) {
+  return guard([&] {
+    check_pw(w);
+    std::vector<CounterDRBG> drbgs;
+    const auto rd = readers(seeds, count, &drbgs);
+    const auto pf = proofs::ModProveBatch(sessions_from(sessions, session_len, count), one_nat(N, w), one_nat(P, w),
+                                          one_nat(Q, w), rd);
+    for (uint32_t i = 0; i < count; ++i) {
+      put(pf[i].W, W + (size_t)i * w, w);
+      put(pf[i].A, A + (size_t)i * w, w);
+      put(pf[i].B, B + (size_t)i * w, w);
+      store(pf[i].X, X + (size_t)i * proofs::kModIterations * w, w);
+      store(pf[i].Z, Z + (size_t)i * proofs::kModIterations * w, w);
+    }
+  });
+}
+
+int mpcxh_mod_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N,
+                           uint32_t count, const uint32_t* W, const uint32_t* X, const uint32_t* A, const uint32_t* B,
+                           const uint32_t* Z, uint8_t* ok) {
+  return guard([&] {
+    check_pw(w);
+    std::vector<proofs::ModProof> pf(count);
+    for (uint32_t i = 0; i < count; ++i) {
+      pf[i].W = Nat::from_words(W + (size_t)i * w, w);
+      pf[i].A = Nat::from_words(A + (size_t)i * w, w);
+      pf[i].B = Nat::from_words(B + (size_t)i * w, w);
+      pf[i].X = nats(X + (size_t)i * proofs::kModIterations * w, w, proofs::kModIterations);
+      pf[i].Z = nats(Z + (size_t)i * proofs::kModIterations * w, w, proofs::kModIterations);
+    }
+    const auto v = proofs::ModVerifyBatch(sessions_from(sessions, session_len, count), one_nat(N, w), pf);
+    std::memcpy(ok, v.data(), count);
+  });
+}
+
+int mpcxh_fac_prove_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N0,
+                          const uint32_t* NCap, const uint32_t* s, const uint32_t* t, const uint32_t* N0p,
+                          const uint32_t* N0q, uint32_t count, const uint64_t* seeds, uint32_t* pf, uint8_t* v_neg) {
+  return guard([&] {
+    check_pw(w);
+    std::vector<CounterDRBG> drbgs;
+    const auto rd = readers(seeds, count, &drbgs);
+    const auto out = proofs::FacProveBatch(sessions_from(sessions, session_len, count), one_nat(N0, w),
+                                           one_nat(NCap, w), one_nat(s, w), one_nat(t, w), one_nat(N0p, w),
+                                           one_nat(N0q, w), rd);
+    for (uint32_t i = 0; i < count; ++i) {
+      uint32_t* b = pf + (size_t)i * MPCXH_FAC_FIELDS * w;
+      const Nat* f[] = {&out[i].P, &out[i].Q, &out[i].A, &out[i].B, &out[i].T, &out[i].Sigma,
+                        &out[i].Z1, &out[i].Z2, &out[i].W1, &out[i].W2, &out[i].V.mag};
+      for (int k = 0; k < MPCXH_FAC_FIELDS; ++k) put(*f[k], b + (size_t)k * w, w);
+      v_neg[i] = out[i].V.neg ? 1 : 0;
+    }
+  });
+}
+
+int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N0,
+                           const uint32_t* NCap, const uint32_t* s, const uint32_t* t, uint32_t count,
+                           const uint32_t* pf, const uint8_t* v_neg, uint8_t* ok) {
+  return guard([&] {
+    check_pw(w);
+    std::vector<proofs::FacProof> in(count);
+    for (uint32_t i = 0; i < count; ++i) {
+      const uint32_t* b = pf + (size_t)i * MPCXH_FAC_FIELDS * w;
+      Nat* f[] = {&in[i].P, &in[i].Q, &in[i].A, &in[i].B, &in[i].T, &in[i].Sigma,
+                  &in[i].Z1, &in[i].Z2, &in[i].W1, &in[i].W2};
+      for (int k = 0; k < 10; ++k) *f[k] = Nat::from_words(b + (size_t)k * w, w);
+      in[i].V = Int(Nat::from_words(b + (size_t)10 * w, w), v_neg && v_neg[i]);
+    }
+    const auto v = proofs::FacVerifyBatch(sessions_from(sessions, session_len, count), one_nat(N0, w),
+                                          one_nat(NCap, w), one_nat(s, w), one_nat(t, w), in);
+    std::memcpy(ok, v.data(), count);
   });
 }
 

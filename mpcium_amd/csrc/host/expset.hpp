@@ -1,0 +1,80 @@
+// expset.hpp -- batches of modular exponentiations against one modulus,
+// issued as few GPU launches (libmpcx.so through Engine). Used by the MtA
+// (mta.cpp) and keygen-proof (proofs.cpp) batch mirrors.
+#pragma once
+
+#include <algorithm>
+#include <map>
+#include <vector>
+
+#include "bignum.hpp"
+#include "engine.hpp"
+
+namespace mpcx::host {
+
+// ------------------------------------------------------------------ ExpSet
+// Modexp requests against one modulus, issued as few GPU launches: large
+// groups of requests that share one exponent object (y = N, y = lambda) go to
+// a shared-exponent launch; the rest are grouped by exponent length (the kernel processes the
+// group's longest exponent, so lengths within a group differ by <= 1/8).
+// Products base^e * mul run fused (mpcx_modexp_mul_batch).
+class ExpSet {
+ public:
+  explicit ExpSet(const Nat& m) : m_(m) {}
+  void add(const Nat& base, const Nat& e, Nat* out, const Nat* mul = nullptr) {
+    reqs_.push_back({&base, &e, mul, out});
+  }
+  size_t size() const { return reqs_.size(); }
+  void run() {
+    if (reqs_.empty()) return;
+    std::map<const Nat*, std::vector<size_t>> by_e;
+    for (size_t i = 0; i < reqs_.size(); ++i) by_e[reqs_[i].e].push_back(i);
+    std::vector<size_t> rest;
+    for (auto& kv : by_e) {
+      // a shared-exponent launch only for a large group (y = N, y = lambda);
+      // a session's own e used by two requests stays in the per-operand groups
+      if (kv.second.size() >= 64 || kv.second.size() == reqs_.size()) {
+        launch(kv.second, true);
+      } else {
+        rest.insert(rest.end(), kv.second.begin(), kv.second.end());
+      }
+    }
+    std::sort(rest.begin(), rest.end(),
+              [&](size_t a, size_t b) { return reqs_[a].e->bit_len() < reqs_[b].e->bit_len(); });
+    size_t g0 = 0;
+    while (g0 < rest.size()) {
+      const uint32_t lo = reqs_[rest[g0]].e->bit_len();
+      size_t g1 = g0 + 1;
+      while (g1 < rest.size() && reqs_[rest[g1]].e->bit_len() <= lo + lo / 8 + 32) ++g1;
+      launch(std::vector<size_t>(rest.begin() + (long)g0, rest.begin() + (long)g1), false);
+      g0 = g1;
+    }
+    reqs_.clear();
+  }
+
+ private:
+  struct Req {
+    const Nat* b;
+    const Nat* e;
+    const Nat* mul;
+    Nat* out;
+  };
+  void launch(const std::vector<size_t>& idx, bool shared) {
+    std::vector<Nat> bases, exps, muls;
+    bases.reserve(idx.size());
+    bool any_mul = false;
+    for (size_t i : idx) any_mul |= reqs_[i].mul != nullptr;
+    for (size_t i : idx) {
+      bases.push_back(*reqs_[i].b);
+      if (!shared) exps.push_back(*reqs_[i].e);
+      if (any_mul) muls.push_back(reqs_[i].mul ? *reqs_[i].mul : Nat(1));
+    }
+    if (shared) exps.push_back(*reqs_[idx[0]].e);
+    std::vector<Nat> r = Engine::get().exp(m_, bases, exps, any_mul ? &muls : nullptr);
+    for (size_t j = 0; j < idx.size(); ++j) *reqs_[idx[j]].out = std::move(r[j]);
+  }
+  const Nat m_;  // by value: callers pass temporaries (pk.NSquare())
+  std::vector<Req> reqs_;
+};
+
+}  // namespace mpcx::host

@@ -1,0 +1,144 @@
+"""ctypes binding of the batched keygen / reshare proofs in libmpcx_host.so
+(include/mpcx_host.h "keygen proofs"; C++ in csrc/host/proofs.cpp): tss-lib
+v2.0.2 up:crypto/dlnproof, up:crypto/modproof, up:crypto/facproof with a batch
+dimension (many proofs over the same public parameters). Every
+exponentiation runs on the GPU through libmpcx.so. Proofs are dicts keyed by
+the Go field names."""
+from __future__ import annotations
+
+import ctypes
+from typing import List, Optional, Sequence
+
+import numpy as np
+
+from . import host as _host
+from .mpcx import ints_to_words, words_to_ints
+
+W = 160  # integer width in 32-bit words (FacProof's v reaches ~4.9 kbit)
+DLN_ITERATIONS, MOD_ITERATIONS = 128, 80
+FAC_FIELDS = ["P", "Q", "A", "B", "T", "Sigma", "Z1", "Z2", "W1", "W2", "V"]
+
+_vp, _u32, _u64, _i = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_int
+
+SIGNATURES = [
+    ("mpcxh_dln_prove_batch", _i, [_u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+    ("mpcxh_dln_verify_batch", _i, [_u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+    ("mpcxh_mod_prove_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("mpcxh_mod_verify_batch", _i, [_u32, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("mpcxh_fac_prove_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+    ("mpcxh_fac_verify_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+]
+_bound = False
+
+
+def lib():
+    global _bound
+    l = _host.lib()
+    if not _bound:
+        for name, res, args in SIGNATURES:
+            f = getattr(l, name)
+            f.restype, f.argtypes = res, args
+        _bound = True
+    return l
+
+
+def _one(v: int) -> np.ndarray:
+    return np.ascontiguousarray(ints_to_words([v], W)[0])
+
+
+def _col(vals: Sequence[int]) -> np.ndarray:
+    return np.ascontiguousarray(ints_to_words(list(vals), W))
+
+
+def _sessions(ss: Sequence[bytes]):
+    n = len(ss[0]) if ss else 0
+    if any(len(s) != n for s in ss):
+        raise ValueError("session ids must have equal length")
+    return np.frombuffer(b"".join(ss), dtype=np.uint8).copy(), n
+
+
+def _rows(a: np.ndarray, count: int, per: int) -> List[List[int]]:
+    v = words_to_ints(a.reshape(count * per, W))
+    return [v[i * per:(i + 1) * per] for i in range(count)]
+
+
+def dln_prove(h1: int, h2: int, x: int, p: int, q: int, N: int, seeds: Sequence[int]) -> List[dict]:
+    """NewDLNProof for len(seeds) proofs -> [{"Alpha": [...], "T": [...]}]."""
+    n = len(seeds)
+    args = [_one(v) for v in (h1, h2, x, p, q, N)]
+    S = np.array(seeds, dtype=np.uint64)
+    al = np.zeros((n, DLN_ITERATIONS * W), dtype="<u4")
+    t = np.zeros_like(al)
+    _host._check(lib().mpcxh_dln_prove_batch(W, *[a.ctypes.data for a in args], n, S.ctypes.data, al.ctypes.data,
+                                             t.ctypes.data))
+    return [{"Alpha": a, "T": b} for a, b in zip(_rows(al, n, DLN_ITERATIONS), _rows(t, n, DLN_ITERATIONS))]
+
+
+def dln_verify(h1: int, h2: int, N: int, pfs: Sequence[dict]) -> List[bool]:
+    n = len(pfs)
+    args = [_one(v) for v in (h1, h2, N)]
+    al = _col([v for p in pfs for v in p["Alpha"]])
+    t = _col([v for p in pfs for v in p["T"]])
+    ok = np.zeros(n, dtype=np.uint8)
+    _host._check(lib().mpcxh_dln_verify_batch(W, *[a.ctypes.data for a in args], n, al.ctypes.data, t.ctypes.data,
+                                              ok.ctypes.data))
+    return [bool(x) for x in ok]
+
+
+def mod_prove(sessions: Sequence[bytes], N: int, P: int, Q: int, seeds: Sequence[int]) -> List[dict]:
+    n = len(seeds)
+    ss, sl = _sessions(sessions)
+    args = [_one(v) for v in (N, P, Q)]
+    S = np.array(seeds, dtype=np.uint64)
+    Wv, A, B = (np.zeros((n, W), dtype="<u4") for _ in range(3))
+    X, Z = (np.zeros((n, MOD_ITERATIONS * W), dtype="<u4") for _ in range(2))
+    _host._check(lib().mpcxh_mod_prove_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n, S.ctypes.data,
+                                             Wv.ctypes.data, X.ctypes.data, A.ctypes.data, B.ctypes.data,
+                                             Z.ctypes.data))
+    return [{"W": w, "X": x, "A": a, "B": b, "Z": z} for w, x, a, b, z in
+            zip(words_to_ints(Wv), _rows(X, n, MOD_ITERATIONS), words_to_ints(A), words_to_ints(B),
+                _rows(Z, n, MOD_ITERATIONS))]
+
+
+def mod_verify(sessions: Sequence[bytes], N: int, pfs: Sequence[dict]) -> List[bool]:
+    n = len(pfs)
+    ss, sl = _sessions(sessions)
+    Nw = _one(N)
+    Wv, A, B = _col([p["W"] for p in pfs]), _col([p["A"] for p in pfs]), _col([p["B"] for p in pfs])
+    X = _col([v for p in pfs for v in p["X"]])
+    Z = _col([v for p in pfs for v in p["Z"]])
+    ok = np.zeros(n, dtype=np.uint8)
+    _host._check(lib().mpcxh_mod_verify_batch(W, ss.ctypes.data, sl, Nw.ctypes.data, n, Wv.ctypes.data, X.ctypes.data,
+                                              A.ctypes.data, B.ctypes.data, Z.ctypes.data, ok.ctypes.data))
+    return [bool(x) for x in ok]
+
+
+def fac_prove(sessions: Sequence[bytes], N0: int, NCap: int, s: int, t: int, N0p: int, N0q: int,
+              seeds: Sequence[int]) -> List[dict]:
+    n = len(seeds)
+    ss, sl = _sessions(sessions)
+    args = [_one(v) for v in (N0, NCap, s, t, N0p, N0q)]
+    S = np.array(seeds, dtype=np.uint64)
+    pf = np.zeros((n, len(FAC_FIELDS) * W), dtype="<u4")
+    neg = np.zeros(n, dtype=np.uint8)
+    _host._check(lib().mpcxh_fac_prove_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n, S.ctypes.data,
+                                             pf.ctypes.data, neg.ctypes.data))
+    out = []
+    for row, ng in zip(_rows(pf, n, len(FAC_FIELDS)), neg):
+        d = dict(zip(FAC_FIELDS, row))
+        if ng:
+            d["V"] = -d["V"]
+        out.append(d)
+    return out
+
+
+def fac_verify(sessions: Sequence[bytes], N0: int, NCap: int, s: int, t: int, pfs: Sequence[dict]) -> List[bool]:
+    n = len(pfs)
+    ss, sl = _sessions(sessions)
+    args = [_one(v) for v in (N0, NCap, s, t)]
+    pf = _col([abs(p[f]) for p in pfs for f in FAC_FIELDS])
+    neg = np.array([1 if p["V"] < 0 else 0 for p in pfs], dtype=np.uint8)
+    ok = np.zeros(n, dtype=np.uint8)
+    _host._check(lib().mpcxh_fac_verify_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n,
+                                              pf.ctypes.data, neg.ctypes.data, ok.ctypes.data))
+    return [bool(x) for x in ok]

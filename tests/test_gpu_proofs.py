@@ -1,0 +1,96 @@
+"""GPU parity tests of the batched keygen / reshare proofs (rows A13-A14):
+DLN, Paillier-Blum modulus and no-small-factor proofs against the oracle's
+golden proofs (tests/golden/proof_vectors.json, oracle/proofs_ref.py), field
+by field, plus rejection of tampered proofs with the same decisions as the
+oracle."""
+import json
+import os
+
+import pytest
+
+from conftest import GOLDEN, H
+from oracle import proofs_ref as PR
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def pr(gpu):
+    from mpcium_amd import host, proofs
+    host.init(0)
+    return proofs
+
+
+@pytest.fixture(scope="module")
+def nodes():
+    d = json.load(open(os.path.join(GOLDEN, "node_preparams.json")))
+    return [{k: int(v, 16) for k, v in n.items() if isinstance(v, str) and k != "paillier_source"} for n in d["nodes"]]
+
+
+@pytest.fixture(scope="module")
+def vec():
+    return json.load(open(os.path.join(GOLDEN, "proof_vectors.json")))
+
+
+def test_dln_golden_and_rejections(pr, nodes, vec):
+    n0 = nodes[0]
+    Nt = n0["NTildei"]
+    args = [(n0["H1i"], n0["H2i"], n0["Alpha"]), (n0["H2i"], n0["H1i"], n0["Beta"])]
+    for (h1, h2, x), g in zip(args, vec["dln"]):
+        got = pr.dln_prove(h1, h2, x, n0["p"], n0["q"], Nt, [g["seed"], g["seed"] + 1000])
+        assert got[0]["Alpha"] == [H(v) for v in g["Alpha"]]
+        assert got[0]["T"] == [H(v) for v in g["T"]]
+        bad_t = {"Alpha": list(got[1]["Alpha"]), "T": list(got[1]["T"])}
+        bad_t["T"][5] += 1
+        bad_a = {"Alpha": list(got[1]["Alpha"]), "T": list(got[1]["T"])}
+        bad_a["Alpha"][127] = 1  # not in (1, N)
+        ok = pr.dln_verify(h1, h2, Nt, [got[0], got[1], bad_t, bad_a])
+        assert ok == [True, True, False, False]
+        assert PR.dln_verify(PR.DLNProof(bad_t["Alpha"], bad_t["T"]), h1, h2, Nt) is False
+    # wrong statement: the (h2, h1) proof does not verify for (h1, h2)
+    assert pr.dln_verify(n0["H1i"], n0["H2i"], Nt, [got[0]]) == [False]
+
+
+def test_mod_golden_and_rejections(pr, nodes, vec):
+    n0 = nodes[0]
+    ss = bytes.fromhex(vec["session"])
+    g = vec["mod"]
+    got = pr.mod_prove([ss, ss], n0["N"], n0["P"], n0["Q"], [g["seed"], g["seed"] + 1])
+    p = got[0]
+    assert p["W"] == H(g["W"]) and p["A"] == H(g["A"]) and p["B"] == H(g["B"])
+    assert p["X"] == [H(v) for v in g["X"]] and p["Z"] == [H(v) for v in g["Z"]]
+    bad_z = dict(got[1], Z=list(got[1]["Z"]))
+    bad_z["Z"][3] = (bad_z["Z"][3] + 1) % n0["N"]
+    bad_x = dict(got[1], X=list(got[1]["X"]))
+    bad_x["X"][79] = (bad_x["X"][79] * 2) % n0["N"]
+    bad_a = dict(got[1], A=got[1]["A"] ^ 1)
+    other_ss = bytes(32)
+    ok = pr.mod_verify([ss, ss, ss, ss, ss, other_ss], n0["N"], [got[0], got[1], bad_z, bad_x, bad_a, got[0]])
+    assert ok == [True, True, False, False, False, False]
+    # a prime "modulus" is rejected
+    P = n0["P"]
+    assert pr.mod_verify([ss], P, [got[0]]) == [False]
+
+
+def test_fac_golden_and_rejections(pr, nodes, vec):
+    n0, n1 = nodes[0], nodes[1]
+    ss = bytes.fromhex(vec["session"])
+    g = vec["fac"]
+    args = (n0["N"], n1["NTildei"], n1["H1i"], n1["H2i"])
+    got = pr.fac_prove([ss, ss], *args, n0["P"], n0["Q"], [g["seed"], g["seed"] + 1])
+    assert {k: got[0][k] for k in pr.FAC_FIELDS} == {k: H(g[k]) for k in pr.FAC_FIELDS}
+    cases = [got[0], got[1]]
+    for f in ("Z1", "W2", "V", "Sigma", "T"):
+        c = dict(got[1])
+        c[f] += 1
+        cases.append(c)
+    neg = dict(got[1])
+    neg["V"] = -neg["V"]  # exercises the negative-exponent path (must fail)
+    cases.append(neg)
+    ok = pr.fac_verify([ss] * len(cases), *args, cases)
+    assert ok == [True, True] + [False] * (len(cases) - 2)
+    for c, o in zip(cases, ok):
+        assert PR.fac_verify(PR.FacProof(**c), ss, *args) == o
+    # the proof is bound to the verifier's N~
+    n2 = nodes[2]
+    assert pr.fac_verify([ss], n0["N"], n2["NTildei"], n2["H1i"], n2["H2i"], [got[0]]) == [False]

@@ -25,8 +25,9 @@ def test_host_header_symbols(hostlib):
     lib = ctypes.CDLL(hostlib._LIB_PATH)
     for n in names:
         assert hasattr(lib, n), n
-    from mpcium_amd import mta
-    assert names == {n for n, _, _ in hostlib.SIGNATURES} | {n for n, _, _ in mta.SIGNATURES}
+    from mpcium_amd import mta, proofs
+    assert names == ({n for n, _, _ in hostlib.SIGNATURES} | {n for n, _, _ in mta.SIGNATURES}
+                     | {n for n, _, _ in proofs.SIGNATURES})
 
 
 def test_drbg_matches_oracle(hostlib):
