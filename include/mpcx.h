@@ -105,9 +105,11 @@ int mpcx_modexp_batch(mpcx_mod_t mod, uint32_t count,
 /* Same contract with device pointers (d_*) on HIP stream `stream` (a
  * hipStream_t, NULL = default stream). Asynchronous: the results are valid
  * after the stream is synchronised. exp_bits is the bit length of the
- * largest exponent (any value >= it and <= 32*exp_words is correct; the
- * kernel processes ceil(exp_bits/4) 4-bit windows). The first call with a
- * larger batch than before grows the kernel workspace (hipMalloc). */
+ * largest exponent (any value >= it and <= 32*exp_words is correct; per-
+ * operand exponents are processed as ceil(exp_bits/4) 4-bit windows; a shared
+ * exponent's sliding-window schedule is built on `stream` by a one-lane
+ * kernel, so the call stays asynchronous). The first call with a larger
+ * batch than before grows the kernel workspace (hipMalloc). */
 int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count,
                              const uint32_t* d_bases, uint32_t base_words,
                              const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
@@ -167,7 +169,9 @@ int mpcx_stream_sync(void* stream);
  *   "force_geom" -1 (default) or a geometry id (0..6, see mpcx_internal.h) to
  *                run every batch of the matching class in that geometry.
  *   "main_geom"  geometry id: make it the main (throughput) geometry of its
- *                class (A/B of kernel layouts). */
+ *                class (A/B of kernel layouts).
+ *   "sched_width" 0..5 (default 5): cap on the sliding-window width used for
+ *                shared exponents; 0 selects Go's 4-bit fixed window. */
 int mpcx_set_option(const char* key, int value);
 
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):

@@ -30,6 +30,7 @@ extern "C" {
 MPCX_FOR_EACH_GEOM(MPCX_GEOM_DECL)
 hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 }
 
@@ -55,6 +56,7 @@ int g_num_cus = 0;
 int g_geom_slots[MPCX_NUM_GEOMS] = {0};  // resident wavefronts per device, per geometry
 bool g_split = false;                    // narrow-geometry tail launch (measured slower: off)
 int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): one geometry for everything
+int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 uint32_t* g_ws = nullptr;  // exponentiation table workspace
 size_t g_ws_bytes = 0;
@@ -230,6 +232,10 @@ int mpcx_set_option(const char* key, int value) {
   } else if (std::strcmp(key, "force_geom") == 0) {
     if (value < -1 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "force_geom %d out of range", value);
     g_force_geom = value;
+  } else if (std::strcmp(key, "sched_width") == 0) {
+    // cap on the sliding-window width of shared exponents; 0: Go's 4-bit fixed window
+    if (value < 0 || value > MPCX_SCHED_MAX_WIDTH) return fail(MPCX_EINVAL, "sched_width %d out of range", value);
+    g_sched_width = value;
   } else if (std::strcmp(key, "main_geom") == 0) {
     // main (throughput) geometry of the geometry's class
     if (value < 0 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "main_geom %d out of range", value);
@@ -415,8 +421,21 @@ static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* 
     const uint32_t G = (uint32_t)MPCX_GEOM_G(parts[i].geom), K = (uint32_t)MPCX_GEOM_K(parts[i].geom);
     ws_words += (size_t)((parts[i].count + G - 1) / G) * MPCX_TABLE_ENTRIES * K * 64u;
   }
+  // a shared exponent's sliding-window schedule lives after the tables
+  const bool use_sched = exp_shared && exp_bits > 0 && g_sched_width > 0;
+  const size_t sched_off = ws_words;
+  if (use_sched) ws_words += MPCX_SCHED_WORDS(32u * exp_words);
   int rc = ensure_workspace(ws_words * sizeof(uint32_t));
   if (rc) return rc;
+  if (use_sched) {
+    mpcx::ExpSchedArgs sa{};
+    sa.exp = d_exps;
+    sa.exp_words = exp_words;
+    sa.max_width = (uint32_t)g_sched_width;
+    sa.sched = g_ws + sched_off;
+    hipError_t e = mpcx_launch_expsched(&sa, st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_expsched");
+  }
   size_t ws_off = 0;
   for (int i = 0; i < nparts; ++i) {
     const Part& pt = parts[i];
@@ -440,6 +459,7 @@ static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* 
     a.out_words = out_words;
     a.n0inv = mod->n0inv;
     a.exp_shared = exp_shared ? 1 : 0;
+    a.sched = use_sched ? g_ws + sched_off : nullptr;
     hipError_t e = mpcx_launch_modexp(pt.geom, &a, waves, st);
     if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
     ws_off += (size_t)waves * MPCX_TABLE_ENTRIES * K * 64u;

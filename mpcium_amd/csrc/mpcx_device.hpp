@@ -25,9 +25,11 @@
 //    one digit: within a lane by register renaming (the K-iteration block is
 //    unrolled), across lanes by ONE DPP wave_shl of a 28-bit value (the slot's
 //    high part is folded into the next slot first).
-//  * Fixed 4-bit window exponentiation like Go (16-entry table per operand in
-//    a global workspace, lane-coalesced layout); b operands are staged in LDS
-//    and read as group-broadcast ds_read_b32.
+//  * Exponentiation: a shared exponent follows a sliding-window schedule (odd
+//    powers, windows of up to 5 bits, built on the device by k_expsched);
+//    per-operand exponents use Go's fixed 4-bit window. Tables (<= 17 entries
+//    per operand) live in a global workspace, lane-coalesced; b operands are
+//    staged in LDS and read as group-broadcast ds_read_b32.
 //  * MFMA is not used: this is not a dense contraction.
 #pragma once
 #include <hip/hip_runtime.h>
@@ -332,25 +334,38 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     lds_store_digits<K>(bl, p, r2);
   }
   const bool has_mul = a.mul != nullptr;
-  // top window and the table entries actually needed: a shared exponent of at
-  // most one window (e.g. the multiply-only call, e = 1) needs p_1..p_wt only
-  // Control state must stay provably wave-uniform (SGPRs): a shared exponent
-  // is read through readfirstlane, so the compiler keeps the step machine,
-  // the table offsets and the zero-window skip off the VGPR file.
-  const bool shared = a.exp_shared != 0;
+  // Control state must stay provably wave-uniform (SGPRs): the schedule and a
+  // shared exponent are read through readfirstlane, so the compiler keeps the
+  // step machine and the table offsets off the VGPR file.
+  //
+  // A shared exponent e >= 1 follows the sliding-window schedule k_expsched
+  // built from it on the same stream (ExpSched layout in mpcx_internal.h):
+  // odd powers x^1, x^3, ..., x^(2 Tn + 1) in table[0..Tn], z = x^top, then
+  // per entry s squarings and one multiply by an odd power. Windows of up to
+  // 5 bits cost ~E/6 multiplies against Go's E/4 * 15/16; every decision
+  // depends on e only, so the wave stays uniform. Per-operand exponents (and
+  // e = 0) keep Go's 4-bit fixed window: their sequences would diverge.
+  const bool sched = a.exp_shared != 0 && a.sched != nullptr &&
+                     __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_TOP]) != MPCX_SCHED_NONE;
   const uint32_t wt = nw > 0 ? window_of(ex, nw - 1u) : 0u;
+  // table entries built: fixed window p_1..p_T (a shared e < 16 needs p_1..p_e only)
   const uint32_t wt_u = __builtin_amdgcn_readfirstlane(wt);
-  const uint32_t T = (shared && nw <= 1u) ? (wt_u > 1u ? wt_u : 1u) : 15u;
-  const uint32_t nexp = nw > 0 ? 5u * (nw - 1u) : 0u;
+  const uint32_t T = sched ? __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_TN])
+                           : (a.exp_shared && nw <= 1u ? (wt_u > 1u ? wt_u : 1u) : 15u);
+  // exponent steps: schedule entries, or windows below the top one
+  const uint32_t nsteps = sched ? __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_N]) : (nw > 0 ? nw - 1u : 0u);
 
   // Montgomery-step state machine (ONE montmul call site keeps the code small):
   //   PRE : mul*R   = mont(mul, R^2)           -> table[16]   (only with a multiplier)
-  //   TAB : p_i     = mont(x, R^2), mont(p_{i-1}, p_1)  i = 1..T -> table[i]
-  //   EXP : per window below the top one: 4 squarings, then mont(z, p_w)
-  //         (a zero window of a shared exponent is skipped: uniform branch)
+  //   TAB : fixed window: p_i = mont(x, R^2), mont(p_{i-1}, p_1)  i = 1..T -> table[i]
+  //         schedule:     x R = mont(x, R^2) -> table[0]
+  //   TSQ : x^2 R (schedule, Tn > 0)
+  //   STAB: x^(2i+1) R = mont(x^(2i-1) R, x^2 R) -> table[i], i = 1..Tn
+  //   EXP : per step: s squarings, then mont(z, table entry)
+  //         (fixed window: s = 4 and the operand's window, p_0 = R mod m)
   //   MULF: z*mul*R = mont(z*R, mul*R)                          (only with a multiplier)
   //   FIN : z       = mont(z*R, 1) <= m
-  enum { ST_PRE, ST_TAB, ST_EXP, ST_MULF, ST_FIN };
+  enum { ST_PRE, ST_TAB, ST_TSQ, ST_STAB, ST_EXP, ST_MULF, ST_FIN };
   int st;
   uint32_t idx = 1;
   bool sqr = false;  // next montmul is a squaring (B == A)
@@ -363,10 +378,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
   wave_lds_fence();
 
-  // prepares LDS (and state) for exponent step idx, skipping zero windows
+  // Exponent steps (one inlined instance): a step is sq_left squarings, then
+  // one multiply by table[pend] (pend < 0: none).
+  uint32_t sq_left = 0;
+  int pend = -1;  // uniform: table entry, or 0x100 for the operand's own window
   auto prepare_exp = [&] __attribute__((always_inline))() {
     for (;;) {
-      if (idx == nexp) {
+      if (sq_left) {
+        --sq_left;
+        lds_store_digits<K>(bl, p, A);
+        sqr = true;
+        return;
+      }
+      if (pend >= 0) {
+        // fixed window: the operand's window of the step just scheduled (idx - 1)
+        lds_from_table(pend == 0x100 ? window_of(ex, nw - 1u - idx) : (uint32_t)pend);
+        pend = -1;
+        return;
+      }
+      if (idx == nsteps) {
         if (has_mul) {
           st = ST_MULF;
           lds_from_table(16);
@@ -376,22 +406,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         }
         return;
       }
-      if (idx % 5u < 4u) {
-        lds_store_digits<K>(bl, p, A);
-        sqr = true;
-        return;
-      }
-      if (shared) {
-        const uint32_t w = __builtin_amdgcn_readfirstlane(window_of(a.exps, nw - 2u - idx / 5u));
-        if (w == 0u) {
-          ++idx;  // multiplying by Montgomery one is the identity mod m
-          continue;
-        }
-        lds_from_table(w);
+      if (sched) {
+        const uint32_t s = __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_STEPS + idx]);
+        sq_left = s >> 8;
+        pend = (s & 0xFFu) == 0xFFu ? -1 : (int)(s & 0xFFu);
       } else {
-        lds_from_table(window_of(ex, nw - 2u - idx / 5u));
+        sq_left = 4;
+        pend = 0x100;
       }
-      return;
+      ++idx;
     }
   };
 
@@ -403,31 +426,54 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
     sqr = false;
     wave_lds_fence();
+    bool start_exp = false, run_exp = false;
     if (st == ST_PRE) {
       tbl_store(16, A);
       load_digits(a.base, a.base_words);  // LDS still holds R^2
       st = ST_TAB;
       idx = 1;
     } else if (st == ST_TAB) {
+      tbl_store(sched ? 0u : idx, A);
+      if (sched && T > 0u) {
+        lds_store_digits<K>(bl, p, A);
+        sqr = true;
+        st = ST_TSQ;
+      } else if (!sched && idx == 1) {
+        lds_store_digits<K>(bl, p, A);  // B = p_1 for the remaining table steps
+      }
+      if (!sched && idx < T) {
+        ++idx;
+      } else if (st == ST_TAB) {
+        start_exp = true;  // table complete
+      }
+    } else if (st == ST_TSQ) {
+      lds_store_digits<K>(bl, p, A);  // B = x^2 R for the odd-power chain
+      tbl_load(0, A);
+      st = ST_STAB;
+      idx = 1;
+    } else if (st == ST_STAB) {
       tbl_store(idx, A);
-      if (idx == 1) lds_store_digits<K>(bl, p, A);  // B = p_1 for the remaining table steps
       if (idx < T) {
         ++idx;
       } else {
-        tbl_load(shared ? wt_u : wt, A);  // z = p_top (Montgomery one if e = 0)
-        st = ST_EXP;
-        idx = 0;
-        prepare_exp();
+        start_exp = true;
       }
     } else if (st == ST_EXP) {
-      ++idx;
-      prepare_exp();
+      run_exp = true;
     } else if (st == ST_MULF) {
       st = ST_FIN;
       lds_one();
     } else {
       break;  // ST_FIN done
     }
+    if (start_exp) {
+      // z = x^top (schedule) or p_top (fixed window; Montgomery one if e = 0)
+      tbl_load(sched ? __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_TOP]) : wt, A);
+      st = ST_EXP;
+      idx = 0;
+      run_exp = true;
+    }
+    if (run_exp) prepare_exp();
     wave_lds_fence();
   }
 

@@ -42,6 +42,24 @@
 // Montgomery form of the optional multiplier (entry 16)
 #define MPCX_TABLE_ENTRIES 17
 
+// Sliding-window schedule of a shared exponent (built by k_expsched on the
+// launch stream, read by k_modexp through scalar loads):
+//   [TOP]   odd-power table index of the top window (x^(2 top + 1)),
+//           MPCX_SCHED_NONE for e = 0
+//   [TN]    highest odd-power index used (table[0..TN] = x^1, x^3, ...)
+//   [N]     number of steps
+//   [WIDTH] window width (bits) the schedule was built with
+//   [STEPS + i]  (squarings << 8) | odd-power index (0xFF: squarings only)
+#define MPCX_SCHED_TOP 0
+#define MPCX_SCHED_TN 1
+#define MPCX_SCHED_N 2
+#define MPCX_SCHED_WIDTH 3
+#define MPCX_SCHED_STEPS 4
+#define MPCX_SCHED_NONE 0xFFFFFFFFu
+#define MPCX_SCHED_MAX_WIDTH 5  // 2^(w-1) <= 16 odd powers fit table[0..15]
+// schedule words for an exponent of `bits` bits (at most one step per bit)
+#define MPCX_SCHED_WORDS(bits) (MPCX_SCHED_STEPS + (bits) + 1)
+
 namespace mpcx {
 
 struct ModexpArgs {
@@ -61,6 +79,14 @@ struct ModexpArgs {
   uint32_t out_words;
   uint32_t n0inv;       // -m^-1 mod 2^28
   int exp_shared;
+  const uint32_t* sched; // shared exponent: its window schedule (nullptr: fixed window)
+};
+
+struct ExpSchedArgs {
+  const uint32_t* exp;  // shared exponent, exp_words little-endian words
+  uint32_t exp_words;
+  uint32_t max_width;   // cap on the window width (1..MPCX_SCHED_MAX_WIDTH)
+  uint32_t* sched;      // MPCX_SCHED_WORDS(32 * exp_words) words
 };
 
 struct FermatArgs {

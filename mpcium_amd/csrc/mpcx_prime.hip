@@ -1,5 +1,6 @@
 // mpcx_prime.hip -- launchers of the safe-prime kernels (Fermat base 2,
-// Miller-Rabin; thread per candidate) and the device self-test.
+// Miller-Rabin; thread per candidate), the shared-exponent window schedule
+// (k_expsched) and the device self-test.
 #include "mpcx_device.hpp"
 
 namespace mpcx {
@@ -12,6 +13,88 @@ __global__ void k_selftest(uint32_t* out) {
   out[128 + lane] = (uint32_t)__builtin_amdgcn_ds_bpermute(((lane / 7) * 7) * 4, (int)(2000 + lane));
   const uint64_t acc = (uint64_t)(0xFFFFFFF0u + lane) * (0xFFFFFFF7u - lane) + 0xFFFFFFFFFFFFull;
   out[192 + lane] = (uint32_t)(acc >> 32);
+}
+
+// ------------------------------------------------- sliding-window schedule
+// The left-to-right sliding-window decomposition of a shared exponent
+// (layout: MPCX_SCHED_* in mpcx_internal.h), built on the launch stream so
+// the device-buffer API stays asynchronous. One lane: ~E scalar steps over a
+// two-word cache of the exponent, microseconds against the exponentiation.
+// Width w minimises table + multiplies: 2^(w-1) products for x^2 and the odd
+// powers (none for w = 1), plus ~E/(w+1) window multiplies.
+__global__ __launch_bounds__(64) void k_expsched(const ExpSchedArgs a) {
+  if (threadIdx.x != 0) return;
+  const uint32_t* e = a.exp;
+  uint32_t* s = a.sched;
+  int top = -1;
+  for (int i = (int)a.exp_words - 1; i >= 0; --i) {
+    const uint32_t v = e[i];
+    if (v) {
+      top = 32 * i + 31 - __builtin_clz(v);
+      break;
+    }
+  }
+  if (top < 0) {  // e = 0: the kernel takes Go's fixed-window path (z = 1)
+    s[MPCX_SCHED_TOP] = MPCX_SCHED_NONE;
+    s[MPCX_SCHED_TN] = 0;
+    s[MPCX_SCHED_N] = 0;
+    s[MPCX_SCHED_WIDTH] = 0;
+    return;
+  }
+  const int E = top + 1;
+  int w = 1;
+  float best = (float)E / 2.0f;
+  for (int c = 2; c <= (int)a.max_width && c <= MPCX_SCHED_MAX_WIDTH; ++c) {
+    const float cost = (float)(1 << (c - 1)) + (float)E / (float)(c + 1);
+    if (cost < best) {
+      best = cost;
+      w = c;
+    }
+  }
+  uint32_t c0i = ~0u, c0 = 0, c1i = ~0u, c1 = 0;  // two most recent exponent words
+  auto word = [&](uint32_t wi) -> uint32_t {
+    if (wi == c0i) return c0;
+    if (wi == c1i) return c1;
+    const uint32_t v = e[wi];
+    c1i = c0i;
+    c1 = c0;
+    c0i = wi;
+    c0 = v;
+    return v;
+  };
+  auto bit = [&](int i) -> uint32_t { return (word((uint32_t)i >> 5) >> (i & 31)) & 1u; };
+  auto bits = [&](int lo, int len) -> uint32_t {
+    uint32_t v = 0;
+    for (int b = len - 1; b >= 0; --b) v = (v << 1) | bit(lo + b);
+    return v;
+  };
+  // top window: bits [lo, top], lo the lowest set bit within w bits of top
+  int lo = top - w + 1 > 0 ? top - w + 1 : 0;
+  while (!bit(lo)) ++lo;
+  const uint32_t top_ent = (bits(lo, top - lo + 1) - 1u) >> 1;
+  uint32_t tn = top_ent, n = 0, sq = 0;
+  int pos = lo - 1;
+  while (pos >= 0) {
+    if (!bit(pos)) {
+      ++sq;
+      --pos;
+      continue;
+    }
+    lo = pos - w + 1 > 0 ? pos - w + 1 : 0;
+    while (!bit(lo)) ++lo;
+    const int len = pos - lo + 1;
+    const uint32_t ent = (bits(lo, len) - 1u) >> 1;
+    sq += (uint32_t)len;
+    s[MPCX_SCHED_STEPS + n++] = (sq << 8) | ent;
+    tn = ent > tn ? ent : tn;
+    sq = 0;
+    pos = lo - 1;
+  }
+  if (sq) s[MPCX_SCHED_STEPS + n++] = (sq << 8) | 0xFFu;
+  s[MPCX_SCHED_TOP] = top_ent;
+  s[MPCX_SCHED_TN] = tn;
+  s[MPCX_SCHED_N] = n;
+  s[MPCX_SCHED_WIDTH] = (uint32_t)w;
 }
 
 }  // namespace mpcx
@@ -27,6 +110,12 @@ __attribute__((visibility("hidden"))) hipError_t mpcx_launch_fermat2(const mpcx:
 __attribute__((visibility("hidden"))) hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks,
                                                                hipStream_t st) {
   hipLaunchKernelGGL((mpcx::k_mr<MPCX_C0_K, MPCX_WAVES_PER_EU_MR>), dim3(blocks), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a,
+                                                                      hipStream_t st) {
+  hipLaunchKernelGGL(mpcx::k_expsched, dim3(1), dim3(64), 0, st, *a);
   return hipGetLastError();
 }
 

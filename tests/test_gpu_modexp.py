@@ -159,3 +159,29 @@ def test_split_plan_large_batch(gpu, paillier_key):
     xs = gpu.words_to_ints(B[idx])
     zs = gpu.words_to_ints(out[idx])
     assert zs == [pow(x, N, N2) for x in xs]
+
+
+SCHED_EXPONENTS = [1, 2, 3, 5, 7, 31, 32, 33, 63, (1 << 64) - 1, 1 << 64, (1 << 64) + 1, 0xAAAA_AAAA_AAAA_AAAA_AAAA,
+                   (1 << 2047) | 1, (1 << 1000) | (1 << 500) | (1 << 37), (1 << 4900) - 1]
+
+
+@pytest.mark.parametrize("width", [0, 1, 2, 3, 4, 5])
+def test_shared_exponent_window_schedules(gpu, paillier_key, width):
+    """Shared exponents take the device-built sliding-window schedule
+    (k_expsched; width capped by the "sched_width" option, 0 = Go's fixed
+    window): sparse, dense, word-boundary and long exponents, with and
+    without the fused multiplier, in the 4096-bit and 2048-bit classes."""
+    N = paillier_key["N"]
+    rng = random.Random(100 + width)
+    gpu.set_option("sched_width", width)
+    try:
+        for m in (N * N, N):
+            mod = gpu.Modulus(m)
+            xs = [rng.randrange(m) for _ in range(mod.G + 1)] + [0, 1, m - 1]
+            for e in SCHED_EXPONENTS + [N, rng.getrandbits(2048), rng.getrandbits(300)]:
+                assert mod.exp(xs, e) == [pow(x, e, m) for x in xs], (width, m.bit_length(), e.bit_length())
+            cs = [rng.randrange(m) for _ in xs]
+            assert mod.exp_mul(xs, N - 1, cs) == [c * pow(x, N - 1, m) % m for x, c in zip(xs, cs)]
+            mod.release()
+    finally:
+        gpu.set_option("sched_width", 5)
