@@ -152,6 +152,31 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
  * probablyPrimeMillerRabin, go:src/math/big/prime.go). */
 int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* bases, uint8_t* ok);
 
+/* Fixed-base comb tables for long-lived bases of a <= 2080-bit modulus (the
+ * h1, h2 of a node's N~ that every MtA range proof and DLN proof
+ * exponentiates: up:crypto/mta/range_proof.go, up:crypto/mta/proofs.go,
+ * up:crypto/dlnproof/proof.go; SURVEY.md 8(b) "_fixed_base"). Registration
+ * precomputes b^(v 2^(8j)) R mod m for every 8-bit window j below
+ * max_exp_bits on the GPU (256 entries per window, ~27 MB for 2816-bit
+ * exponents of a 2048-bit modulus); the table lives until
+ * mpcx_fixedbase_release (release it before its modulus). */
+typedef struct mpcx_fixedbase_s* mpcx_fb_t;
+int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_words,
+                            uint32_t max_exp_bits, mpcx_fb_t* out);
+int mpcx_fixedbase_release(mpcx_fb_t fb);
+/* Largest exponent a table serves and its device footprint. */
+int mpcx_fixedbase_info(mpcx_fb_t fb, uint32_t* max_exp_bits, size_t* table_bytes);
+
+/* out[i] = (muls ? muls[i] : 1) * prod_{t < nbases} b_t^(e_t,i) mod m, with
+ * 1 <= nbases <= 2 tables of the SAME modulus (e.g. z = h1^m h2^rho mod N~
+ * as one product: one Montgomery product per 8-bit window, no squarings).
+ * exps[t]: count x exp_words[t] words (exp_words[t] may be 0: e = 0); every
+ * exponent must fit its table (EINVAL otherwise). Synchronous. */
+int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t count,
+                             const uint32_t* const* exps, const uint32_t* exp_words,
+                             const uint32_t* muls, uint32_t mul_words,
+                             uint32_t* out, uint32_t out_words);
+
 /* Device memory helpers for callers without their own HIP allocator. */
 int mpcx_dev_alloc(size_t bytes, void** out_ptr);
 int mpcx_dev_free(void* ptr);

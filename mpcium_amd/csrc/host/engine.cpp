@@ -2,6 +2,7 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace mpcx::host {
 
@@ -19,6 +20,8 @@ void Engine::init(int device) {
   int rc = mpcx_init(device);
   if (rc) throw_last(rc, "mpcx_init");
   device_ = device;
+  const char* fb = std::getenv("MPCX_FIXED_BASE");
+  fixed_enabled_ = !(fb && fb[0] == '0');
 }
 
 Engine::Mod& Engine::modulus(const Nat& m) {
@@ -78,6 +81,63 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
   }
   if (rc) throw_last(rc, "mpcx_modexp_batch");
   return unpack(out, bases.size(), md.words);
+}
+
+bool Engine::fixed_base_ok(const Nat& m) const {
+  return fixed_enabled_ && m.is_odd() && m.bit_len() <= 2080;
+}
+
+Engine::Fixed& Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
+  auto key = std::make_pair(m.limbs(), base.limbs());
+  auto it = fixed_.find(key);
+  if (it != fixed_.end() && it->second.max_bits >= need_bits) return it->second;
+  if (it != fixed_.end()) {  // grow: rebuild for the longer exponent
+    mpcx_fixedbase_release(it->second.h);
+    fixed_.erase(it);
+  }
+  if (fixed_.size() >= 256) {  // bound the device footprint (~30 MB per table)
+    for (auto& kv : fixed_) mpcx_fixedbase_release(kv.second.h);
+    fixed_.clear();
+  }
+  Mod& md = modulus(m);
+  // MtA exponents on h1, h2 reach ~2818 bits (s2, t2 < q^3 N~ + e q N~); one size serves them all
+  const uint32_t bits = std::max<uint32_t>(3072, (need_bits + 511) / 512 * 512);
+  Fixed f{};
+  std::vector<uint32_t> bw(md.class_words, 0);
+  base.to_words(bw.data(), md.class_words);
+  int rc = mpcx_fixedbase_register(md.h, bw.data(), md.class_words, bits, &f.h);
+  if (rc) throw_last(rc, "mpcx_fixedbase_register");
+  f.max_bits = bits;
+  return fixed_.emplace(key, f).first->second;
+}
+
+std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vector<Nat>& exps,
+                                   const std::vector<Nat>* muls) {
+  if (muls && muls->size() != exps.size()) throw std::invalid_argument("muls: one per exponent");
+  if (exps.empty()) return {};
+  std::lock_guard<std::mutex> lk(mu_);
+  Mod& md = modulus(m);
+  uint32_t ew = 1, need = 1;
+  for (const auto& e : exps) {
+    ew = std::max<uint32_t>(ew, (uint32_t)e.words());
+    need = std::max<uint32_t>(need, e.bit_len());
+  }
+  const Nat b = base.words() > md.class_words || base >= m ? base % m : base;
+  Fixed& f = fixed(m, b, need);
+  auto E = pack(exps, ew);
+  std::vector<uint32_t> Mw;
+  if (muls) {
+    std::vector<Nat> mm(*muls);
+    for (auto& x : mm)
+      if (x.words() > md.class_words) x = x % m;
+    Mw = pack(mm, md.class_words);
+  }
+  std::vector<uint32_t> out((size_t)exps.size() * md.words);
+  const uint32_t* ep = E.data();
+  int rc = mpcx_fixedbase_exp_batch(1, &f.h, (uint32_t)exps.size(), &ep, &ew, muls ? Mw.data() : nullptr,
+                                    muls ? md.class_words : 0, out.data(), md.words);
+  if (rc) throw_last(rc, "mpcx_fixedbase_exp_batch");
+  return unpack(out, exps.size(), md.words);
 }
 
 std::vector<Nat> Engine::mulmod(const Nat& m, const std::vector<Nat>& a, const std::vector<Nat>& b) {

@@ -38,6 +38,14 @@ class Engine {
   std::vector<Nat> exp(const Nat& m, const std::vector<Nat>& bases, const std::vector<Nat>& exps,
                        const std::vector<Nat>* muls = nullptr);
   std::vector<Nat> mulmod(const Nat& m, const std::vector<Nat>& a, const std::vector<Nat>& b);
+  // out[i] = (muls ? muls[i] : 1) * base^exps[i] mod m through a comb table of
+  // `base` (mpcx_fixedbase_*), built on first use and cached: the bases that
+  // recur across every session (h1, h2 of a node's N~) pay for it once.
+  std::vector<Nat> fixed_exp(const Nat& m, const Nat& base, const std::vector<Nat>& exps,
+                             const std::vector<Nat>* muls = nullptr);
+  // fixed-base path usable for m (odd, <= 2080 bits) and enabled
+  // (environment MPCX_FIXED_BASE=0 turns it off, for A/B runs)
+  bool fixed_base_ok(const Nat& m) const;
   std::vector<uint8_t> fermat2(const std::vector<Nat>& cands);
   std::vector<uint8_t> strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases);
 
@@ -48,9 +56,16 @@ class Engine {
     uint32_t words;
   };
   Mod& modulus(const Nat& m);
+  struct Fixed {
+    mpcx_fb_t h;
+    uint32_t max_bits;
+  };
+  Fixed& fixed(const Nat& m, const Nat& base, uint32_t need_bits);
   std::mutex mu_;
   int device_ = -1;
+  bool fixed_enabled_ = true;
   std::map<std::vector<uint32_t>, Mod> mods_;
+  std::map<std::pair<std::vector<uint32_t>, std::vector<uint32_t>>, Fixed> fixed_;
 };
 
 [[noreturn]] void throw_last(int rc, const char* what);

@@ -27,8 +27,26 @@ class ExpSet {
   size_t size() const { return reqs_.size(); }
   void run() {
     if (reqs_.empty()) return;
+    // A base recurring across many requests (h1, h2 of N~ in every session's
+    // range proof) goes to the fixed-base comb path: no squarings, one
+    // product per 8-bit window. Sorted by exponent length, so wavefronts are
+    // homogeneous and skip the windows above their exponents.
+    std::vector<uint8_t> done(reqs_.size(), 0);
+    if (Engine::get().fixed_base_ok(m_)) {
+      std::map<const Nat*, std::vector<size_t>> by_b;
+      for (size_t i = 0; i < reqs_.size(); ++i) by_b[reqs_[i].b].push_back(i);
+      for (auto& kv : by_b) {
+        if (kv.second.size() < kFixedMin) continue;
+        auto& idx = kv.second;
+        std::stable_sort(idx.begin(), idx.end(),
+                         [&](size_t a, size_t b) { return reqs_[a].e->bit_len() < reqs_[b].e->bit_len(); });
+        launch_fixed(idx);
+        for (size_t i : idx) done[i] = 1;
+      }
+    }
     std::map<const Nat*, std::vector<size_t>> by_e;
-    for (size_t i = 0; i < reqs_.size(); ++i) by_e[reqs_[i].e].push_back(i);
+    for (size_t i = 0; i < reqs_.size(); ++i)
+      if (!done[i]) by_e[reqs_[i].e].push_back(i);
     std::vector<size_t> rest;
     for (auto& kv : by_e) {
       // a shared-exponent launch only for a large group (y = N, y = lambda);
@@ -59,6 +77,19 @@ class ExpSet {
     const Nat* mul;
     Nat* out;
   };
+  static constexpr size_t kFixedMin = 64;  // requests on one base before a comb table pays
+  void launch_fixed(const std::vector<size_t>& idx) {
+    std::vector<Nat> exps, muls;
+    exps.reserve(idx.size());
+    bool any_mul = false;
+    for (size_t i : idx) any_mul |= reqs_[i].mul != nullptr;
+    for (size_t i : idx) {
+      exps.push_back(*reqs_[i].e);
+      if (any_mul) muls.push_back(reqs_[i].mul ? *reqs_[i].mul : Nat(1));
+    }
+    std::vector<Nat> r = Engine::get().fixed_exp(m_, *reqs_[idx[0]].b, exps, any_mul ? &muls : nullptr);
+    for (size_t j = 0; j < idx.size(); ++j) *reqs_[idx[j]].out = std::move(r[j]);
+  }
   void launch(const std::vector<size_t>& idx, bool shared) {
     std::vector<Nat> bases, exps, muls;
     bases.reserve(idx.size());

@@ -31,6 +31,8 @@ MPCX_FOR_EACH_GEOM(MPCX_GEOM_DECL)
 hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_g1(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 }
 
@@ -42,6 +44,13 @@ struct mpcx_modulus_s {
   uint32_t* d_const;  // per geometry of the class: 3*L_g digits N, R mod N, R^2 mod N
   uint32_t const_off[MPCX_NUM_GEOMS];  // digit offset of geometry g's block (class members only)
   std::vector<uint32_t> m;
+};
+
+struct mpcx_fixedbase_s {
+  mpcx_mod_t mod;
+  int geom;          // main geometry of the modulus class (table layout)
+  uint32_t nwin;     // 8-bit windows: exponents of up to 8*nwin bits
+  uint32_t* d_table; // nwin x 256 entries x L digits ([k][p] interleaved)
 };
 
 namespace {
@@ -657,3 +666,205 @@ int mpcx_stream_sync(void* stream) {
 }
 
 }  // extern "C"
+
+// ------------------------------------------------------------ fixed base
+// Comb tables for a long-lived base (h1, h2 of a node's N~; SURVEY.md 8(a)
+// "shared bases"): entry (j, v) = b^(v 2^(8j)) R mod m. Built on the GPU by
+// the modexp kernels: b_j = b^(2^(8j)) (per-operand exponents), then
+// T(j, v) = (R mod m) * b_j^v (fused multiplier), then reordered into the
+// kernel geometry's digit layout on the host.
+int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_words, uint32_t max_exp_bits,
+                            mpcx_fb_t* out) {
+  if (!mod || !base || !out) return fail(MPCX_EINVAL, "null argument");
+  if (mod->cls > 1) return fail(MPCX_EINVAL, "fixed-base tables serve moduli of <= %d bits", MPCX_CLASS_MAXBITS(1));
+  const uint32_t cw = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
+  if (base_words == 0 || base_words > cw) return fail(MPCX_EINVAL, "base_words %u outside [1, %u]", base_words, cw);
+  if (max_exp_bits == 0 || max_exp_bits > 65536) return fail(MPCX_EINVAL, "max_exp_bits %u outside [1, 65536]", max_exp_bits);
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  const int geom = MPCX_MAIN_GEOM(mod->cls);
+  const uint32_t L = (uint32_t)MPCX_GEOM_L(geom), P = (uint32_t)MPCX_GEOM_P(geom), K = (uint32_t)MPCX_GEOM_K(geom);
+  const uint32_t nwin = (max_exp_bits + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS;
+  const uint32_t nv = MPCX_FB_ENTRIES - 1;  // v = 1..255 computed; v = 0 is R mod m
+  const size_t n2 = (size_t)nwin * nv;
+  if (n2 > 0xFFFFFFFFull) return fail(MPCX_EINVAL, "table too large");
+  const uint32_t ew1 = (MPCX_FB_WINDOW_BITS * (nwin - 1)) / 32 + 1;  // 2^(8j) needs bit 8j
+  // host inputs
+  std::vector<uint32_t> hb((size_t)nwin * cw, 0), he1((size_t)nwin * ew1, 0);
+  for (uint32_t j = 0; j < nwin; ++j) {
+    std::memcpy(&hb[(size_t)j * cw], base, base_words * 4);
+    const uint32_t bit = MPCX_FB_WINDOW_BITS * j;
+    he1[(size_t)j * ew1 + bit / 32] = 1u << (bit % 32);
+  }
+  const std::vector<uint32_t> r1w = pow2_mod(kDigitBits * L, mod->m);  // R mod m, mod->words words
+  std::vector<uint32_t> he2(n2), hm(n2 * mod->words);
+  for (size_t i = 0; i < n2; ++i) {
+    he2[i] = (uint32_t)(i % nv) + 1u;
+    std::memcpy(&hm[i * mod->words], r1w.data(), mod->words * 4);
+  }
+  uint32_t *d_b = nullptr, *d_e1 = nullptr, *d_bj = nullptr, *d_e2 = nullptr, *d_m = nullptr, *d_t = nullptr;
+  auto cleanup = [&] {
+    for (uint32_t* ptr : {d_b, d_e1, d_bj, d_e2, d_m, d_t})
+      if (ptr) (void)hipFree(ptr);
+  };
+  auto alloc = [&](uint32_t** ptr, size_t words) {
+    return hipMalloc((void**)ptr, std::max<size_t>(words, 1) * 4) == hipSuccess;
+  };
+  if (!alloc(&d_b, hb.size()) || !alloc(&d_e1, he1.size()) || !alloc(&d_bj, (size_t)nwin * cw) ||
+      !alloc(&d_e2, n2) || !alloc(&d_m, hm.size()) || !alloc(&d_t, n2 * cw)) {
+    cleanup();
+    return fail(MPCX_ENOMEM, "hipMalloc(fixed-base build)");
+  }
+  hipError_t e = hipMemcpy(d_b, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_e1, he1.data(), he1.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_e2, he2.data(), he2.size() * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(d_m, hm.data(), hm.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    cleanup();
+    return hip_fail(e, "upload fixed-base inputs");
+  }
+  rc = modexp_device_locked(mod, nwin, d_b, cw, d_e1, ew1, 0, MPCX_FB_WINDOW_BITS * (nwin - 1) + 1, nullptr, 0,
+                            d_bj, cw, nullptr);
+  // T(j, v) = R * b_j^v: operand i = j*255 + (v-1) takes base b_j -> replicate b_j rows
+  std::vector<uint32_t> hbj((size_t)nwin * cw), hb2;
+  if (!rc) {
+    e = hipMemcpy(hbj.data(), d_bj, hbj.size() * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = hip_fail(e, "copy b_j");
+  }
+  if (!rc) {
+    hb2.resize(n2 * cw);
+    for (size_t i = 0; i < n2; ++i) std::memcpy(&hb2[i * cw], &hbj[(i / nv) * cw], cw * 4);
+    (void)hipFree(d_b);
+    d_b = nullptr;
+    if (!alloc(&d_b, hb2.size())) rc = fail(MPCX_ENOMEM, "hipMalloc(fixed-base bases)");
+  }
+  if (!rc) {
+    e = hipMemcpy(d_b, hb2.data(), hb2.size() * 4, hipMemcpyHostToDevice);
+    if (e != hipSuccess) rc = hip_fail(e, "upload b_j");
+  }
+  if (!rc)
+    rc = modexp_device_locked(mod, (uint32_t)n2, d_b, cw, d_e2, 1, 0, MPCX_FB_WINDOW_BITS, d_m, mod->words, d_t,
+                              cw, nullptr);
+  std::vector<uint32_t> ht(n2 * cw);
+  if (!rc) {
+    e = hipMemcpy(ht.data(), d_t, ht.size() * 4, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) rc = hip_fail(e, "copy table");
+  }
+  cleanup();
+  if (rc) return rc;
+  // digits, [k][p] interleaved per entry
+  const size_t ent_words = L;
+  std::vector<uint32_t> tab((size_t)nwin * MPCX_FB_ENTRIES * ent_words);
+  auto put = [&](size_t ent, const std::vector<uint32_t>& words) {
+    const std::vector<uint32_t> d = to_digits(words, L);
+    uint32_t* dst = &tab[ent * ent_words];
+    for (uint32_t pp = 0; pp < P; ++pp)
+      for (uint32_t k = 0; k < K; ++k) dst[k * P + pp] = d[pp * K + k];
+  };
+  std::vector<uint32_t> w(cw);
+  for (uint32_t j = 0; j < nwin; ++j) {
+    put((size_t)j * MPCX_FB_ENTRIES, r1w);
+    for (uint32_t v = 1; v < MPCX_FB_ENTRIES; ++v) {
+      std::memcpy(w.data(), &ht[((size_t)j * nv + (v - 1)) * cw], cw * 4);
+      put((size_t)j * MPCX_FB_ENTRIES + v, w);
+    }
+  }
+  auto* fb = new mpcx_fixedbase_s();
+  fb->mod = mod;
+  fb->geom = geom;
+  fb->nwin = nwin;
+  e = hipMalloc((void**)&fb->d_table, tab.size() * 4);
+  if (e != hipSuccess) {
+    delete fb;
+    return fail(MPCX_ENOMEM, "hipMalloc(fixed-base table %zu B)", tab.size() * 4);
+  }
+  e = hipMemcpy(fb->d_table, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(fb->d_table);
+    delete fb;
+    return hip_fail(e, "upload fixed-base table");
+  }
+  *out = fb;
+  return MPCX_OK;
+}
+
+int mpcx_fixedbase_release(mpcx_fb_t fb) {
+  if (!fb) return fail(MPCX_EINVAL, "null fixed base");
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (fb->d_table) (void)hipFree(fb->d_table);
+  delete fb;
+  return MPCX_OK;
+}
+
+int mpcx_fixedbase_info(mpcx_fb_t fb, uint32_t* max_exp_bits, size_t* table_bytes) {
+  if (!fb) return fail(MPCX_EINVAL, "null fixed base");
+  if (max_exp_bits) *max_exp_bits = fb->nwin * MPCX_FB_WINDOW_BITS;
+  if (table_bytes) *table_bytes = (size_t)fb->nwin * MPCX_FB_ENTRIES * MPCX_GEOM_L(fb->geom) * 4;
+  return MPCX_OK;
+}
+
+int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t count, const uint32_t* const* exps,
+                             const uint32_t* exp_words, const uint32_t* muls, uint32_t mul_words, uint32_t* out,
+                             uint32_t out_words) {
+  if (nbases == 0 || nbases > MPCX_FB_MAX_BASES) return fail(MPCX_EINVAL, "nbases %u outside [1, %d]", nbases, MPCX_FB_MAX_BASES);
+  if (!fbs || !exps || !exp_words) return fail(MPCX_EINVAL, "null argument");
+  for (uint32_t t = 0; t < nbases; ++t) {
+    if (!fbs[t]) return fail(MPCX_EINVAL, "null fixed base %u", t);
+    if (fbs[t]->mod != fbs[0]->mod) return fail(MPCX_EINVAL, "fixed bases of different moduli");
+  }
+  mpcx_mod_t mod = fbs[0]->mod;
+  const uint32_t cw = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
+  if (out_words < mod->words) return fail(MPCX_EINVAL, "out_words %u < modulus words %u", out_words, mod->words);
+  if (muls && (mul_words == 0 || mul_words > cw)) return fail(MPCX_EINVAL, "mul_words %u outside [1, %u]", mul_words, cw);
+  if (count == 0) return MPCX_OK;
+  if (!out) return fail(MPCX_EINVAL, "null output");
+  uint32_t nwin[MPCX_FB_MAX_BASES] = {0, 0};
+  for (uint32_t t = 0; t < nbases; ++t) {
+    if (exp_words[t] && !exps[t]) return fail(MPCX_EINVAL, "null exponents %u", t);
+    uint32_t bits = 0;
+    for (uint32_t i = 0; i < count && exp_words[t]; ++i)
+      bits = std::max(bits, bit_length_words(exps[t] + (size_t)i * exp_words[t], exp_words[t]));
+    if (bits > fbs[t]->nwin * MPCX_FB_WINDOW_BITS)
+      return fail(MPCX_EINVAL, "exponent of %u bits > fixed-base table's %u", bits, fbs[t]->nwin * MPCX_FB_WINDOW_BITS);
+    nwin[t] = (bits + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS;
+  }
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  const size_t eb0 = (size_t)count * exp_words[0] * 4, eb1 = nbases > 1 ? (size_t)count * exp_words[1] * 4 : 0,
+               ob = (size_t)count * out_words * 4, mb = muls ? (size_t)count * mul_words * 4 : 0;
+  if ((rc = ensure_buffer(g_stage[0], eb0)) || (rc = ensure_buffer(g_stage[1], eb1)) ||
+      (rc = ensure_buffer(g_stage[2], ob)) || (muls && (rc = ensure_buffer(g_stage[3], mb))))
+    return rc;
+  hipError_t e = hipSuccess;
+  if (eb0) e = hipMemcpy(g_stage[0].ptr, exps[0], eb0, hipMemcpyHostToDevice);
+  if (e == hipSuccess && eb1) e = hipMemcpy(g_stage[1].ptr, exps[1], eb1, hipMemcpyHostToDevice);
+  if (e == hipSuccess && muls) e = hipMemcpy(g_stage[3].ptr, muls, mb, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "copy inputs");
+  const int geom = fbs[0]->geom;
+  mpcx::FixedBaseArgs a{};
+  a.nd = mod->d_const + mod->const_off[geom];
+  a.r1d = a.nd + MPCX_GEOM_L(geom);
+  a.r2d = a.nd + 2 * MPCX_GEOM_L(geom);
+  for (uint32_t t = 0; t < nbases; ++t) {
+    a.tables[t] = fbs[t]->d_table;
+    a.exps[t] = (const uint32_t*)g_stage[t].ptr;
+    a.exp_words[t] = exp_words[t];
+    a.nwin[t] = nwin[t];
+  }
+  a.nbases = nbases;
+  a.mul = muls ? (const uint32_t*)g_stage[3].ptr : nullptr;
+  a.mul_words = muls ? mul_words : 0;
+  a.out = (uint32_t*)g_stage[2].ptr;
+  a.out_words = out_words;
+  a.count = count;
+  a.n0inv = mod->n0inv;
+  const uint32_t waves = (count + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
+  e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, nullptr)
+                                : mpcx_launch_fixedbase_g1(&a, waves, nullptr);
+  if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
+  e = hipMemcpy(out, g_stage[2].ptr, ob, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "copy results");
+  return MPCX_OK;
+}

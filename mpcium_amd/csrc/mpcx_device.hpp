@@ -246,6 +246,42 @@ __device__ __forceinline__ uint32_t window_of(const uint32_t* e, uint32_t j) {
   return (e[(4u * j) >> 5] >> ((4u * j) & 31u)) & 15u;
 }
 
+// Leaves A (<= m after the Montgomery-domain exit mont(z R, 1)) canonical,
+// maps m -> 0, and writes the operand's out_words words (digits -> words
+// through the group's LDS row).
+template <int P, int K>
+__device__ __forceinline__ void store_result(uint32_t (&A)[K], const uint32_t (&Nd)[K], uint32_t* bl, int p,
+                                             int g_raw, bool idle, bool active, uint32_t* o, uint32_t out_words) {
+  constexpr int L = P * K;
+  canonicalize<P, K>(A);
+  bool eq = true;
+#pragma unroll
+  for (int k = 0; k < K; ++k) eq &= (A[k] == Nd[k]);
+  const uint64_t bal = __ballot(eq || idle);
+  const uint64_t gmask = (P == 64 ? ~0ull : (((1ull << P) - 1ull) << (g_raw * P)));
+  if (!idle && (bal & gmask) == gmask) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) A[k] = 0;
+  }
+  wave_lds_fence();
+  lds_store_digits<K>(bl, p, A);
+  wave_lds_fence();
+  if (active) {
+    for (uint32_t w = (uint32_t)p; w < out_words; w += P) {
+      const uint32_t bit = w * 32u;
+      const uint32_t d0 = bit / DB, s0 = bit % DB;
+      uint32_t v = 0;
+      if (d0 < (uint32_t)L) {
+        // s0 = 32w mod 28 <= 24, so bits [s0, s0+32) lie in two digits
+        const uint64_t lo = bl[d0];
+        const uint64_t hi = (d0 + 1 < (uint32_t)L) ? bl[d0 + 1] : 0u;
+        v = (uint32_t)((lo | (hi << DB)) >> s0);
+      }
+      o[w] = v;
+    }
+  }
+}
+
 // Batched x_i^e_i mod m for one registered odd modulus m.
 template <int P, int K, int G, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp(const ModexpArgs a) {
@@ -477,36 +513,100 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     wave_lds_fence();
   }
 
-  // A < 2m after the first-domain exit is <= m; make digits canonical, map m -> 0.
-  canonicalize<P, K>(A);
-  bool eq = true;
+  store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
+}
+
+// Fixed-base multi-exponentiation: out_i = mul_i * prod_t b_t^(e_t,i) mod m
+// for up to MPCX_FB_MAX_BASES registered bases (h1, h2 of a node's N~;
+// up:crypto/mta/range_proof.go z = h1^m h2^rho, up:crypto/dlnproof/proof.go
+// alpha_i = h1^a_i). With the comb table b^(v 2^(8j)) per 8-bit window there
+// are no squarings at all: one Montgomery product per window of each
+// exponent, z <- mont(z, T[j][v]), against Go's E squarings + E/4 multiplies
+// for the same Exp. Every operand multiplies in every window (v = 0 reads
+// the Montgomery one), so the wave never diverges; windows above every
+// operand's exponent are skipped by a wave-uniform ballot.
+template <int P, int K, int G, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase(const FixedBaseArgs a) {
+  constexpr int L = P * K;
+  __shared__ uint32_t lds[(G + 1) * L + 1];
+  const int lane = threadIdx.x;
+  const int g_raw = lane / P;
+  const bool idle = g_raw >= G;
+  const int g = idle ? G : g_raw;
+  const int p = lane - g_raw * P;
+  const uint32_t op = blockIdx.x * G + (idle ? 0 : g_raw);
+  const bool active = !idle && op < a.count;
+  uint32_t* bl = lds + g * L;
+  const int m_src_addr = (idle ? lane : g_raw * P) * 4;
+
+  uint32_t Nd[K], A[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) eq &= (A[k] == Nd[k]);
-  const uint64_t bal = __ballot(eq || idle);
-  const uint64_t gmask = (P == 64 ? ~0ull : (((1ull << P) - 1ull) << (g_raw * P)));
-  if (!idle && (bal & gmask) == gmask) {
+  for (int k = 0; k < K; ++k) Nd[k] = idle ? 0u : a.nd[p * K + k];
+  auto lds_digits = [&](const uint32_t* src) __attribute__((always_inline)) {  // L digits, [p*K + k]
+    uint32_t t[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) A[k] = 0;
-  }
-  // digits -> words through LDS
-  wave_lds_fence();
-  lds_store_digits<K>(bl, p, A);
-  wave_lds_fence();
-  if (active) {
-    uint32_t* o = a.out + (size_t)op * a.out_words;
-    for (uint32_t w = (uint32_t)p; w < a.out_words; w += P) {
-      const uint32_t bit = w * 32u;
-      const uint32_t d0 = bit / DB, s0 = bit % DB;
-      uint32_t v = 0;
-      if (d0 < (uint32_t)L) {
-        // s0 = 32w mod 28 <= 24, so bits [s0, s0+32) lie in two digits
-        const uint64_t lo = bl[d0];
-        const uint64_t hi = (d0 + 1 < (uint32_t)L) ? bl[d0 + 1] : 0u;
-        v = (uint32_t)((lo | (hi << DB)) >> s0);
+    for (int k = 0; k < K; ++k) t[k] = idle ? 0u : src[p * K + k];
+    lds_store_digits<K>(bl, p, t);
+  };
+  // ONE montmul call site (three would triple the unrolled product and its
+  // register allocation): each pass of the loop below prepares the next B.
+  uint32_t t = 0, j = 0;  // next window: base t, window j
+  // B for the next product: the next window with bits in some operand of
+  // the wave, else the exit multiplier 1; false once the exit product is done
+  bool fin = false;
+  auto next = [&] __attribute__((always_inline))() -> bool {
+    for (; t < a.nbases; ++t, j = 0) {
+      const uint32_t ew = a.exp_words[t];
+      const uint32_t* ex = a.exps[t] + (size_t)(active ? op : 0) * ew;
+      for (; j < a.nwin[t]; ++j) {
+        const uint32_t wi = j >> 2;
+        const uint32_t v = (active && wi < ew) ? (ex[wi] >> ((j & 3u) * 8u)) & 0xFFu : 0u;
+        if (__ballot(v != 0u) == 0ull) continue;  // no operand of the wave has bits here
+        const uint32_t* e = a.tables[t] + ((size_t)j * MPCX_FB_ENTRIES + v) * L;
+        uint32_t tv[K];
+#pragma unroll
+        for (int k = 0; k < K; ++k) tv[k] = idle ? 0u : e[k * P + p];
+        lds_store_digits<K>(bl, p, tv);
+        ++j;
+        return true;
       }
-      o[w] = v;
     }
+    if (fin) return false;
+    fin = true;  // leave the Montgomery domain: z = mont(z R, 1) <= m
+    uint32_t one[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
+    lds_store_digits<K>(bl, p, one);
+    return true;
+  };
+
+  if (a.mul) {
+    // z = mul R = mont(mul, R^2)
+    lds_digits(a.r2d);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      const uint32_t bit = (uint32_t)(p * K + k) * DB;
+      const uint32_t w = bit >> 5, sh = bit & 31u;
+      uint64_t v = 0;
+      if (active) {
+        const uint32_t* x = a.mul + (size_t)op * a.mul_words;
+        const uint32_t lo = w < a.mul_words ? x[w] : 0u;
+        const uint32_t hi = (w + 1) < a.mul_words ? x[w + 1] : 0u;
+        v = ((uint64_t)hi << 32) | lo;
+      }
+      A[k] = (uint32_t)(v >> sh) & M28;
+    }
+  } else {
+#pragma unroll
+    for (int k = 0; k < K; ++k) A[k] = idle ? 0u : a.r1d[p * K + k];  // z = R mod m
+    next();
   }
+  do {
+    wave_lds_fence();
+    montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
+    wave_lds_fence();
+  } while (next());
+  store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
 }
 
 // ---------------------------------------------------------------- Fermat(2)

@@ -36,6 +36,17 @@ __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_g, 
   return hipGetLastError();
 }
 
+#if MPCX_GEOM_ID == MPCX_MAIN_GEOM(0) || MPCX_GEOM_ID == MPCX_MAIN_GEOM(1)
+// fixed-base comb kernel: main geometry of the <= 2080-bit classes (N~, N; tables are laid out for it)
+__attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_fixedbase_g, MPCX_GEOM_ID)(
+    const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st) {
+  hipLaunchKernelGGL((mpcx::k_fixedbase<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
+                                        MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>),
+                     dim3(waves), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+#endif
+
 // resident 64-thread blocks (= wavefronts) per CU
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_modexp_occupancy_g, MPCX_GEOM_ID)(int* blocks_per_cu) {
   return hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks_per_cu, MPCX_THIS_KERNEL, 64, 0);

@@ -82,6 +82,31 @@ struct ModexpArgs {
   const uint32_t* sched; // shared exponent: its window schedule (nullptr: fixed window)
 };
 
+// Fixed-base tables (mpcx_fixedbase_register): for window j < nwin and byte
+// value v < 256, entry (j, v) = b^(v * 2^(8j)) R mod m as L radix-2^28 digits
+// of the class's main geometry, interleaved [digit slot k][lane p] so a
+// group's P lanes read P consecutive words per slot. Entry (j, 0) = R mod m.
+#define MPCX_FB_WINDOW_BITS 8
+#define MPCX_FB_ENTRIES 256
+#define MPCX_FB_MAX_BASES 2
+
+struct FixedBaseArgs {
+  const uint32_t* nd;   // L digits of m
+  const uint32_t* r1d;  // L digits of R mod m (Montgomery one)
+  const uint32_t* r2d;  // L digits of R^2 mod m
+  const uint32_t* tables[MPCX_FB_MAX_BASES];
+  const uint32_t* exps[MPCX_FB_MAX_BASES];  // count x exp_words[t]
+  uint32_t exp_words[MPCX_FB_MAX_BASES];
+  uint32_t nwin[MPCX_FB_MAX_BASES];         // 8-bit windows processed per base
+  uint32_t nbases;
+  const uint32_t* mul;  // optional count x mul_words multipliers
+  uint32_t mul_words;
+  uint32_t* out;        // count x out_words
+  uint32_t out_words;
+  uint32_t count;
+  uint32_t n0inv;
+};
+
 struct ExpSchedArgs {
   const uint32_t* exp;  // shared exponent, exp_words little-endian words
   uint32_t exp_words;

@@ -45,6 +45,12 @@ SIGNATURES = [
                                          ctypes.c_uint32]),
     ("mpcx_fermat2_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
     ("mpcx_mr_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
+    ("mpcx_fixedbase_register", ctypes.c_int, [_vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_vp)]),
+    ("mpcx_fixedbase_release", ctypes.c_int, [_vp]),
+    ("mpcx_fixedbase_info", ctypes.c_int, [_vp, _u32p, ctypes.POINTER(ctypes.c_size_t)]),
+    ("mpcx_fixedbase_exp_batch", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_vp), ctypes.c_uint32,
+                                                ctypes.POINTER(_vp), _u32p, _vp, ctypes.c_uint32, _vp,
+                                                ctypes.c_uint32]),
     ("mpcx_dev_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
     ("mpcx_dev_free", ctypes.c_int, [_vp]),
     ("mpcx_memcpy_h2d", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
@@ -221,6 +227,58 @@ class Modulus:
         B = self._operands(bases, "bases")
         E, shared = self._exps(exps, len(bases))
         return words_to_ints(self.exp_words(B, E, shared))
+
+
+class FixedBase:
+    """A comb table for a long-lived base of a registered modulus of <= 2080
+    bits (mpcx_fixedbase_register): exponents of up to `max_exp_bits` bits."""
+
+    def __init__(self, mod: Modulus, base: int, max_exp_bits: int):
+        self.mod, self.base = mod, base % mod.m
+        w = mod._operands([self.base], "base")
+        h = _vp()
+        _check(lib().mpcx_fixedbase_register(mod.handle, w.ctypes.data, w.shape[1], max_exp_bits, ctypes.byref(h)))
+        self._h = h
+        mb, tb = ctypes.c_uint32(), ctypes.c_size_t()
+        _check(lib().mpcx_fixedbase_info(h, ctypes.byref(mb), ctypes.byref(tb)))
+        self.max_exp_bits, self.table_bytes = mb.value, tb.value
+
+    @property
+    def handle(self):
+        return self._h
+
+    def release(self):
+        if self._h:
+            _check(lib().mpcx_fixedbase_release(self._h))
+            self._h = None
+
+
+def fixedbase_exp(fbs: Sequence[FixedBase], exps: Sequence[Sequence[int]],
+                  muls: Optional[Sequence[int]] = None) -> List[int]:
+    """[mul_i * prod_t b_t^(e_t,i) mod m] (mpcx_fixedbase_exp_batch); exps[t][i]."""
+    nb = len(fbs)
+    if nb != len(exps) or nb == 0:
+        raise ValueError("one exponent list per fixed base")
+    count = len(exps[0])
+    if any(len(e) != count for e in exps):
+        raise ValueError("exponent lists differ in length")
+    if count == 0:
+        return []
+    mod = fbs[0].mod
+    Es = []
+    for e in exps:
+        if any(v < 0 for v in e):
+            raise ValueError("negative exponent")
+        ew = max(nwords(v) for v in e)
+        Es.append(ints_to_words(e, ew))
+    Mu = mod._operands(muls, "muls") if muls is not None else None
+    out = np.zeros((count, mod.words), dtype="<u4")
+    hs = (_vp * nb)(*[f.handle for f in fbs])
+    eps = (_vp * nb)(*[E.ctypes.data for E in Es])
+    ews = (ctypes.c_uint32 * nb)(*[E.shape[1] for E in Es])
+    _check(lib().mpcx_fixedbase_exp_batch(nb, hs, count, eps, ews, Mu.ctypes.data if Mu is not None else None,
+                                          Mu.shape[1] if Mu is not None else 0, out.ctypes.data, mod.words))
+    return words_to_ints(out)
 
 
 def exp_batch(m: int, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> List[int]:

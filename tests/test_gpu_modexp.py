@@ -185,3 +185,38 @@ def test_shared_exponent_window_schedules(gpu, paillier_key, width):
             mod.release()
     finally:
         gpu.set_option("sched_width", 5)
+
+
+def test_fixed_base_tables(gpu, paillier_key):
+    """Fixed-base comb (h1^a h2^b mod N~ shape): one and two bases, with and
+    without a multiplier, zero/one/boundary exponents, ragged batches, and
+    exponents past the table rejected."""
+    N = paillier_key["N"]
+    rng = random.Random(77)
+    mod = gpu.Modulus(N)
+    h1, h2 = rng.randrange(N), rng.randrange(N)
+    f1, f2 = gpu.FixedBase(mod, h1, 2816), gpu.FixedBase(mod, h2, 300)
+    assert f1.max_exp_bits == 2816 and f2.max_exp_bits == 304
+    for count in (1, mod.G - 1, mod.G + 1, 3 * mod.G + 5):
+        a = [rng.getrandbits(rng.choice([0, 1, 8, 9, 256, 2048, 2816])) for _ in range(count)]
+        b = [rng.getrandbits(rng.choice([0, 7, 64, 300])) for _ in range(count)]
+        assert gpu.fixedbase_exp([f1], [a]) == [pow(h1, x, N) for x in a], count
+        want = [pow(h1, x, N) * pow(h2, y, N) % N for x, y in zip(a, b)]
+        assert gpu.fixedbase_exp([f1, f2], [a, b]) == want, count
+        cs = [rng.randrange(N) for _ in range(count)]
+        assert gpu.fixedbase_exp([f1, f2], [a, b], cs) == [c * w % N for c, w in zip(cs, want)], count
+    edge = [0, 1, 255, 256, (1 << 2816) - 1, 1 << 2815]
+    assert gpu.fixedbase_exp([f1], [edge]) == [pow(h1, x, N) for x in edge]
+    with pytest.raises(gpu.MpcxError):
+        gpu.fixedbase_exp([f2], [[1 << 304]])
+    # N~-shape modulus from the node fixtures and the 1024-bit class
+    for m in (paillier_key["P"], rng.getrandbits(1500) | 1 | (1 << 1499)):
+        md = gpu.Modulus(m)
+        fb = gpu.FixedBase(md, 3, 600)
+        es = [rng.getrandbits(600) for _ in range(70)]
+        assert gpu.fixedbase_exp([fb], [es]) == [pow(3, e, m) for e in es]
+        fb.release()
+        md.release()
+    f2.release()
+    f1.release()
+    mod.release()
