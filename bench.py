@@ -185,6 +185,7 @@ def signing_line(args, world, rank):
             "value": args.wallets * world / el, "unit": "sigs/s", "n_gpus": world,
             "wallets_per_gpu": args.wallets, "signers": args.signers, "seconds": el,
             "rounds_s": {"round1_alice_init": r1, "round2_bob_mid": r2, "round3_alice_end": r3},
+            "engine_busy_s": st["engine_busy_s"],
             "sessions_per_gpu": st["sessions"], "checked": "alpha+beta == k*gamma, mu+nu == k*w (mod q), every session",
             "scope": "GG18 signing rounds 1-3 MtA/MtAwc (tss-lib up:crypto/mta); other rounds are secp256k1 work "
                      "outside the Paillier path", "cpu_baseline": None}

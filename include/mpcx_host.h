@@ -174,8 +174,9 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
  * Paillier private keys + own DLN params with factors, width w). Plays every
  * signer (rounds 1-3 of up:ecdsa/signing, see csrc/host/signing.hpp) and
  * checks alpha + beta = k gamma and mu + nu = k w (mod q) for every session.
- * stats_out[8]: round1_s, round2_s, round3_s, total_s, wallets, sessions,
- * errors, relation_failures. */
+ * stats_out[9]: round1_s, round2_s, round3_s, total_s, wallets, sessions,
+ * errors, relation_failures, engine_busy_s (time inside libmpcx calls, summed
+ * over the concurrent per-pair tasks). */
 int mpcxh_bench_signing_mta(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
                             uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out);
 

@@ -438,8 +438,8 @@ int mpcxh_bench_signing_mta(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh
       nodes[i].dln = dln_from(&dlns[i], w);
     }
     const auto st = signing::RunSigningMtA(nodes, (int)signers, wallets, seed);
-    const double v[8] = {st.round1_s, st.round2_s, st.round3_s, st.total_s, (double)st.wallets, (double)st.sessions,
-                         (double)st.errors, (double)st.relation_failures};
+    const double v[9] = {st.round1_s, st.round2_s, st.round3_s, st.total_s, (double)st.wallets, (double)st.sessions,
+                         (double)st.errors, (double)st.relation_failures, st.engine_busy_s};
     std::memcpy(stats_out, v, sizeof v);
   });
 }

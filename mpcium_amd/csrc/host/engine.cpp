@@ -2,6 +2,7 @@
 #include "engine.hpp"
 
 #include <algorithm>
+#include <chrono>
 #include <cstdlib>
 
 namespace mpcx::host {
@@ -53,31 +54,46 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
   if (exps.size() != 1 && exps.size() != bases.size()) throw std::invalid_argument("exps: 1 or one per base");
   if (muls && muls->size() != bases.size()) throw std::invalid_argument("muls: one per base");
   if (bases.empty()) return {};
-  std::lock_guard<std::mutex> lk(mu_);
-  Mod& md = modulus(m);
-  // math/big reduces x mod m first when len(x) > len(m) (nat.expNNMontgomery);
-  // here: only when x does not fit the kernel class width.
-  auto fit = [&](const std::vector<Nat>& v) {
-    std::vector<Nat> r(v);
-    for (auto& x : r)
-      if (x.words() > md.class_words) x = x % m;
-    return r;
+  Mod md;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    md = modulus(m);
+  }
+  // Host-side packing runs outside the lock, so another thread's batch can
+  // use the GPU meanwhile. math/big reduces x mod m first when
+  // len(x) > len(m) (nat.expNNMontgomery); here: only when x does not fit
+  // the kernel class width.
+  auto packed = [&](const std::vector<Nat>& v) {
+    std::vector<uint32_t> out((size_t)v.size() * md.class_words);
+    for (size_t i = 0; i < v.size(); ++i) {
+      if (v[i].words() > md.class_words) {
+        (v[i] % m).to_words(out.data() + i * md.class_words, md.class_words);
+      } else {
+        v[i].to_words(out.data() + i * md.class_words, md.class_words);
+      }
+    }
+    return out;
   };
-  const std::vector<Nat> b = fit(bases);
   const bool shared = exps.size() == 1;
   uint32_t ew = 1;
   for (const auto& e : exps) ew = std::max<uint32_t>(ew, (uint32_t)e.words());
-  auto B = pack(b, md.class_words);
+  auto B = packed(bases);
   auto E = pack(exps, ew);
+  std::vector<uint32_t> M;
+  if (muls) M = packed(*muls);
   std::vector<uint32_t> out((size_t)bases.size() * md.words);
   int rc;
-  if (muls) {
-    auto M = pack(fit(*muls), md.class_words);
-    rc = mpcx_modexp_mul_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
-                               M.data(), md.class_words, out.data(), md.words);
-  } else {
-    rc = mpcx_modexp_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
-                           out.data(), md.words);
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    const auto t0 = std::chrono::steady_clock::now();
+    if (muls) {
+      rc = mpcx_modexp_mul_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
+                                 M.data(), md.class_words, out.data(), md.words);
+    } else {
+      rc = mpcx_modexp_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
+                             out.data(), md.words);
+    }
+    busy_ns_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
   }
   if (rc) throw_last(rc, "mpcx_modexp_batch");
   return unpack(out, bases.size(), md.words);
@@ -115,27 +131,39 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
                                    const std::vector<Nat>* muls) {
   if (muls && muls->size() != exps.size()) throw std::invalid_argument("muls: one per exponent");
   if (exps.empty()) return {};
-  std::lock_guard<std::mutex> lk(mu_);
-  Mod& md = modulus(m);
+  Mod md;
+  {
+    std::lock_guard<std::mutex> lk(mu_);
+    md = modulus(m);
+  }
   uint32_t ew = 1, need = 1;
   for (const auto& e : exps) {
     ew = std::max<uint32_t>(ew, (uint32_t)e.words());
     need = std::max<uint32_t>(need, e.bit_len());
   }
   const Nat b = base.words() > md.class_words || base >= m ? base % m : base;
-  Fixed& f = fixed(m, b, need);
   auto E = pack(exps, ew);
   std::vector<uint32_t> Mw;
   if (muls) {
-    std::vector<Nat> mm(*muls);
-    for (auto& x : mm)
-      if (x.words() > md.class_words) x = x % m;
-    Mw = pack(mm, md.class_words);
+    Mw.assign((size_t)muls->size() * md.class_words, 0);
+    for (size_t i = 0; i < muls->size(); ++i) {
+      const Nat& x = (*muls)[i];
+      (x.words() > md.class_words ? x % m : x).to_words(Mw.data() + i * md.class_words, md.class_words);
+    }
   }
   std::vector<uint32_t> out((size_t)exps.size() * md.words);
-  const uint32_t* ep = E.data();
-  int rc = mpcx_fixedbase_exp_batch(1, &f.h, (uint32_t)exps.size(), &ep, &ew, muls ? Mw.data() : nullptr,
-                                    muls ? md.class_words : 0, out.data(), md.words);
+  int rc;
+  {
+    // the table is looked up (or built) and used under the lock: another
+    // thread may grow or evict it
+    std::lock_guard<std::mutex> lk(mu_);
+    Fixed& f = fixed(m, b, need);
+    const uint32_t* ep = E.data();
+    const auto t0 = std::chrono::steady_clock::now();
+    rc = mpcx_fixedbase_exp_batch(1, &f.h, (uint32_t)exps.size(), &ep, &ew, muls ? Mw.data() : nullptr,
+                                  muls ? md.class_words : 0, out.data(), md.words);
+    busy_ns_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  }
   if (rc) throw_last(rc, "mpcx_fixedbase_exp_batch");
   return unpack(out, exps.size(), md.words);
 }

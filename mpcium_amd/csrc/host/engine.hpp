@@ -4,6 +4,7 @@
 // from this image, so the mirror is C++ (compiled reference -> compiled host).
 #pragma once
 
+#include <atomic>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -46,6 +47,10 @@ class Engine {
   // fixed-base path usable for m (odd, <= 2080 bits) and enabled
   // (environment MPCX_FIXED_BASE=0 turns it off, for A/B runs)
   bool fixed_base_ok(const Nat& m) const;
+  // seconds spent inside libmpcx exponentiation calls (GPU + transfers),
+  // summed over calling threads since the last reset
+  double busy_seconds() const { return (double)busy_ns_.load() * 1e-9; }
+  void reset_busy() { busy_ns_ = 0; }
   std::vector<uint8_t> fermat2(const std::vector<Nat>& cands);
   std::vector<uint8_t> strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases);
 
@@ -64,6 +69,7 @@ class Engine {
   std::mutex mu_;
   int device_ = -1;
   bool fixed_enabled_ = true;
+  std::atomic<uint64_t> busy_ns_{0};
   std::map<std::vector<uint32_t>, Mod> mods_;
   std::map<std::pair<std::vector<uint32_t>, std::vector<uint32_t>>, Fixed> fixed_;
 };

@@ -1,13 +1,34 @@
 // signing.cpp -- see signing.hpp.
 #include "signing.hpp"
 
+#include "engine.hpp"
+
+#include <atomic>
 #include <chrono>
+#include <functional>
+#include <thread>
 #include <stdexcept>
 
 namespace mpcx::host::signing {
 namespace {
 double now() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+// runs every task on its own thread; rethrows the first failure
+void run_tasks(const std::vector<std::function<void()>>& tasks) {
+  std::vector<std::exception_ptr> errs(tasks.size());
+  std::vector<std::thread> th;
+  for (size_t t = 0; t < tasks.size(); ++t)
+    th.emplace_back([&, t] {
+      try {
+        tasks[t]();
+      } catch (...) {
+        errs[t] = std::current_exception();
+      }
+    });
+  for (auto& x : th) x.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
 }
 uint64_t mix(uint64_t seed, uint64_t a, uint64_t b, uint64_t c) {
   uint64_t x = seed ^ (a * 0x9E3779B97F4A7C15ull) ^ (b * 0xC2B2AE3D27D4EB4Full) ^ (c * 0x165667B19E3779F9ull);
@@ -77,38 +98,78 @@ MtaStats RunSigningMtA(const std::vector<NodeKeys>& nodes, int signers, size_t w
       p.rbwc.push_back(p.drbg_bwc[wi].fn());
     }
   }
-  std::vector<uint8_t> err;
+  // Within a round the ordered pairs (and a pair's MtA / MtAwc halves) are
+  // independent: they run as concurrent tasks, so one task's host work
+  // (hashing, random draws, gcds, conversions) overlaps another's GPU batch.
+  std::atomic<uint64_t> errors{0};
+  auto count_err = [&](const std::vector<uint8_t>& err) {
+    uint64_t n = 0;
+    for (auto e : err) n += e != 0;
+    errors += n;
+  };
+  Engine::get().reset_busy();
   const double t0 = now();
   // round 1: AliceInit(pk_i, k_i, N~_j, h1_j, h2_j)
-  for (auto& p : pairs) {
-    mta::AliceInitBatch(nodes[p.i].sk.pub, k[p.i], public_dln(nodes[p.j].dln), p.ra, &p.cA, &p.pfA, &err);
-    for (auto e : err) st.errors += e != 0;
+  {
+    std::vector<std::function<void()>> tasks;
+    for (auto& p : pairs)
+      tasks.push_back([&, pp = &p] {
+        std::vector<uint8_t> err;
+        mta::AliceInitBatch(nodes[pp->i].sk.pub, k[pp->i], public_dln(nodes[pp->j].dln), pp->ra, &pp->cA, &pp->pfA,
+                            &err);
+        count_err(err);
+      });
+    run_tasks(tasks);
   }
   const double t1 = now();
   // round 2: Bob j -- BobMid(gamma_j), BobMidWC(w_j, W_j)
-  for (auto& p : pairs) {
-    const auto dlnA = public_dln(nodes[p.i].dln);
-    mta::BobMidBatch(sess, nodes[p.i].sk.pub, p.pfA, g[p.j], p.cA, dlnA, nodes[p.j].dln, nullptr, p.rb, &p.bob, &err);
-    for (auto e : err) st.errors += e != 0;
-    mta::BobMidBatch(sess, nodes[p.i].sk.pub, p.pfA, w[p.j], p.cA, dlnA, nodes[p.j].dln, &Wp[p.j], p.rbwc, &p.bobwc,
-                     &err);
-    for (auto e : err) st.errors += e != 0;
+  {
+    std::vector<std::function<void()>> tasks;
+    for (auto& p : pairs) {
+      tasks.push_back([&, pp = &p] {
+        std::vector<uint8_t> err;
+        mta::BobMidBatch(sess, nodes[pp->i].sk.pub, pp->pfA, g[pp->j], pp->cA, public_dln(nodes[pp->i].dln),
+                         nodes[pp->j].dln, nullptr, pp->rb, &pp->bob, &err);
+        count_err(err);
+      });
+      tasks.push_back([&, pp = &p] {
+        std::vector<uint8_t> err;
+        mta::BobMidBatch(sess, nodes[pp->i].sk.pub, pp->pfA, w[pp->j], pp->cA, public_dln(nodes[pp->i].dln),
+                         nodes[pp->j].dln, &Wp[pp->j], pp->rbwc, &pp->bobwc, &err);
+        count_err(err);
+      });
+    }
+    run_tasks(tasks);
   }
   const double t2 = now();
   // round 3: Alice i -- AliceEnd, AliceEndWC
-  for (auto& p : pairs) {
-    std::vector<mta::ProofBob> pf(Wn), pfwc(Wn);
-    std::vector<Nat> cB(Wn), cBwc(Wn);
-    for (size_t wi = 0; wi < Wn; ++wi) {
-      pf[wi] = p.bob[wi].pf;
-      pfwc[wi] = p.bobwc[wi].pf;
-      cB[wi] = p.bob[wi].cB;
-      cBwc[wi] = p.bobwc[wi].cB;
+  {
+    std::vector<std::function<void()>> tasks;
+    for (auto& p : pairs) {
+      tasks.push_back([&, pp = &p] {
+        std::vector<mta::ProofBob> pf(Wn);
+        std::vector<Nat> cB(Wn);
+        for (size_t wi = 0; wi < Wn; ++wi) {
+          pf[wi] = pp->bob[wi].pf;
+          cB[wi] = pp->bob[wi].cB;
+        }
+        std::vector<uint8_t> err;
+        mta::AliceEndBatch(sess, nodes[pp->i].sk, pf, nodes[pp->i].dln, pp->cA, cB, nullptr, &pp->alpha, &err);
+        count_err(err);
+      });
+      tasks.push_back([&, pp = &p] {
+        std::vector<mta::ProofBob> pf(Wn);
+        std::vector<Nat> cB(Wn);
+        for (size_t wi = 0; wi < Wn; ++wi) {
+          pf[wi] = pp->bobwc[wi].pf;
+          cB[wi] = pp->bobwc[wi].cB;
+        }
+        std::vector<uint8_t> err;
+        mta::AliceEndBatch(sess, nodes[pp->i].sk, pf, nodes[pp->i].dln, pp->cA, cB, &Wp[pp->j], &pp->mu, &err);
+        count_err(err);
+      });
     }
-    mta::AliceEndBatch(sess, nodes[p.i].sk, pf, nodes[p.i].dln, p.cA, cB, nullptr, &p.alpha, &err);
-    for (auto e : err) st.errors += e != 0;
-    mta::AliceEndBatch(sess, nodes[p.i].sk, pfwc, nodes[p.i].dln, p.cA, cBwc, &Wp[p.j], &p.mu, &err);
-    for (auto e : err) st.errors += e != 0;
+    run_tasks(tasks);
   }
   const double t3 = now();
   for (const auto& p : pairs)
@@ -121,6 +182,8 @@ MtaStats RunSigningMtA(const std::vector<NodeKeys>& nodes, int signers, size_t w
   st.round2_s = t2 - t1;
   st.round3_s = t3 - t2;
   st.total_s = t3 - t0;
+  st.errors = errors.load();
+  st.engine_busy_s = Engine::get().busy_seconds();
   return st;
 }
 

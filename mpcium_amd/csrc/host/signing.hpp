@@ -34,6 +34,7 @@ struct NodeKeys {
 
 struct MtaStats {
   double round1_s = 0, round2_s = 0, round3_s = 0, total_s = 0;
+  double engine_busy_s = 0;  // inside libmpcx calls (GPU + transfers), summed over the concurrent tasks
   uint64_t wallets = 0, pairs = 0, sessions = 0;  // sessions = wallets x ordered pairs
   uint64_t errors = 0;                            // non-OK status codes
   uint64_t relation_failures = 0;                 // alpha + beta != k gamma (or mu + nu != k w)

@@ -270,7 +270,8 @@ def bench_signing_mta(nodes: Sequence[Dict[str, int]], signers: int, wallets: in
     sks = (PaillierKey * len(nodes))(*[_paillier(k, n["N"], n["LambdaN"], n["P"], n["Q"]) for n in nodes])
     dlns = (DLN * len(nodes))(*[_dln(k, {"NTilde": n["NTildei"], "h1": n["H1i"], "h2": n["H2i"],
                                          "P": 2 * n["p"] + 1, "Q": 2 * n["q"] + 1}) for n in nodes])
-    st = np.zeros(8, dtype=np.float64)
+    st = np.zeros(9, dtype=np.float64)
     _check(lib().mpcxh_bench_signing_mta(W, sks, dlns, len(nodes), signers, wallets, seed, st.ctypes.data))
-    keys = ["round1_s", "round2_s", "round3_s", "total_s", "wallets", "sessions", "errors", "relation_failures"]
+    keys = ["round1_s", "round2_s", "round3_s", "total_s", "wallets", "sessions", "errors", "relation_failures",
+            "engine_busy_s"]
     return dict(zip(keys, [float(x) for x in st]))
