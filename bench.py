@@ -97,6 +97,151 @@ def cpu_baseline(N: int, seconds: float, threads: int):
                       f"4-bit window); Go/tss-lib absent from the image"}
 
 
+def _c_exp_words(lib, nw):
+    """x^y mod m through the C restatement of Go's expNNMontgomery (words in/out)."""
+    import ctypes
+    from oracle import crosscheck as cc
+
+    def f(x, y, m):
+        out = (ctypes.c_uint32 * nw)()
+        ew = max(1, (y.bit_length() + 31) // 32)
+        lib.gomodexp_montgomery(out, cc._words(x, nw), nw, cc._words(y, ew), ew, cc._words(m, nw), nw)
+        return int.from_bytes(bytes(out), "little")
+    return f
+
+
+def cpu_baseline_paillier(N: int, seconds: float, threads: int):
+    """Config 1 on host cores: tss-lib Encrypt (Gamma^m r^N mod N^2, both as
+    Go Exps) + HomoMult (c^b), with Go's expNNMontgomery restated in C."""
+    from oracle import crosscheck as cc
+    lib = cc.load_c_oracle()
+    if lib is None:
+        return None
+    N2 = N * N
+    nw = (N2.bit_length() + 31) // 32
+    exp = _c_exp_words(lib, nw)
+    done = [0] * threads
+    stop = time.perf_counter() + seconds
+    Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+    def work(t):
+        import random
+        rng = random.Random(11 + t)
+        while time.perf_counter() < stop:
+            m, r, b = rng.randrange(N), rng.randrange(1, N), rng.randrange(Q)
+            c = exp(N + 1, m, N2) * exp(r, N, N2) % N2
+            exp(c, b, N2)
+            done[t] += 1
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    n = sum(done)
+    return {"value": n / el, "unit": "Encrypt+HomoMult ops/s", "cores": threads, "kind": "port",
+            "sample": f"{n} x (Encrypt: Gamma^m, r^N mod N^2 as Exps; HomoMult: c^b, b < q) in {el:.1f} s on "
+                      f"{threads} host threads; oracle/gomodexp.c (Go expNNMontgomery restated in C)"}
+
+
+def paillier_line(N: int, batch: int, reps: int, cpu: bool, threads: int):
+    """Config 1 (BASELINE.json): tss-lib paillier Encrypt + HomoMult over a
+    batch of `batch` ops, 2048-bit N, through the host mirror of
+    crypto/paillier (libmpcx_host.so -> libmpcx.so; host buffers, so the rate
+    includes PCIe and the Python<->words conversion)."""
+    import random
+    from mpcium_amd import host as mhost
+    from oracle import gomath as gm
+    mhost.init(int(os.environ.get("LOCAL_RANK", "0")))
+    pk = mhost.PublicKey(N)
+    rng = random.Random(0x6D706331)
+    Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+    ms = [rng.randrange(N) for _ in range(batch)]
+    rs = [rng.randrange(1, N) for _ in range(batch)]
+    bs = [rng.randrange(Q) for _ in range(batch)]
+    cs, err = pk.encrypt(ms, rs)
+    out, err2 = pk.homo_mult(bs, cs)
+    if any(err) or any(err2):
+        raise SystemExit("paillier line: error codes")
+    for i in range(0, batch, max(1, batch // 8)):  # untimed spot check vs the oracle formulas
+        if cs[i] != gm.paillier_encrypt(N, ms[i], rs[i]) or out[i] != gm.paillier_homo_mult(N, bs[i], cs[i]):
+            raise SystemExit(f"paillier line: mismatch at {i}")
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        cs, _ = pk.encrypt(ms, rs)
+        pk.homo_mult(bs, cs)
+    el = time.perf_counter() - t0
+    line = {"metric": "tss-lib paillier Encrypt+HomoMult ops/s (config 1: batch of 1024 ops, 2048-bit N)",
+            "value": batch * reps / el, "unit": "Encrypt+HomoMult ops/s", "batch": batch, "reps": reps,
+            "seconds": el, "n_gpus": 1,
+            "note": "host-buffer API end to end (Python ints -> words -> PCIe -> GPU -> back); Encrypt's Gamma^m "
+                    "is the bit-exact 1 + mN shortcut, r^N a shared-exponent GPU batch, c^b per-operand",
+            "cpu_baseline": None}
+    if cpu:
+        line["cpu_baseline"] = cpu_baseline_paillier(N, 10.0, threads)
+    return line
+
+
+def cpu_baseline_fermat(seconds: float, threads: int):
+    """Config 3's work unit on host cores: the 1024-bit Fermat test
+    2^(p-1) mod p of tss-lib's Pocklington check, as a Go Exp (C restatement)."""
+    from oracle import crosscheck as cc
+    lib = cc.load_c_oracle()
+    if lib is None:
+        return None
+    exp = _c_exp_words(lib, 32)
+    done = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def work(t):
+        import random
+        rng = random.Random(23 + t)
+        while time.perf_counter() < stop:
+            p = rng.getrandbits(1024) | 1 | (1 << 1023)
+            exp(2, p - 1, p)
+            done[t] += 1
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    el = time.perf_counter() - t0
+    return {"value": sum(done) / el, "unit": "1024-bit Fermat tests/s", "cores": threads, "kind": "port",
+            "sample": f"{sum(done)} x 2^(p-1) mod p (1024-bit p) in {el:.1f} s on {threads} host threads; "
+                      f"oracle/gomodexp.c"}
+
+
+def safeprime_line(num: int, seed: int, cpu: bool, threads: int):
+    """Config 3 (BASELINE.json): GeneratePreParams' safe-prime search
+    (tss-lib candidate stream, host sieve, GPU Fermat + Miller-Rabin), one GPU:
+    `num` 1024-bit safe primes in stream order."""
+    from mpcium_amd import host as mhost
+    mhost.init(int(os.environ.get("LOCAL_RANK", "0")))
+    mhost.safe_primes(1024, 1, seed=seed + 1)  # warm-up (allocations, first launches)
+    t0 = time.perf_counter()
+    res, st = mhost.safe_primes(1024, num, seed=seed)
+    el = time.perf_counter() - t0
+    for p, q, _ in res:  # untimed: p = 2q + 1, both prime (CPython pow MR spot check)
+        if p != 2 * q + 1 or pow(2, p - 1, p) != 1 or pow(3, q - 1, q) != 1:
+            raise SystemExit("safe-prime line: bad prime")
+    line = {"metric": "1024-bit safe primes/s (config 3: GeneratePreParams search, one GPU)",
+            "value": num / el, "unit": "safe primes/s", "safe_primes": num, "seconds": el,
+            "fermat_tests_per_s": st["fermat_tests"] / el, "candidates": st["candidates"],
+            "sieved_out": st["sieved_out"], "fermat_tests": st["fermat_tests"], "mr_tests": st["mr_tests"],
+            "n_gpus": 1, "cpu_baseline": None}
+    if cpu:
+        b = cpu_baseline_fermat(8.0, threads)
+        if b:
+            # host safe-prime rate at the same Fermat tests per safe prime (the Exp dominates tss-lib's loop)
+            b["safe_primes_per_s_equiv"] = b["value"] / (st["fermat_tests"] / num)
+        line["cpu_baseline"] = b
+    return line
+
+
 def load_nodes():
     with open(os.path.join(ROOT, "tests", "golden", "node_preparams.json")) as f:
         d = json.load(f)
@@ -206,6 +351,8 @@ def main():
     ap.add_argument("--wallets", type=int, default=10000,
                     help="config 4: wallets per GPU for the 2-of-3 signing MtA line (0: skip)")
     ap.add_argument("--signers", type=int, default=2)
+    ap.add_argument("--extra-lines", type=int, default=1,
+                    help="1: add the config-1 (Paillier batch) and config-3 (safe primes) objects at N=1")
     ap.add_argument("--cpu-sign-seconds", type=float, default=20.0)
     ap.add_argument("--modbits", type=int, default=4096, choices=(2048, 4096),
                     help="4096: x^N mod N^2 (config 2, the bench line); 2048: x^N mod N (Paillier N / N~ class)")
@@ -328,6 +475,11 @@ def main():
     if args.wallets > 0:
         result["signing"] = signing_line(args, world, rank)
         result["signing"]["cpu_baseline"] = sign_cpu
+    if args.extra_lines and world == 1:
+        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
+        cpu = rank == 0 and not args.no_cpu_baseline
+        result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, thr)
+        result["safe_prime"] = safeprime_line(8, 0x5AFE, cpu, thr)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -152,6 +152,17 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
  * probablyPrimeMillerRabin, go:src/math/big/prime.go). */
 int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* bases, uint8_t* ok);
 
+/* Safe-prime candidate batch on the GPU (up:common/safe_prime.go
+ * runGenPrimeRoutine steps 1-5): raw = count candidates' (q_bits+7)/8 random
+ * bytes each, in stream order (63 <= q_bits <= 1023). Each candidate q is
+ * masked / delta-walked / length-checked exactly as tss-lib does, q and
+ * p = 2q+1 are trial-divided by the primes 59..2039 (exact: only composites
+ * are dropped), and every survivor gets the Pocklington test 2^(p-1) mod p.
+ * Output, ascending candidate index: *n_out survivors of the sieve, their
+ * indices idx_out[j] and Fermat verdicts ok_out[j] (both sized >= count). */
+int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t count, uint32_t q_bits,
+                                uint32_t* n_out, uint32_t* idx_out, uint8_t* ok_out);
+
 /* Fixed-base comb tables for long-lived bases of a <= 2080-bit modulus (the
  * h1, h2 of a node's N~ that every MtA range proof and DLN proof
  * exponentiates: up:crypto/mta/range_proof.go, up:crypto/mta/proofs.go,

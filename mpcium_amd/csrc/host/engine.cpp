@@ -185,6 +185,19 @@ std::vector<uint8_t> Engine::fermat2(const std::vector<Nat>& cands) {
   return ok;
 }
 
+std::vector<std::pair<uint32_t, bool>> Engine::safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes,
+                                                                      uint32_t count, uint32_t q_bits) {
+  std::vector<uint32_t> idx(count);
+  std::vector<uint8_t> ok(count);
+  uint32_t n = 0;
+  std::lock_guard<std::mutex> lk(mu_);
+  int rc = mpcx_safeprime_sieve_fermat(raw, nbytes, count, q_bits, &n, idx.data(), ok.data());
+  if (rc) throw_last(rc, "mpcx_safeprime_sieve_fermat");
+  std::vector<std::pair<uint32_t, bool>> out(n);
+  for (uint32_t j = 0; j < n; ++j) out[j] = {idx[j], ok[j] != 0};
+  return out;
+}
+
 std::vector<uint8_t> Engine::strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases) {
   if (n.size() != bases.size()) throw std::invalid_argument("one base per candidate");
   if (n.empty()) return {};

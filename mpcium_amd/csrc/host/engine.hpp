@@ -52,6 +52,10 @@ class Engine {
   double busy_seconds() const { return (double)busy_ns_.load() * 1e-9; }
   void reset_busy() { busy_ns_ = 0; }
   std::vector<uint8_t> fermat2(const std::vector<Nat>& cands);
+  // mpcx_safeprime_sieve_fermat: (index, Pocklington verdict) of the sieve
+  // survivors among `count` raw candidates, ascending index
+  std::vector<std::pair<uint32_t, bool>> safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t count,
+                                                                uint32_t q_bits);
   std::vector<uint8_t> strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases);
 
  private:

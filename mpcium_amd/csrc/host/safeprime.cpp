@@ -126,59 +126,81 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, con
   SafePrimeStats st;
   const int qBitLen = bitLen - 1;
   const size_t nbytes = (size_t)(qBitLen + 7) / 8;
+  // GPU sieve (mpcx_safeprime_sieve_fermat) for q of 63..1023 bits: candidate
+  // masks, delta walk, trial division and the Pocklington test all on the
+  // device; the host draws the stream and runs Miller-Rabin on the rare
+  // Fermat survivors. Smaller sizes keep the host sieve.
+  const bool gpu_sieve = qBitLen >= 63;
+  if (batch == 0) batch = gpu_sieve ? 196608 : 16384;
   std::vector<GermainSafePrime> out;
   std::vector<uint8_t> raw(nbytes * batch);
   const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   uint64_t index = 0;
   while ((int)out.size() < numPrimes && index < max_candidates) {
-    // draw a batch from the stream (sequential: stream order is the contract)
-    for (size_t i = 0; i < batch; ++i) rand(raw.data() + i * nbytes, nbytes);
-    std::vector<Nat> qs(batch);
-    std::vector<uint8_t> keep(batch, 0);
-    auto work = [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) {
-        qs[i] = CandidateFromBytes(raw.data() + i * nbytes, nbytes, qBitLen);
-        keep[i] = (qs[i].bit_len() == (uint32_t)qBitLen) && (bitLen <= 12 || passes_trial(qs[i]));
+    // draw a batch from the stream: one read of batch candidates' bytes is the
+    // same byte stream as batch sequential reads (stream order is the contract)
+    rand(raw.data(), nbytes * batch);
+    // Fermat survivors (stream order): candidate index in the batch and q
+    std::vector<size_t> fidx;
+    std::vector<Nat> fq;
+    if (gpu_sieve) {
+      const auto sv = Engine::get().safeprime_sieve_fermat(raw.data(), (uint32_t)nbytes, (uint32_t)batch,
+                                                           (uint32_t)qBitLen);
+      st.sieved_out += batch - sv.size();
+      st.fermat_tests += sv.size();
+      for (const auto& [i, ok] : sv) {
+        if (!ok) continue;
+        fidx.push_back(i);
+        fq.push_back(CandidateFromBytes(raw.data() + (size_t)i * nbytes, nbytes, qBitLen));
       }
-    };
-    std::vector<std::thread> th;
-    const size_t chunk = (batch + nthreads - 1) / nthreads;
-    for (unsigned t = 0; t < nthreads; ++t) {
-      const size_t lo = t * chunk, hi = std::min(batch, lo + chunk);
-      if (lo < hi) th.emplace_back(work, lo, hi);
-    }
-    for (auto& t : th) t.join();
-    std::vector<size_t> idx;
-    std::vector<Nat> ps;
-    for (size_t i = 0; i < batch; ++i) {
-      if (!keep[i]) continue;
-      idx.push_back(i);
-      ps.push_back((qs[i] << 1) + Nat(1));
+    } else {
+      std::vector<Nat> qs(batch);
+      std::vector<uint8_t> keep(batch, 0);
+      auto work = [&](size_t lo, size_t hi) {
+        for (size_t i = lo; i < hi; ++i) {
+          qs[i] = CandidateFromBytes(raw.data() + i * nbytes, nbytes, qBitLen);
+          keep[i] = (qs[i].bit_len() == (uint32_t)qBitLen) && (bitLen <= 12 || passes_trial(qs[i]));
+        }
+      };
+      std::vector<std::thread> th;
+      const size_t chunk = (batch + nthreads - 1) / nthreads;
+      for (unsigned t = 0; t < nthreads; ++t) {
+        const size_t lo = t * chunk, hi = std::min(batch, lo + chunk);
+        if (lo < hi) th.emplace_back(work, lo, hi);
+      }
+      for (auto& t : th) t.join();
+      std::vector<size_t> idx;
+      std::vector<Nat> ps;
+      for (size_t i = 0; i < batch; ++i) {
+        if (!keep[i]) continue;
+        idx.push_back(i);
+        ps.push_back((qs[i] << 1) + Nat(1));
+      }
+      st.sieved_out += batch - idx.size();
+      st.fermat_tests += ps.size();
+      // GPU: Pocklington criterion 2^(p-1) == 1 mod p on every survivor
+      std::vector<uint8_t> f = bitLen >= 4 ? Engine::get().fermat2(ps) : std::vector<uint8_t>(ps.size(), 1);
+      for (size_t j = 0; j < idx.size(); ++j) {
+        if (!f[j]) continue;
+        fidx.push_back(idx[j]);
+        fq.push_back(qs[idx[j]]);
+      }
     }
     st.candidates += batch;
-    st.sieved_out += batch - idx.size();
-    st.fermat_tests += ps.size();
-    // GPU: Pocklington criterion 2^(p-1) == 1 mod p on every survivor
-    std::vector<uint8_t> f = bitLen >= 4 ? Engine::get().fermat2(ps) : std::vector<uint8_t>(ps.size(), 1);
     // GPU: Miller-Rabin on q for the Fermat survivors, in stream order
-    std::vector<size_t> surv;
     std::vector<Nat> mr_n, mr_a;
-    for (size_t j = 0; j < idx.size(); ++j) {
-      if (!f[j]) continue;
-      surv.push_back(j);
-      for (const Nat& a : mr_bases(qs[idx[j]])) {
-        mr_n.push_back(qs[idx[j]]);
+    for (const Nat& q : fq)
+      for (const Nat& a : mr_bases(q)) {
+        mr_n.push_back(q);
         mr_a.push_back(a);
       }
-    }
     st.mr_tests += mr_n.size();
     std::vector<uint8_t> mr = Engine::get().strong_probable_prime(mr_n, mr_a);
-    for (size_t s = 0; s < surv.size() && (int)out.size() < numPrimes; ++s) {
+    for (size_t s = 0; s < fq.size() && (int)out.size() < numPrimes; ++s) {
       bool prime = true;
       for (size_t r = 0; r < 21; ++r) prime &= mr[s * 21 + r] != 0;
       if (!prime) continue;
-      const size_t j = surv[s];
-      out.push_back({ps[j], qs[idx[j]], index + idx[j]});
+      out.push_back({(fq[s] << 1) + Nat(1), fq[s], index + fidx[s]});
     }
     index += batch;
   }

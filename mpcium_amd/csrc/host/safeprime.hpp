@@ -41,7 +41,7 @@ struct SafePrimeStats {
 
 // common.GetRandomSafePrimesConcurrent(ctx, bitLen, numPrimes, 1, rand)
 std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, const RandFn& rand,
-                                                  SafePrimeStats* stats = nullptr, size_t batch = 16384,
+                                                  SafePrimeStats* stats = nullptr, size_t batch = 0,
                                                   uint64_t max_candidates = (1ull << 40));
 
 // Candidate q from raw bytes (steps 1-3); exposed for tests.

@@ -60,6 +60,33 @@ struct Sha256 {
 }  // namespace
 
 void CounterDRBG::read(uint8_t* out, size_t n) {
+  // drain the current block, then -- for bulk reads (a safe-prime candidate
+  // batch) -- compute whole counter blocks in parallel: block c depends only
+  // on (seed, c), so the byte stream is identical to sequential reads
+  if (n >= (64u << 10)) {
+    const size_t take = std::min(n, buf_.size() - pos_);
+    std::memcpy(out, buf_.data() + pos_, take);
+    pos_ += take;
+    out += take;
+    n -= take;
+    const size_t blocks = n / 32;
+    const uint64_t c0 = ctr_;
+    const size_t per = 4096;
+    parallel_for((blocks + per - 1) / per, [&](size_t t) {
+      uint8_t msg[25];
+      std::memcpy(msg, "mpcx-drbg", 9);
+      for (int i = 0; i < 8; ++i) msg[9 + i] = (uint8_t)(seed_ >> (8 * i));
+      const size_t hi = std::min(blocks, (t + 1) * per);
+      for (size_t b = t * per; b < hi; ++b) {
+        const uint64_t c = c0 + b;
+        for (int i = 0; i < 8; ++i) msg[17 + i] = (uint8_t)(c >> (8 * i));
+        Sha256::digest_short(msg, sizeof msg, out + b * 32);
+      }
+    });
+    ctr_ = c0 + blocks;
+    out += blocks * 32;
+    n -= blocks * 32;
+  }
   while (n) {
     if (pos_ == buf_.size()) {
       uint8_t msg[25];

@@ -33,6 +33,7 @@ hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st
 hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g1(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_sieve(const mpcx::SieveArgs* a, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 }
 
@@ -74,6 +75,7 @@ struct Staging {
   size_t bytes = 0;
 };
 Staging g_stage[4];  // bases, exps, out, misc
+Staging g_sieve[3];  // survivors' p words, survivors' indices, trial-division tables + counter
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -303,6 +305,10 @@ int mpcx_shutdown(void) {
   g_ws = nullptr;
   g_ws_bytes = 0;
   for (auto& s : g_stage) {
+    if (s.ptr) (void)hipFree(s.ptr);
+    s = Staging{};
+  }
+  for (auto& s : g_sieve) {
     if (s.ptr) (void)hipFree(s.ptr);
     s = Staging{};
   }
@@ -578,7 +584,7 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
   if ((rc = ensure_buffer(g_stage[0], pb)) || (rc = ensure_buffer(g_stage[3], count))) return rc;
   hipError_t e = hipMemcpy(g_stage[0].ptr, p, pb, hipMemcpyHostToDevice);
   if (e != hipSuccess) return hip_fail(e, "copy candidates");
-  mpcx::FermatArgs a;
+  mpcx::FermatArgs a{};
   a.p = (const uint32_t*)g_stage[0].ptr;
   a.ok = (uint8_t*)g_stage[3].ptr;
   a.count = count;
@@ -866,5 +872,118 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
   if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
   e = hipMemcpy(out, g_stage[2].ptr, ob, hipMemcpyDeviceToHost);
   if (e != hipSuccess) return hip_fail(e, "copy results");
+  return MPCX_OK;
+}
+
+// ------------------------------------------------------------ safe-prime sieve
+namespace {
+// trial-division groups: primes 59..2039 packed into products < 2^32 (the
+// host sieve's grouping, csrc/host/safeprime.cpp)
+struct TrialTables {
+  std::vector<uint32_t> prod, start, primes;
+  std::vector<uint64_t> inv;
+  TrialTables() {
+    std::vector<uint32_t> ps;
+    for (uint32_t v = 59; v < 2048; v += 2) {
+      bool pr = true;
+      for (uint32_t d = 3; d * d <= v; d += 2)
+        if (v % d == 0) {
+          pr = false;
+          break;
+        }
+      if (pr) ps.push_back(v);
+    }
+    uint64_t cur = 1;
+    start.push_back(0);
+    for (uint32_t p : ps) {
+      if (cur * p >= (1ull << 32)) {
+        prod.push_back((uint32_t)cur);
+        start.push_back((uint32_t)primes.size());
+        cur = 1;
+      }
+      cur *= p;
+      primes.push_back(p);
+    }
+    prod.push_back((uint32_t)cur);
+    start.push_back((uint32_t)primes.size());
+    for (uint32_t d : prod) inv.push_back(~0ull / d);
+  }
+};
+}  // namespace
+
+int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t count, uint32_t q_bits,
+                                uint32_t* n_out, uint32_t* idx_out, uint8_t* ok_out) {
+  if (!n_out) return fail(MPCX_EINVAL, "null n_out");
+  *n_out = 0;
+  if (q_bits < 63 || q_bits > 1023) return fail(MPCX_EINVAL, "q_bits %u outside [63, 1023]", q_bits);
+  if (nbytes != (q_bits + 7) / 8) return fail(MPCX_EINVAL, "nbytes %u != (q_bits + 7) / 8", nbytes);
+  if (count == 0) return MPCX_OK;
+  if (!raw || !idx_out || !ok_out) return fail(MPCX_EINVAL, "null buffer");
+  static const TrialTables tt;
+  std::lock_guard<std::mutex> lk(g_mu);
+  int rc = ensure_device();
+  if (rc) return rc;
+  constexpr uint32_t W = MPCX_SIEVE_MAX_BYTES / 4;
+  const size_t ng = tt.prod.size();
+  // misc buffer: counter | prod | start | primes | inv (8-byte aligned)
+  const size_t off_prod = 2, off_start = off_prod + ng, off_primes = off_start + tt.start.size();
+  const size_t off_inv = (off_primes + tt.primes.size() + 1) / 2 * 2;
+  const size_t misc_words = off_inv + 2 * ng;
+  if ((rc = ensure_buffer(g_stage[0], (size_t)count * nbytes)) || (rc = ensure_buffer(g_stage[3], count)) ||
+      (rc = ensure_buffer(g_sieve[0], (size_t)count * W * 4)) || (rc = ensure_buffer(g_sieve[1], (size_t)count * 4)) ||
+      (rc = ensure_buffer(g_sieve[2], misc_words * 4)))
+    return rc;
+  std::vector<uint32_t> misc(misc_words, 0);
+  std::copy(tt.prod.begin(), tt.prod.end(), misc.begin() + off_prod);
+  std::copy(tt.start.begin(), tt.start.end(), misc.begin() + off_start);
+  std::copy(tt.primes.begin(), tt.primes.end(), misc.begin() + off_primes);
+  std::memcpy(misc.data() + off_inv, tt.inv.data(), ng * 8);
+  hipError_t e = hipMemcpy(g_sieve[2].ptr, misc.data(), misc_words * 4, hipMemcpyHostToDevice);
+  if (e == hipSuccess) e = hipMemcpy(g_stage[0].ptr, raw, (size_t)count * nbytes, hipMemcpyHostToDevice);
+  if (e != hipSuccess) return hip_fail(e, "copy sieve inputs");
+  uint32_t* dm = (uint32_t*)g_sieve[2].ptr;
+  mpcx::SieveArgs sa{};
+  sa.raw = (const uint8_t*)g_stage[0].ptr;
+  sa.nbytes = nbytes;
+  sa.count = count;
+  sa.q_bits = q_bits;
+  sa.tprod = dm + off_prod;
+  sa.tstart = dm + off_start;
+  sa.tprimes = dm + off_primes;
+  sa.tinv = (const uint64_t*)(dm + off_inv);
+  sa.ngroups = (uint32_t)ng;
+  sa.out_p = (uint32_t*)g_sieve[0].ptr;
+  sa.out_idx = (uint32_t*)g_sieve[1].ptr;
+  sa.out_count = dm;
+  e = mpcx_launch_sieve(&sa, nullptr);
+  if (e != hipSuccess) return hip_fail(e, "launch k_sieve");
+  mpcx::FermatArgs fa{};
+  fa.p = sa.out_p;
+  fa.ok = (uint8_t*)g_stage[3].ptr;
+  fa.count = count;
+  fa.p_words = W;
+  fa.count_dev = dm;
+  e = mpcx_launch_fermat2(&fa, (count + 63) / 64, nullptr);
+  if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
+  uint32_t n = 0;
+  e = hipMemcpy(&n, dm, 4, hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return hip_fail(e, "copy survivor count");
+  if (n > count) return fail(MPCX_EHIP, "sieve survivor count %u > %u", n, count);
+  std::vector<uint32_t> idx(n);
+  std::vector<uint8_t> ok(n);
+  if (n) {
+    e = hipMemcpy(idx.data(), sa.out_idx, (size_t)n * 4, hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(ok.data(), fa.ok, n, hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "copy survivors");
+  }
+  // stream order
+  std::vector<uint32_t> ord(n);
+  for (uint32_t j = 0; j < n; ++j) ord[j] = j;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return idx[x] < idx[y]; });
+  for (uint32_t j = 0; j < n; ++j) {
+    idx_out[j] = idx[ord[j]];
+    ok_out[j] = ok[ord[j]];
+  }
+  *n_out = n;
   return MPCX_OK;
 }

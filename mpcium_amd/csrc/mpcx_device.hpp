@@ -652,7 +652,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   __shared__ uint32_t lds[65 * L + 1];
   const int lane = threadIdx.x;
   const uint32_t op = blockIdx.x * 64u + lane;
-  const bool active = op < a.count;
+  const uint32_t cnt = a.count_dev ? min(a.count, *a.count_dev) : a.count;
+  if (blockIdx.x * 64u >= cnt) return;  // whole wave beyond the sieve's survivors
+  const bool active = op < cnt;
   uint32_t* bl = lds + lane * L;
   uint32_t Nd[K], A[K];
   const uint32_t* pw = a.p + (size_t)(active ? op : 0) * a.p_words;

@@ -119,6 +119,24 @@ struct FermatArgs {
   uint8_t* ok;
   uint32_t count;
   uint32_t p_words;
+  const uint32_t* count_dev;  // optional: candidates = min(count, *count_dev) (sieve output)
+};
+
+// Safe-prime candidate sieve (tss-lib runGenPrimeRoutine steps 1-3 plus exact
+// trial division of q and 2q+1, up:common/safe_prime.go): one thread per
+// candidate; survivors p = 2q+1 are appended (atomic slot) with their index.
+#define MPCX_SIEVE_MAX_BYTES 128  // q of <= 1023 bits
+struct SieveArgs {
+  const uint8_t* raw;        // count x nbytes big-endian random bytes (the stream)
+  uint32_t nbytes, count, q_bits;
+  const uint32_t* tprod;     // trial groups: product of primes (< 2^32)
+  const uint64_t* tinv;      // floor((2^64 - 1) / tprod)
+  const uint32_t* tstart;    // group g's primes: tprimes[tstart[g] .. tstart[g+1])
+  const uint32_t* tprimes;
+  uint32_t ngroups;
+  uint32_t* out_p;           // survivors: count x 32 words (p = 2q + 1)
+  uint32_t* out_idx;         // survivors' candidate indices
+  uint32_t* out_count;       // survivor counter (zeroed before the launch)
 };
 
 struct MrArgs {

@@ -97,6 +97,116 @@ __global__ __launch_bounds__(64) void k_expsched(const ExpSchedArgs a) {
   s[MPCX_SCHED_WIDTH] = (uint32_t)w;
 }
 
+
+// ----------------------------------------------------- safe-prime sieve
+// One thread per candidate of tss-lib's runGenPrimeRoutine stream
+// (up:common/safe_prime.go; restated in csrc/host/safeprime.cpp
+// CandidateFromBytes and oracle/safeprime_ref.py):
+//  1. (qBitLen+7)/8 big-endian bytes, masked to qBitLen bits with the top two
+//     bits set, made odd;
+//  2. delta walk (+2) until q + delta is coprime to 3..53 (Go's old
+//     crypto/rand.Prime walk over q mod smallPrimesProduct: the residues mod
+//     each prime carry the same information);
+//  3. bit length == qBitLen;
+//  + exact trial division of q and p = 2q+1 by the primes 59..2039 (never
+//     rejects a prime, so the first accepted candidate is unchanged).
+// Survivors p = 2q+1 (32 words) go to an atomically allocated slot with the
+// candidate index; the host restores stream order.
+namespace {
+__device__ __forceinline__ uint32_t mod_step(uint32_t r, uint32_t w, uint32_t d, uint64_t inv) {
+  // (r 2^32 + w) mod d for r < d < 2^32: Barrett with inv = floor((2^64-1)/d)
+  const uint64_t x = ((uint64_t)r << 32) | w;
+  const uint64_t q = __umul64hi(x, inv);
+  uint64_t rem = x - q * d;
+  while (rem >= d) rem -= d;
+  return (uint32_t)rem;
+}
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_sieve(const SieveArgs a) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= a.count) return;
+  constexpr int W = MPCX_SIEVE_MAX_BYTES / 4;
+  uint32_t q[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) q[w] = 0;
+  const uint8_t* b = a.raw + (size_t)i * a.nbytes;
+  const uint32_t n = a.nbytes;
+  uint32_t bm = a.q_bits % 8u;
+  if (bm == 0) bm = 8;
+  // big-endian bytes -> little-endian words, with the masks of step 1
+  for (uint32_t j = 0; j < n; ++j) {
+    uint32_t v = b[j];
+    if (j == 0) {
+      v &= (1u << bm) - 1u;
+      v |= bm >= 2 ? (3u << (bm - 2)) : 1u;
+    }
+    if (j == 1 && bm < 2) v |= 0x80u;
+    if (j == n - 1) v |= 1u;
+    const uint32_t pos = n - 1 - j;  // byte position from the least significant end
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if ((uint32_t)w == (pos >> 2)) q[w] |= v << (8u * (pos & 3u));
+  }
+  // step 2: residues mod 3..53, delta walk
+  constexpr uint32_t sp[15] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53};
+  uint32_t r[15];
+#pragma unroll
+  for (int k = 0; k < 15; ++k) {
+    uint64_t acc = 0;
+#pragma unroll
+    for (int w = W - 1; w >= 0; --w) acc = ((acc << 32) | q[w]) % sp[k];
+    r[k] = (uint32_t)acc;
+  }
+  uint32_t delta = 0;
+  for (uint32_t d = 0; d < (1u << 20); d += 2) {
+    bool bad = false;
+#pragma unroll
+    for (int k = 0; k < 15; ++k) bad |= (r[k] + d) % sp[k] == 0;
+    if (!bad) {
+      delta = d;
+      break;
+    }
+  }
+  {
+    uint64_t c = delta;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      c += q[w];
+      q[w] = (uint32_t)c;
+      c >>= 32;
+    }
+  }
+  // step 3: bit length
+  uint32_t bits = 0;
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (q[w]) bits = 32u * w + 32u - __builtin_clz(q[w]);
+  if (bits != a.q_bits) return;
+  // trial division of q and 2q+1
+  for (uint32_t g = 0; g < a.ngroups; ++g) {
+    const uint32_t d = a.tprod[g];
+    const uint64_t inv = a.tinv[g];
+    uint32_t rr = 0;
+#pragma unroll
+    for (int w = W - 1; w >= 0; --w) rr = mod_step(rr, q[w], d, inv);
+    for (uint32_t t = a.tstart[g]; t < a.tstart[g + 1]; ++t) {
+      const uint32_t pr = a.tprimes[t];
+      const uint32_t rq = rr % pr;
+      if (rq == 0 || (2u * rq + 1u) % pr == 0) return;
+    }
+  }
+  const uint32_t slot = atomicAdd(a.out_count, 1u);
+  a.out_idx[slot] = i;
+  uint32_t* o = a.out_p + (size_t)slot * W;
+  uint32_t c = 1;  // p = 2q + 1
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    o[w] = (q[w] << 1) | c;
+    c = q[w] >> 31;
+  }
+}
+
 }  // namespace mpcx
 
 extern "C" {
@@ -116,6 +226,11 @@ __attribute__((visibility("hidden"))) hipError_t mpcx_launch_mr(const mpcx::MrAr
 __attribute__((visibility("hidden"))) hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a,
                                                                       hipStream_t st) {
   hipLaunchKernelGGL(mpcx::k_expsched, dim3(1), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_sieve(const mpcx::SieveArgs* a, hipStream_t st) {
+  hipLaunchKernelGGL(mpcx::k_sieve, dim3((a->count + 255) / 256), dim3(256), 0, st, *a);
   return hipGetLastError();
 }
 

@@ -51,6 +51,8 @@ SIGNATURES = [
     ("mpcx_fixedbase_exp_batch", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_vp), ctypes.c_uint32,
                                                 ctypes.POINTER(_vp), _u32p, _vp, ctypes.c_uint32, _vp,
                                                 ctypes.c_uint32]),
+    ("mpcx_safeprime_sieve_fermat", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u32p,
+                                                   _vp, _vp]),
     ("mpcx_dev_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
     ("mpcx_dev_free", ctypes.c_int, [_vp]),
     ("mpcx_memcpy_h2d", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
@@ -312,3 +314,17 @@ def mr_batch(ns: Sequence[int], bases: Sequence[int]) -> List[bool]:
     ok = np.zeros(len(ns), dtype=np.uint8)
     _check(lib().mpcx_mr_batch(len(ns), Nw.ctypes.data, w, A.ctypes.data, ok.ctypes.data))
     return [bool(x) for x in ok]
+
+
+def safeprime_sieve_fermat(raw: bytes, q_bits: int):
+    """GPU candidate batch (mpcx_safeprime_sieve_fermat): [(index, fermat_ok)]
+    for the sieve survivors among len(raw) // nbytes candidates."""
+    nb = (q_bits + 7) // 8
+    count = len(raw) // nb
+    buf = np.frombuffer(raw[:count * nb], dtype=np.uint8).copy()
+    idx = np.zeros(max(count, 1), dtype="<u4")
+    ok = np.zeros(max(count, 1), dtype=np.uint8)
+    n = ctypes.c_uint32()
+    _check(lib().mpcx_safeprime_sieve_fermat(buf.ctypes.data, nb, count, q_bits, ctypes.byref(n), idx.ctypes.data,
+                                             ok.ctypes.data))
+    return [(int(i), bool(o)) for i, o in zip(idx[:n.value], ok[:n.value])]

@@ -119,3 +119,45 @@ def test_generate_preparams_relations(host):
     assert pp["Alpha"] * pp["Beta"] % (p * q) == 1
     assert math.gcd(pp["H1i"], Nt) == 1
     assert stats["candidates"] > 0
+
+
+_SIEVE_PRIMES = [v for v in range(59, 2048, 2) if all(v % d for d in range(3, int(v ** 0.5) + 1, 2))]
+
+
+@pytest.mark.parametrize("q_bits", [63, 255, 511, 1023])
+def test_gpu_sieve_fermat_matches_oracle(gpu, q_bits):
+    """mpcx_safeprime_sieve_fermat vs the oracle candidate layout
+    (oracle/safeprime_ref.candidate_from_bytes), exact trial division of q and
+    2q+1 by 59..2039, and pow(2, p-1, p) for every survivor."""
+    nb = (q_bits + 7) // 8
+    count = 3000
+    raw = gm.CounterDRBG(0x51E7E + q_bits).read(nb * count)
+    # a few crafted candidates: all-ones, all-zeros, a top-bit-overflowing walk
+    raw = b"\xff" * nb + b"\x00" * nb + raw[2 * nb:]
+    got = gpu.safeprime_sieve_fermat(raw, q_bits)
+    want = []
+    for i in range(count):
+        q = sp.candidate_from_bytes(raw[i * nb:(i + 1) * nb], q_bits)
+        if q.bit_length() != q_bits:
+            continue
+        p = 2 * q + 1
+        if any(q % t == 0 or p % t == 0 for t in _SIEVE_PRIMES):
+            continue
+        want.append((i, pow(2, p - 1, p) == 1))
+    assert got == want
+    assert any(ok for _, ok in got) or q_bits == 1023
+
+
+def test_safe_primes_1024_gpu_sieve(host):
+    """One GeneratePreParams-size search through the GPU sieve path: p = 2q+1
+    with p, q prime (CPython pow Miller-Rabin spot check), the index's stream
+    bytes give q, and the GPU survivors before it are all rejected."""
+    got, stats = host.safe_primes(1024, 2, seed=0x5AFE)
+    nb = 128
+    for p, q, idx in got:
+        assert p == 2 * q + 1 and p.bit_length() == 1024
+        assert all(pow(a, q - 1, q) == 1 for a in (2, 3, 5, 7)) and pow(2, p - 1, p) == 1
+        raw = gm.CounterDRBG(0x5AFE).read(nb * (idx + 1))[idx * nb:]
+        assert sp.candidate_from_bytes(raw, 1023) == q
+    assert got[0][2] < got[1][2]
+    assert stats["fermat_tests"] > 0 and stats["candidates"] >= got[1][2]

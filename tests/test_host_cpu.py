@@ -33,6 +33,9 @@ def test_host_header_symbols(hostlib):
 def test_drbg_matches_oracle(hostlib):
     for seed in (0, 1, 0x6D706331, 2 ** 64 - 1):
         assert hostlib.drbg_read(seed, 1000) == gm.CounterDRBG(seed).read(1000)
+    # bulk reads (>= 64 KiB: counter blocks computed in parallel) give the same stream
+    for n in (65536, 65536 + 17, 300001):
+        assert hostlib.drbg_read(7, n) == gm.CounterDRBG(7).read(n)
 
 
 def test_candidate_layout_matches_oracle(hostlib):
