@@ -278,6 +278,109 @@ def _signing_worker(args):
     return pairs
 
 
+def _keygen_worker(args):
+    """One process of the config-5 CPU baseline: cycles through the six proof
+    primitives (oracle/proofs_ref.py with Go's expNN restated in C) until the
+    deadline; returns {primitive: [count, seconds]}."""
+    deadline, seed = args
+    from oracle import crosscheck as cc
+    from oracle import proofs_ref as PR
+    from oracle import tss_ref as T
+    lib = cc.load_c_oracle()
+    PR._pw = lambda x, y, m: cc.c_expnn(lib, x % m, y, m)
+    nodes = load_nodes()
+    A, B = nodes[0], nodes[1]
+    rd = T.Reader(seed)
+    ss = rd.read(32)
+    acc = {k: [0, 0.0] for k in ("dln_prove", "dln_verify", "mod_prove", "mod_verify", "fac_prove", "fac_verify")}
+    dln = mod = fac = None
+    while time.time() < deadline:
+        t = time.perf_counter()
+        dln = PR.dln_prove(A["H1i"], A["H2i"], A["Alpha"], A["p"], A["q"], A["NTildei"], rd)
+        acc["dln_prove"][0] += 1
+        acc["dln_prove"][1] += time.perf_counter() - t
+        t = time.perf_counter()
+        assert PR.dln_verify(dln, A["H1i"], A["H2i"], A["NTildei"])
+        acc["dln_verify"][0] += 1
+        acc["dln_verify"][1] += time.perf_counter() - t
+        t = time.perf_counter()
+        mod = PR.mod_prove(ss, A["N"], A["P"], A["Q"], rd)
+        acc["mod_prove"][0] += 1
+        acc["mod_prove"][1] += time.perf_counter() - t
+        t = time.perf_counter()
+        assert PR.mod_verify(mod, ss, A["N"])
+        acc["mod_verify"][0] += 1
+        acc["mod_verify"][1] += time.perf_counter() - t
+        t = time.perf_counter()
+        fac = PR.fac_prove(ss, A["N"], B["NTildei"], B["H1i"], B["H2i"], A["P"], A["Q"], rd)
+        acc["fac_prove"][0] += 1
+        acc["fac_prove"][1] += time.perf_counter() - t
+        t = time.perf_counter()
+        assert PR.fac_verify(fac, ss, A["N"], B["NTildei"], B["H1i"], B["H2i"])
+        acc["fac_verify"][0] += 1
+        acc["fac_verify"][1] += time.perf_counter() - t
+    return acc
+
+
+def cpu_baseline_keygen(seconds: float, procs: int, parties: int):
+    """Config 5 on host cores: per-primitive times of the proof restatement
+    (one process per core, all running at once), composed into the per-session
+    mix of keygenload.hpp: n(2 DLN + Mod + (n-1) Fac) proofs and
+    n(n-1)(2 DLN + Mod + Fac) verifications."""
+    from concurrent.futures import ProcessPoolExecutor
+    import multiprocessing as mp
+    from oracle import crosscheck as cc
+    if cc.load_c_oracle() is None:
+        return None
+    deadline = time.time() + seconds
+    with ProcessPoolExecutor(procs, mp_context=mp.get_context("fork")) as ex:
+        res = list(ex.map(_keygen_worker, [(deadline, 0x6B0 + i) for i in range(procs)]))
+    tot = {k: [sum(r[k][0] for r in res), sum(r[k][1] for r in res)] for k in res[0]}
+    if any(c == 0 for c, _ in tot.values()):
+        return None
+    per = {k: s / c for k, (c, s) in tot.items()}
+    n = parties
+    mix = {"dln_prove": 2 * n, "mod_prove": n, "fac_prove": n * (n - 1),
+           "dln_verify": 2 * n * (n - 1), "mod_verify": n * (n - 1), "fac_verify": n * (n - 1)}
+    cpu_s = sum(mix[k] * per[k] for k in mix)
+    return {"value": procs / cpu_s, "unit": "sessions/s", "cores": procs, "kind": "port",
+            "per_primitive_s": per,
+            "sample": f"{sum(c for c, _ in tot.values())} proof primitives (DLN/Mod/Fac prove + verify) in "
+                      f"{seconds:.0f} s on {procs} processes, composed into one {n}-party session's mix "
+                      f"({cpu_s:.1f} CPU-s per session); oracle/proofs_ref.py with Go expNN restated in C"}
+
+
+def keygen_line(args):
+    """Config 5 (BASELINE.json): keygen / reshare proof work under load --
+    every party of every session proves DLN x2 + Mod + Fac per peer and
+    verifies all peers' proofs (csrc/host/keygenload.hpp), 5 parties (3-of-5),
+    on one GPU. Parties: the 3 fixture nodes plus 2 generated here by the GPU
+    GeneratePreParams (untimed)."""
+    from mpcium_amd import host as mhost
+    from mpcium_amd import proofs as mproofs
+    mhost.init(int(os.environ.get("LOCAL_RANK", "0")))
+    parties = load_nodes()
+    for seed in (0x6D706335, 0x6D706336)[:max(0, args.parties - len(parties))]:
+        pp, _ = mhost.generate_preparams(seed=seed)
+        parties.append(pp)
+    parties = parties[:args.parties]
+    warm = mproofs.bench_keygen_proofs(parties, 4, seed=0x6B66)
+    if warm["failures"]:
+        raise SystemExit(f"keygen proofs warmup: {warm}")
+    st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67)
+    if st["failures"]:
+        raise SystemExit(f"keygen proofs: {st}")
+    line = {"metric": f"{len(parties)}-party keygen/reshare sessions/s (config 5: DLN x2 + Mod + Fac proofs per party, "
+                      f"every peer verified)",
+            "value": st["sessions"] / st["total_s"], "unit": "sessions/s", "n_gpus": 1,
+            "sessions": int(st["sessions"]), "parties": len(parties), "proofs": int(st["proofs"]),
+            "verifications": int(st["verifications"]), "seconds": st["total_s"], "prove_s": st["prove_s"],
+            "verify_s": st["verify_s"], "engine_busy_s": st["engine_busy_s"],
+            "verifications_per_s": st["verifications"] / st["total_s"], "checked": "every verification passes",
+            "cpu_baseline": None}
+    return line
+
+
 def cpu_baseline_signing(seconds: float, procs: int):
     """2-of-3 signing's MtA work on host cores: the oracle restatement of
     tss-lib's MtA (oracle/mta_ref.py) with exponentiations by the C
@@ -351,6 +454,9 @@ def main():
     ap.add_argument("--wallets", type=int, default=10000,
                     help="config 4: wallets per GPU for the 2-of-3 signing MtA line (0: skip)")
     ap.add_argument("--signers", type=int, default=2)
+    ap.add_argument("--keygen-sessions", type=int, default=256,
+                    help="config 5: keygen/reshare sessions for the proof-work line (0: skip)")
+    ap.add_argument("--parties", type=int, default=5)
     ap.add_argument("--extra-lines", type=int, default=1,
                     help="1: add the config-1 (Paillier batch) and config-3 (safe primes) objects at N=1")
     ap.add_argument("--cpu-sign-seconds", type=float, default=20.0)
@@ -369,6 +475,9 @@ def main():
     sign_cpu = None
     if args.wallets > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
         sign_cpu = cpu_baseline_signing(args.cpu_sign_seconds, args.cpu_threads or min(16, os.cpu_count() or 1))
+    keygen_cpu = None
+    if args.keygen_sessions > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        keygen_cpu = cpu_baseline_keygen(16.0, args.cpu_threads or min(16, os.cpu_count() or 1), args.parties)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -480,6 +589,9 @@ def main():
         cpu = rank == 0 and not args.no_cpu_baseline
         result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, thr)
         result["safe_prime"] = safeprime_line(8, 0x5AFE, cpu, thr)
+    if args.keygen_sessions > 0 and world == 1:
+        result["keygen"] = keygen_line(args)
+        result["keygen"]["cpu_baseline"] = keygen_cpu
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -180,6 +180,25 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
 int mpcxh_bench_signing_mta(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
                             uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out);
 
+/* Config-5 driver: the proof work of `sessions` keygen / reshare sessions of
+ * n_parties nodes (csrc/host/keygenload.hpp): every party proves DLN x2,
+ * Paillier-Blum Mod, and a Fac proof to each peer; every party verifies
+ * every peer's proofs. Integers are w words wide (w >= 64).
+ * stats_out[9]: prove_s, verify_s, total_s, sessions, parties, proofs,
+ * verifications, failures, engine_busy_s. */
+typedef struct {
+  mpcxh_paillier_t paillier;  /* the party's own Paillier private key */
+  const uint32_t* NTilde;
+  const uint32_t* h1;
+  const uint32_t* h2;
+  const uint32_t* alpha;      /* h2 = h1^alpha mod N~ */
+  const uint32_t* beta;       /* alpha^-1 mod pq */
+  const uint32_t* p;          /* N~ = (2p+1)(2q+1) */
+  const uint32_t* q;
+} mpcxh_party_t;
+int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
+                              uint64_t seed, double* stats_out);
+
 /* Host-side helpers of the MtA path, exported as test hooks (no GPU needed):
  * common.SHA512_256i / SHA512_256i_TAGGED (tag == NULL: untagged) over count
  * integers of w words -> 32-byte digest; secp256k1 k*G and k*P (k: w words,

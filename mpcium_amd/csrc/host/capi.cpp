@@ -15,6 +15,7 @@
 #include "mta.hpp"
 #include "proofs.hpp"
 #include "safeprime.hpp"
+#include "keygenload.hpp"
 #include "signing.hpp"
 
 using namespace mpcx::host;
@@ -562,3 +563,29 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
 }
 
 }  // extern "C"
+
+int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
+                              uint64_t seed, double* stats_out) {
+  return guard([&] {
+    if (w < 64) throw std::invalid_argument("party integer width must be >= 64 words");
+    if (!parties || !stats_out) throw std::invalid_argument("null argument");
+    std::vector<keygenload::PartyKeys> ps(n_parties);
+    for (uint32_t i = 0; i < n_parties; ++i) {
+      const mpcxh_party_t& a = parties[i];
+      if (!a.NTilde || !a.h1 || !a.h2 || !a.alpha || !a.beta || !a.p || !a.q)
+        throw std::invalid_argument("null party field");
+      ps[i].sk = paillier_from(&a.paillier, w);
+      ps[i].NTilde = Nat::from_words(a.NTilde, w);
+      ps[i].h1 = Nat::from_words(a.h1, w);
+      ps[i].h2 = Nat::from_words(a.h2, w);
+      ps[i].alpha = Nat::from_words(a.alpha, w);
+      ps[i].beta = Nat::from_words(a.beta, w);
+      ps[i].p = Nat::from_words(a.p, w);
+      ps[i].q = Nat::from_words(a.q, w);
+    }
+    const auto st = keygenload::RunKeygenProofs(ps, sessions, seed);
+    const double v[9] = {st.prove_s, st.verify_s, st.total_s, (double)st.sessions, (double)st.parties,
+                         (double)st.proofs, (double)st.verifications, (double)st.failures, st.engine_busy_s};
+    std::memcpy(stats_out, v, sizeof v);
+  });
+}

@@ -27,6 +27,7 @@ SIGNATURES = [
     ("mpcxh_mod_verify_batch", _i, [_u32, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mpcxh_fac_prove_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("mpcxh_fac_verify_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
+    ("mpcxh_bench_keygen_proofs", _i, [_u32, _vp, _u32, _u32, _u64, _vp]),
 ]
 _bound = False
 
@@ -142,3 +143,31 @@ def fac_verify(sessions: Sequence[bytes], N0: int, NCap: int, s: int, t: int, pf
     _host._check(lib().mpcxh_fac_verify_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n,
                                               pf.ctypes.data, neg.ctypes.data, ok.ctypes.data))
     return [bool(x) for x in ok]
+
+
+class _Party(ctypes.Structure):
+    _fields_ = [("N", _vp), ("LambdaN", _vp), ("P", _vp), ("Q", _vp), ("NTilde", _vp), ("h1", _vp), ("h2", _vp),
+                ("alpha", _vp), ("beta", _vp), ("p", _vp), ("q", _vp)]
+
+
+def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B67) -> dict:
+    """Config-5 driver (csrc/host/keygenload.hpp): the DLN / Mod / Fac proof
+    work of `sessions` keygen or reshare sessions of len(parties) nodes.
+    parties: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i, Alpha, Beta, p, q."""
+    keep = []
+
+    def ptr(v):
+        a = _one(v)
+        keep.append(a)
+        return a.ctypes.data
+
+    arr = (_Party * len(parties))()
+    for k, n in enumerate(parties):
+        arr[k] = _Party(ptr(n["N"]), ptr(n["LambdaN"]), ptr(n["P"]), ptr(n["Q"]), ptr(n["NTildei"]), ptr(n["H1i"]),
+                        ptr(n["H2i"]), ptr(n["Alpha"]), ptr(n["Beta"]), ptr(n["p"]), ptr(n["q"]))
+    st = np.zeros(9, dtype=np.float64)
+    rc = lib().mpcxh_bench_keygen_proofs(W, arr, len(parties), sessions, seed, st.ctypes.data)
+    _host._check(rc)
+    keys = ["prove_s", "verify_s", "total_s", "sessions", "parties", "proofs", "verifications", "failures",
+            "engine_busy_s"]
+    return dict(zip(keys, [float(x) for x in st]))

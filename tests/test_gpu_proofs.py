@@ -94,3 +94,19 @@ def test_fac_golden_and_rejections(pr, nodes, vec):
     # the proof is bound to the verifier's N~
     n2 = nodes[2]
     assert pr.fac_verify([ss], n0["N"], n2["NTildei"], n2["H1i"], n2["H2i"], [got[0]]) == [False]
+
+
+def test_keygen_proof_driver_small():
+    """Config-5 driver (csrc/host/keygenload.hpp) on the 3 fixture nodes:
+    every party's DLN x2 / Mod / Fac proofs verify at every peer."""
+    import json
+    import os
+    from mpcium_amd import host as mhost
+    from mpcium_amd import proofs as mproofs
+    mhost.init(0)
+    with open(os.path.join(os.path.dirname(__file__), "golden", "node_preparams.json")) as f:
+        nodes = [{k: int(v, 16) for k, v in n.items() if isinstance(v, str) and k != "paillier_source"}
+                 for n in json.load(f)["nodes"]]
+    st = mproofs.bench_keygen_proofs(nodes, 3, seed=5)
+    assert st["failures"] == 0
+    assert st["proofs"] == 3 * 3 * (3 + 2) and st["verifications"] == 3 * 3 * 2 * 4
