@@ -14,6 +14,7 @@
  *                                 HomoAdd, Decrypt; per-op error codes
  *                                 1 = ErrMessageTooLong, 2 = ErrMessageMalFormed)
  *   mpcxh_safe_primes            up:common/safe_prime.go GetRandomSafePrimesConcurrent
+ *   mpcxh_safe_prime_batch       up:common/safe_prime.go runGenPrimeRoutine (one stream batch, sharded)
  *   mpcxh_generate_preparams     up:ecdsa/keygen/prepare.go GeneratePreParams,
  *                                called at /root/reference/pkg/mpc/node.go:69
  *   mpcxh_dln_*, mpcxh_mod_*,    up:crypto/dlnproof, up:crypto/modproof,
@@ -74,6 +75,16 @@ int mpcxh_paillier_decrypt_batch(const uint32_t* N, uint32_t nw, const uint32_t*
 int mpcxh_safe_primes(int bit_len, int num, uint64_t seed, mpcxh_rand_fn rand_fn, void* rand_ctx,
                       uint32_t* p_out, uint32_t* q_out, uint32_t words, uint64_t* index_out,
                       uint64_t* stats_out);
+
+/* One batch of the same search for sharding across GPUs (up:common/safe_prime.go
+ * runGenPrimeRoutine, one batch of its candidate stream): candidates
+ * [batch_no*batch, (batch_no+1)*batch) of the CounterDRBG(seed) stream
+ * (batch 0 = default 196608). Writes up to max_out accepted primes in stream
+ * order and their count to *n_found. Rank g of G takes batch_no = g (mod G);
+ * the first `num` indices over all ranks equal mpcxh_safe_primes' output. */
+int mpcxh_safe_prime_batch(int bit_len, uint64_t seed, uint64_t batch_no, uint32_t batch, uint32_t max_out,
+                           uint32_t* p_out, uint32_t* q_out, uint32_t words, uint64_t* index_out,
+                           uint32_t* n_found, uint64_t* stats_out);
 
 /* LocalPreParams as 12 fields x 64 words: N, LambdaN, PhiN, P, Q (Paillier),
  * NTildei, H1i, H2i, Alpha, Beta, P, Q (Germain primes of N~). */

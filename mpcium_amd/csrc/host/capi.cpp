@@ -263,6 +263,30 @@ int mpcxh_safe_primes(int bit_len, int num, uint64_t seed, mpcxh_rand_fn rand_fn
   });
 }
 
+int mpcxh_safe_prime_batch(int bit_len, uint64_t seed, uint64_t batch_no, uint32_t batch, uint32_t max_out,
+                           uint32_t* p_out, uint32_t* q_out, uint32_t words, uint64_t* index_out,
+                           uint32_t* n_found, uint64_t* stats_out) {
+  return guard([&] {
+    if (!n_found) throw std::invalid_argument("n_found is NULL");
+    SafePrimeStats st;
+    auto v = SafePrimeBatch(bit_len, seed, batch_no, batch, &st);
+    const uint32_t n = (uint32_t)std::min<size_t>(v.size(), max_out);
+    for (uint32_t i = 0; i < n; ++i) {
+      v[i].p.to_words(p_out + (size_t)i * words, words);
+      v[i].q.to_words(q_out + (size_t)i * words, words);
+      if (index_out) index_out[i] = v[i].index;
+    }
+    *n_found = n;
+    if (stats_out) {
+      stats_out[0] = st.candidates;
+      stats_out[1] = st.sieved_out;
+      stats_out[2] = st.fermat_tests;
+      stats_out[3] = st.mr_tests;
+      stats_out[4] = (uint64_t)(st.seconds * 1e6);
+    }
+  });
+}
+
 int mpcxh_generate_preparams(uint64_t seed, mpcxh_rand_fn rand_fn, void* rand_ctx, uint32_t* out, uint64_t* stats_out) {
   return guard([&] {
     CounterDRBG drbg(seed);

@@ -3,6 +3,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cstdint>
 #include <cstring>
 #include <thread>
 
@@ -117,13 +118,19 @@ std::vector<Nat> mr_bases(const Nat& q) {
 }
 }  // namespace
 
-std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, const RandFn& rand,
-                                                  SafePrimeStats* stats, size_t batch, uint64_t max_candidates) {
+namespace {
+void check_safe_prime_args(int bitLen) {
   if (bitLen < 6) throw std::invalid_argument("safe prime size must be at least 6 bits");
-  if (numPrimes < 1) throw std::invalid_argument("numPrimes should be > 0");
   if (bitLen > 1024) throw std::invalid_argument("GPU candidate class holds safe primes up to 1024 bits");
-  const auto t0 = std::chrono::steady_clock::now();
-  SafePrimeStats st;
+}
+
+size_t default_batch(int bitLen) { return bitLen - 1 >= 63 ? 196608 : 16384; }
+
+// One batch of the candidate stream (raw = batch x nbytes of stream bytes whose
+// first candidate has stream index base_index): sieve, Pocklington, Miller-Rabin.
+// Appends the accepted safe primes in stream order, at most `limit` of them.
+void test_batch(int bitLen, const uint8_t* raw, size_t batch, uint64_t base_index, SafePrimeStats& st,
+                std::vector<GermainSafePrime>& out, size_t limit) {
   const int qBitLen = bitLen - 1;
   const size_t nbytes = (size_t)(qBitLen + 7) / 8;
   // GPU sieve (mpcx_safeprime_sieve_fermat) for q of 63..1023 bits: candidate
@@ -131,87 +138,118 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, con
   // device; the host draws the stream and runs Miller-Rabin on the rare
   // Fermat survivors. Smaller sizes keep the host sieve.
   const bool gpu_sieve = qBitLen >= 63;
-  if (batch == 0) batch = gpu_sieve ? 196608 : 16384;
+  const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  // Fermat survivors (stream order): candidate index in the batch and q
+  std::vector<size_t> fidx;
+  std::vector<Nat> fq;
+  if (gpu_sieve) {
+    const auto sv = Engine::get().safeprime_sieve_fermat(raw, (uint32_t)nbytes, (uint32_t)batch, (uint32_t)qBitLen);
+    st.sieved_out += batch - sv.size();
+    st.fermat_tests += sv.size();
+    for (const auto& [i, ok] : sv) {
+      if (!ok) continue;
+      fidx.push_back(i);
+      fq.push_back(CandidateFromBytes(raw + (size_t)i * nbytes, nbytes, qBitLen));
+    }
+  } else {
+    std::vector<Nat> qs(batch);
+    std::vector<uint8_t> keep(batch, 0);
+    auto work = [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        qs[i] = CandidateFromBytes(raw + i * nbytes, nbytes, qBitLen);
+        keep[i] = (qs[i].bit_len() == (uint32_t)qBitLen) && (bitLen <= 12 || passes_trial(qs[i]));
+      }
+    };
+    std::vector<std::thread> th;
+    const size_t chunk = (batch + nthreads - 1) / nthreads;
+    for (unsigned t = 0; t < nthreads; ++t) {
+      const size_t lo = t * chunk, hi = std::min(batch, lo + chunk);
+      if (lo < hi) th.emplace_back(work, lo, hi);
+    }
+    for (auto& t : th) t.join();
+    std::vector<size_t> idx;
+    std::vector<Nat> ps;
+    for (size_t i = 0; i < batch; ++i) {
+      if (!keep[i]) continue;
+      idx.push_back(i);
+      ps.push_back((qs[i] << 1) + Nat(1));
+    }
+    st.sieved_out += batch - idx.size();
+    st.fermat_tests += ps.size();
+    // GPU: Pocklington criterion 2^(p-1) == 1 mod p on every survivor
+    std::vector<uint8_t> f = bitLen >= 4 ? Engine::get().fermat2(ps) : std::vector<uint8_t>(ps.size(), 1);
+    for (size_t j = 0; j < idx.size(); ++j) {
+      if (!f[j]) continue;
+      fidx.push_back(idx[j]);
+      fq.push_back(qs[idx[j]]);
+    }
+  }
+  st.candidates += batch;
+  // GPU: Miller-Rabin on q for the Fermat survivors, in stream order
+  std::vector<Nat> mr_n, mr_a;
+  for (const Nat& q : fq)
+    for (const Nat& a : mr_bases(q)) {
+      mr_n.push_back(q);
+      mr_a.push_back(a);
+    }
+  st.mr_tests += mr_n.size();
+  std::vector<uint8_t> mr = Engine::get().strong_probable_prime(mr_n, mr_a);
+  for (size_t s = 0; s < fq.size() && out.size() < limit; ++s) {
+    bool prime = true;
+    for (size_t r = 0; r < 21; ++r) prime &= mr[s * 21 + r] != 0;
+    if (!prime) continue;
+    out.push_back({(fq[s] << 1) + Nat(1), fq[s], base_index + fidx[s]});
+  }
+}
+
+void add_stats(SafePrimeStats* stats, const SafePrimeStats& st) {
+  if (!stats) return;
+  stats->candidates += st.candidates;
+  stats->sieved_out += st.sieved_out;
+  stats->fermat_tests += st.fermat_tests;
+  stats->mr_tests += st.mr_tests;
+  stats->seconds += st.seconds;
+}
+}  // namespace
+
+std::vector<GermainSafePrime> SafePrimeBatch(int bitLen, uint64_t seed, uint64_t batch_no, size_t batch,
+                                             SafePrimeStats* stats) {
+  check_safe_prime_args(bitLen);
+  const auto t0 = std::chrono::steady_clock::now();
+  if (batch == 0) batch = default_batch(bitLen);
+  const size_t nbytes = (size_t)(bitLen - 1 + 7) / 8;
+  std::vector<uint8_t> raw(nbytes * batch);
+  CounterDRBG drbg(seed);
+  drbg.seek(batch_no * (uint64_t)raw.size());
+  drbg.read(raw.data(), raw.size());
+  SafePrimeStats st;
+  std::vector<GermainSafePrime> out;
+  test_batch(bitLen, raw.data(), batch, batch_no * batch, st, out, SIZE_MAX);
+  st.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  add_stats(stats, st);
+  return out;
+}
+
+std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, const RandFn& rand,
+                                                  SafePrimeStats* stats, size_t batch, uint64_t max_candidates) {
+  check_safe_prime_args(bitLen);
+  if (numPrimes < 1) throw std::invalid_argument("numPrimes should be > 0");
+  const auto t0 = std::chrono::steady_clock::now();
+  SafePrimeStats st;
+  const size_t nbytes = (size_t)(bitLen - 1 + 7) / 8;
+  if (batch == 0) batch = default_batch(bitLen);
   std::vector<GermainSafePrime> out;
   std::vector<uint8_t> raw(nbytes * batch);
-  const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   uint64_t index = 0;
   while ((int)out.size() < numPrimes && index < max_candidates) {
     // draw a batch from the stream: one read of batch candidates' bytes is the
     // same byte stream as batch sequential reads (stream order is the contract)
     rand(raw.data(), nbytes * batch);
-    // Fermat survivors (stream order): candidate index in the batch and q
-    std::vector<size_t> fidx;
-    std::vector<Nat> fq;
-    if (gpu_sieve) {
-      const auto sv = Engine::get().safeprime_sieve_fermat(raw.data(), (uint32_t)nbytes, (uint32_t)batch,
-                                                           (uint32_t)qBitLen);
-      st.sieved_out += batch - sv.size();
-      st.fermat_tests += sv.size();
-      for (const auto& [i, ok] : sv) {
-        if (!ok) continue;
-        fidx.push_back(i);
-        fq.push_back(CandidateFromBytes(raw.data() + (size_t)i * nbytes, nbytes, qBitLen));
-      }
-    } else {
-      std::vector<Nat> qs(batch);
-      std::vector<uint8_t> keep(batch, 0);
-      auto work = [&](size_t lo, size_t hi) {
-        for (size_t i = lo; i < hi; ++i) {
-          qs[i] = CandidateFromBytes(raw.data() + i * nbytes, nbytes, qBitLen);
-          keep[i] = (qs[i].bit_len() == (uint32_t)qBitLen) && (bitLen <= 12 || passes_trial(qs[i]));
-        }
-      };
-      std::vector<std::thread> th;
-      const size_t chunk = (batch + nthreads - 1) / nthreads;
-      for (unsigned t = 0; t < nthreads; ++t) {
-        const size_t lo = t * chunk, hi = std::min(batch, lo + chunk);
-        if (lo < hi) th.emplace_back(work, lo, hi);
-      }
-      for (auto& t : th) t.join();
-      std::vector<size_t> idx;
-      std::vector<Nat> ps;
-      for (size_t i = 0; i < batch; ++i) {
-        if (!keep[i]) continue;
-        idx.push_back(i);
-        ps.push_back((qs[i] << 1) + Nat(1));
-      }
-      st.sieved_out += batch - idx.size();
-      st.fermat_tests += ps.size();
-      // GPU: Pocklington criterion 2^(p-1) == 1 mod p on every survivor
-      std::vector<uint8_t> f = bitLen >= 4 ? Engine::get().fermat2(ps) : std::vector<uint8_t>(ps.size(), 1);
-      for (size_t j = 0; j < idx.size(); ++j) {
-        if (!f[j]) continue;
-        fidx.push_back(idx[j]);
-        fq.push_back(qs[idx[j]]);
-      }
-    }
-    st.candidates += batch;
-    // GPU: Miller-Rabin on q for the Fermat survivors, in stream order
-    std::vector<Nat> mr_n, mr_a;
-    for (const Nat& q : fq)
-      for (const Nat& a : mr_bases(q)) {
-        mr_n.push_back(q);
-        mr_a.push_back(a);
-      }
-    st.mr_tests += mr_n.size();
-    std::vector<uint8_t> mr = Engine::get().strong_probable_prime(mr_n, mr_a);
-    for (size_t s = 0; s < fq.size() && (int)out.size() < numPrimes; ++s) {
-      bool prime = true;
-      for (size_t r = 0; r < 21; ++r) prime &= mr[s * 21 + r] != 0;
-      if (!prime) continue;
-      out.push_back({(fq[s] << 1) + Nat(1), fq[s], index + fidx[s]});
-    }
+    test_batch(bitLen, raw.data(), batch, index, st, out, (size_t)numPrimes);
     index += batch;
   }
   st.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  if (stats) {
-    stats->candidates += st.candidates;
-    stats->sieved_out += st.sieved_out;
-    stats->fermat_tests += st.fermat_tests;
-    stats->mr_tests += st.mr_tests;
-    stats->seconds += st.seconds;
-  }
+  add_stats(stats, st);
   if ((int)out.size() < numPrimes) throw std::runtime_error("safe prime search exhausted max_candidates");
   return out;
 }

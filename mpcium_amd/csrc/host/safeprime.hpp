@@ -44,6 +44,15 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, con
                                                   SafePrimeStats* stats = nullptr, size_t batch = 0,
                                                   uint64_t max_candidates = (1ull << 40));
 
+// One batch of the CounterDRBG(seed) candidate stream: candidates
+// [batch_no*batch, (batch_no+1)*batch), drawn by seeking the stream to the
+// batch's first byte. Every accepted safe prime of the batch, in stream order.
+// The sharded search (mpcium_amd/shard.py safe_primes_sharded) gives rank g the
+// batches b = g (mod G) and keeps the first numPrimes indices over all ranks:
+// exactly GetRandomSafePrimes' output for the same seed and batch size.
+std::vector<GermainSafePrime> SafePrimeBatch(int bitLen, uint64_t seed, uint64_t batch_no, size_t batch = 0,
+                                             SafePrimeStats* stats = nullptr);
+
 // Candidate q from raw bytes (steps 1-3); exposed for tests.
 Nat CandidateFromBytes(const uint8_t* bytes, size_t n, int qBitLen);
 

@@ -59,6 +59,14 @@ struct Sha256 {
 };
 }  // namespace
 
+void CounterDRBG::seek(uint64_t offset) {
+  ctr_ = offset / 32;
+  buf_.clear();
+  pos_ = 0;
+  uint8_t skip[32];
+  if (offset % 32) read(skip, offset % 32);
+}
+
 void CounterDRBG::read(uint8_t* out, size_t n) {
   // drain the current block, then -- for bulk reads (a safe-prime candidate
   // batch) -- compute whole counter blocks in parallel: block c depends only

@@ -29,6 +29,9 @@ class CounterDRBG {
  public:
   explicit CounterDRBG(uint64_t seed) : seed_(seed) {}
   void read(uint8_t* out, size_t n);
+  // Position the stream at byte `offset` (block c depends only on (seed, c)):
+  // a reader seeked to k bytes yields what a fresh reader yields after k bytes.
+  void seek(uint64_t offset);
   RandFn fn() {
     return [this](uint8_t* b, size_t n) { read(b, n); };
   }

@@ -27,6 +27,7 @@ SIGNATURES = [
     ("mpcxh_paillier_decrypt_batch", _i, [_vp, _u32, _vp, _u32, _vp, _u32, _vp, _u32, _u32, _vp, _u32, _vp, _vp,
                                           _u32, _vp]),
     ("mpcxh_safe_primes", _i, [_i, _i, _u64, _vp, _vp, _vp, _vp, _u32, _vp, _vp]),
+    ("mpcxh_safe_prime_batch", _i, [_i, _u64, _u64, _u32, _u32, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("mpcxh_generate_preparams", _i, [_u64, _vp, _vp, _vp, _vp]),
     ("mpcxh_candidate_from_bytes", _i, [_vp, ctypes.c_size_t, _i, _vp, _u32]),
     ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
@@ -156,6 +157,22 @@ def safe_primes(bit_len: int, num: int, seed: int = 0, rand_fn=None):
                                    Q.ctypes.data, words, idx.ctypes.data, st.ctypes.data))
     stats = dict(zip(["candidates", "sieved_out", "fermat_tests", "mr_tests", "usec"], (int(x) for x in st)))
     return list(zip(words_to_ints(P), words_to_ints(Q), (int(i) for i in idx))), stats
+
+
+def safe_prime_batch(bit_len: int, seed: int, batch_no: int, batch: int = 0, max_out: int = 64):
+    """One batch of the CounterDRBG(seed) candidate stream (sharded search):
+    [(p, q, index)] of its accepted safe primes in stream order + stats dict."""
+    words = (bit_len + 31) // 32
+    P = np.zeros((max_out, words), dtype="<u4")
+    Q = np.zeros((max_out, words), dtype="<u4")
+    idx = np.zeros(max_out, dtype=np.uint64)
+    st = np.zeros(5, dtype=np.uint64)
+    n = ctypes.c_uint32(0)
+    _check(lib().mpcxh_safe_prime_batch(bit_len, seed, batch_no, batch, max_out, P.ctypes.data, Q.ctypes.data, words,
+                                        idx.ctypes.data, ctypes.byref(n), st.ctypes.data))
+    k = n.value
+    stats = dict(zip(["candidates", "sieved_out", "fermat_tests", "mr_tests", "usec"], (int(x) for x in st)))
+    return list(zip(words_to_ints(P[:k]), words_to_ints(Q[:k]), (int(i) for i in idx[:k]))), stats
 
 
 PREPARAM_FIELDS = ["N", "LambdaN", "PhiN", "P", "Q", "NTildei", "H1i", "H2i", "Alpha", "Beta", "p", "q"]

@@ -47,3 +47,33 @@ def max_over_ranks(values: Sequence[float], world: int) -> List[float]:
     t = torch.tensor(list(values), dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return [float(v) for v in t]
+
+
+def safe_primes_sharded(num: int, rank: int, world: int, batch_fn: Callable[[int], List[Tuple[int, int, int]]],
+                        max_rounds: int = 1 << 20):
+    """Config-3 safe-prime search sharded over `world` GPUs:
+    rank g tests stream batches b = r*world + g in round r (batch_fn(b) ->
+    [(p, q, stream index)] accepted in batch b, e.g. host.safe_prime_batch), and
+    after each round every rank all-gathers the (tiny) lists of accepted primes.
+    Once `num` are known, every batch below the round's end has been tested by
+    some rank, so the `num` smallest stream indices are exactly what a
+    single-GPU, stream-order search returns (tss-lib at concurrency 1). The only
+    exchange is that host-side gather of a few integers per round; no
+    collective touches the candidate data. Returns the same list on every rank."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank/world")
+    found: List[Tuple[int, int, int]] = []
+    for r in range(max_rounds):
+        mine = list(batch_fn(r * world + rank))
+        if world == 1:
+            parts = [mine]
+        else:
+            import torch.distributed as dist
+            parts = [None] * world
+            dist.all_gather_object(parts, mine)
+        for p in parts:
+            found.extend(p)
+        if len(found) >= num:
+            found.sort(key=lambda t: t[2])
+            return found[:num]
+    raise RuntimeError("safe prime search exhausted max_rounds")

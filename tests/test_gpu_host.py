@@ -161,3 +161,33 @@ def test_safe_primes_1024_gpu_sieve(host):
         assert sp.candidate_from_bytes(raw, 1023) == q
     assert got[0][2] < got[1][2]
     assert stats["fermat_tests"] > 0 and stats["candidates"] >= got[1][2]
+
+
+@pytest.mark.parametrize("bits,batch", [(128, 1000), (100, 777), (1024, 0)])
+def test_safe_prime_batches_sharded_equal_stream_order(host, bits, batch):
+    """Config-3 sharding: batches of the seeked CounterDRBG stream
+    (mpcxh_safe_prime_batch) dealt to G ranks round-robin give the same first
+    safe primes as the single-stream search, for G = 1, 2, 3 (ranks emulated in
+    one process; the gather itself is covered by tests/test_shard_gloo.py).
+    Batch sizes whose byte length is not a multiple of the DRBG block exercise
+    the mid-block seek."""
+    from mpcium_amd.shard import safe_primes_sharded
+    num = 3 if bits < 1024 else 2
+    seed = 0x5AFE + bits
+    want, _ = host.safe_primes(bits, num, seed=seed)
+    cache = {}
+
+    def fn(b):
+        if b not in cache:
+            cache[b], _ = host.safe_prime_batch(bits, seed, b, batch)
+        return cache[b]
+
+    for world in (1, 2, 3):
+        found = []
+        for r in range(1 << 12):   # all ranks' round-r batches, then the gather
+            for g in range(world):
+                found += fn(r * world + g)
+            if len(found) >= num:
+                break
+        assert sorted(found, key=lambda t: t[2])[:num] == want, world
+    assert safe_primes_sharded(num, 0, 1, fn) == want

@@ -57,3 +57,40 @@ def test_gather_and_max_world2():
         p.join(timeout=60)
     assert ok
     assert t == [1.5, 2.0]
+
+
+def _fake_batch(b):
+    """Stand-in for host.safe_prime_batch: a deterministic, sparse set of
+    'accepted' stream indices per batch of 100 candidates."""
+    import random
+    rng = random.Random(b)
+    return [(2 * i + 3, i + 1, i) for i in sorted(rng.sample(range(b * 100, b * 100 + 100), rng.choice([0, 0, 1, 2])))]
+
+
+def _sp_worker(rank, world, port, q):
+    import torch.distributed as dist
+    from mpcium_amd.shard import safe_primes_sharded
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    out = safe_primes_sharded(7, rank, world, _fake_batch)
+    q.put((rank, out))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_safe_primes_sharded_world2_matches_stream_order():
+    from mpcium_amd.shard import safe_primes_sharded
+    single = safe_primes_sharded(7, 0, 1, _fake_batch)
+    assert [t[2] for t in single] == sorted(t[2] for t in single) and len(single) == 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_sp_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=100) for _ in range(2))
+    for p in procs:
+        p.join(timeout=60)
+    assert res[0] == single and res[1] == single
