@@ -37,6 +37,15 @@ PEAK_INT32_NOMINAL = 256 * 64 * 2.4e9  # 39.3 T 32x32->64 MAC/s: v_mad_u64_u32 i
 PEAK_MAD_MEASURED = 33.8e12            # tools/microbench/valu_rates.hip, 8 waves/SIMD (profiles/r01_valu_rates.txt)
 
 
+
+def gpu_index() -> int:
+    """This rank's GPU: LOCAL_RANK, wrapped onto the visible devices so a
+    multi-rank rehearsal also runs on a one-GPU box (the driver's N-GPU runs
+    have one device per local rank, so this is the identity there).
+    torch.cuda.device_count() does not initialise the GPU on this image."""
+    import torch
+    return int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
+
 def alg_macs(mod_bits: int, exp_bits: int) -> float:
     """W = (E + ceil(E/4)) * 2 L^2 32-bit MACs, L = 32-bit limbs."""
     L = math.ceil(mod_bits / 32)
@@ -154,7 +163,7 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, threads: int):
     import random
     from mpcium_amd import host as mhost
     from oracle import gomath as gm
-    mhost.init(int(os.environ.get("LOCAL_RANK", "0")))
+    mhost.init(gpu_index())
     pk = mhost.PublicKey(N)
     rng = random.Random(0x6D706331)
     Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
@@ -215,24 +224,48 @@ def cpu_baseline_fermat(seconds: float, threads: int):
                       f"oracle/gomodexp.c"}
 
 
-def safeprime_line(num: int, seed: int, cpu: bool, threads: int):
+def safeprime_line(num: int, seed: int, cpu: bool, threads: int, world: int = 1, rank: int = 0):
     """Config 3 (BASELINE.json): GeneratePreParams' safe-prime search
-    (tss-lib candidate stream, host sieve, GPU Fermat + Miller-Rabin), one GPU:
-    `num` 1024-bit safe primes in stream order."""
+    (tss-lib candidate stream, GPU sieve + Fermat, GPU Miller-Rabin): `num`
+    1024-bit safe primes in stream order. One GPU: the single-stream search.
+    world > 1: the stream's batches dealt round-robin to the ranks
+    (shard.safe_primes_sharded, same primes as one GPU), strong scaling."""
     from mpcium_amd import host as mhost
-    mhost.init(int(os.environ.get("LOCAL_RANK", "0")))
+    from mpcium_amd.shard import max_over_ranks, safe_primes_sharded
+    mhost.init(gpu_index())
     mhost.safe_primes(1024, 1, seed=seed + 1)  # warm-up (allocations, first launches)
-    t0 = time.perf_counter()
-    res, st = mhost.safe_primes(1024, num, seed=seed)
-    el = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        acc = {"candidates": 0, "sieved_out": 0, "fermat_tests": 0, "mr_tests": 0}
+
+        def fn(b):
+            r, s_ = mhost.safe_prime_batch(1024, seed, b)
+            for k in acc:
+                acc[k] += s_[k]
+            return r
+
+        dist.barrier()
+        t0 = time.perf_counter()
+        res = safe_primes_sharded(num, rank, world, fn)
+        el = time.perf_counter() - t0
+        el = max_over_ranks([el], world)[0]
+        import torch
+        t = torch.tensor([float(acc[k]) for k in acc], dtype=torch.float64)
+        dist.all_reduce(t)  # whole-job candidate / test counts (gloo, host tensors)
+        st = dict(zip(acc, (int(x) for x in t)))
+    else:
+        t0 = time.perf_counter()
+        res, st = mhost.safe_primes(1024, num, seed=seed)
+        el = time.perf_counter() - t0
     for p, q, _ in res:  # untimed: p = 2q + 1, both prime (CPython pow MR spot check)
         if p != 2 * q + 1 or pow(2, p - 1, p) != 1 or pow(3, q - 1, q) != 1:
             raise SystemExit("safe-prime line: bad prime")
-    line = {"metric": "1024-bit safe primes/s (config 3: GeneratePreParams search, one GPU)",
+    line = {"metric": f"1024-bit safe primes/s (config 3: GeneratePreParams search, {world} GPU(s))",
             "value": num / el, "unit": "safe primes/s", "safe_primes": num, "seconds": el,
             "fermat_tests_per_s": st["fermat_tests"] / el, "candidates": st["candidates"],
             "sieved_out": st["sieved_out"], "fermat_tests": st["fermat_tests"], "mr_tests": st["mr_tests"],
-            "n_gpus": 1, "cpu_baseline": None}
+            "n_gpus": world, "scaling": "strong", "first_index": res[0][2], "last_index": res[-1][2],
+            "cpu_baseline": None}
     if cpu:
         b = cpu_baseline_fermat(8.0, threads)
         if b:
@@ -358,7 +391,7 @@ def keygen_line(args):
     GeneratePreParams (untimed)."""
     from mpcium_amd import host as mhost
     from mpcium_amd import proofs as mproofs
-    mhost.init(int(os.environ.get("LOCAL_RANK", "0")))
+    mhost.init(gpu_index())
     parties = load_nodes()
     for seed in (0x6D706335, 0x6D706336)[:max(0, args.parties - len(parties))]:
         pp, _ = mhost.generate_preparams(seed=seed)
@@ -411,7 +444,7 @@ def signing_line(args, world, rank):
     from mpcium_amd import host as mhost
     from mpcium_amd import mta
     from mpcium_amd.shard import max_over_ranks
-    mhost.init(int(os.environ.get("LOCAL_RANK", "0")))
+    mhost.init(gpu_index())
     nodes = load_nodes()
     warm = mta.bench_signing_mta(nodes, args.signers, 256, seed=0x5167 + 7919 * rank)
     if warm["errors"] or warm["relation_failures"]:
@@ -469,7 +502,7 @@ def main():
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
+    local = gpu_index()
     # The signing CPU baseline forks worker processes: run it before this
     # process touches the GPU.
     sign_cpu = None
@@ -584,11 +617,12 @@ def main():
     if args.wallets > 0:
         result["signing"] = signing_line(args, world, rank)
         result["signing"]["cpu_baseline"] = sign_cpu
-    if args.extra_lines and world == 1:
+    if args.extra_lines:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        cpu = rank == 0 and not args.no_cpu_baseline
-        result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, thr)
-        result["safe_prime"] = safeprime_line(8, 0x5AFE, cpu, thr)
+        cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+        if world == 1:
+            result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, thr)
+        result["safe_prime"] = safeprime_line(8, 0x5AFE, cpu, thr, world, rank)
     if args.keygen_sessions > 0 and world == 1:
         result["keygen"] = keygen_line(args)
         result["keygen"]["cpu_baseline"] = keygen_cpu
