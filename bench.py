@@ -38,6 +38,28 @@ PEAK_MAD_MEASURED = 33.8e12            # tools/microbench/valu_rates.hip, 8 wave
 
 
 
+
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r01", "pmc_traffic", "summary.json")
+
+
+def pmc_traffic(count: int, modbits: int, mod) -> dict:
+    """roofline.traffic: fabric bytes per launch of the bench kernel from the
+    committed rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate --pmc runs of
+    this same bench command, tools/gpu_pmc_traffic.sh). rocprofv3 cannot run
+    inside the timed process. Only reported for the workload those passes
+    measured (65,536 operands, 4096-bit modulus, 4x37 quad geometry); null
+    otherwise. The algorithmic I/O is 1 KB per operand (base in, result out).
+    Most FETCH bytes are window-table re-reads that miss the per-XCD L2
+    (DESIGN.md 5.4); they are served by the MALL, not by HBM."""
+    out = {"traffic": None, "traffic_unit": "bytes/launch", "algorithmic_io_bytes": count * 2 * modbits // 8}
+    if count != 65536 or modbits != 4096 or (mod.P, mod.K) != (4, 37) or not os.path.exists(PMC_TRAFFIC):
+        return out
+    with open(PMC_TRAFFIC) as f:
+        s = json.load(f)
+    out["traffic"] = s["hbm_bytes_per_launch"]
+    out["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) + " (FETCH_SIZE+WRITE_SIZE KB x 1024, uncorrected)"
+    return out
+
 def gpu_index() -> int:
     """This rank's GPU: LOCAL_RANK, wrapped onto the visible devices so a
     multi-rank rehearsal also runs on a one-GPU box (the driver's N-GPU runs
@@ -611,6 +633,7 @@ def main():
                      "alg_ops_per_modexp": W, "kernel_ms": kernel_ms},
         "cpu_baseline": None,
     }
+    result["roofline"].update(pmc_traffic(count, args.modbits, mod))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         thr = args.cpu_threads or min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, thr)

@@ -7,7 +7,7 @@ mkdir -p $OUT
 run() { # name, counters...
   local name=$1; shift
   timeout -k 10 240 rocprofv3 --pmc "$@" --output-format csv -d $OUT/$name -o $name -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --verify 0 --wallets 0 > $OUT/$name.log 2>&1
+    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --verify 0 --wallets 0 --keygen-sessions 0 --extra-lines 0 > $OUT/$name.log 2>&1
   local rc=$?; echo "pass $name rc=$rc"; return $rc
 }
 run fetch FETCH_SIZE && run write WRITE_SIZE && \
