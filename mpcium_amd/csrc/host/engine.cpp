@@ -12,8 +12,10 @@ void throw_last(int rc, const char* what) {
 }
 
 Engine& Engine::get() {
-  static Engine e;
-  return e;
+  // never destroyed: releasing device tables from a static destructor could
+  // run after the HIP runtime has been torn down at process exit
+  static Engine* e = new Engine();
+  return *e;
 }
 
 void Engine::init(int device) {
@@ -23,6 +25,18 @@ void Engine::init(int device) {
   device_ = device;
   const char* fb = std::getenv("MPCX_FIXED_BASE");
   fixed_enabled_ = !(fb && fb[0] == '0');
+}
+
+void Engine::enter_call() {
+  std::lock_guard<std::mutex> lk(busy_mu_);
+  if (inflight_++ == 0) busy_t0_ = std::chrono::steady_clock::now();
+}
+
+void Engine::leave_call() {
+  std::lock_guard<std::mutex> lk(busy_mu_);
+  if (--inflight_ == 0)
+    busy_ns_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() -
+                                                                               busy_t0_).count();
 }
 
 Engine::Mod& Engine::modulus(const Nat& m) {
@@ -83,18 +97,15 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
   if (muls) M = packed(*muls);
   std::vector<uint32_t> out((size_t)bases.size() * md.words);
   int rc;
-  {
-    std::lock_guard<std::mutex> lk(mu_);
-    const auto t0 = std::chrono::steady_clock::now();
-    if (muls) {
-      rc = mpcx_modexp_mul_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
-                                 M.data(), md.class_words, out.data(), md.words);
-    } else {
-      rc = mpcx_modexp_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
-                             out.data(), md.words);
-    }
-    busy_ns_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+  enter_call();
+  if (muls) {
+    rc = mpcx_modexp_mul_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
+                               M.data(), md.class_words, out.data(), md.words);
+  } else {
+    rc = mpcx_modexp_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
+                           out.data(), md.words);
   }
+  leave_call();
   if (rc) throw_last(rc, "mpcx_modexp_batch");
   return unpack(out, bases.size(), md.words);
 }
@@ -103,28 +114,23 @@ bool Engine::fixed_base_ok(const Nat& m) const {
   return fixed_enabled_ && m.is_odd() && m.bit_len() <= 2080;
 }
 
-Engine::Fixed& Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
+Engine::Fixed Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
   auto key = std::make_pair(m.limbs(), base.limbs());
   auto it = fixed_.find(key);
-  if (it != fixed_.end() && it->second.max_bits >= need_bits) return it->second;
-  if (it != fixed_.end()) {  // grow: rebuild for the longer exponent
-    mpcx_fixedbase_release(it->second.h);
-    fixed_.erase(it);
-  }
-  if (fixed_.size() >= 256) {  // bound the device footprint (~30 MB per table)
-    for (auto& kv : fixed_) mpcx_fixedbase_release(kv.second.h);
-    fixed_.clear();
-  }
+  if (it != fixed_.end() && it->second->max_bits >= need_bits) return it->second;
+  if (it != fixed_.end()) fixed_.erase(it);  // grow: rebuild for the longer exponent
+  if (fixed_.size() >= 256) fixed_.clear();  // bound the device footprint (~30 MB per table)
   Mod& md = modulus(m);
   // MtA exponents on h1, h2 reach ~2818 bits (s2, t2 < q^3 N~ + e q N~); one size serves them all
   const uint32_t bits = std::max<uint32_t>(3072, (need_bits + 511) / 512 * 512);
-  Fixed f{};
+  auto f = std::make_shared<FixedTable>();
   std::vector<uint32_t> bw(md.class_words, 0);
   base.to_words(bw.data(), md.class_words);
-  int rc = mpcx_fixedbase_register(md.h, bw.data(), md.class_words, bits, &f.h);
+  int rc = mpcx_fixedbase_register(md.h, bw.data(), md.class_words, bits, &f->h);
   if (rc) throw_last(rc, "mpcx_fixedbase_register");
-  f.max_bits = bits;
-  return fixed_.emplace(key, f).first->second;
+  f->max_bits = bits;
+  fixed_.emplace(key, f);
+  return f;
 }
 
 std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vector<Nat>& exps,
@@ -152,18 +158,18 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
     }
   }
   std::vector<uint32_t> out((size_t)exps.size() * md.words);
-  int rc;
+  Fixed f;
   {
-    // the table is looked up (or built) and used under the lock: another
-    // thread may grow or evict it
+    // look up (or build) under the lock; the shared handle keeps the table
+    // alive while this batch uses it, even if another thread evicts it
     std::lock_guard<std::mutex> lk(mu_);
-    Fixed& f = fixed(m, b, need);
-    const uint32_t* ep = E.data();
-    const auto t0 = std::chrono::steady_clock::now();
-    rc = mpcx_fixedbase_exp_batch(1, &f.h, (uint32_t)exps.size(), &ep, &ew, muls ? Mw.data() : nullptr,
-                                  muls ? md.class_words : 0, out.data(), md.words);
-    busy_ns_ += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0).count();
+    f = fixed(m, b, need);
   }
+  const uint32_t* ep = E.data();
+  enter_call();
+  int rc = mpcx_fixedbase_exp_batch(1, &f->h, (uint32_t)exps.size(), &ep, &ew, muls ? Mw.data() : nullptr,
+                                    muls ? md.class_words : 0, out.data(), md.words);
+  leave_call();
   if (rc) throw_last(rc, "mpcx_fixedbase_exp_batch");
   return unpack(out, exps.size(), md.words);
 }
@@ -179,7 +185,6 @@ std::vector<uint8_t> Engine::fermat2(const std::vector<Nat>& cands) {
   for (const auto& c : cands) w = std::max<uint32_t>(w, (uint32_t)c.words());
   auto P = pack(cands, w);
   std::vector<uint8_t> ok(cands.size());
-  std::lock_guard<std::mutex> lk(mu_);
   int rc = mpcx_fermat2_batch((uint32_t)cands.size(), P.data(), w, ok.data());
   if (rc) throw_last(rc, "mpcx_fermat2_batch");
   return ok;
@@ -190,7 +195,6 @@ std::vector<std::pair<uint32_t, bool>> Engine::safeprime_sieve_fermat(const uint
   std::vector<uint32_t> idx(count);
   std::vector<uint8_t> ok(count);
   uint32_t n = 0;
-  std::lock_guard<std::mutex> lk(mu_);
   int rc = mpcx_safeprime_sieve_fermat(raw, nbytes, count, q_bits, &n, idx.data(), ok.data());
   if (rc) throw_last(rc, "mpcx_safeprime_sieve_fermat");
   std::vector<std::pair<uint32_t, bool>> out(n);
@@ -209,7 +213,6 @@ std::vector<uint8_t> Engine::strong_probable_prime(const std::vector<Nat>& n, co
   auto N = pack(n, w);
   auto A = pack(b, w);
   std::vector<uint8_t> ok(n.size());
-  std::lock_guard<std::mutex> lk(mu_);
   int rc = mpcx_mr_batch((uint32_t)n.size(), N.data(), w, A.data(), ok.data());
   if (rc) throw_last(rc, "mpcx_mr_batch");
   return ok;

@@ -6,7 +6,9 @@
 
 #include <atomic>
 #include <cstdint>
+#include <chrono>
 #include <map>
+#include <memory>
 #include <mutex>
 #include <stdexcept>
 #include <string>
@@ -47,8 +49,9 @@ class Engine {
   // fixed-base path usable for m (odd, <= 2080 bits) and enabled
   // (environment MPCX_FIXED_BASE=0 turns it off, for A/B runs)
   bool fixed_base_ok(const Nat& m) const;
-  // seconds spent inside libmpcx exponentiation calls (GPU + transfers),
-  // summed over calling threads since the last reset
+  // wall-clock seconds during which at least one libmpcx exponentiation call
+  // (GPU + transfers) was in flight, since the last reset. Calls from
+  // different threads run concurrently on libmpcx's lanes (streams).
   double busy_seconds() const { return (double)busy_ns_.load() * 1e-9; }
   void reset_busy() { busy_ns_ = 0; }
   std::vector<uint8_t> fermat2(const std::vector<Nat>& cands);
@@ -65,12 +68,23 @@ class Engine {
     uint32_t words;
   };
   Mod& modulus(const Nat& m);
-  struct Fixed {
-    mpcx_fb_t h;
-    uint32_t max_bits;
+  // A comb table; released when the last user drops it (another thread may
+  // grow or evict the cache entry while a batch still uses the table).
+  struct FixedTable {
+    mpcx_fb_t h = nullptr;
+    uint32_t max_bits = 0;
+    ~FixedTable() {
+      if (h) mpcx_fixedbase_release(h);
+    }
   };
-  Fixed& fixed(const Nat& m, const Nat& base, uint32_t need_bits);
-  std::mutex mu_;
+  using Fixed = std::shared_ptr<FixedTable>;
+  Fixed fixed(const Nat& m, const Nat& base, uint32_t need_bits);
+  // busy-time accounting: union of in-flight intervals
+  void enter_call();
+  void leave_call();
+  std::mutex mu_, busy_mu_;
+  int inflight_ = 0;
+  std::chrono::steady_clock::time_point busy_t0_;
   int device_ = -1;
   bool fixed_enabled_ = true;
   std::atomic<uint64_t> busy_ns_{0};

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -68,14 +69,30 @@ bool g_split = false;                    // narrow-geometry tail launch (measure
 int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): one geometry for everything
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
-uint32_t* g_ws = nullptr;  // exponentiation table workspace
-size_t g_ws_bytes = 0;
 struct Staging {
   void* ptr = nullptr;
   size_t bytes = 0;
 };
-Staging g_stage[4];  // bases, exps, out, misc
-Staging g_sieve[3];  // survivors' p words, survivors' indices, trial-division tables + counter
+// An execution lane: one HIP stream with its own exponentiation-table
+// workspace and staging buffers. Host-buffer calls from different threads run
+// on different lanes concurrently, so small or partial-round batches (a
+// latency-bound Fac-proof group, a 10k-wallet MtA step that fills 40% of the
+// wavefront slots) overlap on the GPU instead of queueing behind one lock.
+// kLanes matches the HW queues HIP gives a process by default.
+struct Lane {
+  std::mutex mu;
+  hipStream_t st = nullptr;  // created on first use (non-blocking)
+  uint32_t* ws = nullptr;    // exponentiation table workspace
+  size_t ws_bytes = 0;
+  Staging stage[4];  // bases, exps, out, misc
+  Staging sieve[3];  // survivors' p words, survivors' indices, trial-division tables + counter
+};
+constexpr int kLanes = 4;
+Lane g_lanes[kLanes];
+// Workspace of the device-buffer entry points (caller's stream, under g_mu;
+// callers order their own device-buffer calls) and of table builds.
+Lane g_dev_lane;
+std::atomic<unsigned> g_lane_rr{0};
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -179,9 +196,56 @@ hipError_t mpcx_modexp_occupancy(int geom, int* blocks_per_cu) {
   }
 }
 
+// Every entry point runs on the caller's thread: bind that thread to the
+// process's GPU (HIP's current device is per thread; a worker thread would
+// otherwise submit to device 0 on a multi-GPU node).
 int ensure_device() {
   if (g_device < 0) return fail(MPCX_ENODEV, "mpcx_init() has not been called");
+  thread_local int t_dev = -1;
+  if (t_dev != g_device) {
+    hipError_t e = hipSetDevice(g_device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    t_dev = g_device;
+  }
   return MPCX_OK;
+}
+
+// A free lane (round-robin start, first one not in use), else wait for one.
+Lane& acquire_lane(std::unique_lock<std::mutex>& lk) {
+  const unsigned start = g_lane_rr.fetch_add(1, std::memory_order_relaxed);
+  for (int i = 0; i < kLanes; ++i) {
+    Lane& l = g_lanes[(start + i) % kLanes];
+    std::unique_lock<std::mutex> t(l.mu, std::try_to_lock);
+    if (t.owns_lock()) {
+      lk = std::move(t);
+      return l;
+    }
+  }
+  Lane& l = g_lanes[start % kLanes];
+  lk = std::unique_lock<std::mutex>(l.mu);
+  return l;
+}
+
+int lane_stream(Lane& l) {
+  if (l.st) return MPCX_OK;
+  hipError_t e = hipStreamCreateWithFlags(&l.st, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    l.st = nullptr;
+    return hip_fail(e, "hipStreamCreate(lane)");
+  }
+  return MPCX_OK;
+}
+
+int h2d(void* d, const void* h, size_t bytes, hipStream_t st) {
+  if (!bytes) return MPCX_OK;
+  hipError_t e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy inputs");
+}
+
+int d2h_sync(void* h, const void* d, size_t bytes, hipStream_t st) {
+  hipError_t e = bytes ? hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, st) : hipSuccess;
+  if (e == hipSuccess) e = hipStreamSynchronize(st);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy results");
 }
 
 int ensure_buffer(Staging& s, size_t bytes) {
@@ -196,14 +260,18 @@ int ensure_buffer(Staging& s, size_t bytes) {
   return MPCX_OK;
 }
 
-int ensure_workspace(size_t bytes) {
-  if (g_ws_bytes >= bytes) return MPCX_OK;
-  if (g_ws) (void)hipFree(g_ws);
-  g_ws = nullptr;
-  g_ws_bytes = 0;
-  hipError_t e = hipMalloc((void**)&g_ws, bytes);
+int ensure_workspace(Lane& l, size_t bytes) {
+  if (l.ws_bytes >= bytes) return MPCX_OK;
+  if (l.ws) {
+    // the lane's previous kernels may still read the old workspace
+    if (l.st) (void)hipStreamSynchronize(l.st);
+    (void)hipFree(l.ws);
+  }
+  l.ws = nullptr;
+  l.ws_bytes = 0;
+  hipError_t e = hipMalloc((void**)&l.ws, bytes);
   if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(workspace %zu): %s", bytes, hipGetErrorString(e));
-  g_ws_bytes = bytes;
+  l.ws_bytes = bytes;
   return MPCX_OK;
 }
 
@@ -301,17 +369,24 @@ int mpcx_init(int device) {
 
 int mpcx_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_ws) (void)hipFree(g_ws);
-  g_ws = nullptr;
-  g_ws_bytes = 0;
-  for (auto& s : g_stage) {
-    if (s.ptr) (void)hipFree(s.ptr);
-    s = Staging{};
-  }
-  for (auto& s : g_sieve) {
-    if (s.ptr) (void)hipFree(s.ptr);
-    s = Staging{};
-  }
+  auto drop = [](Lane& l) {
+    std::lock_guard<std::mutex> ll(l.mu);
+    if (l.st) {
+      (void)hipStreamSynchronize(l.st);
+      (void)hipStreamDestroy(l.st);
+    }
+    l.st = nullptr;
+    if (l.ws) (void)hipFree(l.ws);
+    l.ws = nullptr;
+    l.ws_bytes = 0;
+    for (auto* arr : {l.stage, l.sieve})
+      for (int i = 0; i < (arr == l.stage ? 4 : 3); ++i) {
+        if (arr[i].ptr) (void)hipFree(arr[i].ptr);
+        arr[i] = Staging{};
+      }
+  };
+  for (auto& l : g_lanes) drop(l);
+  drop(g_dev_lane);
   g_device = -1;
   return MPCX_OK;
 }
@@ -389,10 +464,10 @@ int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K,
   return MPCX_OK;
 }
 
-static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
-                                const uint32_t* d_exps, uint32_t exp_words, int exp_shared, uint32_t exp_bits,
-                                const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out, uint32_t out_words,
-                                hipStream_t st) {
+static int modexp_device_locked(Lane& lane, mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases,
+                                uint32_t base_words, const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
+                                uint32_t exp_bits, const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out,
+                                uint32_t out_words, hipStream_t st) {
   const uint32_t class_words = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
   if (base_words == 0 || base_words > class_words)
     return fail(MPCX_EINVAL, "base_words %u outside [1, %u] (reduce mod m first)", base_words, class_words);
@@ -440,14 +515,14 @@ static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* 
   const bool use_sched = exp_shared && exp_bits > 0 && g_sched_width > 0;
   const size_t sched_off = ws_words;
   if (use_sched) ws_words += MPCX_SCHED_WORDS(32u * exp_words);
-  int rc = ensure_workspace(ws_words * sizeof(uint32_t));
+  int rc = ensure_workspace(lane, ws_words * sizeof(uint32_t));
   if (rc) return rc;
   if (use_sched) {
     mpcx::ExpSchedArgs sa{};
     sa.exp = d_exps;
     sa.exp_words = exp_words;
     sa.max_width = (uint32_t)g_sched_width;
-    sa.sched = g_ws + sched_off;
+    sa.sched = lane.ws + sched_off;
     hipError_t e = mpcx_launch_expsched(&sa, st);
     if (e != hipSuccess) return hip_fail(e, "launch k_expsched");
   }
@@ -465,7 +540,7 @@ static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* 
     a.exps = exp_shared ? d_exps : (d_exps ? d_exps + (size_t)pt.first * exp_words : nullptr);
     a.mul = d_muls ? d_muls + (size_t)pt.first * mul_words : nullptr;
     a.out = d_out + (size_t)pt.first * out_words;
-    a.table = g_ws + ws_off;
+    a.table = lane.ws + ws_off;
     a.count = pt.count;
     a.base_words = base_words;
     a.exp_words = exp_words;
@@ -474,7 +549,7 @@ static int modexp_device_locked(mpcx_mod_t mod, uint32_t count, const uint32_t* 
     a.out_words = out_words;
     a.n0inv = mod->n0inv;
     a.exp_shared = exp_shared ? 1 : 0;
-    a.sched = use_sched ? g_ws + sched_off : nullptr;
+    a.sched = use_sched ? lane.ws + sched_off : nullptr;
     hipError_t e = mpcx_launch_modexp(pt.geom, &a, waves, st);
     if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
     ws_off += (size_t)waves * MPCX_TABLE_ENTRIES * K * 64u;
@@ -497,28 +572,27 @@ static int modexp_host(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, ui
   if (!mod) return fail(MPCX_EINVAL, "null modulus");
   if (count == 0) return MPCX_OK;
   if (!bases || !out || (exp_words && !exps)) return fail(MPCX_EINVAL, "null buffer");
-  std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
   const uint32_t exp_bits = max_exp_bits(exps, exp_words, exp_shared, count);
   const size_t n_exp_words = exp_shared ? exp_words : (size_t)count * exp_words;
   const size_t bb = (size_t)count * base_words * 4, eb = std::max<size_t>(n_exp_words * 4, 4),
                ob = (size_t)count * out_words * 4, mb = muls ? (size_t)count * mul_words * 4 : 0;
-  if ((rc = ensure_buffer(g_stage[0], bb)) || (rc = ensure_buffer(g_stage[1], eb)) ||
-      (rc = ensure_buffer(g_stage[2], ob)) || (muls && (rc = ensure_buffer(g_stage[3], mb))))
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(lk);
+  if ((rc = lane_stream(l))) return rc;
+  Staging* sg = l.stage;
+  if ((rc = ensure_buffer(sg[0], bb)) || (rc = ensure_buffer(sg[1], eb)) || (rc = ensure_buffer(sg[2], ob)) ||
+      (muls && (rc = ensure_buffer(sg[3], mb))))
     return rc;
-  hipError_t e = hipMemcpy(g_stage[0].ptr, bases, bb, hipMemcpyHostToDevice);
-  if (e == hipSuccess && n_exp_words) e = hipMemcpy(g_stage[1].ptr, exps, n_exp_words * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess && muls) e = hipMemcpy(g_stage[3].ptr, muls, mb, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "copy inputs");
-  rc = modexp_device_locked(mod, count, (const uint32_t*)g_stage[0].ptr, base_words,
-                            (const uint32_t*)g_stage[1].ptr, exp_words, exp_shared, exp_bits,
-                            muls ? (const uint32_t*)g_stage[3].ptr : nullptr, mul_words, (uint32_t*)g_stage[2].ptr,
-                            out_words, nullptr);
+  if ((rc = h2d(sg[0].ptr, bases, bb, l.st)) || (rc = h2d(sg[1].ptr, exps, n_exp_words * 4, l.st)) ||
+      (muls && (rc = h2d(sg[3].ptr, muls, mb, l.st))))
+    return rc;
+  rc = modexp_device_locked(l, mod, count, (const uint32_t*)sg[0].ptr, base_words, (const uint32_t*)sg[1].ptr,
+                            exp_words, exp_shared, exp_bits, muls ? (const uint32_t*)sg[3].ptr : nullptr, mul_words,
+                            (uint32_t*)sg[2].ptr, out_words, l.st);
   if (rc) return rc;
-  e = hipMemcpy(out, g_stage[2].ptr, ob, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail(e, "copy results");
-  return MPCX_OK;
+  return d2h_sync(out, sg[2].ptr, ob, l.st);
 }
 
 int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
@@ -528,8 +602,8 @@ int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_b
   std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
-  return modexp_device_locked(mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits, nullptr, 0,
-                              d_out, out_words, (hipStream_t)stream);
+  return modexp_device_locked(g_dev_lane, mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits,
+                              nullptr, 0, d_out, out_words, (hipStream_t)stream);
 }
 
 int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
@@ -541,8 +615,8 @@ int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t*
   std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
-  return modexp_device_locked(mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits, d_muls,
-                              mul_words, d_out, out_words, (hipStream_t)stream);
+  return modexp_device_locked(g_dev_lane, mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits,
+                              d_muls, mul_words, d_out, out_words, (hipStream_t)stream);
 }
 
 int mpcx_modexp_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
@@ -577,23 +651,22 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
       return fail(MPCX_EINVAL, "candidate %u has %u bits > %d", i, bits, MPCX_CLASS_MAXBITS(0));
     if (bits < 3 || (pi[0] & 1u) == 0) return fail(MPCX_EINVAL, "candidate %u is not an odd integer >= 5", i);
   }
-  std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(lk);
+  if ((rc = lane_stream(l))) return rc;
   const size_t pb = (size_t)count * p_words * 4;
-  if ((rc = ensure_buffer(g_stage[0], pb)) || (rc = ensure_buffer(g_stage[3], count))) return rc;
-  hipError_t e = hipMemcpy(g_stage[0].ptr, p, pb, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "copy candidates");
+  if ((rc = ensure_buffer(l.stage[0], pb)) || (rc = ensure_buffer(l.stage[3], count))) return rc;
+  if ((rc = h2d(l.stage[0].ptr, p, pb, l.st))) return rc;
   mpcx::FermatArgs a{};
-  a.p = (const uint32_t*)g_stage[0].ptr;
-  a.ok = (uint8_t*)g_stage[3].ptr;
+  a.p = (const uint32_t*)l.stage[0].ptr;
+  a.ok = (uint8_t*)l.stage[3].ptr;
   a.count = count;
   a.p_words = p_words;
-  e = mpcx_launch_fermat2(&a, (count + 63) / 64, nullptr);
+  hipError_t e = mpcx_launch_fermat2(&a, (count + 63) / 64, l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
-  e = hipMemcpy(ok, g_stage[3].ptr, count, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail(e, "copy results");
-  return MPCX_OK;
+  return d2h_sync(ok, l.stage[3].ptr, count, l.st);
 }
 
 int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* bases, uint8_t* ok) {
@@ -606,27 +679,25 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
     if (bit_length_words(ni, n_words) < 3 || (ni[0] & 1u) == 0)
       return fail(MPCX_EINVAL, "candidate %u is not an odd integer >= 5", i);
   }
-  std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(lk);
+  if ((rc = lane_stream(l))) return rc;
   const size_t nb = (size_t)count * n_words * 4;
-  if ((rc = ensure_buffer(g_stage[0], nb)) || (rc = ensure_buffer(g_stage[1], nb)) ||
-      (rc = ensure_buffer(g_stage[3], count)))
+  if ((rc = ensure_buffer(l.stage[0], nb)) || (rc = ensure_buffer(l.stage[1], nb)) ||
+      (rc = ensure_buffer(l.stage[3], count)))
     return rc;
-  hipError_t e = hipMemcpy(g_stage[0].ptr, n, nb, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(g_stage[1].ptr, bases, nb, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "copy candidates");
+  if ((rc = h2d(l.stage[0].ptr, n, nb, l.st)) || (rc = h2d(l.stage[1].ptr, bases, nb, l.st))) return rc;
   mpcx::MrArgs a{};
-  a.n = (const uint32_t*)g_stage[0].ptr;
-  a.a = (const uint32_t*)g_stage[1].ptr;
-  a.ok = (uint8_t*)g_stage[3].ptr;
+  a.n = (const uint32_t*)l.stage[0].ptr;
+  a.a = (const uint32_t*)l.stage[1].ptr;
+  a.ok = (uint8_t*)l.stage[3].ptr;
   a.count = count;
   a.n_words = n_words;
-  e = mpcx_launch_mr(&a, (count + 63) / 64, nullptr);
+  hipError_t e = mpcx_launch_mr(&a, (count + 63) / 64, l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_mr");
-  e = hipMemcpy(ok, g_stage[3].ptr, count, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail(e, "copy results");
-  return MPCX_OK;
+  return d2h_sync(ok, l.stage[3].ptr, count, l.st);
 }
 
 int mpcx_dev_alloc(size_t bytes, void** out_ptr) {
@@ -689,6 +760,10 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
+  // the build reuses the device-buffer workspace on the null stream: drain
+  // any device-buffer call still reading it on a caller's stream (rare: once
+  // per long-lived base)
+  (void)hipDeviceSynchronize();
   const int geom = MPCX_MAIN_GEOM(mod->cls);
   const uint32_t L = (uint32_t)MPCX_GEOM_L(geom), P = (uint32_t)MPCX_GEOM_P(geom), K = (uint32_t)MPCX_GEOM_K(geom);
   const uint32_t nwin = (max_exp_bits + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS;
@@ -730,8 +805,8 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     cleanup();
     return hip_fail(e, "upload fixed-base inputs");
   }
-  rc = modexp_device_locked(mod, nwin, d_b, cw, d_e1, ew1, 0, MPCX_FB_WINDOW_BITS * (nwin - 1) + 1, nullptr, 0,
-                            d_bj, cw, nullptr);
+  rc = modexp_device_locked(g_dev_lane, mod, nwin, d_b, cw, d_e1, ew1, 0, MPCX_FB_WINDOW_BITS * (nwin - 1) + 1,
+                            nullptr, 0, d_bj, cw, nullptr);
   // T(j, v) = R * b_j^v: operand i = j*255 + (v-1) takes base b_j -> replicate b_j rows
   std::vector<uint32_t> hbj((size_t)nwin * cw), hb2;
   if (!rc) {
@@ -750,8 +825,8 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     if (e != hipSuccess) rc = hip_fail(e, "upload b_j");
   }
   if (!rc)
-    rc = modexp_device_locked(mod, (uint32_t)n2, d_b, cw, d_e2, 1, 0, MPCX_FB_WINDOW_BITS, d_m, mod->words, d_t,
-                              cw, nullptr);
+    rc = modexp_device_locked(g_dev_lane, mod, (uint32_t)n2, d_b, cw, d_e2, 1, 0, MPCX_FB_WINDOW_BITS, d_m,
+                              mod->words, d_t, cw, nullptr);
   std::vector<uint32_t> ht(n2 * cw);
   if (!rc) {
     e = hipMemcpy(ht.data(), d_t, ht.size() * 4, hipMemcpyDeviceToHost);
@@ -835,19 +910,21 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
       return fail(MPCX_EINVAL, "exponent of %u bits > fixed-base table's %u", bits, fbs[t]->nwin * MPCX_FB_WINDOW_BITS);
     nwin[t] = (bits + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS;
   }
-  std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
   const size_t eb0 = (size_t)count * exp_words[0] * 4, eb1 = nbases > 1 ? (size_t)count * exp_words[1] * 4 : 0,
                ob = (size_t)count * out_words * 4, mb = muls ? (size_t)count * mul_words * 4 : 0;
-  if ((rc = ensure_buffer(g_stage[0], eb0)) || (rc = ensure_buffer(g_stage[1], eb1)) ||
-      (rc = ensure_buffer(g_stage[2], ob)) || (muls && (rc = ensure_buffer(g_stage[3], mb))))
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(lk);
+  if ((rc = lane_stream(l))) return rc;
+  Staging* sg = l.stage;
+  if ((rc = ensure_buffer(sg[0], eb0)) || (rc = ensure_buffer(sg[1], eb1)) ||
+      (rc = ensure_buffer(sg[2], ob)) || (muls && (rc = ensure_buffer(sg[3], mb))))
     return rc;
-  hipError_t e = hipSuccess;
-  if (eb0) e = hipMemcpy(g_stage[0].ptr, exps[0], eb0, hipMemcpyHostToDevice);
-  if (e == hipSuccess && eb1) e = hipMemcpy(g_stage[1].ptr, exps[1], eb1, hipMemcpyHostToDevice);
-  if (e == hipSuccess && muls) e = hipMemcpy(g_stage[3].ptr, muls, mb, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "copy inputs");
+  if ((rc = h2d(sg[0].ptr, exps[0], eb0, l.st)) || (rc = h2d(sg[1].ptr, exps[1], eb1, l.st)) ||
+      (muls && (rc = h2d(sg[3].ptr, muls, mb, l.st))))
+    return rc;
+  hipError_t e;
   const int geom = fbs[0]->geom;
   mpcx::FixedBaseArgs a{};
   a.nd = mod->d_const + mod->const_off[geom];
@@ -855,24 +932,22 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
   a.r2d = a.nd + 2 * MPCX_GEOM_L(geom);
   for (uint32_t t = 0; t < nbases; ++t) {
     a.tables[t] = fbs[t]->d_table;
-    a.exps[t] = (const uint32_t*)g_stage[t].ptr;
+    a.exps[t] = (const uint32_t*)sg[t].ptr;
     a.exp_words[t] = exp_words[t];
     a.nwin[t] = nwin[t];
   }
   a.nbases = nbases;
-  a.mul = muls ? (const uint32_t*)g_stage[3].ptr : nullptr;
+  a.mul = muls ? (const uint32_t*)sg[3].ptr : nullptr;
   a.mul_words = muls ? mul_words : 0;
-  a.out = (uint32_t*)g_stage[2].ptr;
+  a.out = (uint32_t*)sg[2].ptr;
   a.out_words = out_words;
   a.count = count;
   a.n0inv = mod->n0inv;
   const uint32_t waves = (count + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
-  e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, nullptr)
-                                : mpcx_launch_fixedbase_g1(&a, waves, nullptr);
+  e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
+                                : mpcx_launch_fixedbase_g1(&a, waves, l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
-  e = hipMemcpy(out, g_stage[2].ptr, ob, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail(e, "copy results");
-  return MPCX_OK;
+  return d2h_sync(out, sg[2].ptr, ob, l.st);
 }
 
 // ------------------------------------------------------------ safe-prime sieve
@@ -920,30 +995,33 @@ int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t co
   if (count == 0) return MPCX_OK;
   if (!raw || !idx_out || !ok_out) return fail(MPCX_EINVAL, "null buffer");
   static const TrialTables tt;
-  std::lock_guard<std::mutex> lk(g_mu);
   int rc = ensure_device();
   if (rc) return rc;
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(lk);
+  if ((rc = lane_stream(l))) return rc;
+  Staging *sg = l.stage, *sv = l.sieve;
   constexpr uint32_t W = MPCX_SIEVE_MAX_BYTES / 4;
   const size_t ng = tt.prod.size();
   // misc buffer: counter | prod | start | primes | inv (8-byte aligned)
   const size_t off_prod = 2, off_start = off_prod + ng, off_primes = off_start + tt.start.size();
   const size_t off_inv = (off_primes + tt.primes.size() + 1) / 2 * 2;
   const size_t misc_words = off_inv + 2 * ng;
-  if ((rc = ensure_buffer(g_stage[0], (size_t)count * nbytes)) || (rc = ensure_buffer(g_stage[3], count)) ||
-      (rc = ensure_buffer(g_sieve[0], (size_t)count * W * 4)) || (rc = ensure_buffer(g_sieve[1], (size_t)count * 4)) ||
-      (rc = ensure_buffer(g_sieve[2], misc_words * 4)))
+  if ((rc = ensure_buffer(sg[0], (size_t)count * nbytes)) || (rc = ensure_buffer(sg[3], count)) ||
+      (rc = ensure_buffer(sv[0], (size_t)count * W * 4)) || (rc = ensure_buffer(sv[1], (size_t)count * 4)) ||
+      (rc = ensure_buffer(sv[2], misc_words * 4)))
     return rc;
   std::vector<uint32_t> misc(misc_words, 0);
   std::copy(tt.prod.begin(), tt.prod.end(), misc.begin() + off_prod);
   std::copy(tt.start.begin(), tt.start.end(), misc.begin() + off_start);
   std::copy(tt.primes.begin(), tt.primes.end(), misc.begin() + off_primes);
   std::memcpy(misc.data() + off_inv, tt.inv.data(), ng * 8);
-  hipError_t e = hipMemcpy(g_sieve[2].ptr, misc.data(), misc_words * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(g_stage[0].ptr, raw, (size_t)count * nbytes, hipMemcpyHostToDevice);
-  if (e != hipSuccess) return hip_fail(e, "copy sieve inputs");
-  uint32_t* dm = (uint32_t*)g_sieve[2].ptr;
+  if ((rc = h2d(sv[2].ptr, misc.data(), misc_words * 4, l.st)) ||
+      (rc = h2d(sg[0].ptr, raw, (size_t)count * nbytes, l.st)))
+    return rc;
+  uint32_t* dm = (uint32_t*)sv[2].ptr;
   mpcx::SieveArgs sa{};
-  sa.raw = (const uint8_t*)g_stage[0].ptr;
+  sa.raw = (const uint8_t*)sg[0].ptr;
   sa.nbytes = nbytes;
   sa.count = count;
   sa.q_bits = q_bits;
@@ -952,29 +1030,28 @@ int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t co
   sa.tprimes = dm + off_primes;
   sa.tinv = (const uint64_t*)(dm + off_inv);
   sa.ngroups = (uint32_t)ng;
-  sa.out_p = (uint32_t*)g_sieve[0].ptr;
-  sa.out_idx = (uint32_t*)g_sieve[1].ptr;
+  sa.out_p = (uint32_t*)sv[0].ptr;
+  sa.out_idx = (uint32_t*)sv[1].ptr;
   sa.out_count = dm;
-  e = mpcx_launch_sieve(&sa, nullptr);
+  hipError_t e = mpcx_launch_sieve(&sa, l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_sieve");
   mpcx::FermatArgs fa{};
   fa.p = sa.out_p;
-  fa.ok = (uint8_t*)g_stage[3].ptr;
+  fa.ok = (uint8_t*)sg[3].ptr;
   fa.count = count;
   fa.p_words = W;
   fa.count_dev = dm;
-  e = mpcx_launch_fermat2(&fa, (count + 63) / 64, nullptr);
+  e = mpcx_launch_fermat2(&fa, (count + 63) / 64, l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
   uint32_t n = 0;
-  e = hipMemcpy(&n, dm, 4, hipMemcpyDeviceToHost);
-  if (e != hipSuccess) return hip_fail(e, "copy survivor count");
+  if ((rc = d2h_sync(&n, dm, 4, l.st))) return rc;
   if (n > count) return fail(MPCX_EHIP, "sieve survivor count %u > %u", n, count);
   std::vector<uint32_t> idx(n);
   std::vector<uint8_t> ok(n);
   if (n) {
-    e = hipMemcpy(idx.data(), sa.out_idx, (size_t)n * 4, hipMemcpyDeviceToHost);
-    if (e == hipSuccess) e = hipMemcpy(ok.data(), fa.ok, n, hipMemcpyDeviceToHost);
+    e = hipMemcpyAsync(idx.data(), sa.out_idx, (size_t)n * 4, hipMemcpyDeviceToHost, l.st);
     if (e != hipSuccess) return hip_fail(e, "copy survivors");
+    if ((rc = d2h_sync(ok.data(), fa.ok, n, l.st))) return rc;
   }
   // stream order
   std::vector<uint32_t> ord(n);
