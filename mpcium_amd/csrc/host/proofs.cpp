@@ -194,14 +194,41 @@ std::vector<ModProof> ModProveBatch(const std::vector<Bytes>& session, const Nat
     out[i].A = A;
     out[i].B = B;
   });
-  ExpSet e(N);
-  for (size_t i = 0; i < n; ++i)
+  // X_i = Y'_i^expo mod N (fourth root), Z_i = Y_i^(N^-1 mod phi) mod N, by CRT
+  // over the prover's P and Q (same integers: x^e mod p = x^e_p mod p with
+  // e_p = ((e - 1) mod (p - 1)) + 1 for e >= 1, also when p | x): two 1024-bit
+  // exponents mod 1024-bit primes instead of a 2048-bit one mod N.
+  auto red = [&](const Nat& ex, const Nat& pm1) { return ex.is_zero() ? ex : (ex - one) % pm1 + one; };
+  const Nat xP = red(expo, Pm1), xQ = red(expo, Qm1), zP = red(invN, Pm1), zQ = red(invN, Qm1);
+  std::vector<std::vector<Nat>> rP(n, std::vector<Nat>(2 * kModIterations)),
+      rQ(n, std::vector<Nat>(2 * kModIterations));
+  {
+    ExpSet sP(P), sQ(Q);
+    for (size_t i = 0; i < n; ++i)
+      for (int k = 0; k < kModIterations; ++k) {
+        if (!found[i][k]) continue;
+        sP.add(Yp[i][k], xP, &rP[i][2 * k]);
+        sQ.add(Yp[i][k], xQ, &rQ[i][2 * k]);
+        sP.add(Y[i][k], zP, &rP[i][2 * k + 1]);
+        sQ.add(Y[i][k], zQ, &rQ[i][2 * k + 1]);
+      }
+    sP.run();
+    sQ.run();
+  }
+  Nat qinv;
+  if (!mod_inverse(Int(Q % P), P, &qinv)) throw std::invalid_argument("ModProof: P, Q not coprime");
+  auto crt = [&](const Nat& a, const Nat& b) {  // x mod P = a, x mod Q = b -> x mod N
+    const Nat bp = b % P;
+    const Nat d = a < bp ? a + P - bp : a - bp;
+    return b + Q * mulmod(d, qinv, P);
+  };
+  parallel_for(n, [&](size_t i) {
     for (int k = 0; k < kModIterations; ++k) {
       if (!found[i][k]) continue;
-      e.add(Yp[i][k], expo, &out[i].X[k]);  // X_i = Y'_i^expo mod N (fourth root)
-      e.add(Y[i][k], invN, &out[i].Z[k]);   // Z_i = Y_i^(N^-1 mod phi) mod N
+      out[i].X[k] = crt(rP[i][2 * k], rQ[i][2 * k]);
+      out[i].Z[k] = crt(rP[i][2 * k + 1], rQ[i][2 * k + 1]);
     }
-  e.run();
+  });
   return out;
 }
 

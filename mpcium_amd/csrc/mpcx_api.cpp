@@ -67,6 +67,7 @@ int g_num_cus = 0;
 int g_geom_slots[MPCX_NUM_GEOMS] = {0};  // resident wavefronts per device, per geometry
 bool g_split = false;                    // narrow-geometry tail launch (measured slower: off)
 int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): one geometry for everything
+double g_narrow_rounds = 0.15;           // mpcx_set_option("narrow_rounds", 100x): narrow-geometry threshold
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 struct Staging {
@@ -315,6 +316,10 @@ int mpcx_set_option(const char* key, int value) {
     // cap on the sliding-window width of shared exponents; 0: Go's 4-bit fixed window
     if (value < 0 || value > MPCX_SCHED_MAX_WIDTH) return fail(MPCX_EINVAL, "sched_width %d out of range", value);
     g_sched_width = value;
+  } else if (std::strcmp(key, "narrow_rounds") == 0) {
+    // batches below value/100 of a resident round run in the narrow geometry
+    if (value < 0 || value > 100) return fail(MPCX_EINVAL, "narrow_rounds %d out of range", value);
+    g_narrow_rounds = value / 100.0;
   } else if (std::strcmp(key, "main_geom") == 0) {
     // main (throughput) geometry of the geometry's class
     if (value < 0 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "main_geom %d out of range", value);
@@ -496,7 +501,7 @@ static int modexp_device_locked(Lane& lane, mpcx_mod_t mod, uint32_t count, cons
     // at ~45% of SIMD peak, so tiny batches (< 0.15 of a round) finish sooner
     // spread over the narrow geometry's 3x more wavefronts; from ~0.3 rounds up
     // the main geometry wins, and a narrow tail launch did not pay.
-    if (gn >= 0 && rounds < 0.15) {
+    if (gn >= 0 && rounds < g_narrow_rounds) {
       parts[nparts++] = {gn, 0, count};
     } else if (!g_split || gn < 0 || rounds < 1.0 || frac == 0.0 || frac > 0.75) {
       parts[nparts++] = {gm, 0, count};
