@@ -201,12 +201,14 @@ int mpcx_stream_sync(void* stream);
  *   "split"      0 (default) / 1: run the partial last round of resident
  *                wavefronts of a large batch in the class's narrow geometry
  *                (more lanes per operand, shorter wavefronts). Batches under
- *                0.15 of a round always use the narrow geometry.
+ *                "narrow_rounds"/100 of a round always use the narrow geometry.
+ *   "narrow_rounds" 0..100 (default 15): that threshold, in hundredths of a
+ *                round of resident wavefronts in the main geometry.
  *   "force_geom" -1 (default) or a geometry id (0..6, see mpcx_internal.h) to
  *                run every batch of the matching class in that geometry.
  *   "main_geom"  geometry id: make it the main (throughput) geometry of its
  *                class (A/B of kernel layouts).
- *   "sched_width" 0..5 (default 5): cap on the sliding-window width used for
+ *   "sched_width" 0..6 (default 6): cap on the sliding-window width used for
  *                shared exponents; 0 selects Go's 4-bit fixed window. */
 int mpcx_set_option(const char* key, int value);
 

@@ -26,8 +26,8 @@
 //    unrolled), across lanes by ONE DPP wave_shl of a 28-bit value (the slot's
 //    high part is folded into the next slot first).
 //  * Exponentiation: a shared exponent follows a sliding-window schedule (odd
-//    powers, windows of up to 5 bits, built on the device by k_expsched);
-//    per-operand exponents use Go's fixed 4-bit window. Tables (<= 17 entries
+//    powers, windows of up to 6 bits, built on the device by k_expsched);
+//    per-operand exponents use Go's fixed 4-bit window. Tables (<= 33 entries
 //    per operand) live in a global workspace, lane-coalesced; b operands are
 //    staged in LDS and read as group-broadcast ds_read_b32.
 //  * MFMA is not used: this is not a dense contraction.
@@ -378,7 +378,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   // built from it on the same stream (ExpSched layout in mpcx_internal.h):
   // odd powers x^1, x^3, ..., x^(2 Tn + 1) in table[0..Tn], z = x^top, then
   // per entry s squarings and one multiply by an odd power. Windows of up to
-  // 5 bits cost ~E/6 multiplies against Go's E/4 * 15/16; every decision
+  // 6 bits cost ~E/7 multiplies against Go's E/4 * 15/16; every decision
   // depends on e only, so the wave stays uniform. Per-operand exponents (and
   // e = 0) keep Go's 4-bit fixed window: their sequences would diverge.
   const bool sched = a.exp_shared != 0 && a.sched != nullptr &&
@@ -392,7 +392,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const uint32_t nsteps = sched ? __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_N]) : (nw > 0 ? nw - 1u : 0u);
 
   // Montgomery-step state machine (ONE montmul call site keeps the code small):
-  //   PRE : mul*R   = mont(mul, R^2)           -> table[16]   (only with a multiplier)
+  //   PRE : mul*R   = mont(mul, R^2)           -> table[MPCX_MUL_ENTRY]   (only with a multiplier)
   //   TAB : fixed window: p_i = mont(x, R^2), mont(p_{i-1}, p_1)  i = 1..T -> table[i]
   //         schedule:     x R = mont(x, R^2) -> table[0]
   //   TSQ : x^2 R (schedule, Tn > 0)
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       if (idx == nsteps) {
         if (has_mul) {
           st = ST_MULF;
-          lds_from_table(16);
+          lds_from_table(MPCX_MUL_ENTRY);
         } else {
           st = ST_FIN;
           lds_one();
@@ -464,7 +464,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     wave_lds_fence();
     bool start_exp = false, run_exp = false;
     if (st == ST_PRE) {
-      tbl_store(16, A);
+      tbl_store(MPCX_MUL_ENTRY, A);
       load_digits(a.base, a.base_words);  // LDS still holds R^2
       st = ST_TAB;
       idx = 1;

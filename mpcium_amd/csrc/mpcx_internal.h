@@ -38,9 +38,11 @@
 // 1024-bit class used by the Fermat / Miller-Rabin kernels (thread per operand)
 #define MPCX_C0_K 37
 
-// table entries per wavefront in the workspace: powers p_0..p_15 + the
-// Montgomery form of the optional multiplier (entry 16)
-#define MPCX_TABLE_ENTRIES 17
+// table entries per wavefront in the workspace: powers p_0..p_15 (fixed
+// window) or the odd powers x, x^3, ..., x^63 (sliding window, table[0..31]),
+// + the Montgomery form of the optional multiplier (entry 32)
+#define MPCX_TABLE_ENTRIES 33
+#define MPCX_MUL_ENTRY 32
 
 // Sliding-window schedule of a shared exponent (built by k_expsched on the
 // launch stream, read by k_modexp through scalar loads):
@@ -56,7 +58,7 @@
 #define MPCX_SCHED_WIDTH 3
 #define MPCX_SCHED_STEPS 4
 #define MPCX_SCHED_NONE 0xFFFFFFFFu
-#define MPCX_SCHED_MAX_WIDTH 5  // 2^(w-1) <= 16 odd powers fit table[0..15]
+#define MPCX_SCHED_MAX_WIDTH 6  // 2^(w-1) <= 32 odd powers fit table[0..31]
 // schedule words for an exponent of `bits` bits (at most one step per bit)
 #define MPCX_SCHED_WORDS(bits) (MPCX_SCHED_STEPS + (bits) + 1)
 

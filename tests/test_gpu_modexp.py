@@ -165,7 +165,7 @@ SCHED_EXPONENTS = [1, 2, 3, 5, 7, 31, 32, 33, 63, (1 << 64) - 1, 1 << 64, (1 << 
                    (1 << 2047) | 1, (1 << 1000) | (1 << 500) | (1 << 37), (1 << 4900) - 1]
 
 
-@pytest.mark.parametrize("width", [0, 1, 2, 3, 4, 5])
+@pytest.mark.parametrize("width", [0, 1, 2, 3, 4, 5, 6])
 def test_shared_exponent_window_schedules(gpu, paillier_key, width):
     """Shared exponents take the device-built sliding-window schedule
     (k_expsched; width capped by the "sched_width" option, 0 = Go's fixed
@@ -184,7 +184,7 @@ def test_shared_exponent_window_schedules(gpu, paillier_key, width):
             assert mod.exp_mul(xs, N - 1, cs) == [c * pow(x, N - 1, m) % m for x, c in zip(xs, cs)]
             mod.release()
     finally:
-        gpu.set_option("sched_width", 5)
+        gpu.set_option("sched_width", 6)
 
 
 def test_fixed_base_tables(gpu, paillier_key):
