@@ -81,15 +81,18 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
 }
 
 // Broadcast lane 0 of each P-lane operand group to the whole group. Quads
-// (P = 4) and pairs (P = 2) use a DPP quad_perm -- a VALU move with a few
-// cycles of latency on the per-iteration serial path; other group widths go
-// through the LDS crossbar (ds_bpermute, ~100+ cycles of latency).
+// (P = 4) and pairs (P = 2) use a DPP quad_perm, 16-lane groups (one DPP row)
+// DPP row_newbcast -- a VALU move with a few cycles of latency on the
+// per-iteration serial path; other group widths go through the LDS crossbar
+// (ds_bpermute, ~100+ cycles of latency).
 template <int P>
 __device__ __forceinline__ uint32_t group_bcast(uint32_t v, int src_addr) {
   if constexpr (P == 4) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);  // quad_perm [0,0,0,0]
   } else if constexpr (P == 2) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
+  } else if constexpr (P == 16) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150, 0xF, 0xF, false);  // row_newbcast:0
   } else {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(src_addr, (int)v);
   }
