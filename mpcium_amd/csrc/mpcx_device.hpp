@@ -82,7 +82,7 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
 
 // Broadcast lane 0 of each P-lane operand group to the whole group. Quads
 // (P = 4) and pairs (P = 2) use a DPP quad_perm, 16-lane groups (one DPP row)
-// DPP row_newbcast -- a VALU move with a few cycles of latency on the
+// DPP row_newbcast, 32-lane groups row_newbcast + row_bcast:15 -- a VALU move with a few cycles of latency on the
 // per-iteration serial path; other group widths go through the LDS crossbar
 // (ds_bpermute, ~100+ cycles of latency).
 template <int P>
@@ -93,6 +93,11 @@ __device__ __forceinline__ uint32_t group_bcast(uint32_t v, int src_addr) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
   } else if constexpr (P == 16) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150, 0xF, 0xF, false);  // row_newbcast:0
+  } else if constexpr (P == 32) {
+    // every row takes its lane 0, then rows 1 and 3 take lane 15 of the row
+    // below (= lane 0 of rows 0 and 2) by row_bcast:15
+    const int t = __builtin_amdgcn_mov_dpp((int)v, 0x150, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(t, t, 0x142, 0xA, 0xF, false);
   } else {
     return (uint32_t)__builtin_amdgcn_ds_bpermute(src_addr, (int)v);
   }

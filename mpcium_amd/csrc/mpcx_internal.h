@@ -24,13 +24,13 @@
 //   2: 4 x 37, 16, class 2  quad per operand (Paillier N^2)
 //   3: 16 x 5,  4, class 1  narrow: small latency-bound batches; one DPP row per operand,
 //                           m_i broadcast by DPP row_newbcast
-//   4: 21 x 7,  3, class 2  narrow
+//   4: 32 x 5,  2, class 2  narrow; two DPP rows per operand, m_i by row_newbcast + row_bcast:15
 //   5: 3 x 25, 21, class 1  7-lane/3-lane groups, m_i by ds_bpermute (round-1 main)
 //   6: 7 x 21,  9, class 2  (round-1 main)
 #define MPCX_NUM_GEOMS 7
-#define MPCX_GEOM_P(g) ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 16 : (g) == 4 ? 21 : (g) == 5 ? 3 : 7)
-#define MPCX_GEOM_K(g) ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 7 : (g) == 5 ? 25 : 21)
-#define MPCX_GEOM_G(g) ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 3 : (g) == 5 ? 21 : 9)
+#define MPCX_GEOM_P(g) ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 16 : (g) == 4 ? 32 : (g) == 5 ? 3 : 7)
+#define MPCX_GEOM_K(g) ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 5 : (g) == 5 ? 25 : 21)
+#define MPCX_GEOM_G(g) ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 2 : (g) == 5 ? 21 : 9)
 #define MPCX_GEOM_CLASS(g) ((g) == 0 ? 0 : ((g) == 1 || (g) == 3 || (g) == 5) ? 1 : 2)
 #define MPCX_GEOM_L(g) (MPCX_GEOM_P(g) * MPCX_GEOM_K(g))
 // default main (throughput) and narrow geometry of each class
