@@ -168,13 +168,16 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
   uint32_t bnext = bl[0];
   for (int o = 0; o < P; ++o) {
     const uint32_t* bo = bl + o * K;
-    // diagonal-register factor of this lane for the whole block
-    const uint32_t fdiag = p > o ? 2u : (p == o ? 1u : 0u);
+    // diagonal-register factor of this lane for the whole block (2 above the
+    // diagonal lane, 1 on it, 0 below) as a right shift of b2 = 2*b_i: digits
+    // are < 2^29, so b2 < 2^30 and b2 >> 31 == 0. One v_lshrrev_b32 instead of
+    // a v_mul_lo_u32 (which issues at MAD rate) per squaring iteration.
+    const uint32_t dsh = p > o ? 0u : (p == o ? 1u : 31u);
     static_for<0, K>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
       const uint32_t bi = bnext;
       const uint32_t b2 = bi << 1;
-      const uint32_t bd = bi * fdiag;
+      const uint32_t bd = b2 >> dsh;
       auto ab = [&](auto kc) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
         if constexpr (!SQR) {
