@@ -31,6 +31,9 @@
  *                                 drives through party.UpdateFromBytes.
  *   mpcx_modexp_batch_device   -- same, device-resident buffers + stream
  *                                 (pipelines that keep operands in HBM).
+ *   mpcx_modexp_submit/_job_*  -- the same batch, asynchronous (the Go
+ *                                 batcher's submit / wait)
+ *   mpcx_init_devices          -- one node process driving all its GPUs
  *   mpcx_fermat2_batch         -- up:common/safe_prime.go
  *                                 isPocklingtonCriterionSatisfied(p):
  *                                 2^(p-1) mod p == 1 for a batch of
@@ -66,9 +69,38 @@ const char* mpcx_last_error(void);
 /* Number of visible HIP devices (0 without a GPU; never initialises one). */
 int mpcx_device_count(int* out_count);
 
-/* Bind this process to HIP device `device` (one process per GPU) and run the
- * device self-test. Idempotent for the same device. */
+#define MPCX_MAX_DEVICES 16
+
+/* Bind HIP device `device` (adds it to the process's set of bound GPUs) and
+ * run its self-test. Idempotent per device. One process drives every GPU of
+ * the node: an mpcium node is one Go process whose sessions share one set of
+ * preparams (/root/reference/pkg/mpc/node.go:69,109,170). */
 int mpcx_init(int device);
+
+/* Bind devices 0 .. n_gpus-1 (n_gpus <= 0: every visible device). The
+ * host-buffer entry points then spread over all bound devices: a batch of at
+ * least 2 x "device_split_min" operands (mpcx_set_option, default 4096) is cut
+ * into one contiguous operand range per device, run concurrently and
+ * gathered into the caller's buffers (independent operands: no collective);
+ * smaller batches go to one device, round-robin across calls. */
+int mpcx_init_devices(int n_gpus);
+
+/* The slice plan the host-buffer entry points use for a batch of `count`
+ * operands over n_devices bound devices (pure function, no GPU needed):
+ * *n_slices contiguous ranges [first[s], first[s] + n[s]) (arrays sized
+ * >= n_devices), one per device 0..n_slices-1; one range (run on one device,
+ * round-robin) unless every range gets >= min_slice operands. */
+int mpcx_partition(uint32_t count, int n_devices, uint32_t min_slice, uint32_t* first, uint32_t* n,
+                   uint32_t* n_slices);
+
+/* Number of bound devices and (optionally) their HIP ordinals, bind order. */
+int mpcx_bound_devices(int* out_count, int* ordinals, int max_ordinals);
+
+/* Device (index into the bound set, default 0) used by THIS thread's
+ * device-buffer calls, modulus registration, comb-table builds, mpcx_dev_alloc
+ * and mpcx_stream_create. Moduli and comb tables are usable on every bound
+ * device (their constants are uploaded to a device on first use there). */
+int mpcx_select_device(int index);
 
 /* Release all device resources (registered moduli become invalid). */
 int mpcx_shutdown(void);
@@ -103,13 +135,16 @@ int mpcx_modexp_batch(mpcx_mod_t mod, uint32_t count,
                       uint32_t* out, uint32_t out_words);
 
 /* Same contract with device pointers (d_*) on HIP stream `stream` (a
- * hipStream_t, NULL = default stream). Asynchronous: the results are valid
- * after the stream is synchronised. exp_bits is the bit length of the
- * largest exponent (any value >= it and <= 32*exp_words is correct; per-
- * operand exponents are processed as ceil(exp_bits/4) 4-bit windows; a shared
- * exponent's sliding-window schedule is built on `stream` by a one-lane
- * kernel, so the call stays asynchronous). The first call with a larger
- * batch than before grows the kernel workspace (hipMalloc). */
+ * hipStream_t of the thread's selected device, NULL = default stream).
+ * Asynchronous: the results are valid after the stream is synchronised.
+ * exp_bits is the bit length of the largest exponent (any value >= it and <=
+ * 32*exp_words is correct; per-operand exponents are processed as
+ * ceil(exp_bits/4) 4-bit windows; a shared exponent's sliding-window schedule
+ * is built on `stream` by a one-lane kernel, so the call stays asynchronous).
+ * Every (device, stream) pair has its own kernel workspace, so calls on
+ * different streams may run concurrently; the first call on a stream with a
+ * larger batch than before grows that stream's workspace (hipMalloc, after
+ * synchronising the stream). */
 int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count,
                              const uint32_t* d_bases, uint32_t base_words,
                              const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
@@ -132,6 +167,20 @@ int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count,
                                  uint32_t exp_bits,
                                  const uint32_t* d_muls, uint32_t mul_words,
                                  uint32_t* d_out, uint32_t out_words, void* stream);
+
+/* Asynchronous host-buffer submission (SURVEY.md 8(b) "async submit +
+ * mpcx_sync"): the same work as mpcx_modexp_mul_batch (muls may be NULL:
+ * mpcx_modexp_batch), run by libmpcx's submission threads. The caller keeps
+ * every buffer alive and unmodified until mpcx_job_wait returns. *job is
+ * released by mpcx_job_wait, which returns the batch's status. */
+typedef struct mpcx_job_s* mpcx_job_t;
+int mpcx_modexp_submit(mpcx_mod_t mod, uint32_t count,
+                       const uint32_t* bases, uint32_t base_words,
+                       const uint32_t* exps, uint32_t exp_words, int exp_shared,
+                       const uint32_t* muls, uint32_t mul_words,
+                       uint32_t* out, uint32_t out_words, mpcx_job_t* job);
+int mpcx_job_test(mpcx_job_t job, int* done);
+int mpcx_job_wait(mpcx_job_t job);
 
 /* out[i] = a[i] * b[i] mod m -- up:common/int.go (*modInt).Mul and
  * paillier.(*PublicKey).HomoAdd (c1*c2 mod N^2), batched. */
@@ -172,6 +221,7 @@ int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t co
  * exponents of a 2048-bit modulus); the table lives until
  * mpcx_fixedbase_release (release it before its modulus). */
 typedef struct mpcx_fixedbase_s* mpcx_fb_t;
+#define MPCX_FB_MAX_EXP_BITS 65536
 int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_words,
                             uint32_t max_exp_bits, mpcx_fb_t* out);
 int mpcx_fixedbase_release(mpcx_fb_t fb);
@@ -196,6 +246,8 @@ int mpcx_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes);
 int mpcx_stream_create(void** out_stream);
 int mpcx_stream_destroy(void* stream);
 int mpcx_stream_sync(void* stream);
+/* SURVEY.md 8(b) name of mpcx_stream_sync. */
+int mpcx_sync(void* stream);
 
 /* Tuning knobs (process-wide):
  *   "split"      0 (default) / 1: run the partial last round of resident
@@ -209,7 +261,10 @@ int mpcx_stream_sync(void* stream);
  *   "main_geom"  geometry id: make it the main (throughput) geometry of its
  *                class (A/B of kernel layouts).
  *   "sched_width" 0..6 (default 6): cap on the sliding-window width used for
- *                shared exponents; 0 selects Go's 4-bit fixed window. */
+ *                shared exponents; 0 selects Go's 4-bit fixed window.
+ *   "device_split_min" operands (default 4096): smallest per-device slice
+ *                of a host-buffer batch split across the bound devices
+ *                (0: never split). */
 int mpcx_set_option(const char* key, int value);
 
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):

@@ -35,13 +35,30 @@
 extern "C" {
 #endif
 
-/* io.Reader stand-in: fill buf[0..n) with random bytes. */
+/* io.Reader stand-in: fill buf[0..n) with random bytes (io.ReadFull). */
 typedef void (*mpcxh_rand_fn)(void* ctx, uint8_t* buf, size_t n);
+
+/* One session's randomness source: tss-lib draws every MtA / proof random
+ * value from the party's io.Reader inside party.UpdateFromBytes
+ * (/root/reference/pkg/mpc/session.go:199). fn != NULL: fn(ctx, ...) is that
+ * reader (a cgo export wrapping the Go io.Reader); it is
+ * called from libmpcx_host's worker threads, never concurrently for one
+ * session, but concurrently across sessions (a reader shared by several
+ * sessions must be thread-safe, as crypto/rand.Reader is). fn == NULL: the
+ * build's CounterDRBG stream seeded with `seed` (tests, benchmarks). */
+typedef struct {
+  mpcxh_rand_fn fn;
+  void* ctx;
+  uint64_t seed;
+} mpcxh_reader_t;
 
 #define MPCXH_PREPARAM_FIELDS 12
 
 const char* mpcxh_last_error(void);
+/* Bind one more GPU (mpcx_init) / GPUs 0..n_gpus-1 (mpcx_init_devices, n_gpus
+ * <= 0: all visible). Every batch below spreads over the bound GPUs. */
 int mpcxh_init(int device);
+int mpcxh_init_devices(int n_gpus);
 
 /* z_i = x_i^y_i mod m with Go semantics; ok[i] = 0 where Go returns nil
  * (y < 0 and x not invertible). y_shared != 0: one y for every x. m odd,
@@ -103,8 +120,8 @@ int mpcxh_generate_preparams(uint64_t seed, mpcxh_rand_fn rand_fn, void* rand_ct
  *   ProofBob[WC]   (12 fields): Z, ZPrm, T, V, W, S, S1, S2, T1, T2, U.x, U.y
  *                               (U = 0, 0 for the plain ProofBob)
  * Points (B, the MtAwc public value) are count x 16 words: x (8), y (8).
- * Session ids are count x session_len bytes. seeds[i]: session i's io.Reader
- * (CounterDRBG stream). err[i]: 0 ok, 1 ErrMessageTooLong, 2
+ * Session ids are count x session_len bytes. readers[i]: session i's
+ * io.Reader. err[i]: 0 ok, 1 ErrMessageTooLong, 2
  * ErrMessageMalFormed, 3 proof verification failed. */
 typedef struct {
   const uint32_t* N;       /* Paillier N */
@@ -126,7 +143,8 @@ typedef struct {
 
 /* mta.AliceInit(ec, pkA, a, NTildeB, h1B, h2B, rand) -> cA, RangeProofAlice */
 int mpcxh_mta_alice_init_batch(uint32_t w, const mpcxh_paillier_t* pkA, const mpcxh_dln_t* dlnB, uint32_t count,
-                               const uint32_t* a, const uint64_t* seeds, uint32_t* cA, uint32_t* pf, uint8_t* err);
+                               const uint32_t* a, const mpcxh_reader_t* readers, uint32_t* cA, uint32_t* pf,
+                               uint8_t* err);
 /* (*RangeProofAlice).Verify(ec, pk, NTilde, h1, h2, c) */
 int mpcxh_mta_verify_range_alice_batch(uint32_t w, const mpcxh_paillier_t* pk, const mpcxh_dln_t* dln,
                                        uint32_t count, const uint32_t* c, const uint32_t* pf, uint8_t* ok);
@@ -134,8 +152,9 @@ int mpcxh_mta_verify_range_alice_batch(uint32_t w, const mpcxh_paillier_t* pk, c
  * NTildeB, h1B, h2B[, B], rand) -> beta, cB, betaPrm, ProofBob[WC] */
 int mpcxh_mta_bob_mid_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* pkA,
                             const mpcxh_dln_t* dlnA, const mpcxh_dln_t* dlnB, uint32_t count, const uint32_t* pfA,
-                            const uint32_t* b, const uint32_t* cA, const uint32_t* B, const uint64_t* seeds,
-                            uint32_t* beta, uint32_t* cB, uint32_t* betaPrm, uint32_t* pfB, uint8_t* err);
+                            const uint32_t* b, const uint32_t* cA, const uint32_t* B,
+                            const mpcxh_reader_t* readers, uint32_t* beta, uint32_t* cB, uint32_t* betaPrm,
+                            uint32_t* pfB, uint8_t* err);
 /* (*ProofBob).Verify / (*ProofBobWC).Verify(Session, ec, pk, NTilde, h1, h2, c1, c2[, X]) */
 int mpcxh_mta_verify_bob_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* pk,
                                const mpcxh_dln_t* dln, uint32_t count, const uint32_t* c1, const uint32_t* c2,
@@ -152,8 +171,8 @@ int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t sess
  * (/root/reference/pkg/mpc/ecdsa_keygen_session.go:85-92,
  * /root/reference/pkg/mpc/ecdsa_resharing_session.go:132-143). A batch holds
  * `count` proofs over the same public parameters; integers are `w` words
- * (w >= 160: FacProof's v and sigma reach ~4.9 kbit), seeds[i] is proof i's
- * io.Reader (CounterDRBG), sessions are count x session_len bytes.
+ * (w >= 160: FacProof's v and sigma reach ~4.9 kbit), readers[i] is proof i's
+ * io.Reader, sessions are count x session_len bytes.
  *   DLN proof: alpha (count x 128 x w), t (count x 128 x w)
  *   Mod proof: W (count x w), X (count x 80 x w), A, B (count x w), Z (count x 80 x w)
  *   Fac proof: count x 11 x w fields P, Q, A, B, T, Sigma, Z1, Z2, W1, W2, |V|
@@ -163,19 +182,20 @@ int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t sess
 #define MPCXH_MOD_ITERATIONS 80
 #define MPCXH_FAC_FIELDS 11
 int mpcxh_dln_prove_batch(uint32_t w, const uint32_t* h1, const uint32_t* h2, const uint32_t* x, const uint32_t* p,
-                          const uint32_t* q, const uint32_t* N, uint32_t count, const uint64_t* seeds, uint32_t* alpha,
-                          uint32_t* t);
+                          const uint32_t* q, const uint32_t* N, uint32_t count, const mpcxh_reader_t* readers,
+                          uint32_t* alpha, uint32_t* t);
 int mpcxh_dln_verify_batch(uint32_t w, const uint32_t* h1, const uint32_t* h2, const uint32_t* N, uint32_t count,
                            const uint32_t* alpha, const uint32_t* t, uint8_t* ok);
 int mpcxh_mod_prove_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N,
-                          const uint32_t* P, const uint32_t* Q, uint32_t count, const uint64_t* seeds, uint32_t* W,
-                          uint32_t* X, uint32_t* A, uint32_t* B, uint32_t* Z);
+                          const uint32_t* P, const uint32_t* Q, uint32_t count, const mpcxh_reader_t* readers,
+                          uint32_t* W, uint32_t* X, uint32_t* A, uint32_t* B, uint32_t* Z);
 int mpcxh_mod_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N,
                            uint32_t count, const uint32_t* W, const uint32_t* X, const uint32_t* A, const uint32_t* B,
                            const uint32_t* Z, uint8_t* ok);
 int mpcxh_fac_prove_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N0,
                           const uint32_t* NCap, const uint32_t* s, const uint32_t* t, const uint32_t* N0p,
-                          const uint32_t* N0q, uint32_t count, const uint64_t* seeds, uint32_t* pf, uint8_t* v_neg);
+                          const uint32_t* N0q, uint32_t count, const mpcxh_reader_t* readers, uint32_t* pf,
+                          uint8_t* v_neg);
 int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N0,
                            const uint32_t* NCap, const uint32_t* s, const uint32_t* t, uint32_t count,
                            const uint32_t* pf, const uint8_t* v_neg, uint8_t* ok);

@@ -85,15 +85,23 @@ void check_width(uint32_t w) {
   if (w < 128) throw std::invalid_argument("MtA integer width must be >= 128 words (N^2)");
 }
 
-std::vector<RandFn> readers(const uint64_t* seeds, uint32_t count, std::vector<CounterDRBG>* drbgs) {
-  if (!seeds) throw std::invalid_argument("null seeds");
+// Per-session io.Readers: the caller's callback, or a CounterDRBG owned by
+// `drbgs` (reserved up front: the RandFns point into it).
+std::vector<RandFn> readers(const mpcxh_reader_t* rd, uint32_t count, std::vector<CounterDRBG>* drbgs) {
+  if (!rd && count) throw std::invalid_argument("null readers");
   drbgs->clear();
   drbgs->reserve(count);
   std::vector<RandFn> r;
   r.reserve(count);
   for (uint32_t i = 0; i < count; ++i) {
-    drbgs->emplace_back(seeds[i]);
-    r.push_back(drbgs->back().fn());
+    if (rd[i].fn) {
+      const mpcxh_rand_fn fn = rd[i].fn;
+      void* ctx = rd[i].ctx;
+      r.push_back([fn, ctx](uint8_t* b, size_t n) { fn(ctx, b, n); });
+    } else {
+      drbgs->emplace_back(rd[i].seed);
+      r.push_back(drbgs->back().fn());
+    }
   }
   return r;
 }
@@ -168,6 +176,10 @@ const char* mpcxh_last_error(void) { return g_herr.c_str(); }
 
 int mpcxh_init(int device) {
   return guard([&] { Engine::get().init(device); });
+}
+
+int mpcxh_init_devices(int n_gpus) {
+  return guard([&] { Engine::get().init_devices(n_gpus); });
 }
 
 int mpcxh_modint_exp_batch(const uint32_t* m, uint32_t mw, uint32_t count, const uint32_t* xs, uint32_t xw,
@@ -321,7 +333,8 @@ int mpcxh_drbg_read(uint64_t seed, uint8_t* out, size_t n) {
 
 // ------------------------------------------------------------------ MtA
 int mpcxh_mta_alice_init_batch(uint32_t w, const mpcxh_paillier_t* pkA, const mpcxh_dln_t* dlnB, uint32_t count,
-                               const uint32_t* a, const uint64_t* seeds, uint32_t* cA, uint32_t* pf, uint8_t* err) {
+                               const uint32_t* a, const mpcxh_reader_t* seeds, uint32_t* cA, uint32_t* pf,
+                               uint8_t* err) {
   return guard([&] {
     check_width(w);
     const auto sk = paillier_from(pkA, w);
@@ -350,8 +363,9 @@ int mpcxh_mta_verify_range_alice_batch(uint32_t w, const mpcxh_paillier_t* pk, c
 
 int mpcxh_mta_bob_mid_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const mpcxh_paillier_t* pkA,
                             const mpcxh_dln_t* dlnA, const mpcxh_dln_t* dlnB, uint32_t count, const uint32_t* pfA,
-                            const uint32_t* b, const uint32_t* cA, const uint32_t* B, const uint64_t* seeds,
-                            uint32_t* beta, uint32_t* cB, uint32_t* betaPrm, uint32_t* pfB, uint8_t* err) {
+                            const uint32_t* b, const uint32_t* cA, const uint32_t* B,
+                            const mpcxh_reader_t* seeds, uint32_t* beta, uint32_t* cB, uint32_t* betaPrm,
+                            uint32_t* pfB, uint8_t* err) {
   return guard([&] {
     check_width(w);
     const auto sk = paillier_from(pkA, w);
@@ -479,8 +493,8 @@ static Nat one_nat(const uint32_t* p, uint32_t w) {
 }
 
 int mpcxh_dln_prove_batch(uint32_t w, const uint32_t* h1, const uint32_t* h2, const uint32_t* x, const uint32_t* p,
-                          const uint32_t* q, const uint32_t* N, uint32_t count, const uint64_t* seeds, uint32_t* alpha,
-                          uint32_t* t) {
+                          const uint32_t* q, const uint32_t* N, uint32_t count, const mpcxh_reader_t* seeds,
+                          uint32_t* alpha, uint32_t* t) {
   return guard([&] {
     check_pw(w);
     std::vector<CounterDRBG> drbgs;
@@ -511,8 +525,8 @@ int mpcxh_dln_verify_batch(uint32_t w, const uint32_t* h1, const uint32_t* h2, c
 }
 
 int mpcxh_mod_prove_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N,
-                          const uint32_t* P, const uint32_t* Q, uint32_t count, const uint64_t* seeds, uint32_t* W,
-                          uint32_t* X, uint32_t* A, uint32_t* B, uint32_t* Z) {
+                          const uint32_t* P, const uint32_t* Q, uint32_t count, const mpcxh_reader_t* seeds,
+                          uint32_t* W, uint32_t* X, uint32_t* A, uint32_t* B, uint32_t* Z) {
   return guard([&] {
     check_pw(w);
     std::vector<CounterDRBG> drbgs;
@@ -549,7 +563,8 @@ int mpcxh_mod_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
 
 int mpcxh_fac_prove_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len, const uint32_t* N0,
                           const uint32_t* NCap, const uint32_t* s, const uint32_t* t, const uint32_t* N0p,
-                          const uint32_t* N0q, uint32_t count, const uint64_t* seeds, uint32_t* pf, uint8_t* v_neg) {
+                          const uint32_t* N0q, uint32_t count, const mpcxh_reader_t* seeds, uint32_t* pf,
+                          uint8_t* v_neg) {
   return guard([&] {
     check_pw(w);
     std::vector<CounterDRBG> drbgs;

@@ -22,7 +22,16 @@ void Engine::init(int device) {
   std::lock_guard<std::mutex> lk(mu_);
   int rc = mpcx_init(device);
   if (rc) throw_last(rc, "mpcx_init");
-  device_ = device;
+  bound_ = true;
+  const char* fb = std::getenv("MPCX_FIXED_BASE");
+  fixed_enabled_ = !(fb && fb[0] == '0');
+}
+
+void Engine::init_devices(int n_gpus) {
+  std::lock_guard<std::mutex> lk(mu_);
+  int rc = mpcx_init_devices(n_gpus);
+  if (rc) throw_last(rc, "mpcx_init_devices");
+  bound_ = true;
   const char* fb = std::getenv("MPCX_FIXED_BASE");
   fixed_enabled_ = !(fb && fb[0] == '0');
 }
@@ -120,6 +129,7 @@ Engine::Fixed Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
   if (it != fixed_.end() && it->second->max_bits >= need_bits) return it->second;
   if (it != fixed_.end()) fixed_.erase(it);  // grow: rebuild for the longer exponent
   if (fixed_.size() >= 256) fixed_.clear();  // bound the device footprint (~30 MB per table)
+  if (need_bits > kFixedMaxBits) throw std::invalid_argument("fixed-base exponent above kFixedMaxBits");
   Mod& md = modulus(m);
   // MtA exponents on h1, h2 reach ~2818 bits (s2, t2 < q^3 N~ + e q N~); one size serves them all
   const uint32_t bits = std::max<uint32_t>(3072, (need_bits + 511) / 512 * 512);

@@ -25,15 +25,22 @@ class EngineError : public std::runtime_error {
   int code;
 };
 
-// Process-wide handle on one GPU (one process per GPU) plus a cache of
-// registered moduli: a node's N^2, N, N~ are registered once and reused by
-// every session, exactly like mpcium reuses its preparams
-// (/root/reference/pkg/mpc/node.go:69,109,170).
+// Process-wide handle on the node's GPUs (libmpcx spreads every batch over
+// the bound devices) plus a cache of registered moduli: a node's N^2, N, N~
+// are registered once and reused by every session, exactly like mpcium
+// reuses its preparams (/root/reference/pkg/mpc/node.go:69,109,170).
 class Engine {
  public:
   static Engine& get();
-  void init(int device);
-  bool initialized() const { return device_ >= 0; }
+  void init(int device);         // bind one more GPU
+  void init_devices(int n_gpus);  // bind GPUs 0..n_gpus-1 (<= 0: all visible)
+  bool initialized() const { return bound_; }
+  // Longest exponent the fixed-base comb path takes: every honest protocol
+  // exponent on h1, h2, s, t (MtA s2/t2 ~2.8 kbit, FacProof sigma/v ~4.9 kbit)
+  // fits; a longer (peer-supplied) exponent runs on the per-operand path, so
+  // one adversarial proof can neither force a huge table build nor fail the
+  // whole batch.
+  static constexpr uint32_t kFixedMaxBits = 5120;
 
   // out[i] = (muls ? muls[i] : 1) * bases[i]^e_i mod m, m odd, 1 <= m < 2^4096.
   // exps.size() == 1: shared exponent; else one per base. Bases of any size
@@ -85,7 +92,7 @@ class Engine {
   std::mutex mu_, busy_mu_;
   int inflight_ = 0;
   std::chrono::steady_clock::time_point busy_t0_;
-  int device_ = -1;
+  bool bound_ = false;
   bool fixed_enabled_ = true;
   std::atomic<uint64_t> busy_ns_{0};
   std::map<std::vector<uint32_t>, Mod> mods_;

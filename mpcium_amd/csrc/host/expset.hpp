@@ -34,7 +34,8 @@ class ExpSet {
     std::vector<uint8_t> done(reqs_.size(), 0);
     if (Engine::get().fixed_base_ok(m_)) {
       std::map<const Nat*, std::vector<size_t>> by_b;
-      for (size_t i = 0; i < reqs_.size(); ++i) by_b[reqs_[i].b].push_back(i);
+      for (size_t i = 0; i < reqs_.size(); ++i)  // over-long (peer-supplied) exponents: per-operand path
+        if (reqs_[i].e->bit_len() <= Engine::kFixedMaxBits) by_b[reqs_[i].b].push_back(i);
       for (auto& kv : by_b) {
         if (kv.second.size() < kFixedMin) continue;
         auto& idx = kv.second;

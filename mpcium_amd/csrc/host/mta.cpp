@@ -101,7 +101,7 @@ std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const 
   const Nat N2 = pk.NSquare();
   const Nat gamma = pk.Gamma();
   std::vector<uint8_t> ok(n, 0);
-  std::vector<Nat> e(n), gs1(n), L1(n), R1(n), t(n), L2(n), R2(n);
+  std::vector<Nat> e(n), gs1(n), L1(n), R1(n), t(n), L2(n), R2(n), cr(n);
   parallel_for(n, [&](size_t i) {
     const auto& p = pf[i];
     if (!IsInInterval(p.Z, dln.NTilde) || !IsInInterval(p.U, N2) || !IsInInterval(p.W, dln.NTilde) ||
@@ -111,7 +111,12 @@ std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const 
         !coprime_to(p.W, dln.NTilde, dln.P, dln.Q) || !coprime_odd(p.S, pk.N))
       return;
     if (p.S1 > q3()) return;
-    if (!(c[i] < N2) || !coprime_odd(c[i], pk.N)) return;  // c^-e defined (Go: nil -> panic)
+    // Go's Exp(c, -e, N^2) accepts any c invertible mod N^2 (c >= N^2 is
+    // reduced by ModInverse); a non-invertible c gives nil and the following
+    // Mul panics -- reported here as a verification failure. The hash binds
+    // the caller's c as given.
+    cr[i] = c[i] < N2 ? c[i] : c[i] % N2;
+    if (!coprime_odd(cr[i], pk.N)) return;
     e[i] = RejectionSample(Q(), SHA512_256i({&pk.N, &gamma, &c[i], &p.Z, &p.U, &p.W}));
     gs1[i] = gamma_pow(p.S1, pk.N);
     ok[i] = 1;
@@ -120,7 +125,7 @@ std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const 
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
     const auto& p = pf[i];
-    eN2.add(c[i], e[i], &L1[i], &p.U);      // u c^e
+    eN2.add(cr[i], e[i], &L1[i], &p.U);     // u c^e
     eN2.add(p.S, pk.N, &R1[i], &gs1[i]);    // Gamma^s1 s^N
     eNt.add(dln.h1, p.S1, &t[i]);           // h1^s1
     eNt.add(p.Z, e[i], &L2[i], &p.W);       // w z^e

@@ -1,21 +1,36 @@
 // mpcx_api.cpp -- C-ABI host side of libmpcx.so (see include/mpcx.h).
 //
-// Owns device selection, the per-modulus Montgomery constants (what Go's
-// nat.expNNMontgomery recomputes on every call: k0 and RR,
-// go:src/math/big/nat.go), the kernel workspace and the staging buffers, and
-// launches the gfx950 kernels of mpcx_kernels.hip. No CPU compute fallback:
-// every modexp runs on the GPU or the call fails with an error code.
+// Owns the bound GPUs (one process drives every GPU of the node, as one mpcium
+// node process reuses its preparams for every wallet:
+// /root/reference/pkg/mpc/node.go:69,109,170), the per-modulus Montgomery
+// constants (what Go's nat.expNNMontgomery recomputes on every call: k0 and
+// RR, go:src/math/big/nat.go), the kernel workspaces and staging buffers, and
+// launches the gfx950 kernels of mpcx_geom.hip / mpcx_prime.hip. No CPU
+// compute fallback: every modexp runs on a GPU or the call fails with an
+// error code.
+//
+// Multi-GPU: a host-buffer batch large enough to fill more than one GPU is cut
+// into contiguous operand ranges, one per bound device, run concurrently (one
+// host thread per device, each on one of that device's lanes) and gathered
+// into the caller's output buffer. Independent operands: no collective, no
+// peer traffic.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cmath>
+#include <condition_variable>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
-#include <atomic>
+#include <deque>
+#include <functional>
+#include <map>
+#include <memory>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/mpcx.h"
@@ -38,21 +53,29 @@ hipError_t mpcx_launch_sieve(const mpcx::SieveArgs* a, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 }
 
+namespace {
+constexpr int kMaxDevices = MPCX_MAX_DEVICES;
+}
+
 struct mpcx_modulus_s {
   int cls;
   uint32_t bits;
   uint32_t words;  // normalized length of m in 32-bit words
   uint32_t n0inv;
-  uint32_t* d_const;  // per geometry of the class: 3*L_g digits N, R mod N, R^2 mod N
   uint32_t const_off[MPCX_NUM_GEOMS];  // digit offset of geometry g's block (class members only)
   std::vector<uint32_t> m;
+  std::vector<uint32_t> host_const;  // per geometry of the class: 3*L_g digits N, R mod N, R^2 mod N
+  std::mutex mu;                     // guards the lazy per-device uploads
+  uint32_t* d_const[kMaxDevices] = {};
 };
 
 struct mpcx_fixedbase_s {
   mpcx_mod_t mod;
-  int geom;          // main geometry of the modulus class (table layout)
-  uint32_t nwin;     // 8-bit windows: exponents of up to 8*nwin bits
-  uint32_t* d_table; // nwin x 256 entries x L digits ([k][p] interleaved)
+  int geom;                          // main geometry of the modulus class (table layout)
+  uint32_t nwin;                     // 8-bit windows: exponents of up to 8*nwin bits
+  std::vector<uint32_t> host_table;  // nwin x 256 entries x L digits ([k][p] interleaved)
+  std::mutex mu;
+  uint32_t* d_table[kMaxDevices] = {};
 };
 
 namespace {
@@ -61,15 +84,13 @@ constexpr int kDigitBits = 28;
 constexpr uint32_t kM28 = (1u << kDigitBits) - 1u;
 
 thread_local std::string g_err;
-std::mutex g_mu;
-int g_device = -1;
-int g_num_cus = 0;
-int g_geom_slots[MPCX_NUM_GEOMS] = {0};  // resident wavefronts per device, per geometry
+std::mutex g_mu;  // options, device binding, shutdown
 bool g_split = false;                    // narrow-geometry tail launch (measured slower: off)
 int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): one geometry for everything
 double g_narrow_rounds = 0.15;           // mpcx_set_option("narrow_rounds", 100x): narrow-geometry threshold
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
+uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
 struct Staging {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -82,18 +103,34 @@ struct Staging {
 // kLanes matches the HW queues HIP gives a process by default.
 struct Lane {
   std::mutex mu;
-  hipStream_t st = nullptr;  // created on first use (non-blocking)
+  hipStream_t st = nullptr;  // created on first use (non-blocking); or a caller's stream (own_stream false)
+  bool own_stream = true;
   uint32_t* ws = nullptr;    // exponentiation table workspace
   size_t ws_bytes = 0;
   Staging stage[4];  // bases, exps, out, misc
   Staging sieve[3];  // survivors' p words, survivors' indices, trial-division tables + counter
 };
 constexpr int kLanes = 4;
-Lane g_lanes[kLanes];
-// Workspace of the device-buffer entry points (caller's stream, under g_mu;
-// callers order their own device-buffer calls) and of table builds.
-Lane g_dev_lane;
-std::atomic<unsigned> g_lane_rr{0};
+
+// One bound GPU.
+struct Device {
+  int ordinal = -1;
+  int num_cus = 0;
+  int geom_slots[MPCX_NUM_GEOMS] = {0};  // resident wavefronts per geometry
+  Lane lanes[kLanes];
+  std::atomic<unsigned> lane_rr{0};
+  // Workspaces of the device-buffer entry points, one per caller stream: two
+  // asynchronous calls on different streams never share a window table or a
+  // shared-exponent schedule.
+  std::mutex dev_mu;
+  std::map<hipStream_t, std::unique_ptr<Lane>> dev_lanes;
+  Lane build_lane;  // fixed-base table builds
+};
+Device g_devs[kMaxDevices];
+std::atomic<int> g_ndev{0};
+std::atomic<unsigned> g_dev_rr{0};
+thread_local int t_sel = 0;    // bound-device index of this thread's device-buffer calls
+thread_local int t_hip = -1;   // HIP device this thread is bound to
 
 int fail(int code, const char* fmt, ...) {
   char buf[512];
@@ -197,38 +234,50 @@ hipError_t mpcx_modexp_occupancy(int geom, int* blocks_per_cu) {
   }
 }
 
-// Every entry point runs on the caller's thread: bind that thread to the
-// process's GPU (HIP's current device is per thread; a worker thread would
-// otherwise submit to device 0 on a multi-GPU node).
-int ensure_device() {
-  if (g_device < 0) return fail(MPCX_ENODEV, "mpcx_init() has not been called");
-  thread_local int t_dev = -1;
-  if (t_dev != g_device) {
-    hipError_t e = hipSetDevice(g_device);
+// HIP's current device is per thread: every entry point binds its thread to
+// the device it submits to.
+int bind(const Device& d) {
+  if (t_hip != d.ordinal) {
+    hipError_t e = hipSetDevice(d.ordinal);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-    t_dev = g_device;
+    t_hip = d.ordinal;
   }
   return MPCX_OK;
 }
 
-// A free lane (round-robin start, first one not in use), else wait for one.
-Lane& acquire_lane(std::unique_lock<std::mutex>& lk) {
-  const unsigned start = g_lane_rr.fetch_add(1, std::memory_order_relaxed);
+int ndev_or_fail() {
+  const int n = g_ndev.load(std::memory_order_acquire);
+  if (n <= 0) return -fail(MPCX_ENODEV, "mpcx_init() has not been called");
+  return n;
+}
+
+// The device this thread's device-buffer calls use (mpcx_select_device).
+int selected(Device** out) {
+  const int n = ndev_or_fail();
+  if (n < 0) return -n;
+  if (t_sel < 0 || t_sel >= n) return fail(MPCX_EINVAL, "selected device %d not bound (%d bound)", t_sel, n);
+  *out = &g_devs[t_sel];
+  return bind(**out);
+}
+
+// A free lane of device d (round-robin start, first one not in use), else wait for one.
+Lane& acquire_lane(Device& d, std::unique_lock<std::mutex>& lk) {
+  const unsigned start = d.lane_rr.fetch_add(1, std::memory_order_relaxed);
   for (int i = 0; i < kLanes; ++i) {
-    Lane& l = g_lanes[(start + i) % kLanes];
+    Lane& l = d.lanes[(start + i) % kLanes];
     std::unique_lock<std::mutex> t(l.mu, std::try_to_lock);
     if (t.owns_lock()) {
       lk = std::move(t);
       return l;
     }
   }
-  Lane& l = g_lanes[start % kLanes];
+  Lane& l = d.lanes[start % kLanes];
   lk = std::unique_lock<std::mutex>(l.mu);
   return l;
 }
 
 int lane_stream(Lane& l) {
-  if (l.st) return MPCX_OK;
+  if (l.st || !l.own_stream) return MPCX_OK;
   hipError_t e = hipStreamCreateWithFlags(&l.st, hipStreamNonBlocking);
   if (e != hipSuccess) {
     l.st = nullptr;
@@ -265,7 +314,7 @@ int ensure_workspace(Lane& l, size_t bytes) {
   if (l.ws_bytes >= bytes) return MPCX_OK;
   if (l.ws) {
     // the lane's previous kernels may still read the old workspace
-    if (l.st) (void)hipStreamSynchronize(l.st);
+    (void)hipStreamSynchronize(l.st);
     (void)hipFree(l.ws);
   }
   l.ws = nullptr;
@@ -274,6 +323,38 @@ int ensure_workspace(Lane& l, size_t bytes) {
   if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(workspace %zu): %s", bytes, hipGetErrorString(e));
   l.ws_bytes = bytes;
   return MPCX_OK;
+}
+
+void drop_lane(Lane& l) {
+  std::lock_guard<std::mutex> ll(l.mu);
+  if (l.st) {
+    (void)hipStreamSynchronize(l.st);
+    if (l.own_stream) (void)hipStreamDestroy(l.st);
+  }
+  l.st = nullptr;
+  if (l.ws) (void)hipFree(l.ws);
+  l.ws = nullptr;
+  l.ws_bytes = 0;
+  for (auto& s : l.stage) {
+    if (s.ptr) (void)hipFree(s.ptr);
+    s = Staging{};
+  }
+  for (auto& s : l.sieve) {
+    if (s.ptr) (void)hipFree(s.ptr);
+    s = Staging{};
+  }
+}
+
+// Device-buffer workspace of (device, caller stream).
+Lane& stream_lane(Device& d, hipStream_t st) {
+  std::lock_guard<std::mutex> lk(d.dev_mu);
+  auto& p = d.dev_lanes[st];
+  if (!p) {
+    p.reset(new Lane());
+    p->own_stream = false;
+    p->st = st;
+  }
+  return *p;
 }
 
 int run_selftest() {
@@ -298,11 +379,135 @@ int run_selftest() {
   return MPCX_OK;
 }
 
+// Bind HIP ordinal `ordinal` as the next device (g_mu held).
+int bind_new_device(int ordinal) {
+  const int n = g_ndev.load();
+  for (int i = 0; i < n; ++i)
+    if (g_devs[i].ordinal == ordinal) return MPCX_OK;
+  if (n >= kMaxDevices) return fail(MPCX_EINVAL, "more than %d devices", kMaxDevices);
+  int vis = 0;
+  hipError_t e = hipGetDeviceCount(&vis);
+  if (e != hipSuccess || vis <= 0) return fail(MPCX_ENODEV, "no HIP device visible");
+  if (ordinal < 0 || ordinal >= vis) return fail(MPCX_EINVAL, "device %d out of range [0,%d)", ordinal, vis);
+  e = hipSetDevice(ordinal);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  t_hip = ordinal;
+  hipDeviceProp_t prop;
+  e = hipGetDeviceProperties(&prop, ordinal);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(MPCX_ENODEV, "device %d is %s; libmpcx is built for gfx950 only", ordinal, prop.gcnArchName);
+  Device& d = g_devs[n];
+  d.ordinal = ordinal;
+  d.num_cus = prop.multiProcessorCount;
+  for (int g = 0; g < MPCX_NUM_GEOMS; ++g) {
+    int b = 0;
+    if (mpcx_modexp_occupancy(g, &b) != hipSuccess || b <= 0) b = 1;
+    d.geom_slots[g] = b * d.num_cus;
+  }
+  int rc = run_selftest();
+  if (rc != MPCX_OK) {
+    d.ordinal = -1;
+    return rc;
+  }
+  g_ndev.store(n + 1, std::memory_order_release);
+  return MPCX_OK;
+}
+
+// The modulus constants on bound device di (uploaded on first use there).
+int mod_const(mpcx_mod_t mod, int di, const uint32_t** out) {
+  std::lock_guard<std::mutex> lk(mod->mu);
+  if (!mod->d_const[di]) {
+    uint32_t* p = nullptr;
+    hipError_t e = hipMalloc((void**)&p, mod->host_const.size() * sizeof(uint32_t));
+    if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(modulus): %s", hipGetErrorString(e));
+    e = hipMemcpy(p, mod->host_const.data(), mod->host_const.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(p);
+      return hip_fail(e, "upload modulus");
+    }
+    mod->d_const[di] = p;
+  }
+  *out = mod->d_const[di];
+  return MPCX_OK;
+}
+
+int fb_table(mpcx_fb_t fb, int di, const uint32_t** out) {
+  std::lock_guard<std::mutex> lk(fb->mu);
+  if (!fb->d_table[di]) {
+    uint32_t* p = nullptr;
+    const size_t bytes = fb->host_table.size() * sizeof(uint32_t);
+    hipError_t e = hipMalloc((void**)&p, bytes);
+    if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(fixed-base table %zu B)", bytes);
+    e = hipMemcpy(p, fb->host_table.data(), bytes, hipMemcpyHostToDevice);
+    if (e != hipSuccess) {
+      (void)hipFree(p);
+      return hip_fail(e, "upload fixed-base table");
+    }
+    fb->d_table[di] = p;
+  }
+  *out = fb->d_table[di];
+  return MPCX_OK;
+}
+
+// Slice plan of a batch over n_dev devices (mpcx_partition): one contiguous
+// operand range per device when every range gets at least min_slice
+// operands, else one range.
+uint32_t partition(uint32_t count, int n_dev, uint32_t min_slice, uint32_t* first, uint32_t* cnt) {
+  uint32_t slices = n_dev > 0 ? (uint32_t)n_dev : 1u;
+  if (min_slice == 0) slices = 1;
+  else slices = std::min<uint32_t>(slices, std::max<uint32_t>(1, count / min_slice));
+  const uint32_t per = (count + slices - 1) / std::max<uint32_t>(slices, 1);
+  uint32_t used = 0;
+  for (uint32_t s = 0; s < slices; ++s) {
+    const uint32_t f = std::min(count, s * per), c = std::min(count, f + per) - f;
+    if (first) first[s] = f;
+    if (cnt) cnt[s] = c;
+    used = s + 1;
+  }
+  return used;
+}
+
+// Runs fn(device index, first, n) over [0, count) by the partition plan:
+// several slices run concurrently, one host thread per device, and gather by
+// writing disjoint output ranges; a single range runs on one device chosen
+// round-robin, so concurrent callers spread over the node's GPUs. The first
+// failing slice's status and message are returned on the calling thread.
+int run_sliced(uint32_t count, uint32_t min_slice, const std::function<int(int, uint32_t, uint32_t)>& fn) {
+  const int n = ndev_or_fail();
+  if (n < 0) return -n;
+  uint32_t first[kMaxDevices], cnt[kMaxDevices];
+  const uint32_t slices = partition(count, n, min_slice, first, cnt);
+  if (slices <= 1) {
+    const int di = (int)(g_dev_rr.fetch_add(1, std::memory_order_relaxed) % (unsigned)n);
+    int rc = bind(g_devs[di]);
+    return rc ? rc : fn(di, 0, count);
+  }
+  std::vector<int> rcs(slices, MPCX_OK);
+  std::vector<std::string> msgs(slices);
+  std::vector<std::thread> th;
+  for (uint32_t s = 0; s < slices; ++s) {
+    th.emplace_back([&, s] {
+      int rc = bind(g_devs[s]);
+      if (!rc) rc = fn((int)s, first[s], cnt[s]);
+      rcs[s] = rc;
+      if (rc) msgs[s] = g_err;
+    });
+  }
+  for (auto& t : th) t.join();
+  for (uint32_t s = 0; s < slices; ++s)
+    if (rcs[s]) {
+      g_err = msgs[s];
+      return rcs[s];
+    }
+  return MPCX_OK;
+}
+
 }  // namespace
 
 extern "C" {
 
-int mpcx_version(void) { return 100; }
+int mpcx_version(void) { return 200; }
 
 int mpcx_set_option(const char* key, int value) {
   if (!key) return fail(MPCX_EINVAL, "null option");
@@ -324,6 +529,10 @@ int mpcx_set_option(const char* key, int value) {
     // main (throughput) geometry of the geometry's class
     if (value < 0 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "main_geom %d out of range", value);
     g_main_geom[MPCX_GEOM_CLASS(value)] = value;
+  } else if (std::strcmp(key, "device_split_min") == 0) {
+    // smallest per-device slice of a host-buffer batch split across the bound GPUs (0: never split)
+    if (value < 0) return fail(MPCX_EINVAL, "device_split_min %d < 0", value);
+    g_split_min = (uint32_t)value;
   } else {
     return fail(MPCX_EINVAL, "unknown option %s", key);
   }
@@ -343,64 +552,70 @@ int mpcx_device_count(int* out_count) {
 
 int mpcx_init(int device) {
   std::lock_guard<std::mutex> lk(g_mu);
-  if (g_device >= 0) {
-    if (g_device == device) return MPCX_OK;
-    return fail(MPCX_EINVAL, "already bound to device %d (one process per GPU)", g_device);
-  }
-  int n = 0;
-  hipError_t e = hipGetDeviceCount(&n);
-  if (e != hipSuccess || n <= 0) return fail(MPCX_ENODEV, "no HIP device visible");
-  if (device < 0 || device >= n) return fail(MPCX_EINVAL, "device %d out of range [0,%d)", device, n);
-  e = hipSetDevice(device);
-  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
-  hipDeviceProp_t prop;
-  e = hipGetDeviceProperties(&prop, device);
-  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
-  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
-    return fail(MPCX_ENODEV, "device %d is %s; libmpcx is built for gfx950 only", device, prop.gcnArchName);
-  g_device = device;
-  g_num_cus = prop.multiProcessorCount;
-  for (int g = 0; g < MPCX_NUM_GEOMS; ++g) {
-    int b = 0;
-    if (mpcx_modexp_occupancy(g, &b) != hipSuccess || b <= 0) b = 1;
-    g_geom_slots[g] = b * g_num_cus;
-  }
   const char* sp = std::getenv("MPCX_SPLIT");
   if (sp) g_split = sp[0] != '0';
-  int rc = run_selftest();
-  if (rc != MPCX_OK) g_device = -1;
-  return rc;
+  return bind_new_device(device);
+}
+
+int mpcx_init_devices(int n_gpus) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  int vis = 0;
+  hipError_t e = hipGetDeviceCount(&vis);
+  if (e != hipSuccess || vis <= 0) return fail(MPCX_ENODEV, "no HIP device visible");
+  if (n_gpus <= 0) n_gpus = vis;
+  if (n_gpus > vis) return fail(MPCX_EINVAL, "%d GPUs requested, %d visible", n_gpus, vis);
+  for (int i = 0; i < n_gpus; ++i)
+    if (int rc = bind_new_device(i)) return rc;
+  return MPCX_OK;
+}
+
+int mpcx_bound_devices(int* out_count, int* ordinals, int max_ordinals) {
+  if (!out_count) return fail(MPCX_EINVAL, "null out_count");
+  const int n = g_ndev.load(std::memory_order_acquire);
+  *out_count = n;
+  for (int i = 0; ordinals && i < n && i < max_ordinals; ++i) ordinals[i] = g_devs[i].ordinal;
+  return MPCX_OK;
+}
+
+int mpcx_partition(uint32_t count, int n_devices, uint32_t min_slice, uint32_t* first, uint32_t* n,
+                   uint32_t* n_slices) {
+  if (!n_slices) return fail(MPCX_EINVAL, "null n_slices");
+  if (n_devices < 1 || n_devices > kMaxDevices) return fail(MPCX_EINVAL, "n_devices %d outside [1, %d]", n_devices, kMaxDevices);
+  *n_slices = partition(count, n_devices, min_slice, first, n);
+  return MPCX_OK;
+}
+
+int mpcx_select_device(int index) {
+  const int n = g_ndev.load(std::memory_order_acquire);
+  if (index < 0 || index >= n) return fail(MPCX_EINVAL, "device index %d not bound (%d bound)", index, n);
+  t_sel = index;
+  return bind(g_devs[index]);
 }
 
 int mpcx_shutdown(void) {
   std::lock_guard<std::mutex> lk(g_mu);
-  auto drop = [](Lane& l) {
-    std::lock_guard<std::mutex> ll(l.mu);
-    if (l.st) {
-      (void)hipStreamSynchronize(l.st);
-      (void)hipStreamDestroy(l.st);
+  const int n = g_ndev.load();
+  for (int i = 0; i < n; ++i) {
+    Device& d = g_devs[i];
+    if (hipSetDevice(d.ordinal) != hipSuccess) continue;
+    t_hip = d.ordinal;
+    for (auto& l : d.lanes) drop_lane(l);
+    drop_lane(d.build_lane);
+    {
+      std::lock_guard<std::mutex> dl(d.dev_mu);
+      for (auto& kv : d.dev_lanes) drop_lane(*kv.second);
+      d.dev_lanes.clear();
     }
-    l.st = nullptr;
-    if (l.ws) (void)hipFree(l.ws);
-    l.ws = nullptr;
-    l.ws_bytes = 0;
-    for (auto* arr : {l.stage, l.sieve})
-      for (int i = 0; i < (arr == l.stage ? 4 : 3); ++i) {
-        if (arr[i].ptr) (void)hipFree(arr[i].ptr);
-        arr[i] = Staging{};
-      }
-  };
-  for (auto& l : g_lanes) drop(l);
-  drop(g_dev_lane);
-  g_device = -1;
+    d.ordinal = -1;
+  }
+  g_ndev.store(0);
   return MPCX_OK;
 }
 
 int mpcx_modulus_register(const uint32_t* m_words, uint32_t m_len, mpcx_mod_t* out) {
   if (!m_words || !out || m_len == 0) return fail(MPCX_EINVAL, "null modulus or output");
-  std::lock_guard<std::mutex> lk(g_mu);
-  int rc = ensure_device();
-  if (rc) return rc;
+  Device* dev = nullptr;
+  if (int rc = selected(&dev)) return rc;
   std::vector<uint32_t> m(m_words, m_words + m_len);
   while (m.size() > 1 && m.back() == 0) m.pop_back();
   const uint32_t bits = bit_length(m);
@@ -416,29 +631,25 @@ int mpcx_modulus_register(const uint32_t* m_words, uint32_t m_len, mpcx_mod_t* o
   uint32_t inv = m[0];
   for (int i = 0; i < 5; ++i) inv *= 2u - m[0] * inv;
   mod->n0inv = (0u - inv) & kM28;
-  std::vector<uint32_t> host;
   for (int g = 0; g < MPCX_NUM_GEOMS; ++g) {
     mod->const_off[g] = 0;
     if (MPCX_GEOM_CLASS(g) != cls) continue;
     const uint32_t L = (uint32_t)MPCX_GEOM_L(g);
-    mod->const_off[g] = (uint32_t)host.size();
+    mod->const_off[g] = (uint32_t)mod->host_const.size();
     auto nd = to_digits(m, L);
     auto r1 = to_digits(pow2_mod(kDigitBits * L, m), L);
     auto r2 = to_digits(pow2_mod(2 * kDigitBits * L, m), L);
-    host.insert(host.end(), nd.begin(), nd.end());
-    host.insert(host.end(), r1.begin(), r1.end());
-    host.insert(host.end(), r2.begin(), r2.end());
+    auto& h = mod->host_const;
+    h.insert(h.end(), nd.begin(), nd.end());
+    h.insert(h.end(), r1.begin(), r1.end());
+    h.insert(h.end(), r2.begin(), r2.end());
   }
-  hipError_t e = hipMalloc((void**)&mod->d_const, host.size() * sizeof(uint32_t));
-  if (e != hipSuccess) {
+  // upload to the selected device now (fails loudly without memory); other
+  // bound devices receive the constants on first use
+  const uint32_t* p = nullptr;
+  if (int rc = mod_const(mod, (int)(dev - g_devs), &p)) {
     delete mod;
-    return fail(MPCX_ENOMEM, "hipMalloc(modulus): %s", hipGetErrorString(e));
-  }
-  e = hipMemcpy(mod->d_const, host.data(), host.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    (void)hipFree(mod->d_const);
-    delete mod;
-    return hip_fail(e, "upload modulus");
+    return rc;
   }
   *out = mod;
   return MPCX_OK;
@@ -446,8 +657,9 @@ int mpcx_modulus_register(const uint32_t* m_words, uint32_t m_len, mpcx_mod_t* o
 
 int mpcx_modulus_release(mpcx_mod_t mod) {
   if (!mod) return fail(MPCX_EINVAL, "null modulus");
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (mod->d_const) (void)hipFree(mod->d_const);
+  const int n = g_ndev.load();
+  for (int i = 0; i < n && i < kMaxDevices; ++i)
+    if (mod->d_const[i] && bind(g_devs[i]) == MPCX_OK) (void)hipFree(mod->d_const[i]);
   delete mod;
   return MPCX_OK;
 }
@@ -469,10 +681,16 @@ int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K,
   return MPCX_OK;
 }
 
-static int modexp_device_locked(Lane& lane, mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases,
-                                uint32_t base_words, const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
-                                uint32_t exp_bits, const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out,
-                                uint32_t out_words, hipStream_t st) {
+}  // extern "C"
+
+// Enqueue one batch on lane `lane` of device `di` (lane locked by the caller;
+// its stream is lane.st).
+static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases,
+                          uint32_t base_words, const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
+                          uint32_t exp_bits, const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out,
+                          uint32_t out_words) {
+  const Device& dev = g_devs[di];
+  hipStream_t st = lane.st;
   const uint32_t class_words = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
   if (base_words == 0 || base_words > class_words)
     return fail(MPCX_EINVAL, "base_words %u outside [1, %u] (reduce mod m first)", base_words, class_words);
@@ -482,6 +700,8 @@ static int modexp_device_locked(Lane& lane, mpcx_mod_t mod, uint32_t count, cons
   if (exp_bits > 32u * exp_words) return fail(MPCX_EINVAL, "exp_bits %u > 32*exp_words", exp_bits);
   if (count == 0) return MPCX_OK;
   if (!d_bases || !d_out || (exp_words && !d_exps)) return fail(MPCX_EINVAL, "null buffer");
+  const uint32_t* dconst = nullptr;
+  if (int rc = mod_const(mod, di, &dconst)) return rc;
   // Geometry plan: whole rounds of resident wavefronts in the main geometry,
   // the partial last round (or a small batch) in the narrow geometry.
   struct Part {
@@ -495,7 +715,7 @@ static int modexp_device_locked(Lane& lane, mpcx_mod_t mod, uint32_t count, cons
   } else {
     const uint32_t G = (uint32_t)MPCX_GEOM_G(gm);
     const double waves = (double)((count + G - 1) / G);
-    const double rounds = waves / (double)std::max(1, g_geom_slots[gm]);
+    const double rounds = waves / (double)std::max(1, dev.geom_slots[gm]);
     const double full = std::floor(rounds), frac = rounds - full;
     // Measured on MI355X (profiles/r01): a lone wavefront issues v_mad_u64_u32
     // at ~45% of SIMD peak, so tiny batches (< 0.15 of a round) finish sooner
@@ -506,7 +726,7 @@ static int modexp_device_locked(Lane& lane, mpcx_mod_t mod, uint32_t count, cons
     } else if (!g_split || gn < 0 || rounds < 1.0 || frac == 0.0 || frac > 0.75) {
       parts[nparts++] = {gm, 0, count};
     } else {
-      const uint32_t nmain = (uint32_t)full * (uint32_t)g_geom_slots[gm] * G;
+      const uint32_t nmain = (uint32_t)full * (uint32_t)dev.geom_slots[gm] * G;
       parts[nparts++] = {gm, 0, nmain};
       parts[nparts++] = {gn, nmain, count - nmain};
     }
@@ -538,7 +758,7 @@ static int modexp_device_locked(Lane& lane, mpcx_mod_t mod, uint32_t count, cons
     const uint32_t waves = (pt.count + G - 1) / G;
     mpcx::ModexpArgs a{};
     const uint32_t L = (uint32_t)MPCX_GEOM_L(pt.geom);
-    a.nd = mod->d_const + mod->const_off[pt.geom];
+    a.nd = dconst + mod->const_off[pt.geom];
     a.r1d = a.nd + L;
     a.r2d = a.nd + 2 * L;
     a.base = d_bases + (size_t)pt.first * base_words;
@@ -570,21 +790,17 @@ static uint32_t max_exp_bits(const uint32_t* exps, uint32_t exp_words, int exp_s
   return bits;
 }
 
-// host-buffer path: stage inputs, launch, copy back (synchronous)
-static int modexp_host(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
-                       const uint32_t* exps, uint32_t exp_words, int exp_shared, const uint32_t* muls,
-                       uint32_t mul_words, uint32_t* out, uint32_t out_words) {
-  if (!mod) return fail(MPCX_EINVAL, "null modulus");
-  if (count == 0) return MPCX_OK;
-  if (!bases || !out || (exp_words && !exps)) return fail(MPCX_EINVAL, "null buffer");
-  int rc = ensure_device();
-  if (rc) return rc;
+// host-buffer path: stage one operand range on one device, launch, copy back (synchronous)
+static int modexp_host_range(int di, mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
+                             const uint32_t* exps, uint32_t exp_words, int exp_shared, const uint32_t* muls,
+                             uint32_t mul_words, uint32_t* out, uint32_t out_words) {
   const uint32_t exp_bits = max_exp_bits(exps, exp_words, exp_shared, count);
   const size_t n_exp_words = exp_shared ? exp_words : (size_t)count * exp_words;
   const size_t bb = (size_t)count * base_words * 4, eb = std::max<size_t>(n_exp_words * 4, 4),
                ob = (size_t)count * out_words * 4, mb = muls ? (size_t)count * mul_words * 4 : 0;
   std::unique_lock<std::mutex> lk;
-  Lane& l = acquire_lane(lk);
+  Lane& l = acquire_lane(g_devs[di], lk);
+  int rc;
   if ((rc = lane_stream(l))) return rc;
   Staging* sg = l.stage;
   if ((rc = ensure_buffer(sg[0], bb)) || (rc = ensure_buffer(sg[1], eb)) || (rc = ensure_buffer(sg[2], ob)) ||
@@ -593,22 +809,86 @@ static int modexp_host(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, ui
   if ((rc = h2d(sg[0].ptr, bases, bb, l.st)) || (rc = h2d(sg[1].ptr, exps, n_exp_words * 4, l.st)) ||
       (muls && (rc = h2d(sg[3].ptr, muls, mb, l.st))))
     return rc;
-  rc = modexp_device_locked(l, mod, count, (const uint32_t*)sg[0].ptr, base_words, (const uint32_t*)sg[1].ptr,
-                            exp_words, exp_shared, exp_bits, muls ? (const uint32_t*)sg[3].ptr : nullptr, mul_words,
-                            (uint32_t*)sg[2].ptr, out_words, l.st);
+  rc = modexp_enqueue(di, l, mod, count, (const uint32_t*)sg[0].ptr, base_words, (const uint32_t*)sg[1].ptr,
+                      exp_words, exp_shared, exp_bits, muls ? (const uint32_t*)sg[3].ptr : nullptr, mul_words,
+                      (uint32_t*)sg[2].ptr, out_words);
   if (rc) return rc;
   return d2h_sync(out, sg[2].ptr, ob, l.st);
 }
+
+static int modexp_host(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
+                       const uint32_t* exps, uint32_t exp_words, int exp_shared, const uint32_t* muls,
+                       uint32_t mul_words, uint32_t* out, uint32_t out_words) {
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  if (count == 0) return MPCX_OK;
+  if (!bases || !out || (exp_words && !exps)) return fail(MPCX_EINVAL, "null buffer");
+  return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t n) {
+    return modexp_host_range(di, mod, n, bases + (size_t)first * base_words, base_words,
+                             exps ? (exp_shared ? exps : exps + (size_t)first * exp_words) : nullptr, exp_words,
+                             exp_shared, muls ? muls + (size_t)first * mul_words : nullptr, mul_words,
+                             out + (size_t)first * out_words, out_words);
+  });
+}
+
+// ------------------------------------------------------------ async jobs
+// mpcx_modexp_submit: a host-buffer batch run by a small pool of submission
+// threads, so a batcher (the Go side's one goroutine per modulus,
+// INTEGRATION.md) can stage batch k+1 while batch k runs.
+struct mpcx_job_s {
+  std::mutex mu;
+  std::condition_variable cv;
+  bool done = false;
+  int rc = MPCX_OK;
+  std::string msg;
+  std::function<int()> work;
+};
+
+namespace {
+struct JobPool {
+  std::mutex mu;
+  std::condition_variable cv;
+  std::deque<mpcx_job_t> q;
+  std::vector<std::thread> th;
+  void start(size_t n) {
+    while (th.size() < n)
+      th.emplace_back([this] {
+        for (;;) {
+          mpcx_job_t j;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return !q.empty(); });
+            j = q.front();
+            q.pop_front();
+          }
+          const int rc = j->work();
+          std::lock_guard<std::mutex> lk(j->mu);
+          j->rc = rc;
+          if (rc) j->msg = g_err;
+          j->done = true;
+          j->cv.notify_all();
+        }
+      });
+  }
+};
+JobPool& job_pool() {
+  // never destroyed: worker threads live for the process
+  static JobPool* p = new JobPool();
+  return *p;
+}
+}  // namespace
+
+extern "C" {
 
 int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
                              const uint32_t* d_exps, uint32_t exp_words, int exp_shared, uint32_t exp_bits,
                              uint32_t* d_out, uint32_t out_words, void* stream) {
   if (!mod) return fail(MPCX_EINVAL, "null modulus");
-  std::lock_guard<std::mutex> lk(g_mu);
-  int rc = ensure_device();
-  if (rc) return rc;
-  return modexp_device_locked(g_dev_lane, mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits,
-                              nullptr, 0, d_out, out_words, (hipStream_t)stream);
+  Device* dev = nullptr;
+  if (int rc = selected(&dev)) return rc;
+  Lane& l = stream_lane(*dev, (hipStream_t)stream);
+  std::lock_guard<std::mutex> lk(l.mu);
+  return modexp_enqueue((int)(dev - g_devs), l, mod, count, d_bases, base_words, d_exps, exp_words, exp_shared,
+                        exp_bits, nullptr, 0, d_out, out_words);
 }
 
 int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
@@ -617,11 +897,12 @@ int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t*
                                  void* stream) {
   if (!mod) return fail(MPCX_EINVAL, "null modulus");
   if (!d_muls) return fail(MPCX_EINVAL, "null multipliers");
-  std::lock_guard<std::mutex> lk(g_mu);
-  int rc = ensure_device();
-  if (rc) return rc;
-  return modexp_device_locked(g_dev_lane, mod, count, d_bases, base_words, d_exps, exp_words, exp_shared, exp_bits,
-                              d_muls, mul_words, d_out, out_words, (hipStream_t)stream);
+  Device* dev = nullptr;
+  if (int rc = selected(&dev)) return rc;
+  Lane& l = stream_lane(*dev, (hipStream_t)stream);
+  std::lock_guard<std::mutex> lk(l.mu);
+  return modexp_enqueue((int)(dev - g_devs), l, mod, count, d_bases, base_words, d_exps, exp_words, exp_shared,
+                        exp_bits, d_muls, mul_words, d_out, out_words);
 }
 
 int mpcx_modexp_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
@@ -635,6 +916,49 @@ int mpcx_modexp_mul_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* bases,
                           uint32_t mul_words, uint32_t* out, uint32_t out_words) {
   if (!muls) return fail(MPCX_EINVAL, "null multipliers");
   return modexp_host(mod, count, bases, base_words, exps, exp_words, exp_shared, muls, mul_words, out, out_words);
+}
+
+int mpcx_modexp_submit(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
+                       const uint32_t* exps, uint32_t exp_words, int exp_shared, const uint32_t* muls,
+                       uint32_t mul_words, uint32_t* out, uint32_t out_words, mpcx_job_t* job) {
+  if (!job) return fail(MPCX_EINVAL, "null job");
+  *job = nullptr;
+  if (!mod) return fail(MPCX_EINVAL, "null modulus");
+  const int n = ndev_or_fail();
+  if (n < 0) return -n;
+  auto* j = new mpcx_job_s();
+  j->work = [=] {
+    return modexp_host(mod, count, bases, base_words, exps, exp_words, exp_shared, muls, mul_words, out, out_words);
+  };
+  JobPool& p = job_pool();
+  {
+    std::lock_guard<std::mutex> lk(p.mu);
+    p.start((size_t)n * kLanes);
+    p.q.push_back(j);
+  }
+  p.cv.notify_one();
+  *job = j;
+  return MPCX_OK;
+}
+
+int mpcx_job_test(mpcx_job_t job, int* done) {
+  if (!job || !done) return fail(MPCX_EINVAL, "null job");
+  std::lock_guard<std::mutex> lk(job->mu);
+  *done = job->done ? 1 : 0;
+  return MPCX_OK;
+}
+
+int mpcx_job_wait(mpcx_job_t job) {
+  if (!job) return fail(MPCX_EINVAL, "null job");
+  int rc;
+  {
+    std::unique_lock<std::mutex> lk(job->mu);
+    job->cv.wait(lk, [&] { return job->done; });
+    rc = job->rc;
+    if (rc) g_err = job->msg;
+  }
+  delete job;
+  return rc;
 }
 
 int mpcx_mulmod_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* a, uint32_t a_words, const uint32_t* b,
@@ -656,22 +980,23 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
       return fail(MPCX_EINVAL, "candidate %u has %u bits > %d", i, bits, MPCX_CLASS_MAXBITS(0));
     if (bits < 3 || (pi[0] & 1u) == 0) return fail(MPCX_EINVAL, "candidate %u is not an odd integer >= 5", i);
   }
-  int rc = ensure_device();
-  if (rc) return rc;
-  std::unique_lock<std::mutex> lk;
-  Lane& l = acquire_lane(lk);
-  if ((rc = lane_stream(l))) return rc;
-  const size_t pb = (size_t)count * p_words * 4;
-  if ((rc = ensure_buffer(l.stage[0], pb)) || (rc = ensure_buffer(l.stage[3], count))) return rc;
-  if ((rc = h2d(l.stage[0].ptr, p, pb, l.st))) return rc;
-  mpcx::FermatArgs a{};
-  a.p = (const uint32_t*)l.stage[0].ptr;
-  a.ok = (uint8_t*)l.stage[3].ptr;
-  a.count = count;
-  a.p_words = p_words;
-  hipError_t e = mpcx_launch_fermat2(&a, (count + 63) / 64, l.st);
-  if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
-  return d2h_sync(ok, l.stage[3].ptr, count, l.st);
+  return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t n) {
+    std::unique_lock<std::mutex> lk;
+    Lane& l = acquire_lane(g_devs[di], lk);
+    int rc;
+    if ((rc = lane_stream(l))) return rc;
+    const size_t pb = (size_t)n * p_words * 4;
+    if ((rc = ensure_buffer(l.stage[0], pb)) || (rc = ensure_buffer(l.stage[3], n))) return rc;
+    if ((rc = h2d(l.stage[0].ptr, p + (size_t)first * p_words, pb, l.st))) return rc;
+    mpcx::FermatArgs a{};
+    a.p = (const uint32_t*)l.stage[0].ptr;
+    a.ok = (uint8_t*)l.stage[3].ptr;
+    a.count = n;
+    a.p_words = p_words;
+    hipError_t e = mpcx_launch_fermat2(&a, (n + 63) / 64, l.st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
+    return d2h_sync(ok + first, l.stage[3].ptr, n, l.st);
+  });
 }
 
 int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* bases, uint8_t* ok) {
@@ -684,30 +1009,34 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
     if (bit_length_words(ni, n_words) < 3 || (ni[0] & 1u) == 0)
       return fail(MPCX_EINVAL, "candidate %u is not an odd integer >= 5", i);
   }
-  int rc = ensure_device();
-  if (rc) return rc;
-  std::unique_lock<std::mutex> lk;
-  Lane& l = acquire_lane(lk);
-  if ((rc = lane_stream(l))) return rc;
-  const size_t nb = (size_t)count * n_words * 4;
-  if ((rc = ensure_buffer(l.stage[0], nb)) || (rc = ensure_buffer(l.stage[1], nb)) ||
-      (rc = ensure_buffer(l.stage[3], count)))
-    return rc;
-  if ((rc = h2d(l.stage[0].ptr, n, nb, l.st)) || (rc = h2d(l.stage[1].ptr, bases, nb, l.st))) return rc;
-  mpcx::MrArgs a{};
-  a.n = (const uint32_t*)l.stage[0].ptr;
-  a.a = (const uint32_t*)l.stage[1].ptr;
-  a.ok = (uint8_t*)l.stage[3].ptr;
-  a.count = count;
-  a.n_words = n_words;
-  hipError_t e = mpcx_launch_mr(&a, (count + 63) / 64, l.st);
-  if (e != hipSuccess) return hip_fail(e, "launch k_mr");
-  return d2h_sync(ok, l.stage[3].ptr, count, l.st);
+  return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t cnt) {
+    std::unique_lock<std::mutex> lk;
+    Lane& l = acquire_lane(g_devs[di], lk);
+    int rc;
+    if ((rc = lane_stream(l))) return rc;
+    const size_t nb = (size_t)cnt * n_words * 4;
+    if ((rc = ensure_buffer(l.stage[0], nb)) || (rc = ensure_buffer(l.stage[1], nb)) ||
+        (rc = ensure_buffer(l.stage[3], cnt)))
+      return rc;
+    if ((rc = h2d(l.stage[0].ptr, n + (size_t)first * n_words, nb, l.st)) ||
+        (rc = h2d(l.stage[1].ptr, bases + (size_t)first * n_words, nb, l.st)))
+      return rc;
+    mpcx::MrArgs a{};
+    a.n = (const uint32_t*)l.stage[0].ptr;
+    a.a = (const uint32_t*)l.stage[1].ptr;
+    a.ok = (uint8_t*)l.stage[3].ptr;
+    a.count = cnt;
+    a.n_words = n_words;
+    hipError_t e = mpcx_launch_mr(&a, (cnt + 63) / 64, l.st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_mr");
+    return d2h_sync(ok + first, l.stage[3].ptr, cnt, l.st);
+  });
 }
 
 int mpcx_dev_alloc(size_t bytes, void** out_ptr) {
   if (!out_ptr) return fail(MPCX_EINVAL, "null out_ptr");
-  if (int rc = ensure_device()) return rc;
+  Device* dev = nullptr;
+  if (int rc = selected(&dev)) return rc;
   hipError_t e = hipMalloc(out_ptr, bytes);
   if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   return MPCX_OK;
@@ -730,6 +1059,8 @@ int mpcx_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes) {
 
 int mpcx_stream_create(void** out_stream) {
   if (!out_stream) return fail(MPCX_EINVAL, "null out_stream");
+  Device* dev = nullptr;
+  if (int rc = selected(&dev)) return rc;
   hipStream_t s;
   hipError_t e = hipStreamCreateWithFlags(&s, hipStreamNonBlocking);
   if (e != hipSuccess) return hip_fail(e, "hipStreamCreate");
@@ -738,6 +1069,20 @@ int mpcx_stream_create(void** out_stream) {
 }
 
 int mpcx_stream_destroy(void* stream) {
+  // drop the device-buffer workspace this stream owned on every device
+  const int n = g_ndev.load();
+  for (int i = 0; i < n; ++i) {
+    Device& d = g_devs[i];
+    std::unique_ptr<Lane> l;
+    {
+      std::lock_guard<std::mutex> lk(d.dev_mu);
+      auto it = d.dev_lanes.find((hipStream_t)stream);
+      if (it == d.dev_lanes.end()) continue;
+      l = std::move(it->second);
+      d.dev_lanes.erase(it);
+    }
+    if (bind(d) == MPCX_OK) drop_lane(*l);
+  }
   hipError_t e = hipStreamDestroy((hipStream_t)stream);
   return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipStreamDestroy");
 }
@@ -747,28 +1092,32 @@ int mpcx_stream_sync(void* stream) {
   return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipStreamSynchronize");
 }
 
+int mpcx_sync(void* stream) { return mpcx_stream_sync(stream); }
+
 }  // extern "C"
 
 // ------------------------------------------------------------ fixed base
 // Comb tables for a long-lived base (h1, h2 of a node's N~; SURVEY.md 8(a)
 // "shared bases"): entry (j, v) = b^(v 2^(8j)) R mod m. Built on the GPU by
-// the modexp kernels: b_j = b^(2^(8j)) (per-operand exponents), then
-// T(j, v) = (R mod m) * b_j^v (fused multiplier), then reordered into the
-// kernel geometry's digit layout on the host.
+// the modexp kernels on the selected device: b_j = b^(2^(8j)) (per-operand
+// exponents), then T(j, v) = (R mod m) * b_j^v (fused multiplier), then
+// reordered into the kernel geometry's digit layout on the host; the host copy
+// is kept so other bound devices receive the table on first use.
 int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_words, uint32_t max_exp_bits,
                             mpcx_fb_t* out) {
   if (!mod || !base || !out) return fail(MPCX_EINVAL, "null argument");
   if (mod->cls > 1) return fail(MPCX_EINVAL, "fixed-base tables serve moduli of <= %d bits", MPCX_CLASS_MAXBITS(1));
   const uint32_t cw = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
   if (base_words == 0 || base_words > cw) return fail(MPCX_EINVAL, "base_words %u outside [1, %u]", base_words, cw);
-  if (max_exp_bits == 0 || max_exp_bits > 65536) return fail(MPCX_EINVAL, "max_exp_bits %u outside [1, 65536]", max_exp_bits);
-  std::lock_guard<std::mutex> lk(g_mu);
-  int rc = ensure_device();
-  if (rc) return rc;
-  // the build reuses the device-buffer workspace on the null stream: drain
-  // any device-buffer call still reading it on a caller's stream (rare: once
-  // per long-lived base)
-  (void)hipDeviceSynchronize();
+  if (max_exp_bits == 0 || max_exp_bits > MPCX_FB_MAX_EXP_BITS)
+    return fail(MPCX_EINVAL, "max_exp_bits %u outside [1, %d]", max_exp_bits, MPCX_FB_MAX_EXP_BITS);
+  Device* dev = nullptr;
+  if (int rc = selected(&dev)) return rc;
+  const int di = (int)(dev - g_devs);
+  Lane& bl = dev->build_lane;
+  std::lock_guard<std::mutex> blk(bl.mu);
+  int rc;
+  if ((rc = lane_stream(bl))) return rc;
   const int geom = MPCX_MAIN_GEOM(mod->cls);
   const uint32_t L = (uint32_t)MPCX_GEOM_L(geom), P = (uint32_t)MPCX_GEOM_P(geom), K = (uint32_t)MPCX_GEOM_K(geom);
   const uint32_t nwin = (max_exp_bits + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS;
@@ -810,14 +1159,11 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     cleanup();
     return hip_fail(e, "upload fixed-base inputs");
   }
-  rc = modexp_device_locked(g_dev_lane, mod, nwin, d_b, cw, d_e1, ew1, 0, MPCX_FB_WINDOW_BITS * (nwin - 1) + 1,
-                            nullptr, 0, d_bj, cw, nullptr);
+  rc = modexp_enqueue(di, bl, mod, nwin, d_b, cw, d_e1, ew1, 0, MPCX_FB_WINDOW_BITS * (nwin - 1) + 1, nullptr, 0,
+                      d_bj, cw);
   // T(j, v) = R * b_j^v: operand i = j*255 + (v-1) takes base b_j -> replicate b_j rows
   std::vector<uint32_t> hbj((size_t)nwin * cw), hb2;
-  if (!rc) {
-    e = hipMemcpy(hbj.data(), d_bj, hbj.size() * 4, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) rc = hip_fail(e, "copy b_j");
-  }
+  if (!rc) rc = d2h_sync(hbj.data(), d_bj, hbj.size() * 4, bl.st);
   if (!rc) {
     hb2.resize(n2 * cw);
     for (size_t i = 0; i < n2; ++i) std::memcpy(&hb2[i * cw], &hbj[(i / nv) * cw], cw * 4);
@@ -825,23 +1171,22 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     d_b = nullptr;
     if (!alloc(&d_b, hb2.size())) rc = fail(MPCX_ENOMEM, "hipMalloc(fixed-base bases)");
   }
-  if (!rc) {
-    e = hipMemcpy(d_b, hb2.data(), hb2.size() * 4, hipMemcpyHostToDevice);
-    if (e != hipSuccess) rc = hip_fail(e, "upload b_j");
-  }
+  if (!rc) rc = h2d(d_b, hb2.data(), hb2.size() * 4, bl.st);
   if (!rc)
-    rc = modexp_device_locked(g_dev_lane, mod, (uint32_t)n2, d_b, cw, d_e2, 1, 0, MPCX_FB_WINDOW_BITS, d_m,
-                              mod->words, d_t, cw, nullptr);
+    rc = modexp_enqueue(di, bl, mod, (uint32_t)n2, d_b, cw, d_e2, 1, 0, MPCX_FB_WINDOW_BITS, d_m, mod->words, d_t,
+                        cw);
   std::vector<uint32_t> ht(n2 * cw);
-  if (!rc) {
-    e = hipMemcpy(ht.data(), d_t, ht.size() * 4, hipMemcpyDeviceToHost);
-    if (e != hipSuccess) rc = hip_fail(e, "copy table");
-  }
+  if (!rc) rc = d2h_sync(ht.data(), d_t, ht.size() * 4, bl.st);
   cleanup();
   if (rc) return rc;
+  auto* fb = new mpcx_fixedbase_s();
+  fb->mod = mod;
+  fb->geom = geom;
+  fb->nwin = nwin;
   // digits, [k][p] interleaved per entry
   const size_t ent_words = L;
-  std::vector<uint32_t> tab((size_t)nwin * MPCX_FB_ENTRIES * ent_words);
+  auto& tab = fb->host_table;
+  tab.assign((size_t)nwin * MPCX_FB_ENTRIES * ent_words, 0);
   auto put = [&](size_t ent, const std::vector<uint32_t>& words) {
     const std::vector<uint32_t> d = to_digits(words, L);
     uint32_t* dst = &tab[ent * ent_words];
@@ -856,20 +1201,10 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
       put((size_t)j * MPCX_FB_ENTRIES + v, w);
     }
   }
-  auto* fb = new mpcx_fixedbase_s();
-  fb->mod = mod;
-  fb->geom = geom;
-  fb->nwin = nwin;
-  e = hipMalloc((void**)&fb->d_table, tab.size() * 4);
-  if (e != hipSuccess) {
+  const uint32_t* dt = nullptr;
+  if ((rc = fb_table(fb, di, &dt))) {
     delete fb;
-    return fail(MPCX_ENOMEM, "hipMalloc(fixed-base table %zu B)", tab.size() * 4);
-  }
-  e = hipMemcpy(fb->d_table, tab.data(), tab.size() * 4, hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
-    (void)hipFree(fb->d_table);
-    delete fb;
-    return hip_fail(e, "upload fixed-base table");
+    return rc;
   }
   *out = fb;
   return MPCX_OK;
@@ -877,8 +1212,9 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
 
 int mpcx_fixedbase_release(mpcx_fb_t fb) {
   if (!fb) return fail(MPCX_EINVAL, "null fixed base");
-  std::lock_guard<std::mutex> lk(g_mu);
-  if (fb->d_table) (void)hipFree(fb->d_table);
+  const int n = g_ndev.load();
+  for (int i = 0; i < n && i < kMaxDevices; ++i)
+    if (fb->d_table[i] && bind(g_devs[i]) == MPCX_OK) (void)hipFree(fb->d_table[i]);
   delete fb;
   return MPCX_OK;
 }
@@ -915,44 +1251,50 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
       return fail(MPCX_EINVAL, "exponent of %u bits > fixed-base table's %u", bits, fbs[t]->nwin * MPCX_FB_WINDOW_BITS);
     nwin[t] = (bits + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS;
   }
-  int rc = ensure_device();
-  if (rc) return rc;
-  const size_t eb0 = (size_t)count * exp_words[0] * 4, eb1 = nbases > 1 ? (size_t)count * exp_words[1] * 4 : 0,
-               ob = (size_t)count * out_words * 4, mb = muls ? (size_t)count * mul_words * 4 : 0;
-  std::unique_lock<std::mutex> lk;
-  Lane& l = acquire_lane(lk);
-  if ((rc = lane_stream(l))) return rc;
-  Staging* sg = l.stage;
-  if ((rc = ensure_buffer(sg[0], eb0)) || (rc = ensure_buffer(sg[1], eb1)) ||
-      (rc = ensure_buffer(sg[2], ob)) || (muls && (rc = ensure_buffer(sg[3], mb))))
-    return rc;
-  if ((rc = h2d(sg[0].ptr, exps[0], eb0, l.st)) || (rc = h2d(sg[1].ptr, exps[1], eb1, l.st)) ||
-      (muls && (rc = h2d(sg[3].ptr, muls, mb, l.st))))
-    return rc;
-  hipError_t e;
-  const int geom = fbs[0]->geom;
-  mpcx::FixedBaseArgs a{};
-  a.nd = mod->d_const + mod->const_off[geom];
-  a.r1d = a.nd + MPCX_GEOM_L(geom);
-  a.r2d = a.nd + 2 * MPCX_GEOM_L(geom);
-  for (uint32_t t = 0; t < nbases; ++t) {
-    a.tables[t] = fbs[t]->d_table;
-    a.exps[t] = (const uint32_t*)sg[t].ptr;
-    a.exp_words[t] = exp_words[t];
-    a.nwin[t] = nwin[t];
-  }
-  a.nbases = nbases;
-  a.mul = muls ? (const uint32_t*)sg[3].ptr : nullptr;
-  a.mul_words = muls ? mul_words : 0;
-  a.out = (uint32_t*)sg[2].ptr;
-  a.out_words = out_words;
-  a.count = count;
-  a.n0inv = mod->n0inv;
-  const uint32_t waves = (count + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
-  e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
-                                : mpcx_launch_fixedbase_g1(&a, waves, l.st);
-  if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
-  return d2h_sync(out, sg[2].ptr, ob, l.st);
+  return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t n) {
+    const uint32_t* dconst = nullptr;
+    const uint32_t* dtab[MPCX_FB_MAX_BASES] = {nullptr, nullptr};
+    int rc;
+    if ((rc = mod_const(mod, di, &dconst))) return rc;
+    for (uint32_t t = 0; t < nbases; ++t)
+      if ((rc = fb_table(fbs[t], di, &dtab[t]))) return rc;
+    const size_t eb[MPCX_FB_MAX_BASES] = {(size_t)n * exp_words[0] * 4,
+                                          nbases > 1 ? (size_t)n * exp_words[1] * 4 : 0};
+    const size_t ob = (size_t)n * out_words * 4, mb = muls ? (size_t)n * mul_words * 4 : 0;
+    std::unique_lock<std::mutex> lk;
+    Lane& l = acquire_lane(g_devs[di], lk);
+    if ((rc = lane_stream(l))) return rc;
+    Staging* sg = l.stage;
+    if ((rc = ensure_buffer(sg[0], eb[0])) || (rc = ensure_buffer(sg[1], eb[1])) ||
+        (rc = ensure_buffer(sg[2], ob)) || (muls && (rc = ensure_buffer(sg[3], mb))))
+      return rc;
+    for (uint32_t t = 0; t < nbases; ++t)  // exps[t] exists only for t < nbases
+      if (eb[t] && (rc = h2d(sg[t].ptr, exps[t] + (size_t)first * exp_words[t], eb[t], l.st))) return rc;
+    if (muls && (rc = h2d(sg[3].ptr, muls + (size_t)first * mul_words, mb, l.st))) return rc;
+    const int geom = fbs[0]->geom;
+    mpcx::FixedBaseArgs a{};
+    a.nd = dconst + mod->const_off[geom];
+    a.r1d = a.nd + MPCX_GEOM_L(geom);
+    a.r2d = a.nd + 2 * MPCX_GEOM_L(geom);
+    for (uint32_t t = 0; t < nbases; ++t) {
+      a.tables[t] = dtab[t];
+      a.exps[t] = (const uint32_t*)sg[t].ptr;
+      a.exp_words[t] = exp_words[t];
+      a.nwin[t] = nwin[t];
+    }
+    a.nbases = nbases;
+    a.mul = muls ? (const uint32_t*)sg[3].ptr : nullptr;
+    a.mul_words = muls ? mul_words : 0;
+    a.out = (uint32_t*)sg[2].ptr;
+    a.out_words = out_words;
+    a.count = n;
+    a.n0inv = mod->n0inv;
+    const uint32_t waves = (n + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
+    hipError_t e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
+                                             : mpcx_launch_fixedbase_g1(&a, waves, l.st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
+    return d2h_sync(out + (size_t)first * out_words, sg[2].ptr, ob, l.st);
+  });
 }
 
 // ------------------------------------------------------------ safe-prime sieve
@@ -1000,72 +1342,75 @@ int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t co
   if (count == 0) return MPCX_OK;
   if (!raw || !idx_out || !ok_out) return fail(MPCX_EINVAL, "null buffer");
   static const TrialTables tt;
-  int rc = ensure_device();
-  if (rc) return rc;
-  std::unique_lock<std::mutex> lk;
-  Lane& l = acquire_lane(lk);
-  if ((rc = lane_stream(l))) return rc;
-  Staging *sg = l.stage, *sv = l.sieve;
-  constexpr uint32_t W = MPCX_SIEVE_MAX_BYTES / 4;
-  const size_t ng = tt.prod.size();
-  // misc buffer: counter | prod | start | primes | inv (8-byte aligned)
-  const size_t off_prod = 2, off_start = off_prod + ng, off_primes = off_start + tt.start.size();
-  const size_t off_inv = (off_primes + tt.primes.size() + 1) / 2 * 2;
-  const size_t misc_words = off_inv + 2 * ng;
-  if ((rc = ensure_buffer(sg[0], (size_t)count * nbytes)) || (rc = ensure_buffer(sg[3], count)) ||
-      (rc = ensure_buffer(sv[0], (size_t)count * W * 4)) || (rc = ensure_buffer(sv[1], (size_t)count * 4)) ||
-      (rc = ensure_buffer(sv[2], misc_words * 4)))
-    return rc;
-  std::vector<uint32_t> misc(misc_words, 0);
-  std::copy(tt.prod.begin(), tt.prod.end(), misc.begin() + off_prod);
-  std::copy(tt.start.begin(), tt.start.end(), misc.begin() + off_start);
-  std::copy(tt.primes.begin(), tt.primes.end(), misc.begin() + off_primes);
-  std::memcpy(misc.data() + off_inv, tt.inv.data(), ng * 8);
-  if ((rc = h2d(sv[2].ptr, misc.data(), misc_words * 4, l.st)) ||
-      (rc = h2d(sg[0].ptr, raw, (size_t)count * nbytes, l.st)))
-    return rc;
-  uint32_t* dm = (uint32_t*)sv[2].ptr;
-  mpcx::SieveArgs sa{};
-  sa.raw = (const uint8_t*)sg[0].ptr;
-  sa.nbytes = nbytes;
-  sa.count = count;
-  sa.q_bits = q_bits;
-  sa.tprod = dm + off_prod;
-  sa.tstart = dm + off_start;
-  sa.tprimes = dm + off_primes;
-  sa.tinv = (const uint64_t*)(dm + off_inv);
-  sa.ngroups = (uint32_t)ng;
-  sa.out_p = (uint32_t*)sv[0].ptr;
-  sa.out_idx = (uint32_t*)sv[1].ptr;
-  sa.out_count = dm;
-  hipError_t e = mpcx_launch_sieve(&sa, l.st);
-  if (e != hipSuccess) return hip_fail(e, "launch k_sieve");
-  mpcx::FermatArgs fa{};
-  fa.p = sa.out_p;
-  fa.ok = (uint8_t*)sg[3].ptr;
-  fa.count = count;
-  fa.p_words = W;
-  fa.count_dev = dm;
-  e = mpcx_launch_fermat2(&fa, (count + 63) / 64, l.st);
-  if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
-  uint32_t n = 0;
-  if ((rc = d2h_sync(&n, dm, 4, l.st))) return rc;
-  if (n > count) return fail(MPCX_EHIP, "sieve survivor count %u > %u", n, count);
-  std::vector<uint32_t> idx(n);
-  std::vector<uint8_t> ok(n);
-  if (n) {
-    e = hipMemcpyAsync(idx.data(), sa.out_idx, (size_t)n * 4, hipMemcpyDeviceToHost, l.st);
-    if (e != hipSuccess) return hip_fail(e, "copy survivors");
-    if ((rc = d2h_sync(ok.data(), fa.ok, n, l.st))) return rc;
-  }
-  // stream order
-  std::vector<uint32_t> ord(n);
-  for (uint32_t j = 0; j < n; ++j) ord[j] = j;
-  std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return idx[x] < idx[y]; });
-  for (uint32_t j = 0; j < n; ++j) {
-    idx_out[j] = idx[ord[j]];
-    ok_out[j] = ok[ord[j]];
-  }
-  *n_out = n;
-  return MPCX_OK;
+  // one device per candidate batch (round-robin): a search keeps several
+  // batches in flight on different GPUs (csrc/host/safeprime.cpp)
+  return run_sliced(count, 0, [&](int di, uint32_t, uint32_t) {
+    std::unique_lock<std::mutex> lk;
+    Lane& l = acquire_lane(g_devs[di], lk);
+    int rc;
+    if ((rc = lane_stream(l))) return rc;
+    Staging *sg = l.stage, *sv = l.sieve;
+    constexpr uint32_t W = MPCX_SIEVE_MAX_BYTES / 4;
+    const size_t ng = tt.prod.size();
+    // misc buffer: counter | prod | start | primes | inv (8-byte aligned)
+    const size_t off_prod = 2, off_start = off_prod + ng, off_primes = off_start + tt.start.size();
+    const size_t off_inv = (off_primes + tt.primes.size() + 1) / 2 * 2;
+    const size_t misc_words = off_inv + 2 * ng;
+    if ((rc = ensure_buffer(sg[0], (size_t)count * nbytes)) || (rc = ensure_buffer(sg[3], count)) ||
+        (rc = ensure_buffer(sv[0], (size_t)count * W * 4)) || (rc = ensure_buffer(sv[1], (size_t)count * 4)) ||
+        (rc = ensure_buffer(sv[2], misc_words * 4)))
+      return rc;
+    std::vector<uint32_t> misc(misc_words, 0);
+    std::copy(tt.prod.begin(), tt.prod.end(), misc.begin() + off_prod);
+    std::copy(tt.start.begin(), tt.start.end(), misc.begin() + off_start);
+    std::copy(tt.primes.begin(), tt.primes.end(), misc.begin() + off_primes);
+    std::memcpy(misc.data() + off_inv, tt.inv.data(), ng * 8);
+    if ((rc = h2d(sv[2].ptr, misc.data(), misc_words * 4, l.st)) ||
+        (rc = h2d(sg[0].ptr, raw, (size_t)count * nbytes, l.st)))
+      return rc;
+    uint32_t* dm = (uint32_t*)sv[2].ptr;
+    mpcx::SieveArgs sa{};
+    sa.raw = (const uint8_t*)sg[0].ptr;
+    sa.nbytes = nbytes;
+    sa.count = count;
+    sa.q_bits = q_bits;
+    sa.tprod = dm + off_prod;
+    sa.tstart = dm + off_start;
+    sa.tprimes = dm + off_primes;
+    sa.tinv = (const uint64_t*)(dm + off_inv);
+    sa.ngroups = (uint32_t)ng;
+    sa.out_p = (uint32_t*)sv[0].ptr;
+    sa.out_idx = (uint32_t*)sv[1].ptr;
+    sa.out_count = dm;
+    hipError_t e = mpcx_launch_sieve(&sa, l.st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_sieve");
+    mpcx::FermatArgs fa{};
+    fa.p = sa.out_p;
+    fa.ok = (uint8_t*)sg[3].ptr;
+    fa.count = count;
+    fa.p_words = W;
+    fa.count_dev = dm;
+    e = mpcx_launch_fermat2(&fa, (count + 63) / 64, l.st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
+    uint32_t n = 0;
+    if ((rc = d2h_sync(&n, dm, 4, l.st))) return rc;
+    if (n > count) return fail(MPCX_EHIP, "sieve survivor count %u > %u", n, count);
+    std::vector<uint32_t> idx(n);
+    std::vector<uint8_t> ok(n);
+    if (n) {
+      e = hipMemcpyAsync(idx.data(), sa.out_idx, (size_t)n * 4, hipMemcpyDeviceToHost, l.st);
+      if (e != hipSuccess) return hip_fail(e, "copy survivors");
+      if ((rc = d2h_sync(ok.data(), fa.ok, n, l.st))) return rc;
+    }
+    // stream order
+    std::vector<uint32_t> ord(n);
+    for (uint32_t j = 0; j < n; ++j) ord[j] = j;
+    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return idx[x] < idx[y]; });
+    for (uint32_t j = 0; j < n; ++j) {
+      idx_out[j] = idx[ord[j]];
+      ok_out[j] = ok[ord[j]];
+    }
+    *n_out = n;
+    return MPCX_OK;
+  });
 }

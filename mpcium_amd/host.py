@@ -17,9 +17,43 @@ _vp, _u32, _u64, _i = ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.
 
 RAND_FN = ctypes.CFUNCTYPE(None, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint8), ctypes.c_size_t)
 
+
+class ReaderT(ctypes.Structure):
+    """mpcxh_reader_t: one session's io.Reader (fn, ctx) or CounterDRBG seed."""
+    _fields_ = [("fn", _vp), ("ctx", _vp), ("seed", _u64)]
+
+
+class Readers:
+    """A ctypes array of mpcxh_reader_t for a batch. Each source is an int
+    (the CounterDRBG seed) or an object with .read(n) -> bytes (an io.Reader,
+    called back from libmpcx_host's worker threads). Keep the object alive
+    for the duration of the call."""
+
+    def __init__(self, sources):
+        self._cbs = []
+        arr = (ReaderT * max(1, len(sources)))()
+        for i, s in enumerate(sources):
+            if isinstance(s, (int, np.integer)):
+                arr[i].seed = int(s) & 0xFFFFFFFFFFFFFFFF
+            else:
+                def read(_ctx, buf, n, _s=s):
+                    b = _s.read(n)
+                    if len(b) != n:
+                        raise ValueError("short read")
+                    ctypes.memmove(buf, b, n)
+                cb = RAND_FN(read)
+                self._cbs.append(cb)
+                arr[i].fn = ctypes.cast(cb, _vp)
+        self.arr = arr
+
+    @property
+    def ptr(self):
+        return ctypes.addressof(self.arr)
+
 SIGNATURES = [
     ("mpcxh_last_error", ctypes.c_char_p, []),
     ("mpcxh_init", _i, [_i]),
+    ("mpcxh_init_devices", _i, [_i]),
     ("mpcxh_modint_exp_batch", _i, [_vp, _u32, _u32, _vp, _u32, _vp, _vp, _u32, _vp, _i, _vp, _u32, _vp]),
     ("mpcxh_paillier_encrypt_batch", _i, [_vp, _u32, _u32, _vp, _u32, _vp, _vp, _u32, _vp, _u32, _vp]),
     ("mpcxh_paillier_homomult_batch", _i, [_vp, _u32, _u32, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _u32, _vp]),
@@ -58,6 +92,11 @@ def _check(rc):
 
 def init(device: int = 0):
     _check(lib().mpcxh_init(device))
+
+
+def init_devices(n_gpus: int = 0):
+    """Bind GPUs 0..n_gpus-1 (0: every visible GPU) in this process."""
+    _check(lib().mpcxh_init_devices(n_gpus))
 
 
 def _signed(vals: Sequence[int]) -> Tuple[np.ndarray, np.ndarray]:

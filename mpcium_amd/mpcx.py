@@ -27,6 +27,10 @@ SIGNATURES = [
     ("mpcx_last_error", ctypes.c_char_p, []),
     ("mpcx_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     ("mpcx_init", ctypes.c_int, [ctypes.c_int]),
+    ("mpcx_init_devices", ctypes.c_int, [ctypes.c_int]),
+    ("mpcx_bound_devices", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
+    ("mpcx_select_device", ctypes.c_int, [ctypes.c_int]),
+    ("mpcx_partition", ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, _u32p, _u32p, _u32p]),
     ("mpcx_shutdown", ctypes.c_int, []),
     ("mpcx_modulus_register", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(_vp)]),
     ("mpcx_modulus_release", ctypes.c_int, [_vp]),
@@ -41,6 +45,11 @@ SIGNATURES = [
     ("mpcx_modexp_mul_batch_device", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp,
                                                     ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, _vp,
                                                     ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    ("mpcx_modexp_submit", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
+                                          ctypes.c_int, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
+                                          ctypes.POINTER(_vp)]),
+    ("mpcx_job_test", ctypes.c_int, [_vp, ctypes.POINTER(ctypes.c_int)]),
+    ("mpcx_job_wait", ctypes.c_int, [_vp]),
     ("mpcx_mulmod_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp,
                                          ctypes.c_uint32]),
     ("mpcx_fermat2_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
@@ -60,6 +69,7 @@ SIGNATURES = [
     ("mpcx_stream_create", ctypes.c_int, [ctypes.POINTER(_vp)]),
     ("mpcx_stream_destroy", ctypes.c_int, [_vp]),
     ("mpcx_stream_sync", ctypes.c_int, [_vp]),
+    ("mpcx_sync", ctypes.c_int, [_vp]),
 ]
 
 
@@ -100,6 +110,31 @@ def device_count() -> int:
 
 def init(device: int = 0):
     _check(lib().mpcx_init(device))
+
+
+def init_devices(n_gpus: int = 0):
+    """Bind GPUs 0..n_gpus-1 (0: all visible) in this process."""
+    _check(lib().mpcx_init_devices(n_gpus))
+
+
+def bound_devices() -> List[int]:
+    n = ctypes.c_int(0)
+    ords = (ctypes.c_int * 16)()
+    _check(lib().mpcx_bound_devices(ctypes.byref(n), ords, 16))
+    return list(ords[:n.value])
+
+
+def partition(count: int, n_devices: int, min_slice: int = 4096):
+    """[(first, n)] slice plan of a host-buffer batch over n_devices GPUs."""
+    f = (ctypes.c_uint32 * 16)()
+    n = (ctypes.c_uint32 * 16)()
+    k = ctypes.c_uint32(0)
+    _check(lib().mpcx_partition(count, n_devices, min_slice, f, n, ctypes.byref(k)))
+    return [(f[i], n[i]) for i in range(k.value)]
+
+
+def select_device(index: int):
+    _check(lib().mpcx_select_device(index))
 
 
 def set_option(key: str, value: int):
@@ -222,6 +257,17 @@ class Modulus:
         ew = max(nwords(e) for e in exps)
         return ints_to_words(exps, ew), False
 
+    def submit(self, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> "Job":
+        """Asynchronous [b^e mod m] (mpcx_modexp_submit); Job.wait() -> list."""
+        B = self._operands(bases, "bases")
+        E, shared = self._exps(exps, len(bases))
+        out = np.zeros((len(bases), self.words), dtype="<u4")
+        h = _vp()
+        _check(lib().mpcx_modexp_submit(self._h, len(bases), B.ctypes.data, B.shape[1],
+                                        E.ctypes.data if E.size else None, E.shape[-1] if E.size else 0,
+                                        1 if shared else 0, None, 0, out.ctypes.data, self.words, ctypes.byref(h)))
+        return Job(h, (B, E, out), lambda: words_to_ints(out))
+
     def exp(self, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> List[int]:
         """[b^e mod m] for non-negative ints; `exps` is one shared int or one per base."""
         if len(bases) == 0:
@@ -229,6 +275,27 @@ class Modulus:
         B = self._operands(bases, "bases")
         E, shared = self._exps(exps, len(bases))
         return words_to_ints(self.exp_words(B, E, shared))
+
+
+class Job:
+    """An mpcx_job_t: keeps the submitted buffers alive until wait()."""
+
+    def __init__(self, h, bufs, result):
+        self._h, self._bufs, self._result = h, bufs, result
+
+    def done(self) -> bool:
+        d = ctypes.c_int(0)
+        _check(lib().mpcx_job_test(self._h, ctypes.byref(d)))
+        return bool(d.value)
+
+    def wait(self):
+        h, self._h = self._h, None
+        if h is None:
+            raise RuntimeError("job already waited")
+        _check(lib().mpcx_job_wait(h))
+        r = self._result()
+        self._bufs = None
+        return r
 
 
 class FixedBase:

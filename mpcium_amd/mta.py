@@ -142,17 +142,19 @@ def _sessions(ss: Sequence[bytes]) -> Tuple[np.ndarray, int]:
     return np.frombuffer(b"".join(ss), dtype=np.uint8).copy(), n
 
 
-def alice_init(pkA_N: int, a: Sequence[int], dlnB: Dict[str, int], seeds: Sequence[int]):
-    """AliceInit for a batch -> (cA list, RangeProofAlice list, err list)."""
+def alice_init(pkA_N: int, a: Sequence[int], dlnB: Dict[str, int], seeds: Sequence):
+    """AliceInit for a batch -> (cA list, RangeProofAlice list, err list).
+    seeds[i]: session i's io.Reader -- an int (CounterDRBG seed) or an object
+    with .read(n)."""
     k = _Keep()
     pk, dln = _paillier(k, pkA_N), _dln(k, dlnB)
     n = len(a)
     A = _col(a)
-    S = np.array(seeds, dtype=np.uint64)
+    S = _host.Readers(seeds)
     cA = np.zeros((n, W), dtype="<u4")
     pf = np.zeros((n, 6 * W), dtype="<u4")
     err = np.zeros(n, dtype=np.uint8)
-    _check(lib().mpcxh_mta_alice_init_batch(W, ctypes.byref(pk), ctypes.byref(dln), n, A.ctypes.data, S.ctypes.data,
+    _check(lib().mpcxh_mta_alice_init_batch(W, ctypes.byref(pk), ctypes.byref(dln), n, A.ctypes.data, S.ptr,
                                             cA.ctypes.data, pf.ctypes.data, err.ctypes.data))
     return words_to_ints(cA), _proofs(pf, RANGE_FIELDS, n), [int(e) for e in err]
 
@@ -169,7 +171,7 @@ def verify_range_alice(pk_N: int, dln_: Dict[str, int], c: Sequence[int], pfs: S
 
 
 def bob_mid(sessions: Sequence[bytes], pkA_N: int, pfA: Sequence[dict], b: Sequence[int], cA: Sequence[int],
-            dlnA: Dict[str, int], dlnB: Dict[str, int], seeds: Sequence[int],
+            dlnA: Dict[str, int], dlnB: Dict[str, int], seeds: Sequence,
             B: Optional[Sequence[Tuple[int, int]]] = None):
     """BobMid (B None) / BobMidWC -> (beta, cB, betaPrm, ProofBob[WC], err) lists."""
     k = _Keep()
@@ -178,12 +180,12 @@ def bob_mid(sessions: Sequence[bytes], pkA_N: int, pfA: Sequence[dict], b: Seque
     ss, sl = _sessions(sessions)
     PA, Bw, CA = _proof_buf(pfA, RANGE_FIELDS, 6), _col(b), _col(cA)
     Bp = _points(B)
-    S = np.array(seeds, dtype=np.uint64)
+    S = _host.Readers(seeds)
     beta, cB, bp = (np.zeros((n, W), dtype="<u4") for _ in range(3))
     pfB = np.zeros((n, 12 * W), dtype="<u4")
     err = np.zeros(n, dtype=np.uint8)
     _check(lib().mpcxh_mta_bob_mid_batch(W, ss.ctypes.data, sl, ctypes.byref(pk), ctypes.byref(da), ctypes.byref(db),
-                                         n, PA.ctypes.data, Bw.ctypes.data, CA.ctypes.data, _ptr(Bp), S.ctypes.data,
+                                         n, PA.ctypes.data, Bw.ctypes.data, CA.ctypes.data, _ptr(Bp), S.ptr,
                                          beta.ctypes.data, cB.ctypes.data, bp.ctypes.data, pfB.ctypes.data,
                                          err.ctypes.data))
     return (words_to_ints(beta), words_to_ints(cB), words_to_ints(bp), _proofs(pfB, BOB_FIELDS, n, B is not None),

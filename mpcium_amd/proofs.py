@@ -67,10 +67,10 @@ def dln_prove(h1: int, h2: int, x: int, p: int, q: int, N: int, seeds: Sequence[
     """NewDLNProof for len(seeds) proofs -> [{"Alpha": [...], "T": [...]}]."""
     n = len(seeds)
     args = [_one(v) for v in (h1, h2, x, p, q, N)]
-    S = np.array(seeds, dtype=np.uint64)
+    S = _host.Readers(seeds)
     al = np.zeros((n, DLN_ITERATIONS * W), dtype="<u4")
     t = np.zeros_like(al)
-    _host._check(lib().mpcxh_dln_prove_batch(W, *[a.ctypes.data for a in args], n, S.ctypes.data, al.ctypes.data,
+    _host._check(lib().mpcxh_dln_prove_batch(W, *[a.ctypes.data for a in args], n, S.ptr, al.ctypes.data,
                                              t.ctypes.data))
     return [{"Alpha": a, "T": b} for a, b in zip(_rows(al, n, DLN_ITERATIONS), _rows(t, n, DLN_ITERATIONS))]
 
@@ -90,10 +90,10 @@ def mod_prove(sessions: Sequence[bytes], N: int, P: int, Q: int, seeds: Sequence
     n = len(seeds)
     ss, sl = _sessions(sessions)
     args = [_one(v) for v in (N, P, Q)]
-    S = np.array(seeds, dtype=np.uint64)
+    S = _host.Readers(seeds)
     Wv, A, B = (np.zeros((n, W), dtype="<u4") for _ in range(3))
     X, Z = (np.zeros((n, MOD_ITERATIONS * W), dtype="<u4") for _ in range(2))
-    _host._check(lib().mpcxh_mod_prove_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n, S.ctypes.data,
+    _host._check(lib().mpcxh_mod_prove_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n, S.ptr,
                                              Wv.ctypes.data, X.ctypes.data, A.ctypes.data, B.ctypes.data,
                                              Z.ctypes.data))
     return [{"W": w, "X": x, "A": a, "B": b, "Z": z} for w, x, a, b, z in
@@ -119,10 +119,10 @@ def fac_prove(sessions: Sequence[bytes], N0: int, NCap: int, s: int, t: int, N0p
     n = len(seeds)
     ss, sl = _sessions(sessions)
     args = [_one(v) for v in (N0, NCap, s, t, N0p, N0q)]
-    S = np.array(seeds, dtype=np.uint64)
+    S = _host.Readers(seeds)
     pf = np.zeros((n, len(FAC_FIELDS) * W), dtype="<u4")
     neg = np.zeros(n, dtype=np.uint8)
-    _host._check(lib().mpcxh_fac_prove_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n, S.ctypes.data,
+    _host._check(lib().mpcxh_fac_prove_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n, S.ptr,
                                              pf.ctypes.data, neg.ctypes.data))
     out = []
     for row, ng in zip(_rows(pf, n, len(FAC_FIELDS)), neg):

@@ -12,10 +12,13 @@
  *   nat.expNN                      go:src/math/big/nat.go    -> nat_expNN()
  *   nat.expNNMontgomery            go:src/math/big/nat.go    -> nat_expNNMontgomery()
  *   nat.montgomery (AMM, Gueron)   go:src/math/big/nat.go    -> nat_montgomery()
- * Go on amd64 uses 64-bit Words; this restatement uses 32-bit words, which
- * changes the number of Montgomery steps per word but not the integer result
- * (the value x^y mod m is unique). The single-word-exponent square-and-multiply
- * branch of expNN is taken, as on amd64, when y < 2^64.
+ * Word size: built twice by oracle/Makefile. libgomodexp.so uses 32-bit words
+ * (the parity oracle of the tests); libgomodexp64.so (-DGOMODEXP_W64) uses
+ * 64-bit Words with 128-bit products, Go's amd64 configuration (_W = 64,
+ * arith_amd64.s addMulVVW = MULQ/ADC chains), and is the CPU baseline of
+ * bench.py. The word size changes the number of Montgomery steps per word but
+ * not the integer result (x^y mod m is unique). The single-word-exponent
+ * square-and-multiply branch of expNN is taken, as on amd64, when y < 2^64.
  *
  * Parity status: the reference (Go + tss-lib) cannot be built or run in this
  * image (no Go toolchain, tss-lib absent). This restatement is
@@ -29,9 +32,21 @@
 #include <stdlib.h>
 #include <string.h>
 
+#ifdef GOMODEXP_W64
+typedef uint64_t Word;
+typedef unsigned __int128 DWord;
+typedef __int128 SDWord;
+#define WBITS 64
+#define CLZ(x) __builtin_clzll(x)
+#define EXPORT static __attribute__((unused))
+#else
 typedef uint32_t Word;
 typedef uint64_t DWord;
+typedef int64_t SDWord;
 #define WBITS 32
+#define CLZ(x) __builtin_clz(x)
+#define EXPORT
+#endif
 
 /* ---------- nat helpers (go:src/math/big/arith.go, nat.go) ---------- */
 
@@ -56,7 +71,7 @@ static Word subVV(Word* z, const Word* x, const Word* y, int n) {
   for (int i = 0; i < n; i++) {
     DWord d = (DWord)x[i] - y[i] - c;
     z[i] = (Word)d;
-    c = (Word)((d >> 63) & 1);
+    c = (Word)((d >> (2 * WBITS - 1)) & 1);
   }
   return c;
 }
@@ -67,7 +82,7 @@ static Word addMulVVW(Word* z, const Word* x, Word y, int n) {
   for (int i = 0; i < n; i++) {
     DWord t = (DWord)x[i] * y + z[i] + c;
     z[i] = (Word)t;
-    c = (Word)(t >> 32);
+    c = (Word)(t >> WBITS);
   }
   return c;
 }
@@ -83,51 +98,51 @@ static void nat_rem(Word* r, const Word* u_in, int nu, const Word* v_in, int nv)
   }
   if (nv == 1) {
     DWord rem = 0;
-    for (int i = nu - 1; i >= 0; i--) rem = ((rem << 32) | u_in[i]) % v_in[0];
+    for (int i = nu - 1; i >= 0; i--) rem = ((rem << WBITS) | u_in[i]) % v_in[0];
     r[0] = (Word)rem;
     return;
   }
-  int s = __builtin_clz(v_in[nv - 1]);
+  int s = CLZ(v_in[nv - 1]);
   Word* v = (Word*)calloc(nv, sizeof(Word));
   Word* u = (Word*)calloc(nu + 1, sizeof(Word));
-  for (int i = nv - 1; i > 0; i--) v[i] = s ? (v_in[i] << s) | (v_in[i - 1] >> (32 - s)) : v_in[i];
+  for (int i = nv - 1; i > 0; i--) v[i] = s ? (v_in[i] << s) | (v_in[i - 1] >> (WBITS - s)) : v_in[i];
   v[0] = v_in[0] << s;
-  u[nu] = s ? u_in[nu - 1] >> (32 - s) : 0;
-  for (int i = nu - 1; i > 0; i--) u[i] = s ? (u_in[i] << s) | (u_in[i - 1] >> (32 - s)) : u_in[i];
+  u[nu] = s ? u_in[nu - 1] >> (WBITS - s) : 0;
+  for (int i = nu - 1; i > 0; i--) u[i] = s ? (u_in[i] << s) | (u_in[i - 1] >> (WBITS - s)) : u_in[i];
   u[0] = u_in[0] << s;
   for (int j = nu - nv; j >= 0; j--) {
-    DWord num = ((DWord)u[j + nv] << 32) | u[j + nv - 1];
+    DWord num = ((DWord)u[j + nv] << WBITS) | u[j + nv - 1];
     DWord qhat = num / v[nv - 1];
     DWord rhat = num % v[nv - 1];
-    while (qhat >= ((DWord)1 << 32) ||
-           qhat * v[nv - 2] > ((rhat << 32) | u[j + nv - 2])) {
+    while (qhat >= ((DWord)1 << WBITS) ||
+           qhat * v[nv - 2] > ((rhat << WBITS) | u[j + nv - 2])) {
       qhat--;
       rhat += v[nv - 1];
-      if (rhat >= ((DWord)1 << 32)) break;
+      if (rhat >= ((DWord)1 << WBITS)) break;
     }
     /* multiply and subtract */
-    int64_t borrow = 0;
+    SDWord borrow = 0;
     DWord carry = 0;
     for (int i = 0; i < nv; i++) {
       DWord p = qhat * v[i] + carry;
-      carry = p >> 32;
-      int64_t t = (int64_t)u[i + j] - (int64_t)(Word)p + borrow;
+      carry = p >> WBITS;
+      SDWord t = (SDWord)u[i + j] - (SDWord)(Word)p + borrow;
       u[i + j] = (Word)t;
-      borrow = t >> 32;
+      borrow = t >> WBITS;
     }
-    int64_t t = (int64_t)u[j + nv] - (int64_t)carry + borrow;
+    SDWord t = (SDWord)u[j + nv] - (SDWord)carry + borrow;
     u[j + nv] = (Word)t;
     if (t < 0) { /* add back */
       DWord c = 0;
       for (int i = 0; i < nv; i++) {
         DWord sum = (DWord)u[i + j] + v[i] + c;
         u[i + j] = (Word)sum;
-        c = sum >> 32;
+        c = sum >> WBITS;
       }
       u[j + nv] += (Word)c;
     }
   }
-  for (int i = 0; i < nv; i++) r[i] = s ? (u[i] >> s) | (u[i + 1] << (32 - s)) : u[i];
+  for (int i = 0; i < nv; i++) r[i] = s ? (u[i] >> s) | (u[i + 1] << (WBITS - s)) : u[i];
   free(u);
   free(v);
 }
@@ -251,7 +266,7 @@ static int nat_expNN(Word* z, const Word* x, int nx, const Word* y, int ny, cons
     nat_rem(z, x, nx, m, nm);
     return nat_norm(z, nm);
   }
-  int multiword = ny > 2; /* amd64 Words are 64-bit: len(y) > 1 <=> y >= 2^64 */
+  int multiword = ny > 64 / WBITS; /* amd64 Words are 64-bit: len(y) > 1 <=> y >= 2^64 */
   if (multiword && (m[0] & 1)) {
     nat_expNNMontgomery(z, x, nx, y, ny, m, nm);
     return nat_norm(z, nm);
@@ -263,9 +278,9 @@ static int nat_expNN(Word* z, const Word* x, int nx, const Word* y, int ny, cons
   nat_rem(xr, x, nx, m, nm);
   memcpy(zc, xr, sizeof(Word) * nm);
   int top = ny - 1;
-  int nb = 32 - __builtin_clz(y[top]);
+  int nb = WBITS - CLZ(y[top]);
   for (int i = top; i >= 0; i--) {
-    int start = (i == top) ? nb - 2 : 31;
+    int start = (i == top) ? nb - 2 : WBITS - 1;
     for (int b = start; b >= 0; b--) {
       nat_mul(prod, zc, nm, zc, nm);
       nat_rem(zc, prod, 2 * nm, m, nm);
@@ -283,7 +298,7 @@ static int nat_expNN(Word* z, const Word* x, int nx, const Word* y, int ny, cons
 /* ---------- exported entry points (test infrastructure) ---------- */
 
 /* Unsigned x^y mod m with Go expNN semantics. out has nm words. Returns 0, or -1 if m == 0. */
-int gomodexp_expnn(Word* out, const Word* x, int nx, const Word* y, int ny, const Word* m, int nm) {
+EXPORT int gomodexp_expnn(Word* out, const Word* x, int nx, const Word* y, int ny, const Word* m, int nm) {
   if (nat_norm(m, nm) == 0) return -1;
   nat_expNN(out, x, nx, y, ny, m, nm);
   return 0;
@@ -291,14 +306,14 @@ int gomodexp_expnn(Word* out, const Word* x, int nx, const Word* y, int ny, cons
 
 /* Force the Montgomery path (odd m), used by the CPU baseline: same 4-bit-window
  * AMM algorithm Go runs for multi-word exponents. */
-int gomodexp_montgomery(Word* out, const Word* x, int nx, const Word* y, int ny, const Word* m, int nm) {
+EXPORT int gomodexp_montgomery(Word* out, const Word* x, int nx, const Word* y, int ny, const Word* m, int nm) {
   if (nm <= 0 || (m[0] & 1) == 0) return -1;
   nat_expNNMontgomery(out, x, nx, y, ny, m, nm);
   return 0;
 }
 
 /* Batched Montgomery path with a shared exponent; operands are count x nm words. */
-int gomodexp_montgomery_batch(Word* out, const Word* x, int count, const Word* y, int ny, const Word* m, int nm) {
+EXPORT int gomodexp_montgomery_batch(Word* out, const Word* x, int count, const Word* y, int ny, const Word* m, int nm) {
   for (int i = 0; i < count; i++) {
     int rc = gomodexp_montgomery(out + (size_t)i * nm, x + (size_t)i * nm, nm, y, ny, m, nm);
     if (rc) return rc;
@@ -307,3 +322,39 @@ int gomodexp_montgomery_batch(Word* out, const Word* x, int count, const Word* y
 }
 
 int gomodexp_word_bits(void) { return WBITS; }
+
+#ifdef GOMODEXP_W64
+/* 64-bit-Word build: the same entry points over little-endian 32-bit words
+ * (packed into 64-bit Words on entry, unpacked on exit; n32 = 32-bit words). */
+static Word* pack64(const uint32_t* x, int n32, int* n64) {
+  *n64 = (n32 + 1) / 2;
+  Word* w = (Word*)calloc((size_t)(*n64 > 0 ? *n64 : 1), sizeof(Word));
+  for (int i = 0; i < n32; i++) w[i / 2] |= (Word)x[i] << (32 * (i % 2));
+  return w;
+}
+
+static void unpack64(uint32_t* out, int n32, const Word* w) {
+  for (int i = 0; i < n32; i++) out[i] = (uint32_t)(w[i / 2] >> (32 * (i % 2)));
+}
+
+int gomodexp64_montgomery(uint32_t* out, const uint32_t* x, int nx, const uint32_t* y, int ny, const uint32_t* m,
+                          int nm) {
+  int ax, ay, am;
+  Word *X = pack64(x, nx, &ax), *Y = pack64(y, ny, &ay), *M = pack64(m, nm, &am);
+  Word* Z = (Word*)calloc((size_t)am, sizeof(Word));
+  int rc = gomodexp_montgomery(Z, X, ax, Y, ay, M, am);
+  if (rc == 0) unpack64(out, nm, Z);
+  free(X); free(Y); free(M); free(Z);
+  return rc;
+}
+
+int gomodexp64_expnn(uint32_t* out, const uint32_t* x, int nx, const uint32_t* y, int ny, const uint32_t* m, int nm) {
+  int ax, ay, am;
+  Word *X = pack64(x, nx, &ax), *Y = pack64(y, ny, &ay), *M = pack64(m, nm, &am);
+  Word* Z = (Word*)calloc((size_t)am, sizeof(Word));
+  int rc = gomodexp_expnn(Z, X, ax, Y, ay, M, am);
+  if (rc == 0) unpack64(out, nm, Z);
+  free(X); free(Y); free(M); free(Z);
+  return rc;
+}
+#endif

@@ -61,3 +61,25 @@ def test_missing_library_raises(monkeypatch, tmp_path):
     monkeypatch.setattr(mpcx, "_lib", None)
     with pytest.raises(mpcx.MpcxError):
         mpcx.lib()
+
+
+def test_device_partition_plan(libs):
+    """The host-buffer batch split across a node's GPUs (mpcx_partition, the
+    plan run_sliced executes): contiguous, disjoint, covering, balanced, and
+    one range when the slices would be smaller than min_slice."""
+    from mpcium_amd import mpcx
+    for count in (0, 1, 4095, 8191, 8192, 65536, 65537, 100003):
+        for ndev in (1, 2, 3, 4, 8):
+            for mn in (0, 1, 4096):
+                plan = mpcx.partition(count, ndev, mn)
+                assert 1 <= len(plan) <= ndev
+                assert plan[0][0] == 0 and sum(n for _, n in plan) == count
+                for (f0, n0), (f1, _) in zip(plan, plan[1:]):
+                    assert f0 + n0 == f1
+                if mn == 0 or count < 2 * mn:
+                    assert len(plan) == 1
+                else:
+                    assert len(plan) == min(ndev, count // mn)
+                    assert max(n for _, n in plan) - min(n for _, n in plan) <= len(plan)
+    with pytest.raises(mpcx.MpcxError):
+        mpcx.partition(10, 0, 1)

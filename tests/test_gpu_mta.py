@@ -165,3 +165,40 @@ def test_random_batch_relations(mta, nodes):
         alpha, err = mta.alice_end(ss, (A["N"], A["LambdaN"], A["P"], A["Q"]), pfB, dln(A, own=True), cA, cB, B=Bp)
         assert err == [0] * n
         assert [(x + y) % q for x, y in zip(alpha, beta)] == [x * y % q for x, y in zip(a, b)]
+
+
+def test_golden_sessions_through_reader_callbacks(mta, nodes, vec):
+    """The same golden sessions with every random draw made through the
+    io.Reader callback (mpcxh_reader_t.fn -> a Python reader object called from
+    libmpcx_host's worker threads), as a Go integration threads tss-lib's
+    party reader through the batch entry points."""
+    A, B = nodes[0], nodes[1]
+    n = len(vec)
+    a = [H(v["a"]) for v in vec]
+    cA, pfA, err = mta.alice_init(A["N"], a, dln(B), [T.Reader(v["seed_a"]) for v in vec])
+    assert err == [0] * n
+    assert cA == [H(v["cA"]) for v in vec]
+    assert pfA == [hx(v["pfA"]) for v in vec]
+    ss = [bytes.fromhex(v["session"]) for v in vec]
+    Bpts = [(H(v["Bx"]), H(v["By"])) for v in vec]
+    beta, cB, bp, pfB, err = mta.bob_mid(ss, A["N"], pfA, [H(v["wB"]) for v in vec], cA, dln(A), dln(B, own=True),
+                                         [T.Reader(v["seed_bwc"]) for v in vec], B=Bpts)
+    assert err == [0] * n
+    assert cB == [H(v["bob_wc"]["cB"]) for v in vec]
+    assert pfB == [bob_pf(v["bob_wc"]["pf"], True) for v in vec]
+
+
+def test_overlong_exponent_does_not_fail_the_batch(mta, nodes, vec, monkeypatch):
+    """a peer-supplied exponent far above any protocol bound (a
+    70,000-bit S2 in one of 80 range proofs) takes the per-operand path; the
+    honest proofs of the same batch still verify and the bad one is
+    rejected -- one adversarial input never throws for the whole batch."""
+    A, B = nodes[0], nodes[1]
+    v = vec[0]
+    c, pf = H(v["cA"]), hx(v["pfA"])
+    bad = dict(pf)
+    bad["S2"] = (1 << 70000) + 12345
+    monkeypatch.setattr(mta, "W", 2240)  # integer width (words) that carries a 70,000-bit field
+    pfs = [pf] * 79 + [bad]
+    ok = mta.verify_range_alice(A["N"], dln(B), [c] * 80, pfs)
+    assert ok == [True] * 79 + [False]

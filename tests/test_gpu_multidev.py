@@ -1,0 +1,122 @@
+"""GPU tests of the one-process-many-GPUs boundary (include/mpcx.h
+mpcx_init_devices / mpcx_select_device / mpcx_modexp_submit): every visible
+GPU bound in this process (one on the test box), batches split by the
+partition plan with forced small slices, asynchronous jobs, and two
+device-buffer calls on different streams in flight at once (each stream has
+its own workspace)."""
+import numpy as np
+import pytest
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def mx(gpu):
+    from mpcium_amd import mpcx
+    mpcx.init_devices(0)
+    return mpcx
+
+
+def _key():
+    k = load_golden("paillier_key_2048.json")
+    return int(k["N"], 16)
+
+
+def test_bound_devices(mx):
+    devs = mx.bound_devices()
+    assert len(devs) == mx.device_count() and devs == list(range(len(devs)))
+    mx.select_device(0)
+    with pytest.raises(mx.MpcxError):
+        mx.select_device(len(devs))
+
+
+def test_split_batches_match_pow(mx):
+    """Small device_split_min forces multi-slice plans (one slice per bound
+    device); results are gathered in operand order."""
+    import random
+    N = _key()
+    N2 = N * N
+    rng = random.Random(5)
+    mod = mx.Modulus(N2)
+    try:
+        xs = [rng.randrange(N2) for _ in range(97)]
+        es = [rng.getrandbits(rng.choice([64, 256, 700])) for _ in range(97)]
+        mx.set_option("device_split_min", 8)
+        try:
+            got = mod.exp(xs, es)
+            got_shared = mod.exp(xs, N)
+        finally:
+            mx.set_option("device_split_min", 4096)
+        assert got == [pow(x, e, N2) for x, e in zip(xs, es)]
+        assert got_shared == [pow(x, N, N2) for x in xs]
+    finally:
+        mod.release()
+
+
+def test_async_jobs(mx):
+    import random
+    N = _key()
+    rng = random.Random(6)
+    mod = mx.Modulus(N)
+    try:
+        batches = [[rng.randrange(N) for _ in range(50 + 13 * i)] for i in range(4)]
+        jobs = [mod.submit(b, N - 1 - i) for i, b in enumerate(batches)]
+        for i, (b, j) in enumerate(zip(batches, jobs)):
+            assert j.wait() == [pow(x, N - 1 - i, N) for x in b]
+    finally:
+        mod.release()
+
+
+def test_device_buffers_on_two_streams(mx):
+    """Two asynchronous device-buffer batches with different shared
+    exponents on two streams: each stream's schedule and window tables live in
+    its own workspace (a single shared workspace raced here)."""
+    import ctypes
+    N = _key()
+    mod = mx.Modulus(N)
+    L = mx.lib()
+    try:
+        count, w = 4096, mod.class_words
+        rng = np.random.default_rng(9)
+        host = rng.integers(0, 1 << 32, size=(count, w), dtype=np.uint64).astype(np.uint32)
+        host[:, -1] = 0
+        host[:, (N.bit_length() - 1) // 32:] = 0
+        e1, e2 = N, (N - 1) // 2
+        E1, E2 = mx.int_to_words(e1, mx.nwords(e1)), mx.int_to_words(e2, mx.nwords(e2))
+        ptr = {}
+        for name, nbytes in (("b", host.nbytes), ("e1", E1.nbytes), ("e2", E2.nbytes), ("o1", count * w * 4),
+                             ("o2", count * w * 4)):
+            p = ctypes.c_void_p()
+            mx._check(L.mpcx_dev_alloc(nbytes, ctypes.byref(p)))
+            ptr[name] = p
+        s1, s2 = ctypes.c_void_p(), ctypes.c_void_p()
+        mx._check(L.mpcx_stream_create(ctypes.byref(s1)))
+        mx._check(L.mpcx_stream_create(ctypes.byref(s2)))
+        try:
+            mx._check(L.mpcx_memcpy_h2d(ptr["b"], host.ctypes.data, host.nbytes))
+            mx._check(L.mpcx_memcpy_h2d(ptr["e1"], E1.ctypes.data, E1.nbytes))
+            mx._check(L.mpcx_memcpy_h2d(ptr["e2"], E2.ctypes.data, E2.nbytes))
+            for _ in range(2):
+                mx._check(L.mpcx_modexp_batch_device(mod.handle, count, ptr["b"], w, ptr["e1"], len(E1), 1,
+                                                     e1.bit_length(), ptr["o1"], w, s1))
+                mx._check(L.mpcx_modexp_batch_device(mod.handle, count, ptr["b"], w, ptr["e2"], len(E2), 1,
+                                                     e2.bit_length(), ptr["o2"], w, s2))
+            mx._check(L.mpcx_sync(s1))
+            mx._check(L.mpcx_sync(s2))
+            o1 = np.zeros((count, w), dtype="<u4")
+            o2 = np.zeros((count, w), dtype="<u4")
+            mx._check(L.mpcx_memcpy_d2h(o1.ctypes.data, ptr["o1"], o1.nbytes))
+            mx._check(L.mpcx_memcpy_d2h(o2.ctypes.data, ptr["o2"], o2.nbytes))
+        finally:
+            mx._check(L.mpcx_stream_destroy(s1))
+            mx._check(L.mpcx_stream_destroy(s2))
+            for p in ptr.values():
+                L.mpcx_dev_free(p)
+        xs = mx.words_to_ints(host)
+        r1, r2 = mx.words_to_ints(o1), mx.words_to_ints(o2)
+        for i in range(0, count, 97):
+            assert r1[i] == pow(xs[i], e1, N) and r2[i] == pow(xs[i], e2, N), i
+    finally:
+        mod.release()
