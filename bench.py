@@ -89,43 +89,118 @@ def synth_bases(N2: int, count: int, seed: int, words: int) -> np.ndarray:
     return x
 
 
-def cpu_baseline(N: int, seconds: float, threads: int):
-    """C restatement of Go expNNMontgomery (oracle/libgomodexp.so) on host cores."""
+def host_info() -> dict:
+    """The host the CPU baseline ran on: nproc, this process's CPU affinity,
+    the cgroup CPU quota (a GPU box gives a job a share of the machine:
+    os.cpu_count() shows every CPU, the quota what may run at once) and the CPU
+    model. usable_threads = min(affinity, quota): the CPU legs run there."""
+    info = {"nproc": os.cpu_count(), "affinity": len(os.sched_getaffinity(0)), "cgroup_quota_cpus": None,
+            "cpu_model": None}
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            a, b = f.read().split()[:2]
+        if a != "max":
+            info["cgroup_quota_cpus"] = int(a) / int(b)
+    except (OSError, ValueError):
+        pass
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    info["cpu_model"] = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    usable = info["affinity"]
+    if info["cgroup_quota_cpus"]:
+        usable = min(usable, max(1, int(info["cgroup_quota_cpus"])))
+    info["usable_threads"] = usable
+    return info
+
+
+def _time_threads(make_work, seconds: float, threads: int):
+    """Run make_work(t)() repeatedly on `threads` Python threads (the work is
+    a ctypes call that releases the GIL) for `seconds`; -> (ops, elapsed)."""
+    done = [0] * threads
+    stop = time.perf_counter() + seconds
+
+    def run(t):
+        w = make_work(t)
+        while time.perf_counter() < stop:
+            w()
+            done[t] += 1
+
+    t0 = time.perf_counter()
+    ths = [threading.Thread(target=run, args=(i,)) for i in range(threads)]
+    for th in ths:
+        th.start()
+    for th in ths:
+        th.join()
+    return sum(done), time.perf_counter() - t0
+
+
+def _one_and_all(make_work, seconds: float, info: dict):
+    """1-thread and all-usable-thread rates of the same work (seconds split 1:2)."""
+    n1, e1 = _time_threads(make_work, seconds / 3, 1)
+    thr = info["usable_threads"]
+    nn, en = _time_threads(make_work, 2 * seconds / 3, thr) if thr > 1 else (n1, e1)
+    return n1 / e1, nn / en, thr, (n1, e1, nn, en)
+
+
+def cpu_baseline(N: int, seconds: float, info: dict):
+    """Config 2 on this host's cores: x^N mod N^2 by the C restatement of Go
+    expNNMontgomery with Go's amd64 64-bit Words (oracle/libgomodexp64.so,
+    `value`, one thread and all usable threads), GMP mpz_powm (a faster proxy
+    for math/big) and the 32-bit-word restatement alongside."""
     import ctypes
     from oracle import crosscheck as cc  # test infrastructure: cpu_baseline leg only
-    lib = cc.load_c_oracle()
-    if lib is None:
+    lib64, lib32 = cc.load_c_oracle(64), cc.load_c_oracle(32)
+    if lib64 is None:
         return None
     N2 = N * N
     nw = (N2.bit_length() + 31) // 32
     ew = (N.bit_length() + 31) // 32
     mw = cc._words(N2, nw)
     yw = cc._words(N, ew)
-    done = [0] * threads
-    stop = time.perf_counter() + seconds
 
-    def work(t):
-        rng = np.random.default_rng(7 + t)
-        out = (ctypes.c_uint32 * nw)()
-        xs = rng.integers(0, 1 << 32, size=nw, dtype=np.uint64).astype(np.uint32)
-        xs[-1] = xs[-1] % max((N2 >> (32 * (nw - 1))), 1)
-        xw = (ctypes.c_uint32 * nw)(*[int(v) for v in xs])
-        while time.perf_counter() < stop:
-            lib.gomodexp_montgomery(out, xw, nw, yw, ew, mw, nw)
-            done[t] += 1
+    def c_work(lib):
+        def make(t):
+            rng = np.random.default_rng(7 + t)
+            out = (ctypes.c_uint32 * nw)()
+            xs = rng.integers(0, 1 << 32, size=nw, dtype=np.uint64).astype(np.uint32)
+            xs[-1] = xs[-1] % max((N2 >> (32 * (nw - 1))), 1)
+            xw = (ctypes.c_uint32 * nw)(*[int(v) for v in xs])
+            return lambda: lib.gomodexp_montgomery(out, xw, nw, yw, ew, mw, nw)
+        return make
 
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    el = time.perf_counter() - t0
-    n = sum(done)
-    return {"value": n / el, "unit": "modexp/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x (x^N mod N^2, 4096-bit modulus, 2048-bit exponent) in {el:.1f} s on {threads} "
-                      f"host threads; C restatement of Go expNNMontgomery (oracle/gomodexp.c, 32-bit words, "
-                      f"4-bit window); Go/tss-lib absent from the image"}
+    r1, rn, thr, raw = _one_and_all(c_work(lib64), seconds * 0.5, info)
+    out = {"value": rn, "unit": "modexp/s", "cores": thr, "kind": "port", "one_core": r1,
+           "all_cores_extrapolated": r1 * info["nproc"],
+           "sample": f"{raw[2]} x (x^N mod N^2, 4096-bit modulus, 2048-bit exponent) in {raw[3]:.1f} s on {thr} "
+                     f"threads (+ {raw[0]} on 1 thread in {raw[1]:.1f} s); C restatement of Go expNNMontgomery with "
+                     f"Go's amd64 64-bit Words and 4-bit window (oracle/gomodexp.c -DGOMODEXP_W64); Go/tss-lib absent",
+           "note": "value = all usable threads (min(affinity, cgroup quota)); all_cores_extrapolated = one_core x "
+                   "nproc, the node's host capacity if every CPU ran this work at the one-thread rate",
+           **info}
+    g = cc.GmpPowm(1, N, N2)
+    if g.ok:
+        g.close()
+
+        def gmp_make(t):
+            import random
+            rng = random.Random(31 + t)
+            gp = cc.GmpPowm(rng.randrange(N2), N, N2)
+            return gp.run
+        g1, gn, gthr, graw = _one_and_all(gmp_make, seconds * 0.3, info)
+        out["gmp_mpz_powm"] = {"one_core": g1, "value": gn, "cores": gthr, "version": cc.gmp_version(),
+                               "all_cores_extrapolated": g1 * info["nproc"],
+                               "sample": f"{graw[2]} mpz_powm in {graw[3]:.1f} s on {gthr} threads"}
+    else:
+        out["gmp_mpz_powm"] = None
+    if lib32 is not None:
+        n32, e32 = _time_threads(c_work(lib32), seconds * 0.2, 1)
+        out["port_32bit_words_one_core"] = n32 / e32
+    return out
 
 
 def _c_exp_words(lib, nw):
@@ -141,43 +216,45 @@ def _c_exp_words(lib, nw):
     return f
 
 
-def cpu_baseline_paillier(N: int, seconds: float, threads: int):
-    """Config 1 on host cores: tss-lib Encrypt (Gamma^m r^N mod N^2, both as
-    Go Exps) + HomoMult (c^b), with Go's expNNMontgomery restated in C."""
+def cpu_baseline_paillier(N: int, seconds: float, info: dict):
+    """Config 1 on host cores: tss-lib Encrypt (Gamma^m r^N mod N^2) +
+    HomoMult (c^b) with Go's expNNMontgomery restated in C (64-bit Words).
+    `value`: tss-lib's own work (Gamma^m as a full Exp, as up:crypto/paillier
+    does); `same_work_as_gpu`: with the GPU's bit-exact 1 + mN shortcut."""
     from oracle import crosscheck as cc
-    lib = cc.load_c_oracle()
+    lib = cc.load_c_oracle(64)
     if lib is None:
         return None
     N2 = N * N
     nw = (N2.bit_length() + 31) // 32
     exp = _c_exp_words(lib, nw)
-    done = [0] * threads
-    stop = time.perf_counter() + seconds
     Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
 
-    def work(t):
-        import random
-        rng = random.Random(11 + t)
-        while time.perf_counter() < stop:
-            m, r, b = rng.randrange(N), rng.randrange(1, N), rng.randrange(Q)
-            c = exp(N + 1, m, N2) * exp(r, N, N2) % N2
-            exp(c, b, N2)
-            done[t] += 1
+    def make(shortcut):
+        def mk(t):
+            import random
+            rng = random.Random(11 + t)
 
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    el = time.perf_counter() - t0
-    n = sum(done)
-    return {"value": n / el, "unit": "Encrypt+HomoMult ops/s", "cores": threads, "kind": "port",
-            "sample": f"{n} x (Encrypt: Gamma^m, r^N mod N^2 as Exps; HomoMult: c^b, b < q) in {el:.1f} s on "
-                      f"{threads} host threads; oracle/gomodexp.c (Go expNNMontgomery restated in C)"}
+            def one():
+                m, r, b = rng.randrange(N), rng.randrange(1, N), rng.randrange(Q)
+                gm = (1 + m * N) % N2 if shortcut else exp(N + 1, m, N2)
+                c = gm * exp(r, N, N2) % N2
+                exp(c, b, N2)
+            return one
+        return mk
+
+    r1, rn, thr, raw = _one_and_all(make(False), seconds * 0.6, info)
+    s1, sn, _, sraw = _one_and_all(make(True), seconds * 0.4, info)
+    return {"value": rn, "unit": "Encrypt+HomoMult ops/s", "cores": thr, "kind": "port", "one_core": r1,
+            "all_cores_extrapolated": r1 * info["nproc"],
+            "same_work_as_gpu": {"value": sn, "one_core": s1, "cores": thr,
+                                 "all_cores_extrapolated": s1 * info["nproc"]},
+            "sample": f"{raw[2]} x (Encrypt: Gamma^m and r^N mod N^2 as Exps; HomoMult: c^b, b < q) in {raw[3]:.1f} s "
+                      f"on {thr} threads; same_work_as_gpu: Gamma^m = 1 + mN; oracle/gomodexp.c (64-bit Words)",
+            **info}
 
 
-def paillier_line(N: int, batch: int, reps: int, cpu: bool, threads: int):
+def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict):
     """Config 1 (BASELINE.json): tss-lib paillier Encrypt + HomoMult over a
     batch of `batch` ops, 2048-bit N, through the host mirror of
     crypto/paillier (libmpcx_host.so -> libmpcx.so; host buffers, so the rate
@@ -211,42 +288,37 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, threads: int):
                     "is the bit-exact 1 + mN shortcut, r^N a shared-exponent GPU batch, c^b per-operand",
             "cpu_baseline": None}
     if cpu:
-        line["cpu_baseline"] = cpu_baseline_paillier(N, 10.0, threads)
+        line["cpu_baseline"] = cpu_baseline_paillier(N, 12.0, info)
     return line
 
 
-def cpu_baseline_fermat(seconds: float, threads: int):
+def cpu_baseline_fermat(seconds: float, info: dict):
     """Config 3's work unit on host cores: the 1024-bit Fermat test
-    2^(p-1) mod p of tss-lib's Pocklington check, as a Go Exp (C restatement)."""
+    2^(p-1) mod p of tss-lib's Pocklington check, as a Go Exp (C restatement,
+    Go's 64-bit Words)."""
     from oracle import crosscheck as cc
-    lib = cc.load_c_oracle()
+    lib = cc.load_c_oracle(64)
     if lib is None:
         return None
     exp = _c_exp_words(lib, 32)
-    done = [0] * threads
-    stop = time.perf_counter() + seconds
 
-    def work(t):
+    def make(t):
         import random
         rng = random.Random(23 + t)
-        while time.perf_counter() < stop:
+
+        def one():
             p = rng.getrandbits(1024) | 1 | (1 << 1023)
             exp(2, p - 1, p)
-            done[t] += 1
+        return one
 
-    t0 = time.perf_counter()
-    ths = [threading.Thread(target=work, args=(i,)) for i in range(threads)]
-    for th in ths:
-        th.start()
-    for th in ths:
-        th.join()
-    el = time.perf_counter() - t0
-    return {"value": sum(done) / el, "unit": "1024-bit Fermat tests/s", "cores": threads, "kind": "port",
-            "sample": f"{sum(done)} x 2^(p-1) mod p (1024-bit p) in {el:.1f} s on {threads} host threads; "
-                      f"oracle/gomodexp.c"}
+    r1, rn, thr, raw = _one_and_all(make, seconds, info)
+    return {"value": rn, "unit": "1024-bit Fermat tests/s", "cores": thr, "kind": "port", "one_core": r1,
+            "all_cores_extrapolated": r1 * info["nproc"],
+            "sample": f"{raw[2]} x 2^(p-1) mod p (1024-bit p) in {raw[3]:.1f} s on {thr} threads; "
+                      f"oracle/gomodexp.c (64-bit Words)", **info}
 
 
-def safeprime_line(num: int, seed: int, cpu: bool, threads: int, world: int = 1, rank: int = 0):
+def safeprime_line(num: int, seed: int, cpu: bool, info: dict, world: int = 1, rank: int = 0):
     """Config 3 (BASELINE.json): GeneratePreParams' safe-prime search
     (tss-lib candidate stream, GPU sieve + Fermat, GPU Miller-Rabin): `num`
     1024-bit safe primes in stream order. One GPU: the single-stream search.
@@ -287,9 +359,10 @@ def safeprime_line(num: int, seed: int, cpu: bool, threads: int, world: int = 1,
             "fermat_tests_per_s": st["fermat_tests"] / el, "candidates": st["candidates"],
             "sieved_out": st["sieved_out"], "fermat_tests": st["fermat_tests"], "mr_tests": st["mr_tests"],
             "n_gpus": world, "scaling": "strong", "first_index": res[0][2], "last_index": res[-1][2],
+            "roofline": _job_roofline((st["fermat_tests"] + st["mr_tests"]) * alg_macs(1024, 1023), el, world),
             "cpu_baseline": None}
     if cpu:
-        b = cpu_baseline_fermat(8.0, threads)
+        b = cpu_baseline_fermat(8.0, info)
         if b:
             # host safe-prime rate at the same Fermat tests per safe prime (the Exp dominates tss-lib's loop)
             b["safe_primes_per_s_equiv"] = b["value"] / (st["fermat_tests"] / num)
@@ -311,7 +384,7 @@ def _signing_worker(args):
     deadline, seed = args
     from oracle import mta_ref as M
     from oracle import tss_ref as T
-    M.use_go_modexp()
+    M.use_go_modexp(64)
     nodes = load_nodes()
     rd = T.Reader(seed)
     pairs = 0
@@ -341,7 +414,7 @@ def _keygen_worker(args):
     from oracle import crosscheck as cc
     from oracle import proofs_ref as PR
     from oracle import tss_ref as T
-    lib = cc.load_c_oracle()
+    lib = cc.load_c_oracle(64)
     PR._pw = lambda x, y, m: cc.c_expnn(lib, x % m, y, m)
     nodes = load_nodes()
     A, B = nodes[0], nodes[1]
@@ -377,7 +450,7 @@ def _keygen_worker(args):
     return acc
 
 
-def cpu_baseline_keygen(seconds: float, procs: int, parties: int):
+def cpu_baseline_keygen(seconds: float, info: dict, parties: int):
     """Config 5 on host cores: per-primitive times of the proof restatement
     (one process per core, all running at once), composed into the per-session
     mix of keygenload.hpp: n(2 DLN + Mod + (n-1) Fac) proofs and
@@ -385,8 +458,9 @@ def cpu_baseline_keygen(seconds: float, procs: int, parties: int):
     from concurrent.futures import ProcessPoolExecutor
     import multiprocessing as mp
     from oracle import crosscheck as cc
-    if cc.load_c_oracle() is None:
+    if cc.load_c_oracle(64) is None:
         return None
+    procs = info["usable_threads"]
     deadline = time.time() + seconds
     with ProcessPoolExecutor(procs, mp_context=mp.get_context("fork")) as ex:
         res = list(ex.map(_keygen_worker, [(deadline, 0x6B0 + i) for i in range(procs)]))
@@ -399,10 +473,12 @@ def cpu_baseline_keygen(seconds: float, procs: int, parties: int):
            "dln_verify": 2 * n * (n - 1), "mod_verify": n * (n - 1), "fac_verify": n * (n - 1)}
     cpu_s = sum(mix[k] * per[k] for k in mix)
     return {"value": procs / cpu_s, "unit": "sessions/s", "cores": procs, "kind": "port",
-            "per_primitive_s": per,
+            "one_core": 1.0 / cpu_s, "all_cores_extrapolated": info["nproc"] / cpu_s,
+            "per_primitive_s": per, **info,
             "sample": f"{sum(c for c, _ in tot.values())} proof primitives (DLN/Mod/Fac prove + verify) in "
                       f"{seconds:.0f} s on {procs} processes, composed into one {n}-party session's mix "
-                      f"({cpu_s:.1f} CPU-s per session); oracle/proofs_ref.py with Go expNN restated in C"}
+                      f"({cpu_s:.1f} CPU-s per session); oracle/proofs_ref.py with Go expNN restated in C "
+                      f"(64-bit Words); one_core = 1 / CPU-s per session"}
 
 
 def keygen_line(args):
@@ -432,18 +508,20 @@ def keygen_line(args):
             "verifications": int(st["verifications"]), "seconds": st["total_s"], "prove_s": st["prove_s"],
             "verify_s": st["verify_s"], "engine_busy_s": st["engine_busy_s"],
             "verifications_per_s": st["verifications"] / st["total_s"], "checked": "every verification passes",
+            "roofline": _job_roofline(st["alg_macs"], st["total_s"]),
             "cpu_baseline": None}
     return line
 
 
-def cpu_baseline_signing(seconds: float, procs: int):
+def cpu_baseline_signing(seconds: float, info: dict):
     """2-of-3 signing's MtA work on host cores: the oracle restatement of
     tss-lib's MtA (oracle/mta_ref.py) with exponentiations by the C
     restatement of Go's nat.expNN, one process per core."""
     from concurrent.futures import ProcessPoolExecutor
     from oracle import crosscheck as cc
-    if cc.load_c_oracle() is None:
+    if cc.load_c_oracle(64) is None:
         return None
+    procs = info["usable_threads"]
     t0 = time.time()
     deadline = t0 + seconds
     import multiprocessing as mp
@@ -451,16 +529,33 @@ def cpu_baseline_signing(seconds: float, procs: int):
         n = sum(ex.map(_signing_worker, [(deadline, 0x51C0 + i) for i in range(procs)]))
     el = max(time.time() - t0, seconds)
     return {"value": n / 2 / el, "unit": "sigs/s", "cores": procs, "kind": "port",
+            "one_core": n / 2 / el / procs, "all_cores_extrapolated": n / 2 / el / procs * info["nproc"], **info,
             "sample": f"{n} ordered signer pairs = {n / 2:g} 2-signer signatures' MtA/MtAwc (per pair: AliceInit, "
                       f"BobMid, BobMidWC, AliceEnd, AliceEndWC, all proofs verified) in {el:.1f} s on {procs} "
                       f"processes; "
-                      f"oracle/mta_ref.py with Go expNN restated in C (oracle/gomodexp.c)"}
+                      f"oracle/mta_ref.py with Go expNN restated in C (oracle/gomodexp.c, 64-bit Words); "
+                      f"one_core = per process while all ran"}
 
 
-def signing_line(args, world, rank):
-    """Config 4 (BASELINE.json): 2-of-3 ECDSA signing's MtA / MtAwc work with
-    range proofs, `wallets` wallets per GPU (csrc/host/signing.hpp). Each rank
-    signs its own wallets (weak scaling); value = all ranks' wallets / max time."""
+def _job_roofline(alg_macs: float, seconds: float, world: int = 1) -> dict:
+    """Whole-job roofline of a protocol line: the Go-equivalent algorithmic
+    work the host mirror sent to the GPU (Engine::alg_macs, SURVEY.md 8(d) W
+    per exponentiation) over the line's wall time, against the nominal INT32
+    MAD peak of the GPUs. Host-side work (hashing, draws, gcds, packing) is in
+    the wall time, so this is an end-to-end figure, not a kernel roofline."""
+    achieved = alg_macs * world / seconds
+    return {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_INT32_NOMINAL * world / 1e12,
+            "unit": "TOP/s", "frac": achieved / (PEAK_INT32_NOMINAL * world), "traffic": None,
+            "alg_ops_per_job": alg_macs, "scope": "end to end (wall time incl. host work)"}
+
+
+def signing_line(args, world, rank, signers: int):
+    """Config 4 (BASELINE.json): GG18 ECDSA signing of `wallets` wallets per
+    GPU by `signers` of the 3 nodes (csrc/host/signing.hpp): MtA / MtAwc with
+    range proofs on the GPU, then delta, sigma, R, s and ecdsa.Verify of every
+    signature (/root/reference/pkg/mpc/ecdsa_signing_session.go:162). Each rank
+    signs its own wallets (weak scaling); value = all ranks' verified
+    signatures / max time."""
     import torch
     import torch.distributed as dist
     from mpcium_amd import host as mhost
@@ -468,30 +563,38 @@ def signing_line(args, world, rank):
     from mpcium_amd.shard import max_over_ranks
     mhost.init(gpu_index())
     nodes = load_nodes()
-    warm = mta.bench_signing_mta(nodes, args.signers, 256, seed=0x5167 + 7919 * rank)
-    if warm["errors"] or warm["relation_failures"]:
+    warm = mta.bench_signing(nodes, signers, 256, seed=0x5167 + 7919 * rank)
+    if warm["errors"] or warm["relation_failures"] or warm["verified"] != 256:
         raise SystemExit(f"rank {rank}: signing warmup failed: {warm}")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    st = mta.bench_signing_mta(nodes, args.signers, args.wallets, seed=0x5168 + 7919 * rank)
+    st = mta.bench_signing(nodes, signers, args.wallets, seed=0x5168 + 7919 * rank)
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if st["errors"] or st["relation_failures"]:
-        raise SystemExit(f"rank {rank}: signing MtA failed: {st}")
-    el, r1, r2, r3 = max_over_ranks([el, st["round1_s"], st["round2_s"], st["round3_s"]], world)
-    line = {"metric": f"{args.signers}-of-3 ECDSA sigs/s over {args.wallets * world // 1000}k wallets "
-                      f"(MtA/MtAwc + range proofs, every Paillier/DLN exponentiation on the GPU)",
+    if st["errors"] or st["relation_failures"] or st["verified"] != args.wallets:
+        raise SystemExit(f"rank {rank}: signing failed: {st}")
+    el, r1, r2, r3, fin = max_over_ranks([el, st["round1_s"], st["round2_s"], st["round3_s"], st["finalize_s"]],
+                                         world)
+    line = {"metric": f"{signers}-of-3 ECDSA sigs/s over {args.wallets * world // 1000}k wallets "
+                      f"(GG18 signing, every Paillier/DLN exponentiation on the GPU, every signature verified)",
             "value": args.wallets * world / el, "unit": "sigs/s", "n_gpus": world,
-            "wallets_per_gpu": args.wallets, "signers": args.signers, "seconds": el,
-            "rounds_s": {"round1_alice_init": r1, "round2_bob_mid": r2, "round3_alice_end": r3},
-            "engine_busy_s": st["engine_busy_s"],
-            "sessions_per_gpu": st["sessions"], "checked": "alpha+beta == k*gamma, mu+nu == k*w (mod q), every session",
-            "scope": "GG18 signing rounds 1-3 MtA/MtAwc (tss-lib up:crypto/mta); other rounds are secp256k1 work "
-                     "outside the Paillier path", "cpu_baseline": None}
+            "wallets_per_gpu": args.wallets, "signers": signers, "seconds": el,
+            "signatures_verified": int(st["verified"]) * world,
+            "rounds_s": {"round1_alice_init": r1, "round2_bob_mid": r2, "round3_alice_end": r3,
+                         "rounds4_9_finalize_verify": fin},
+            "engine_busy_s": st["engine_busy_s"], "host_share": 1.0 - st["engine_busy_s"] / max(el, 1e-9),
+            "sessions_per_gpu": int(st["sessions"]),
+            "checked": "alpha+beta == k*gamma, mu+nu == k*w (mod q) on every session; ecdsa.Verify on every "
+                       "signature",
+            "roofline": _job_roofline(st["alg_macs"], el, world),
+            "alg_ops_per_signature": st["alg_macs"] / args.wallets,
+            "scope": "MtA/MtAwc + range proofs (rounds 1-3) on the GPU; signature algebra + ecdsa.Verify on the "
+                     "host; phase-5 commitments/Schnorr proofs (no Paillier work, no effect on (r, s)) not replayed",
+            "cpu_baseline": None}
     return line
 
 
@@ -501,7 +604,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--count", type=int, default=65536, help="operands per GPU per step")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--verify", type=int, default=16, help="results checked against CPython pow (untimed)")
@@ -527,12 +630,15 @@ def main():
     local = gpu_index()
     # The signing CPU baseline forks worker processes: run it before this
     # process touches the GPU.
+    info = host_info()
+    if args.cpu_threads:
+        info["usable_threads"] = args.cpu_threads
     sign_cpu = None
     if args.wallets > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sign_cpu = cpu_baseline_signing(args.cpu_sign_seconds, args.cpu_threads or min(16, os.cpu_count() or 1))
+        sign_cpu = cpu_baseline_signing(args.cpu_sign_seconds, info)
     keygen_cpu = None
     if args.keygen_sessions > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
-        keygen_cpu = cpu_baseline_keygen(16.0, args.cpu_threads or min(16, os.cpu_count() or 1), args.parties)
+        keygen_cpu = cpu_baseline_keygen(16.0, info, args.parties)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -635,17 +741,17 @@ def main():
     }
     result["roofline"].update(pmc_traffic(count, args.modbits, mod))
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
-        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, thr)
+        result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, info)
     if args.wallets > 0:
-        result["signing"] = signing_line(args, world, rank)
+        result["signing"] = signing_line(args, world, rank, args.signers)
         result["signing"]["cpu_baseline"] = sign_cpu
+        if args.signers != 3:  # mpcium signs with every ready peer (/root/reference/pkg/mpc/node.go:148)
+            result["signing_3_signers"] = signing_line(args, world, rank, 3)
     if args.extra_lines:
-        thr = args.cpu_threads or min(16, os.cpu_count() or 1)
         cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
         if world == 1:
-            result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, thr)
-        result["safe_prime"] = safeprime_line(8, 0x5AFE, cpu, thr, world, rank)
+            result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, info)
+        result["safe_prime"] = safeprime_line(8, 0x5AFE, cpu, info, world, rank)
     if args.keygen_sessions > 0 and world == 1:
         result["keygen"] = keygen_line(args)
         result["keygen"]["cpu_baseline"] = keygen_cpu

@@ -200,23 +200,33 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
                            const uint32_t* NCap, const uint32_t* s, const uint32_t* t, uint32_t count,
                            const uint32_t* pf, const uint8_t* v_neg, uint8_t* ok);
 
-/* Config-4 driver: the MtA / MtAwc work of one GG18 signature for each of
- * `wallets` wallets, signed by the first `signers` of `n_nodes` nodes (keys:
- * Paillier private keys + own DLN params with factors, width w). Plays every
- * signer (rounds 1-3 of up:ecdsa/signing, see csrc/host/signing.hpp) and
- * checks alpha + beta = k gamma and mu + nu = k w (mod q) for every session.
- * stats_out[9]: round1_s, round2_s, round3_s, total_s, wallets, sessions,
- * errors, relation_failures, engine_busy_s (time inside libmpcx calls, summed
- * over the concurrent per-pair tasks). */
-int mpcxh_bench_signing_mta(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
-                            uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out);
+/* Config-4 driver: one GG18 signature for each of `wallets` wallets, signed by
+ * the first `signers` of `n_nodes` nodes (keys: Paillier private keys + own
+ * DLN params with factors, width w). Plays every signer: rounds 1-3 MtA /
+ * MtAwc of up:ecdsa/signing on the GPU (csrc/host/signing.hpp), checking
+ * alpha + beta = k gamma and mu + nu = k w (mod q) for every session; then
+ * delta, sigma, R = delta^-1 Gamma, r, s (low-s) and ecdsa.Verify of every
+ * signature against the wallet key, as mpcium does when the party ends
+ * (/root/reference/pkg/mpc/ecdsa_signing_session.go:162).
+ * stats_out[MPCXH_SIGNING_STATS]: round1_s, round2_s, round3_s, total_s,
+ * wallets, sessions, errors, relation_failures, engine_busy_s (time inside
+ * libmpcx calls), finalize_s, signatures, verified, alg_macs (Go-equivalent
+ * algorithmic work of the exponentiations sent to the GPU).
+ * trace_wallets > 0: trace_out receives, for the first trace_wallets wallets,
+ * per ordered pair (i-major) and wallet 40 words (alpha, beta, mu, nu as 8
+ * words each, SHA512_256i over the session's cA, RangeProofAlice, cB,
+ * ProofBob, cB', ProofBobWC fields), then per wallet 17 words (r, s, recid). */
+#define MPCXH_SIGNING_STATS 13
+int mpcxh_bench_signing(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
+                        uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out, uint32_t trace_wallets,
+                        uint32_t* trace_out);
 
 /* Config-5 driver: the proof work of `sessions` keygen / reshare sessions of
  * n_parties nodes (csrc/host/keygenload.hpp): every party proves DLN x2,
  * Paillier-Blum Mod, and a Fac proof to each peer; every party verifies
  * every peer's proofs. Integers are w words wide (w >= 64).
- * stats_out[9]: prove_s, verify_s, total_s, sessions, parties, proofs,
- * verifications, failures, engine_busy_s. */
+ * stats_out[10]: prove_s, verify_s, total_s, sessions, parties, proofs,
+ * verifications, failures, engine_busy_s, alg_macs. */
 typedef struct {
   mpcxh_paillier_t paillier;  /* the party's own Paillier private key */
   const uint32_t* NTilde;

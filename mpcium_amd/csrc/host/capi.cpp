@@ -467,19 +467,26 @@ int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int
   });
 }
 
-int mpcxh_bench_signing_mta(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
-                            uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out) {
+int mpcxh_bench_signing(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
+                        uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out, uint32_t trace_wallets,
+                        uint32_t* trace_out) {
   return guard([&] {
     check_width(w);
+    if (!stats_out) throw std::invalid_argument("null stats_out");
+    if (trace_wallets && !trace_out) throw std::invalid_argument("null trace_out");
     std::vector<signing::NodeKeys> nodes(n_nodes);
     for (uint32_t i = 0; i < n_nodes; ++i) {
       nodes[i].sk = paillier_from(&sks[i], w);
       nodes[i].dln = dln_from(&dlns[i], w);
     }
-    const auto st = signing::RunSigningMtA(nodes, (int)signers, wallets, seed);
-    const double v[9] = {st.round1_s, st.round2_s, st.round3_s, st.total_s, (double)st.wallets, (double)st.sessions,
-                         (double)st.errors, (double)st.relation_failures, st.engine_busy_s};
+    std::vector<uint32_t> tr;
+    const auto st = signing::RunSigning(nodes, (int)signers, wallets, seed, trace_wallets, &tr);
+    const double v[MPCXH_SIGNING_STATS] = {st.round1_s, st.round2_s, st.round3_s, st.total_s, (double)st.wallets,
+                                           (double)st.sessions, (double)st.errors, (double)st.relation_failures,
+                                           st.engine_busy_s, st.finalize_s, (double)st.signatures,
+                                           (double)st.verified, st.alg_macs};
     std::memcpy(stats_out, v, sizeof v);
+    if (trace_wallets) std::memcpy(trace_out, tr.data(), tr.size() * sizeof(uint32_t));
   });
 }
 
@@ -623,8 +630,9 @@ int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t
       ps[i].q = Nat::from_words(a.q, w);
     }
     const auto st = keygenload::RunKeygenProofs(ps, sessions, seed);
-    const double v[9] = {st.prove_s, st.verify_s, st.total_s, (double)st.sessions, (double)st.parties,
-                         (double)st.proofs, (double)st.verifications, (double)st.failures, st.engine_busy_s};
+    const double v[10] = {st.prove_s, st.verify_s, st.total_s, (double)st.sessions, (double)st.parties,
+                          (double)st.proofs, (double)st.verifications, (double)st.failures, st.engine_busy_s,
+                          st.alg_macs};
     std::memcpy(stats_out, v, sizeof v);
   });
 }

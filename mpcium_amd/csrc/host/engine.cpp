@@ -48,6 +48,21 @@ void Engine::leave_call() {
                                                                                busy_t0_).count();
 }
 
+void Engine::count_work(const Nat& m, const std::vector<Nat>& exps, size_t count) {
+  const uint64_t L = m.words(), l2 = 2 * L * L;
+  uint64_t w = 0;
+  auto one = [&](const Nat& e) {
+    const uint64_t E = e.bit_len();
+    return (E + (E + 3) / 4) * l2;
+  };
+  if (exps.size() == 1 && count != 1) {
+    w = one(exps[0]) * count;
+  } else {
+    for (const auto& e : exps) w += one(e);
+  }
+  alg_macs_ += w;
+}
+
 Engine::Mod& Engine::modulus(const Nat& m) {
   auto it = mods_.find(m.limbs());
   if (it != mods_.end()) return it->second;
@@ -105,6 +120,7 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
   std::vector<uint32_t> M;
   if (muls) M = packed(*muls);
   std::vector<uint32_t> out((size_t)bases.size() * md.words);
+  count_work(m, exps, bases.size());
   int rc;
   enter_call();
   if (muls) {
@@ -176,6 +192,7 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
     f = fixed(m, b, need);
   }
   const uint32_t* ep = E.data();
+  count_work(m, exps, exps.size());
   enter_call();
   int rc = mpcx_fixedbase_exp_batch(1, &f->h, (uint32_t)exps.size(), &ep, &ew, muls ? Mw.data() : nullptr,
                                     muls ? md.class_words : 0, out.data(), md.words);

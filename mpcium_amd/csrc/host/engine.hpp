@@ -60,7 +60,18 @@ class Engine {
   // (GPU + transfers) was in flight, since the last reset. Calls from
   // different threads run concurrently on libmpcx's lanes (streams).
   double busy_seconds() const { return (double)busy_ns_.load() * 1e-9; }
-  void reset_busy() { busy_ns_ = 0; }
+  // Go-equivalent algorithmic work of the exponentiations sent to libmpcx
+  // since the last reset: SURVEY.md 8(d) W = (E + ceil(E/4)) 2 L^2 32-bit
+  // MACs per x^e mod m (E = bit length of e, L = 32-bit words of m), the
+  // work Go's 4-bit-window expNNMontgomery does for it, whatever window,
+  // comb table or geometry the GPU uses. Algebraic shortcuts the host takes
+  // instead of an exponentiation (Gamma^m = 1 + mN, CRT halves) count only
+  // what is actually launched.
+  double alg_macs() const { return (double)alg_macs_.load(); }
+  void reset_busy() {
+    busy_ns_ = 0;
+    alg_macs_ = 0;
+  }
   std::vector<uint8_t> fermat2(const std::vector<Nat>& cands);
   // mpcx_safeprime_sieve_fermat: (index, Pocklington verdict) of the sieve
   // survivors among `count` raw candidates, ascending index
@@ -95,6 +106,8 @@ class Engine {
   bool bound_ = false;
   bool fixed_enabled_ = true;
   std::atomic<uint64_t> busy_ns_{0};
+  std::atomic<uint64_t> alg_macs_{0};
+  void count_work(const Nat& m, const std::vector<Nat>& exps, size_t count);
   std::map<std::vector<uint32_t>, Mod> mods_;
   std::map<std::pair<std::vector<uint32_t>, std::vector<uint32_t>>, Fixed> fixed_;
 };

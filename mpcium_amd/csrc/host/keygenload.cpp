@@ -160,6 +160,7 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
   st.total_s = t2 - t0;
   st.failures = fails.load();
   st.engine_busy_s = Engine::get().busy_seconds();
+  st.alg_macs = Engine::get().alg_macs();
   return st;
 }
 

@@ -38,6 +38,7 @@ struct PartyKeys {
 
 struct ProofStats {
   double prove_s = 0, verify_s = 0, total_s = 0, engine_busy_s = 0;
+  double alg_macs = 0;  // Go-equivalent algorithmic work sent to the GPU (Engine::alg_macs)
   uint64_t sessions = 0, parties = 0, proofs = 0, verifications = 0;
   uint64_t failures = 0;  // verifications that did not pass (honest proofs: must be 0)
 };

@@ -620,11 +620,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
 }
 
-// ---------------------------------------------------------------- Fermat(2)
-// ok[i] = 2^(p_i - 1) mod p_i == 1, one candidate per lane (P = 1, thread per
-// operand, per-lane modulus). Square-and-double: squarings are Montgomery
-// squarings, the "multiply by 2" is a digit doubling with no reduction (values
-// stay < 4p << R/4, which the almost-Montgomery bound absorbs).
+// ------------------------------------------- per-candidate-modulus helpers
+// Thread-per-operand kernels (P = 1, K digits per lane) whose modulus differs
+// per lane: safe-prime candidates. Every Montgomery constant is derived on the
+// device from the candidate itself.
 template <int K>
 __device__ __forceinline__ bool ge_digits(const uint32_t (&x)[K], const uint32_t (&y)[K]) {
   // branch-free lexicographic compare from the top digit
@@ -656,99 +655,300 @@ __device__ __forceinline__ void norm_serial(uint32_t (&x)[K]) {
     c = t >> DB;
   }
 }
-
-template <int K, int WPE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fermat2(const FermatArgs a) {
-  constexpr int L = K;
-  __shared__ uint32_t lds[65 * L + 1];
-  const int lane = threadIdx.x;
-  const uint32_t op = blockIdx.x * 64u + lane;
-  const uint32_t cnt = a.count_dev ? min(a.count, *a.count_dev) : a.count;
-  if (blockIdx.x * 64u >= cnt) return;  // whole wave beyond the sieve's survivors
-  const bool active = op < cnt;
-  uint32_t* bl = lds + lane * L;
-  uint32_t Nd[K], A[K];
-  const uint32_t* pw = a.p + (size_t)(active ? op : 0) * a.p_words;
+template <int K>
+__device__ __forceinline__ void canon_serial(uint32_t (&x)[K], const uint32_t (&n)[K]) {
+  norm_serial<K>(x);
+  for (int it = 0; it < 8 && ge_digits<K>(x, n); ++it) sub_digits<K>(x, n);
+}
+template <int K>
+__device__ __forceinline__ bool eq_digits(const uint32_t (&x)[K], const uint32_t (&y)[K]) {
+  bool e = true;
+#pragma unroll
+  for (int k = 0; k < K; ++k) e &= x[k] == y[k];
+  return e;
+}
+// x = (x + y) mod-lazy: digit sum, normalised (no reduction)
+template <int K>
+__device__ __forceinline__ void add_digits(uint32_t (&x)[K], const uint32_t (&y)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) x[k] += y[k];
+  norm_serial<K>(x);
+}
+// candidate words -> radix-2^28 digits (inactive lanes: the odd dummy 1)
+template <int K>
+__device__ __forceinline__ void load_candidate(const uint32_t* w, uint32_t words, bool active, uint32_t (&Nd)[K]) {
 #pragma unroll
   for (int k = 0; k < K; ++k) {
-    const uint32_t bit = (uint32_t)k * DB;
-    const uint32_t w = bit >> 5, s = bit & 31u;
+    const uint32_t bit = (uint32_t)k * DB, wi = bit >> 5, sh = bit & 31u;
     uint64_t v = 0;
-    if (active) {
-      const uint32_t lo = w < a.p_words ? pw[w] : 0u;
-      const uint32_t hi = (w + 1) < a.p_words ? pw[w + 1] : 0u;
-      v = ((uint64_t)hi << 32) | lo;
-    }
-    Nd[k] = (uint32_t)(v >> s) & M28;
+    if (active) v = ((uint64_t)((wi + 1) < words ? w[wi + 1] : 0u) << 32) | (wi < words ? w[wi] : 0u);
+    Nd[k] = (uint32_t)(v >> sh) & M28;
   }
-  if (!active) Nd[0] = 1;  // dummy odd modulus
-  // n0inv = -p^-1 mod 2^28 (Newton on 32 bits)
-  uint32_t inv = Nd[0];
-  for (int i = 0; i < 5; ++i) inv *= 2u - Nd[0] * inv;
-  const uint32_t n0inv = (0u - inv) & M28;
-  // bit length of p (unrolled: no dynamic register indexing)
-  int pbits = 1;
+  if (!active) Nd[0] = 1;
+}
+// -n^-1 mod 2^28 (Newton on 32 bits)
+__device__ __forceinline__ uint32_t neg_inv28(uint32_t n0) {
+  uint32_t inv = n0;
+  for (int i = 0; i < 5; ++i) inv *= 2u - n0 * inv;
+  return (0u - inv) & M28;
+}
+template <int K>
+__device__ __forceinline__ int bitlen_digits(const uint32_t (&Nd)[K]) {
+  int nbits = 1;  // unrolled: no dynamic register indexing
 #pragma unroll
   for (int k = 0; k < K; ++k)
-    if (Nd[k] != 0u) pbits = k * DB + (32 - __builtin_clz(Nd[k]));
-  // R mod p, R = 2^(28K): t = 2^pbits - p (< p), then (28K - pbits) doublings mod p
+    if (Nd[k] != 0u) nbits = k * DB + (32 - __builtin_clz(Nd[k]));
+  return nbits;
+}
+// R mod n (canonical), R = 2^(28K): 2^nbits - n (< n), then doublings mod n
+template <int K>
+__device__ __forceinline__ void r_mod(const uint32_t (&Nd)[K], int nbits, uint32_t (&A)[K]) {
+  uint32_t c = 1;  // two's complement of n within nbits bits
 #pragma unroll
-  for (int k = 0; k < K; ++k) A[k] = 0;
-  {
-    // two's complement of p within pbits bits
-    uint32_t c = 1;
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int lo = k * DB;
-      uint32_t maskk = 0;
-      if (pbits >= lo + DB) maskk = M28;
-      else if (pbits > lo) maskk = (1u << (pbits - lo)) - 1u;
-      const uint32_t t = ((~Nd[k]) & maskk) + c;
-      c = t >> DB;
-      A[k] = t & maskk;
-    }
+  for (int k = 0; k < K; ++k) {
+    const int lo = k * DB;
+    uint32_t maskk = 0;
+    if (nbits >= lo + DB) maskk = M28;
+    else if (nbits > lo) maskk = (1u << (nbits - lo)) - 1u;
+    const uint32_t t = ((~Nd[k]) & maskk) + c;
+    c = t >> DB;
+    A[k] = t & maskk;
   }
-  for (int i = pbits; i < DB * K; ++i) {
+  for (int i = nbits; i < DB * K; ++i) {
 #pragma unroll
     for (int k = 0; k < K; ++k) A[k] <<= 1;
     norm_serial<K>(A);
     if (ge_digits<K>(A, Nd)) sub_digits<K>(A, Nd);
   }
-  // A = R mod p = Montgomery form of 1. The top bit of e = p - 1 is set, so
-  // start from 2 (Montgomery form 2R, left unreduced: < 2p).
+}
+// bit j of the candidate (from its words in memory: no dynamic register index)
+__device__ __forceinline__ uint32_t word_bit(const uint32_t* w, int j) { return (w[j >> 5] >> (j & 31)) & 1u; }
+
+// -------------------------------------------- base-2 tests (k_prime2)
+// Fermat items: ok = 2^(n-1) == 1 (mod n) -- tss-lib's Pocklington check on
+// p = 2q+1 (up:common/safe_prime.go isPocklingtonCriterionSatisfied).
+// Strong items: n - 1 = 2^s d, x = 2^d; ok iff x == 1, or x^(2^j) == n-1
+// for some j < s -- the base-2 Miller-Rabin round of q.ProbablyPrime
+// (go:src/math/big/prime.go, its forced last base), run first so the other
+// rounds only see its survivors. One wave-uniform mode per block.
+// Square-and-double: squarings are Montgomery squarings and the "multiply by
+// 2" a digit doubling without reduction (values < 4n, and R > 16n keeps every
+// almost-Montgomery output below 2n).
+template <int K, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_prime2(const Prime2Args a) {
+  constexpr int L = K;
+  __shared__ uint32_t lds[65 * L + 1];
+  const int lane = threadIdx.x;
+  const bool strong = blockIdx.x >= a.f_blocks;
+  uint32_t op, cnt;
+  const uint32_t* src;
+  if (!strong) {
+    cnt = a.count_dev ? min(a.count_f, *a.count_dev) : a.count_f;
+    if (blockIdx.x * 64u >= cnt) return;  // whole wave beyond the sieve's survivors
+    op = blockIdx.x * 64u + lane;
+    src = a.nf;
+  } else {
+    cnt = a.count_s;
+    if ((blockIdx.x - a.f_blocks) * 64u >= cnt) return;
+    op = (blockIdx.x - a.f_blocks) * 64u + lane;
+    src = a.ns;
+  }
+  const bool active = op < cnt;
+  uint32_t* bl = lds + lane * L;
+  const uint32_t* nw = src + (size_t)(active ? op : 0) * a.n_words;
+  uint32_t Nd[K], A[K], R1[K];
+  load_candidate<K>(nw, a.n_words, active, Nd);
+  const uint32_t n0inv = neg_inv28(Nd[0]);
+  const int nbits = bitlen_digits<K>(Nd);
+  r_mod<K>(Nd, nbits, R1);
+  int s = 0;  // Fermat: e = n - 1; strong: e = (n - 1) >> s, s = v2(n - 1)
+  if (strong && active) {
+    s = 1;
+    while (s < nbits && !word_bit(nw, s)) ++s;
+  }
+  // the top bit of e is the top bit of n: start from Montgomery 2
 #pragma unroll
-  for (int k = 0; k < K; ++k) A[k] <<= 1;
+  for (int k = 0; k < K; ++k) A[k] = R1[k] << 1;
   norm_serial<K>(A);
   const int m_src_addr = lane * 4;
-  for (int i = pbits - 2; i >= 0; --i) {
-    // A <- A^2 / R
+  for (int i = nbits - s - 2; i >= 0; --i) {
     lds_store_digits<K>(bl, 0, A);
     wave_lds_fence();
     montmul<1, K, true>(A, bl, Nd, n0inv, m_src_addr, 0);
     wave_lds_fence();
-    uint32_t ebit = active ? (pw[i >> 5] >> (i & 31)) & 1u : 0u;
-    if (i == 0) ebit = 0;  // e = p - 1
-    if (ebit) {
+    const int j = i + s;  // bit j of n - 1: bit j of n, except bit 0 (n odd)
+    if (j > 0 && active && word_bit(nw, j)) {
 #pragma unroll
       for (int k = 0; k < K; ++k) A[k] <<= 1;
       norm_serial<K>(A);
     }
   }
-  // leave the Montgomery domain: A * 1 / R, then canonical compare with 1
-  {
-    uint32_t one[K];
+  canon_serial<K>(A, Nd);
+  bool pass = eq_digits<K>(A, R1);  // 2^e == 1
+  if (strong) {
+    uint32_t NR1[K];  // Montgomery form of n - 1
 #pragma unroll
-    for (int k = 0; k < K; ++k) one[k] = (k == 0) ? 1u : 0u;
-    lds_store_digits<K>(bl, 0, one);
-    wave_lds_fence();
-    montmul<1, K, false>(A, bl, Nd, n0inv, m_src_addr, 0);
+    for (int k = 0; k < K; ++k) NR1[k] = Nd[k];
+    sub_digits<K>(NR1, R1);
+    pass = pass || eq_digits<K>(A, NR1);
+    for (int j = 1; j < s && !pass; ++j) {
+      lds_store_digits<K>(bl, 0, A);
+      wave_lds_fence();
+      montmul<1, K, true>(A, bl, Nd, n0inv, m_src_addr, 0);
+      wave_lds_fence();
+      canon_serial<K>(A, Nd);
+      if (eq_digits<K>(A, R1)) break;  // nontrivial square root of 1: composite
+      pass = eq_digits<K>(A, NR1);
+    }
   }
-  norm_serial<K>(A);
-  while (ge_digits<K>(A, Nd)) sub_digits<K>(A, Nd);
-  bool is_one = A[0] == 1u;
+  if (!active) return;
+  if (strong) {
+    a.ok_s[op] = pass ? 1 : 0;
+    return;
+  }
+  if (a.ok_f) a.ok_f[op] = pass ? 1 : 0;
+  if (pass && a.pass_count) {
+    const uint32_t slot = atomicAdd(a.pass_count, 1u);
+    a.pass_idx[slot] = a.sieve_idx ? a.sieve_idx[op] : op;
+    for (uint32_t w = 0; w < a.n_words; ++w) a.pass_n[(size_t)slot * a.n_words + w] = nw[w];
+  }
+}
+
+// -------------------------------------------- strong Lucas test (k_lucas)
+// Go math/big probablyPrimeLucas (go:src/math/big/prime.go), the last step of
+// ProbablyPrime: with P from Baillie-OEIS method C (the smallest P >= 3 with
+// Jacobi(P^2 - 4, n) = -1, found by the caller; Q = 1), n + 1 = 2^r s (s odd):
+// n passes iff V_s == +-2 and U_s == 0 (checked as P V_s == 2 V_{s+1},
+// Crandall-Pomerance 3.13), or V_{2^t s} == 0 for some 0 <= t < r - 1.
+// V is built by the binary ladder V_2k = V_k^2 - 2, V_2k+1 = V_k V_k+1 - P in
+// the Montgomery domain: each step is one product and one squaring for every
+// lane (the bit only selects where the two results go, so the wave never
+// diverges); the subtractions are additions of 2n - c (values stay < 4n).
+template <int K, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_lucas(const LucasArgs a) {
+  constexpr int L = K;
+  __shared__ uint32_t lds[65 * L + 1];
+  const int lane = threadIdx.x;
+  const uint32_t op = blockIdx.x * 64u + lane;
+  if (blockIdx.x * 64u >= a.count) return;
+  const bool active = op < a.count;
+  uint32_t* bl = lds + lane * L;
+  const int m_src_addr = lane * 4;
+  const uint32_t* nw = a.n + (size_t)(active ? op : 0) * a.n_words;
+  uint32_t Nd[K], R1[K];
+  load_candidate<K>(nw, a.n_words, active, Nd);
+  const uint32_t n0inv = neg_inv28(Nd[0]);
+  const int nbits = bitlen_digits<K>(Nd);
+  r_mod<K>(Nd, nbits, R1);
+  const uint32_t P = active ? a.P[op] : 3u;
+  // PR = P R mod n (Horner over P's bits), TwoR = 2 R mod n
+  uint32_t PR[K], TwoR[K], N2[K], CP[K], C2[K];
 #pragma unroll
-  for (int k = 1; k < K; ++k) is_one &= A[k] == 0u;
-  if (active) a.ok[op] = is_one ? 1 : 0;
+  for (int k = 0; k < K; ++k) PR[k] = 0;
+  for (int b = 13; b >= 0; --b) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) PR[k] <<= 1;
+    norm_serial<K>(PR);
+    if (ge_digits<K>(PR, Nd)) sub_digits<K>(PR, Nd);
+    if ((P >> b) & 1u) {
+      add_digits<K>(PR, R1);
+      if (ge_digits<K>(PR, Nd)) sub_digits<K>(PR, Nd);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    TwoR[k] = R1[k] << 1;
+    N2[k] = Nd[k] << 1;
+  }
+  norm_serial<K>(TwoR);
+  if (ge_digits<K>(TwoR, Nd)) sub_digits<K>(TwoR, Nd);
+  norm_serial<K>(N2);
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    CP[k] = N2[k];
+    C2[k] = N2[k];
+  }
+  sub_digits<K>(CP, PR);    // 2n - P R: adding it subtracts P
+  sub_digits<K>(C2, TwoR);  // 2n - 2 R
+  // n + 1 = 2^r s: r = trailing ones of n; bit j of n + 1 is 0 below r, 1 at
+  // r, and bit j of n above
+  int r = 0;
+  if (active)
+    while (r < nbits && word_bit(nw, r)) ++r;
+  const int sbits = (r == nbits) ? 1 : nbits - r;
+  uint32_t vk[K], vk1[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    vk[k] = TwoR[k];  // V_0 = 2
+    vk1[k] = PR[k];   // V_1 = P
+  }
+  for (int i = sbits - 1; i >= 0; --i) {
+    const int j = i + r;
+    const bool bit = (j == r) || (active && word_bit(nw, j));
+    // X = V_k V_k+1 - P; Y = (bit ? V_k+1 : V_k)^2 - 2
+    uint32_t X[K], Y[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      X[k] = vk[k];
+      Y[k] = bit ? vk1[k] : vk[k];
+    }
+    lds_store_digits<K>(bl, 0, vk1);
+    wave_lds_fence();
+    montmul<1, K, false>(X, bl, Nd, n0inv, m_src_addr, 0);
+    wave_lds_fence();
+    add_digits<K>(X, CP);
+    lds_store_digits<K>(bl, 0, Y);
+    wave_lds_fence();
+    montmul<1, K, true>(Y, bl, Nd, n0inv, m_src_addr, 0);
+    wave_lds_fence();
+    add_digits<K>(Y, C2);
+    // bit: k' = 2k+1 -> (V_2k+1, V_2k+2) = (X, Y); else k' = 2k -> (V_2k, V_2k+1) = (Y, X)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      vk[k] = bit ? X[k] : Y[k];
+      vk1[k] = bit ? Y[k] : X[k];
+    }
+  }
+  uint32_t NTwoR[K];  // Montgomery form of n - 2
+#pragma unroll
+  for (int k = 0; k < K; ++k) NTwoR[k] = Nd[k];
+  sub_digits<K>(NTwoR, TwoR);
+  canon_serial<K>(vk, Nd);
+  bool pass = false;
+  if (eq_digits<K>(vk, TwoR) || eq_digits<K>(vk, NTwoR)) {
+    // U_s == 0  <=>  P V_s == 2 V_s+1 (mod n)
+    uint32_t U1[K], U2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      U1[k] = vk[k];
+      U2[k] = vk1[k];
+    }
+    lds_store_digits<K>(bl, 0, PR);
+    wave_lds_fence();
+    montmul<1, K, false>(U1, bl, Nd, n0inv, m_src_addr, 0);  // P V_s R
+    wave_lds_fence();
+    canon_serial<K>(U1, Nd);
+    add_digits<K>(U2, vk1);  // 2 V_s+1 R (< 8n)
+    canon_serial<K>(U2, Nd);
+    pass = eq_digits<K>(U1, U2);
+  }
+  for (int t = 0; t < r - 1 && !pass; ++t) {
+    bool zero = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) zero &= vk[k] == 0u;
+    if (zero) {
+      pass = true;
+      break;
+    }
+    if (eq_digits<K>(vk, TwoR)) break;  // V = 2 is a fixed point of V^2 - 2: never 0
+    lds_store_digits<K>(bl, 0, vk);
+    wave_lds_fence();
+    montmul<1, K, true>(vk, bl, Nd, n0inv, m_src_addr, 0);
+    wave_lds_fence();
+    add_digits<K>(vk, C2);
+    canon_serial<K>(vk, Nd);
+  }
+  if (active) a.ok[op] = pass ? 1 : 0;
 }
 
 // ---------------------------------------------------------- Miller-Rabin
@@ -757,12 +957,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 // for some j < s. Serves q.ProbablyPrime(20) in the safe-prime search
 // (up:common/safe_prime.go). All Montgomery constants are derived on the
 // device: R mod n by doubling, R^2 mod n = Mont(2^(28K)) by square-and-double.
-template <int K>
-__device__ __forceinline__ void canon_serial(uint32_t (&x)[K], const uint32_t (&n)[K]) {
-  norm_serial<K>(x);
-  for (int it = 0; it < 8 && ge_digits<K>(x, n); ++it) sub_digits<K>(x, n);
-}
-
 template <int K, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_mr(const MrArgs a) {
   constexpr int L = K;

@@ -117,13 +117,6 @@ struct ExpSchedArgs {
   uint32_t* sched;      // MPCX_SCHED_WORDS(32 * exp_words) words
 };
 
-struct FermatArgs {
-  const uint32_t* p;  // count x p_words candidates
-  uint8_t* ok;
-  uint32_t count;
-  uint32_t p_words;
-  const uint32_t* count_dev;  // optional: candidates = min(count, *count_dev) (sieve output)
-};
 
 // Safe-prime candidate sieve (tss-lib runGenPrimeRoutine steps 1-3 plus exact
 // trial division of q and 2q+1, up:common/safe_prime.go): one thread per
@@ -140,6 +133,50 @@ struct SieveArgs {
   uint32_t* out_p;           // survivors: count x 32 words (p = 2q + 1)
   uint32_t* out_idx;         // survivors' candidate indices
   uint32_t* out_count;       // survivor counter (zeroed before the launch)
+};
+
+// Base-2 tests of the safe-prime search (k_prime2), one candidate per lane:
+// blocks [0, f_blocks): Fermat items 2^(n-1) == 1 (mod n) over the sieve
+// survivors nf[0 .. min(count_f, *count_dev)); blocks [f_blocks, ...): strong
+// probable-prime-to-base-2 items over ns[0 .. count_s) (the Fermat passes' q
+// of an earlier batch riding along in the same launch). n: n_words words.
+struct Prime2Args {
+  const uint32_t* nf;
+  uint32_t count_f;
+  const uint32_t* count_dev;  // optional: Fermat items = min(count_f, *count_dev)
+  uint32_t f_blocks;
+  uint8_t* ok_f;              // optional: per-item Fermat verdicts
+  // optional compaction of the Fermat passes: slot = atomicAdd(pass_count, 1),
+  // pass_idx[slot] = sieve_idx[item], pass_n[slot] = the item's n_words words
+  const uint32_t* sieve_idx;
+  uint32_t* pass_count;
+  uint32_t* pass_idx;
+  uint32_t* pass_n;
+  const uint32_t* ns;
+  uint32_t count_s;
+  uint8_t* ok_s;
+  uint32_t n_words;
+};
+
+// Strong Lucas probable-prime test (Go math/big probablyPrimeLucas, the
+// "extra strong" test with Baillie-OEIS method C parameters P, Q = 1,
+// D = P^2 - 4 with Jacobi(D, n) = -1; P is chosen by the caller).
+struct LucasArgs {
+  const uint32_t* n;   // count x n_words odd candidates, 5 <= n < 2^1024
+  const uint32_t* P;   // count parameters (3 <= P < 2^14)
+  uint8_t* ok;
+  uint32_t count;
+  uint32_t n_words;
+};
+
+// The build's CounterDRBG stream on the device: block c (32 bytes) =
+// SHA-256("mpcx-drbg" || seed as 8 LE bytes || c as 8 LE bytes); out[i] =
+// stream byte off + i for i < n.
+struct DrbgArgs {
+  uint64_t seed;
+  uint64_t off;
+  uint64_t n;
+  uint8_t* out;
 };
 
 struct MrArgs {

@@ -1,6 +1,7 @@
-// mpcx_prime.hip -- launchers of the safe-prime kernels (Fermat base 2,
-// Miller-Rabin; thread per candidate), the shared-exponent window schedule
-// (k_expsched) and the device self-test.
+// mpcx_prime.hip -- launchers of the safe-prime kernels (candidate stream
+// DRBG, sieve, base-2 Fermat / strong tests, Miller-Rabin, strong Lucas;
+// thread per candidate), the shared-exponent window schedule (k_expsched) and
+// the device self-test.
 #include "mpcx_device.hpp"
 
 namespace mpcx {
@@ -97,6 +98,88 @@ __global__ __launch_bounds__(64) void k_expsched(const ExpSchedArgs a) {
   s[MPCX_SCHED_WIDTH] = (uint32_t)w;
 }
 
+
+// ----------------------------------------------------- candidate stream
+// The build's CounterDRBG (csrc/host/tsscommon.cpp, oracle/gomath.py) on the
+// device: 32-byte block c = SHA-256("mpcx-drbg" || seed LE64 || c LE64). One
+// thread per block; the safe-prime search draws its candidates' bytes here
+// instead of hashing ~25 MB per batch on the host and copying them over PCIe.
+namespace {
+__device__ __forceinline__ uint32_t ror32(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
+__constant__ uint32_t kSha256K[64] = {
+    0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+    0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+    0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+    0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+    0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+    0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+    0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+    0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+}  // namespace
+
+__global__ __launch_bounds__(256) void k_drbg(const DrbgArgs a) {
+  const uint64_t b0 = a.off >> 5, b1 = (a.off + a.n + 31) >> 5;
+  const uint64_t c = b0 + (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (c >= b1) return;
+  // one padded block: "mpcx-drbg" (9) | seed (8, LE) | c (8, LE) | 0x80 | zeros | bit length 200
+  uint8_t m[64];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) m[i] = 0;
+  const char tag[9] = {'m', 'p', 'c', 'x', '-', 'd', 'r', 'b', 'g'};
+#pragma unroll
+  for (int i = 0; i < 9; ++i) m[i] = (uint8_t)tag[i];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    m[9 + i] = (uint8_t)(a.seed >> (8 * i));
+    m[17 + i] = (uint8_t)(c >> (8 * i));
+  }
+  m[25] = 0x80;
+  m[62] = 0x00;
+  m[63] = 200;  // 25 bytes * 8
+  uint32_t w[64];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    w[i] = (uint32_t)m[4 * i] << 24 | (uint32_t)m[4 * i + 1] << 16 | (uint32_t)m[4 * i + 2] << 8 | m[4 * i + 3];
+#pragma unroll
+  for (int i = 16; i < 64; ++i) {
+    const uint32_t s0 = ror32(w[i - 15], 7) ^ ror32(w[i - 15], 18) ^ (w[i - 15] >> 3);
+    const uint32_t s1 = ror32(w[i - 2], 17) ^ ror32(w[i - 2], 19) ^ (w[i - 2] >> 10);
+    w[i] = w[i - 16] + s0 + w[i - 7] + s1;
+  }
+  uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
+  uint32_t A = h[0], B = h[1], C = h[2], D = h[3], E = h[4], F = h[5], G = h[6], H = h[7];
+#pragma unroll
+  for (int i = 0; i < 64; ++i) {
+    const uint32_t S1 = ror32(E, 6) ^ ror32(E, 11) ^ ror32(E, 25);
+    const uint32_t ch = (E & F) ^ (~E & G);
+    const uint32_t t1 = H + S1 + ch + kSha256K[i] + w[i];
+    const uint32_t S0 = ror32(A, 2) ^ ror32(A, 13) ^ ror32(A, 22);
+    const uint32_t mj = (A & B) ^ (A & C) ^ (B & C);
+    const uint32_t t2 = S0 + mj;
+    H = G;
+    G = F;
+    F = E;
+    E = D + t1;
+    D = C;
+    C = B;
+    B = A;
+    A = t1 + t2;
+  }
+  h[0] += A; h[1] += B; h[2] += C; h[3] += D; h[4] += E; h[5] += F; h[6] += G; h[7] += H;
+  const uint64_t pos0 = c << 5;
+  if (pos0 >= a.off && pos0 + 32 <= a.off + a.n && ((pos0 - a.off) & 3u) == 0) {
+    // whole block inside the range, 4-byte aligned: 8 word stores (big-endian digest bytes)
+    uint32_t* o = (uint32_t*)(a.out + (pos0 - a.off));
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = __builtin_bswap32(h[i]);
+    return;
+  }
+#pragma unroll
+  for (int i = 0; i < 32; ++i) {
+    const uint64_t pos = pos0 + i;
+    if (pos >= a.off && pos < a.off + a.n) a.out[pos - a.off] = (uint8_t)(h[i >> 2] >> (24 - 8 * (i & 3)));
+  }
+}
 
 // ----------------------------------------------------- safe-prime sieve
 // One thread per candidate of tss-lib's runGenPrimeRoutine stream
@@ -211,9 +294,22 @@ __global__ __launch_bounds__(256) void k_sieve(const SieveArgs a) {
 
 extern "C" {
 
-__attribute__((visibility("hidden"))) hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks,
-                                                                    hipStream_t st) {
-  hipLaunchKernelGGL((mpcx::k_fermat2<MPCX_C0_K, MPCX_WAVES_PER_EU_FERMAT>), dim3(blocks), dim3(64), 0, st, *a);
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_prime2(const mpcx::Prime2Args* a, uint32_t blocks,
+                                                                   hipStream_t st) {
+  hipLaunchKernelGGL((mpcx::k_prime2<MPCX_C0_K, MPCX_WAVES_PER_EU_FERMAT>), dim3(blocks), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_lucas(const mpcx::LucasArgs* a, uint32_t blocks,
+                                                                  hipStream_t st) {
+  hipLaunchKernelGGL((mpcx::k_lucas<MPCX_C0_K, MPCX_WAVES_PER_EU_MR>), dim3(blocks), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_drbg(const mpcx::DrbgArgs* a, hipStream_t st) {
+  const uint64_t blocks = ((a->off + a->n + 31) >> 5) - (a->off >> 5);
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL(mpcx::k_drbg, dim3((uint32_t)((blocks + 255) / 256)), dim3(256), 0, st, *a);
   return hipGetLastError();
 }
 

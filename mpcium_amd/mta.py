@@ -45,7 +45,7 @@ SIGNATURES = [
     ("mpcxh_secp_scalar_base_mult", _i, [_vp, _u32, _vp]),
     ("mpcxh_secp_scalar_mult", _i, [_vp, _vp, _u32, _vp]),
     ("mpcxh_random_draws", _i, [_u64, _vp, _u32, _i, _u32, _vp]),
-    ("mpcxh_bench_signing_mta", _i, [_u32, _vp, _vp, _u32, _u32, _u32, _u64, _vp]),
+    ("mpcxh_bench_signing", _i, [_u32, _vp, _vp, _u32, _u32, _u32, _u64, _vp, _u32, _vp]),
 ]
 
 _bound = False
@@ -264,16 +264,48 @@ def random_draws(seed: int, less_than: int, count: int, relprime: bool = False) 
     return words_to_ints(o)
 
 
-def bench_signing_mta(nodes: Sequence[Dict[str, int]], signers: int, wallets: int, seed: int = 0x5167) -> dict:
-    """Config-4 driver (csrc/host/signing.hpp): the MtA work of one signature
-    for each of `wallets` wallets. nodes: dicts with N, LambdaN, P, Q, NTildei,
-    H1i, H2i, p, q (node_preparams.json fields)."""
+SIGNING_STATS = ["round1_s", "round2_s", "round3_s", "total_s", "wallets", "sessions", "errors",
+                 "relation_failures", "engine_busy_s", "finalize_s", "signatures", "verified", "alg_macs"]
+
+
+def bench_signing(nodes: Sequence[Dict[str, int]], signers: int, wallets: int, seed: int = 0x5167,
+                  trace_wallets: int = 0):
+    """Config-4 driver (csrc/host/signing.hpp): one GG18 signature for each of
+    `wallets` wallets -- MtA / MtAwc on the GPU, then the signature and
+    ecdsa.Verify. nodes: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i, p, q
+    (node_preparams.json fields). Returns the stats dict, and with
+    trace_wallets > 0 also the trace: {"pairs": [[{alpha, beta, mu, nu,
+    digest} per wallet] per ordered pair], "sigs": [(r, s, recid)]}."""
     k = _Keep()
     sks = (PaillierKey * len(nodes))(*[_paillier(k, n["N"], n["LambdaN"], n["P"], n["Q"]) for n in nodes])
     dlns = (DLN * len(nodes))(*[_dln(k, {"NTilde": n["NTildei"], "h1": n["H1i"], "h2": n["H2i"],
                                          "P": 2 * n["p"] + 1, "Q": 2 * n["q"] + 1}) for n in nodes])
-    st = np.zeros(9, dtype=np.float64)
-    _check(lib().mpcxh_bench_signing_mta(W, sks, dlns, len(nodes), signers, wallets, seed, st.ctypes.data))
-    keys = ["round1_s", "round2_s", "round3_s", "total_s", "wallets", "sessions", "errors", "relation_failures",
-            "engine_busy_s"]
-    return dict(zip(keys, [float(x) for x in st]))
+    st = np.zeros(len(SIGNING_STATS), dtype=np.float64)
+    npairs = signers * (signers - 1)
+    tw = min(trace_wallets, wallets)
+    tr = np.zeros(max(1, npairs * tw * 40 + tw * 17), dtype="<u4")
+    _check(lib().mpcxh_bench_signing(W, sks, dlns, len(nodes), signers, wallets, seed, st.ctypes.data, tw,
+                                     tr.ctypes.data if tw else None))
+    stats = dict(zip(SIGNING_STATS, [float(x) for x in st]))
+    if not tw:
+        return stats
+    pairs = []
+    for p in range(npairs):
+        rows = []
+        for wi in range(tw):
+            o = (p * tw + wi) * 40
+            a, b, m, n_, d = words_to_ints(tr[o:o + 40].reshape(5, 8))
+            rows.append({"alpha": a, "beta": b, "mu": m, "nu": n_, "digest": d})
+        pairs.append(rows)
+    base = npairs * tw * 40
+    sigs = []
+    for wi in range(tw):
+        o = base + wi * 17
+        r, s = words_to_ints(tr[o:o + 16].reshape(2, 8))
+        sigs.append((r, s, int(tr[o + 16])))
+    return stats, {"pairs": pairs, "sigs": sigs}
+
+
+def bench_signing_mta(nodes, signers: int, wallets: int, seed: int = 0x5167) -> dict:
+    """Back-compatible name of bench_signing (stats only)."""
+    return bench_signing(nodes, signers, wallets, seed)

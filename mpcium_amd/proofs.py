@@ -165,9 +165,9 @@ def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B
     for k, n in enumerate(parties):
         arr[k] = _Party(ptr(n["N"]), ptr(n["LambdaN"]), ptr(n["P"]), ptr(n["Q"]), ptr(n["NTildei"]), ptr(n["H1i"]),
                         ptr(n["H2i"]), ptr(n["Alpha"]), ptr(n["Beta"]), ptr(n["p"]), ptr(n["q"]))
-    st = np.zeros(9, dtype=np.float64)
+    st = np.zeros(10, dtype=np.float64)
     rc = lib().mpcxh_bench_keygen_proofs(W, arr, len(parties), sessions, seed, st.ctypes.data)
     _host._check(rc)
     keys = ["prove_s", "verify_s", "total_s", "sessions", "parties", "proofs", "verifications", "failures",
-            "engine_busy_s"]
+            "engine_busy_s", "alg_macs"]
     return dict(zip(keys, [float(x) for x in st]))

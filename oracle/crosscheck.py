@@ -96,17 +96,68 @@ def _from_words(arr, n: int) -> int:
     return sum(int(arr[i]) << (32 * i) for i in range(n))
 
 
-def load_c_oracle():
-    path = os.path.join(_HERE, "libgomodexp.so")
+_ARGS7 = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+
+
+def load_c_oracle(word_bits: int = 32):
+    """The C restatement of Go's expNN: word_bits 32 -> libgomodexp.so (the
+    parity oracle), 64 -> libgomodexp64.so (Go's amd64 word size, the CPU
+    baseline). Both expose gomodexp_expnn / gomodexp_montgomery over
+    little-endian 32-bit words."""
+    name = "libgomodexp.so" if word_bits == 32 else "libgomodexp64.so"
+    path = os.path.join(_HERE, name)
     if not os.path.exists(path):
         return None
     lib = ctypes.CDLL(path)
+    if word_bits == 64:
+        lib.gomodexp_expnn = lib.gomodexp64_expnn
+        lib.gomodexp_montgomery = lib.gomodexp64_montgomery
     for f in ("gomodexp_expnn", "gomodexp_montgomery"):
-        getattr(lib, f).argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
+        getattr(lib, f).argtypes = _ARGS7
         getattr(lib, f).restype = ctypes.c_int
-    lib.gomodexp_montgomery_batch.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p, ctypes.c_int]
-    lib.gomodexp_montgomery_batch.restype = ctypes.c_int
+    if word_bits == 32:
+        lib.gomodexp_montgomery_batch.argtypes = _ARGS7
+        lib.gomodexp_montgomery_batch.restype = ctypes.c_int
     return lib
+
+
+class GmpPowm:
+    """Repeated mpz_powm(x, y, m) on pre-set operands (CPU-baseline timing of
+    GMP, a faster proxy for Go math/big); None-safe: .ok is False without
+    libgmp."""
+
+    def __init__(self, x: int, y: int, m: int):
+        self.ok = _gmp is not None
+        if not self.ok:
+            return
+        self.zs = [_Mpz() for _ in range(4)]
+        g = lambda name: getattr(_gmp, name)  # noqa: E731 (no class-private name mangling)
+        for z in self.zs:
+            g("__gmpz_init")(ctypes.byref(z))
+        for z, v in zip(self.zs, (x, y, m)):
+            g("__gmpz_set_str")(ctypes.byref(z), ("%x" % v).encode(), 16)
+        self._powm = g("__gmpz_powm")
+        self._clear = g("__gmpz_clear")
+        self._args = [ctypes.byref(self.zs[3]), ctypes.byref(self.zs[0]), ctypes.byref(self.zs[1]),
+                      ctypes.byref(self.zs[2])]
+
+    def run(self):
+        self._powm(*self._args)
+
+    def close(self):
+        if self.ok:
+            for z in self.zs:
+                self._clear(ctypes.byref(z))
+            self.ok = False
+
+
+def gmp_version() -> Optional[str]:
+    if _gmp is None:
+        return None
+    try:
+        return ctypes.c_char_p.in_dll(_gmp, "__gmp_version").value.decode()
+    except (ValueError, AttributeError):
+        return "unknown"
 
 
 def c_expnn(lib, x: int, y: int, m: int) -> Optional[int]:

@@ -41,10 +41,12 @@ Q = T.SECP_N  # ec.Params().N for tss.EC() = secp256k1
 _pw = pow
 
 
-def use_go_modexp() -> bool:
+def use_go_modexp(word_bits: int = 32) -> bool:
+    """Route exponentiations through the C restatement of Go's expNN
+    (word_bits 64: Go's amd64 word size, the CPU baseline)."""
     global _pw
     from .crosscheck import c_expnn, load_c_oracle
-    lib = load_c_oracle()
+    lib = load_c_oracle(word_bits)
     if lib is None:
         return False
     _pw = lambda x, y, m: c_expnn(lib, x % m, y, m)  # noqa: E731
