@@ -330,7 +330,7 @@ def safeprime_line(num: int, seed: int, cpu: bool, info: dict, world: int = 1, r
     mhost.safe_primes(1024, 1, seed=seed + 1)  # warm-up (allocations, first launches)
     if world > 1:
         import torch.distributed as dist
-        acc = {"candidates": 0, "sieved_out": 0, "fermat_tests": 0, "mr_tests": 0}
+        acc = {"candidates": 0, "sieved_out": 0, "fermat_tests": 0, "mr_tests": 0, "lucas_tests": 0}
 
         def fn(b):
             r, s_ = mhost.safe_prime_batch(1024, seed, b)
@@ -352,12 +352,13 @@ def safeprime_line(num: int, seed: int, cpu: bool, info: dict, world: int = 1, r
         res, st = mhost.safe_primes(1024, num, seed=seed)
         el = time.perf_counter() - t0
     for p, q, _ in res:  # untimed: p = 2q + 1, both prime (CPython pow MR spot check)
-        if p != 2 * q + 1 or pow(2, p - 1, p) != 1 or pow(3, q - 1, q) != 1:
+        if p != 2 * q + 1 or pow(2, p - 1, p) != 1 or pow(3, q - 1, q) != 1 or q.bit_length() != 1023:
             raise SystemExit("safe-prime line: bad prime")
     line = {"metric": f"1024-bit safe primes/s (config 3: GeneratePreParams search, {world} GPU(s))",
             "value": num / el, "unit": "safe primes/s", "safe_primes": num, "seconds": el,
             "fermat_tests_per_s": st["fermat_tests"] / el, "candidates": st["candidates"],
             "sieved_out": st["sieved_out"], "fermat_tests": st["fermat_tests"], "mr_tests": st["mr_tests"],
+            "lucas_tests": st.get("lucas_tests", 0),
             "n_gpus": world, "scaling": "strong", "first_index": res[0][2], "last_index": res[-1][2],
             "roofline": _job_roofline((st["fermat_tests"] + st["mr_tests"]) * alg_macs(1024, 1023), el, world),
             "cpu_baseline": None}
@@ -569,6 +570,7 @@ def signing_line(args, world, rank, signers: int):
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    mhost.profile_report(reset=True)
     t0 = time.perf_counter()
     st = mta.bench_signing(nodes, signers, args.wallets, seed=0x5168 + 7919 * rank)
     torch.cuda.synchronize()
@@ -595,6 +597,9 @@ def signing_line(args, world, rank, signers: int):
             "scope": "MtA/MtAwc + range proofs (rounds 1-3) on the GPU; signature algebra + ecdsa.Verify on the "
                      "host; phase-5 commitments/Schnorr proofs (no Paillier work, no effect on (r, s)) not replayed",
             "cpu_baseline": None}
+    prof = mhost.profile_report()
+    if prof:  # MPCX_HOST_PROFILE=1: host seconds per label, summed over threads
+        line["host_profile"] = prof.strip().splitlines()
     return line
 
 
@@ -618,6 +623,7 @@ def main():
     ap.add_argument("--extra-lines", type=int, default=1,
                     help="1: add the config-1 (Paillier batch) and config-3 (safe primes) objects at N=1")
     ap.add_argument("--cpu-sign-seconds", type=float, default=20.0)
+    ap.add_argument("--safe-primes", type=int, default=64, help="config 3: 1024-bit safe primes to find")
     ap.add_argument("--modbits", type=int, default=4096, choices=(2048, 4096),
                     help="4096: x^N mod N^2 (config 2, the bench line); 2048: x^N mod N (Paillier N / N~ class)")
     args = ap.parse_args()
@@ -679,16 +685,6 @@ def main():
         step()
     torch.cuda.synchronize()
 
-    # untimed correctness sample
-    if args.verify:
-        out = d_out.cpu().numpy().view(np.uint32)
-        idx = np.linspace(0, count - 1, args.verify).astype(int)
-        xs = mpcx.words_to_ints(bases[idx])
-        zs = mpcx.words_to_ints(out[idx])
-        bad = [int(i) for i, x, z in zip(idx, xs, zs) if pow(x, N, N2) != z]
-        if bad:
-            raise SystemExit(f"rank {rank}: GPU results differ from pow() at operands {bad[:5]}")
-
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
@@ -703,6 +699,17 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step on `stream`
+
+    # untimed correctness sample of the last step's outputs (after the timed
+    # region so that --warmup 0 still checks real results)
+    if args.verify and args.steps + args.warmup > 0:
+        out = d_out.cpu().numpy().view(np.uint32)
+        idx = np.linspace(0, count - 1, args.verify).astype(int)
+        xs = mpcx.words_to_ints(bases[idx])
+        zs = mpcx.words_to_ints(out[idx])
+        bad = [int(i) for i, x, z in zip(idx, xs, zs) if pow(x, N, N2) != z]
+        if bad:
+            raise SystemExit(f"rank {rank}: GPU results differ from pow() at operands {bad[:5]}")
 
     from mpcium_amd.shard import max_over_ranks
     elapsed, kernel_ms = max_over_ranks([elapsed, kernel_ms], world)
@@ -751,7 +758,7 @@ def main():
         cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
         if world == 1:
             result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, info)
-        result["safe_prime"] = safeprime_line(8, 0x5AFE, cpu, info, world, rank)
+        result["safe_prime"] = safeprime_line(args.safe_primes, 0x5AFE, cpu, info, world, rank)
     if args.keygen_sessions > 0 and world == 1:
         result["keygen"] = keygen_line(args)
         result["keygen"]["cpu_baseline"] = keygen_cpu

@@ -201,6 +201,34 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
  * probablyPrimeMillerRabin, go:src/math/big/prime.go). */
 int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* bases, uint8_t* ok);
 
+/* Strong Lucas probable-prime test, the last step of Go's ProbablyPrime
+ * (go:src/math/big/prime.go probablyPrimeLucas, the "extra strong" test):
+ * ok[i] = n_i passes with parameters P[i], Q = 1 (Baillie-OEIS method C: the
+ * caller supplies the smallest P >= 3 with Jacobi(P^2 - 4, n_i) = -1 and
+ * handles the Jacobi = 0 / perfect-square exits). 5 <= n_i < 2^1024 odd,
+ * 3 <= P[i] < 2^14. Each candidate is its own modulus. */
+int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* P, uint8_t* ok);
+
+/* One pipelined step of the safe-prime search (up:common/safe_prime.go
+ * runGenPrimeRoutine) on one bound device, all in one stream:
+ *  - count candidates of nbytes = (q_bits+7)/8 stream bytes each: raw !=
+ *    NULL: count x nbytes bytes from the host reader; raw == NULL: the
+ *    CounterDRBG(seed) stream's bytes [stream_off, stream_off + count*nbytes),
+ *    drawn on the device (no host hashing, no PCIe copy);
+ *  - masks, delta walk, bit-length check and exact trial division of q and
+ *    p = 2q+1 (as mpcx_safeprime_sieve_fermat);
+ *  - in ONE launch: the Pocklington test 2^(p-1) == 1 (mod p) on every sieve
+ *    survivor, and the base-2 strong probable-prime test on n_sprp given q
+ *    (sprp_q: n_sprp x 32 words -- an earlier step's Fermat passes riding
+ *    along).
+ * Out: *n_sieved survivors (Fermat tests); *n_pass Fermat passes in stream
+ * order: pass_idx (candidate index within the step) and pass_p (p, 32 words each;
+ * both sized >= max_pass, else MPCX_ENOMEM); sprp_ok[n_sprp]. count may be 0
+ * (ride-along only). 63 <= q_bits <= 1023. */
+int mpcx_safeprime_step(uint64_t seed, const uint8_t* raw, uint64_t stream_off, uint32_t count, uint32_t q_bits,
+                        const uint32_t* sprp_q, uint32_t n_sprp, uint32_t max_pass, uint32_t* n_sieved,
+                        uint32_t* n_pass, uint32_t* pass_idx, uint32_t* pass_p, uint8_t* sprp_ok);
+
 /* Safe-prime candidate batch on the GPU (up:common/safe_prime.go
  * runGenPrimeRoutine steps 1-5): raw = count candidates' (q_bits+7)/8 random
  * bytes each, in stream order (63 <= q_bits <= 1023). Each candidate q is

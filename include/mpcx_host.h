@@ -86,9 +86,10 @@ int mpcxh_paillier_decrypt_batch(const uint32_t* N, uint32_t nw, const uint32_t*
                                  uint32_t* m, uint32_t mw, uint8_t* err);
 
 /* First `num` safe primes p = 2q+1 of bit_len bits in candidate-stream order.
- * Random source: rand_fn(rand_ctx, ...) if non-NULL, else the CounterDRBG
- * seeded with `seed`. p_out/q_out: num x words. index_out: stream positions.
- * stats_out[5]: candidates, sieved out, GPU Fermat tests, GPU MR tests, usec. */
+ * Random source: rand_fn(rand_ctx, ...) if non-NULL (read on the host), else
+ * the CounterDRBG seeded with `seed` (drawn on the GPU). p_out/q_out: num x
+ * words. index_out: stream positions. stats_out[6]: candidates, sieved out,
+ * GPU Fermat tests, GPU Miller-Rabin rounds, usec, GPU strong Lucas tests. */
 int mpcxh_safe_primes(int bit_len, int num, uint64_t seed, mpcxh_rand_fn rand_fn, void* rand_ctx,
                       uint32_t* p_out, uint32_t* q_out, uint32_t words, uint64_t* index_out,
                       uint64_t* stats_out);
@@ -104,7 +105,10 @@ int mpcxh_safe_prime_batch(int bit_len, uint64_t seed, uint64_t batch_no, uint32
                            uint32_t* n_found, uint64_t* stats_out);
 
 /* LocalPreParams as 12 fields x 64 words: N, LambdaN, PhiN, P, Q (Paillier),
- * NTildei, H1i, H2i, Alpha, Beta, P, Q (Germain primes of N~). */
+ * NTildei, H1i, H2i, Alpha, Beta, P, Q (Germain primes of N~). One stream:
+ * the Paillier search, then N~'s, then f and alpha; each search consumes the
+ * stream up to its last accepted candidate, as tss-lib at concurrency 1.
+ * stats_out[6] as mpcxh_safe_primes. */
 int mpcxh_generate_preparams(uint64_t seed, mpcxh_rand_fn rand_fn, void* rand_ctx,
                              uint32_t* out, uint64_t* stats_out);
 
@@ -252,6 +256,18 @@ int mpcxh_secp_scalar_base_mult(const uint32_t* k, uint32_t w, uint32_t* out16);
 int mpcxh_secp_scalar_mult(const uint32_t* p16, const uint32_t* k, uint32_t w, uint32_t* out16);
 int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int relprime, uint32_t count,
                        uint32_t* out);
+
+/* Go (*Int).ProbablyPrime(reps) for count odd or even n of `words` words
+ * (go:src/math/big/prime.go: small-prime exits, Miller-Rabin with base 2 and
+ * `reps` further bases, strong Lucas test for n < 2^1024; bases beyond 2 are
+ * the build's deterministic stream, not Go's math/rand one -- decisions agree
+ * except on a composite passing BPSW). ok[i] = 1: probably prime. */
+int mpcxh_probably_prime_batch(uint32_t count, const uint32_t* n, uint32_t words, int reps, uint8_t* ok);
+
+/* Host-time profile (environment MPCX_HOST_PROFILE=1 at process start, else
+ * empty): "label: seconds (calls)" lines summed over threads, largest first,
+ * written NUL-terminated into buf (truncated to cap); reset != 0 clears it. */
+int mpcxh_profile_report(char* buf, size_t cap, int reset);
 
 /* tss-lib candidate q from raw stream bytes (masking + delta walk; test hook). */
 int mpcxh_candidate_from_bytes(const uint8_t* bytes, size_t n, int q_bit_len, uint32_t* q_out, uint32_t words);

@@ -1,6 +1,8 @@
 // bignum.cpp -- see bignum.hpp.
 #include "bignum.hpp"
 
+#include "hostprof.hpp"
+
 #include <algorithm>
 #include <stdexcept>
 
@@ -351,6 +353,7 @@ void sub_shift(V64& a, const V64& b) {
 }  // namespace
 
 bool coprime_odd(const Nat& x, const Nat& m) {
+  MPCX_PROF("gcd.coprime_odd");
   if (m.is_zero() || !m.is_odd()) throw std::invalid_argument("coprime_odd: modulus must be odd");
   if (m == Nat(1)) return true;
   const Nat a = x >= m ? x % m : x;

@@ -4,12 +4,14 @@
 // libmpcx.so directly and keep its own ModInt/paillier code).
 #include "mpcx_host.h"
 
+#include <algorithm>
 #include <cstring>
 #include <functional>
 #include <string>
 #include <vector>
 
 #include "engine.hpp"
+#include "hostprof.hpp"
 #include "modint.hpp"
 #include "paillier.hpp"
 #include "mta.hpp"
@@ -253,25 +255,32 @@ int mpcxh_paillier_decrypt_batch(const uint32_t* N, uint32_t nw, const uint32_t*
   });
 }
 
+namespace {
+void put_stats(const SafePrimeStats& st, uint64_t* out) {
+  if (!out) return;
+  out[0] = st.candidates;
+  out[1] = st.sieved_out;
+  out[2] = st.fermat_tests;
+  out[3] = st.mr_tests;
+  out[4] = (uint64_t)(st.seconds * 1e6);
+  out[5] = st.lucas_tests;
+}
+}  // namespace
+
 int mpcxh_safe_primes(int bit_len, int num, uint64_t seed, mpcxh_rand_fn rand_fn, void* rand_ctx, uint32_t* p_out,
                       uint32_t* q_out, uint32_t words, uint64_t* index_out, uint64_t* stats_out) {
   return guard([&] {
     CounterDRBG drbg(seed);
-    RandFn rnd = rand_from(seed, rand_fn, rand_ctx, &drbg);
+    // CounterDRBG streams are drawn on the GPU; a caller's reader on the host
+    Stream src = rand_fn ? Stream(rand_from(seed, rand_fn, rand_ctx, &drbg)) : Stream(&drbg);
     SafePrimeStats st;
-    auto v = GetRandomSafePrimes(bit_len, num, rnd, &st);
+    auto v = GetRandomSafePrimes(bit_len, num, src, &st);
     for (int i = 0; i < num; ++i) {
       v[i].p.to_words(p_out + (size_t)i * words, words);
       v[i].q.to_words(q_out + (size_t)i * words, words);
       if (index_out) index_out[i] = v[i].index;
     }
-    if (stats_out) {
-      stats_out[0] = st.candidates;
-      stats_out[1] = st.sieved_out;
-      stats_out[2] = st.fermat_tests;
-      stats_out[3] = st.mr_tests;
-      stats_out[4] = (uint64_t)(st.seconds * 1e6);
-    }
+    put_stats(st, stats_out);
   });
 }
 
@@ -289,34 +298,41 @@ int mpcxh_safe_prime_batch(int bit_len, uint64_t seed, uint64_t batch_no, uint32
       if (index_out) index_out[i] = v[i].index;
     }
     *n_found = n;
-    if (stats_out) {
-      stats_out[0] = st.candidates;
-      stats_out[1] = st.sieved_out;
-      stats_out[2] = st.fermat_tests;
-      stats_out[3] = st.mr_tests;
-      stats_out[4] = (uint64_t)(st.seconds * 1e6);
-    }
+    put_stats(st, stats_out);
   });
 }
 
 int mpcxh_generate_preparams(uint64_t seed, mpcxh_rand_fn rand_fn, void* rand_ctx, uint32_t* out, uint64_t* stats_out) {
   return guard([&] {
     CounterDRBG drbg(seed);
-    RandFn rnd = rand_from(seed, rand_fn, rand_ctx, &drbg);
+    Stream src = rand_fn ? Stream(rand_from(seed, rand_fn, rand_ctx, &drbg)) : Stream(&drbg);
     SafePrimeStats st;
-    LocalPreParams pp = GeneratePreParams(rnd, &st);
+    LocalPreParams pp = GeneratePreParams(src, &st);
     const Nat* f[MPCXH_PREPARAM_FIELDS] = {&pp.PaillierSK.pub.N, &pp.PaillierSK.LambdaN, &pp.PaillierSK.PhiN,
                                            &pp.PaillierSK.P,     &pp.PaillierSK.Q,       &pp.NTildei,
                                            &pp.H1i,              &pp.H2i,                &pp.Alpha,
                                            &pp.Beta,             &pp.P,                  &pp.Q};
     for (int i = 0; i < MPCXH_PREPARAM_FIELDS; ++i) f[i]->to_words(out + (size_t)i * 64, 64);
-    if (stats_out) {
-      stats_out[0] = st.candidates;
-      stats_out[1] = st.sieved_out;
-      stats_out[2] = st.fermat_tests;
-      stats_out[3] = st.mr_tests;
-      stats_out[4] = (uint64_t)(st.seconds * 1e6);
-    }
+    put_stats(st, stats_out);
+  });
+}
+
+int mpcxh_probably_prime_batch(uint32_t count, const uint32_t* n, uint32_t words, int reps, uint8_t* ok) {
+  return guard([&] {
+    if (reps < 0) throw std::invalid_argument("negative reps");
+    const auto v = ProbablyPrimeBatch(nats(n, words, count), reps);
+    std::memcpy(ok, v.data(), count);
+  });
+}
+
+int mpcxh_profile_report(char* buf, size_t cap, int reset) {
+  return guard([&] {
+    if (!buf || !cap) throw std::invalid_argument("null buffer");
+    const std::string r = prof::report();
+    const size_t n = std::min(cap - 1, r.size());
+    std::memcpy(buf, r.data(), n);
+    buf[n] = 0;
+    if (reset) prof::reset();
   });
 }
 

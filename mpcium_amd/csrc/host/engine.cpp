@@ -1,6 +1,8 @@
 // engine.cpp -- see engine.hpp.
 #include "engine.hpp"
 
+#include "hostprof.hpp"
+
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
@@ -115,13 +117,17 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
   const bool shared = exps.size() == 1;
   uint32_t ew = 1;
   for (const auto& e : exps) ew = std::max<uint32_t>(ew, (uint32_t)e.words());
-  auto B = packed(bases);
-  auto E = pack(exps, ew);
-  std::vector<uint32_t> M;
-  if (muls) M = packed(*muls);
+  std::vector<uint32_t> B, E, M;
+  {
+    MPCX_PROF("engine.exp.pack");
+    B = packed(bases);
+    E = pack(exps, ew);
+    if (muls) M = packed(*muls);
+  }
   std::vector<uint32_t> out((size_t)bases.size() * md.words);
   count_work(m, exps, bases.size());
   int rc;
+  MPCX_PROF("engine.exp.gpu+unpack");
   enter_call();
   if (muls) {
     rc = mpcx_modexp_mul_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
@@ -193,6 +199,7 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
   }
   const uint32_t* ep = E.data();
   count_work(m, exps, exps.size());
+  MPCX_PROF("engine.fixed.gpu+unpack");
   enter_call();
   int rc = mpcx_fixedbase_exp_batch(1, &f->h, (uint32_t)exps.size(), &ep, &ew, muls ? Mw.data() : nullptr,
                                     muls ? md.class_words : 0, out.data(), md.words);
@@ -217,16 +224,41 @@ std::vector<uint8_t> Engine::fermat2(const std::vector<Nat>& cands) {
   return ok;
 }
 
-std::vector<std::pair<uint32_t, bool>> Engine::safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes,
-                                                                      uint32_t count, uint32_t q_bits) {
-  std::vector<uint32_t> idx(count);
-  std::vector<uint8_t> ok(count);
-  uint32_t n = 0;
-  int rc = mpcx_safeprime_sieve_fermat(raw, nbytes, count, q_bits, &n, idx.data(), ok.data());
-  if (rc) throw_last(rc, "mpcx_safeprime_sieve_fermat");
-  std::vector<std::pair<uint32_t, bool>> out(n);
-  for (uint32_t j = 0; j < n; ++j) out[j] = {idx[j], ok[j] != 0};
-  return out;
+Engine::StepOut Engine::safeprime_step(uint64_t seed, const uint8_t* raw, uint64_t stream_off, uint32_t count,
+                                       uint32_t q_bits, const std::vector<Nat>& sprp_q) {
+  constexpr uint32_t W = 32;  // MPCX_SIEVE_MAX_BYTES / 4
+  StepOut o;
+  // Pocklington passes per candidate fall like 1 / bits: size the pass buffers
+  // to the batch for small candidates, to 1/64 of it from 512-bit q up
+  const uint32_t max_pass = q_bits >= 511 ? std::max<uint32_t>(1024, count / 64) : std::max<uint32_t>(count, 1);
+  std::vector<uint32_t> pidx(max_pass), pp((size_t)max_pass * W), sq = pack(sprp_q, W);
+  std::vector<uint8_t> sok(std::max<size_t>(sprp_q.size(), 1));
+  uint32_t ns = 0, np = 0;
+  enter_call();
+  int rc = mpcx_safeprime_step(seed, raw, stream_off, count, q_bits, sprp_q.empty() ? nullptr : sq.data(),
+                               (uint32_t)sprp_q.size(), max_pass, &ns, &np, pidx.data(), pp.data(), sok.data());
+  leave_call();
+  if (rc) throw_last(rc, "mpcx_safeprime_step");
+  o.sieved = ns;
+  o.idx.assign(pidx.begin(), pidx.begin() + np);
+  o.p.resize(np);
+  for (uint32_t j = 0; j < np; ++j) o.p[j] = Nat::from_words(pp.data() + (size_t)j * W, W);
+  o.sprp.assign(sok.begin(), sok.begin() + sprp_q.size());
+  return o;
+}
+
+std::vector<uint8_t> Engine::lucas(const std::vector<Nat>& n, const std::vector<uint32_t>& P) {
+  if (n.size() != P.size()) throw std::invalid_argument("one P per candidate");
+  if (n.empty()) return {};
+  uint32_t w = 1;
+  for (const auto& c : n) w = std::max<uint32_t>(w, (uint32_t)c.words());
+  auto N = pack(n, w);
+  std::vector<uint8_t> ok(n.size());
+  enter_call();
+  int rc = mpcx_lucas_batch((uint32_t)n.size(), N.data(), w, P.data(), ok.data());
+  leave_call();
+  if (rc) throw_last(rc, "mpcx_lucas_batch");
+  return ok;
 }
 
 std::vector<uint8_t> Engine::strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases) {
@@ -240,7 +272,9 @@ std::vector<uint8_t> Engine::strong_probable_prime(const std::vector<Nat>& n, co
   auto N = pack(n, w);
   auto A = pack(b, w);
   std::vector<uint8_t> ok(n.size());
+  enter_call();
   int rc = mpcx_mr_batch((uint32_t)n.size(), N.data(), w, A.data(), ok.data());
+  leave_call();
   if (rc) throw_last(rc, "mpcx_mr_batch");
   return ok;
 }

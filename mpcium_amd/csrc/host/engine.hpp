@@ -73,11 +73,20 @@ class Engine {
     alg_macs_ = 0;
   }
   std::vector<uint8_t> fermat2(const std::vector<Nat>& cands);
-  // mpcx_safeprime_sieve_fermat: (index, Pocklington verdict) of the sieve
-  // survivors among `count` raw candidates, ascending index
-  std::vector<std::pair<uint32_t, bool>> safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t count,
-                                                                uint32_t q_bits);
+  // mpcx_safeprime_step: sieve + Pocklington over `count` stream candidates
+  // (raw bytes, or the CounterDRBG(seed) stream from byte stream_off), plus
+  // the base-2 strong test on sprp_q riding along in the same launch
+  struct StepOut {
+    uint32_t sieved = 0;           // sieve survivors = Pocklington tests
+    std::vector<uint32_t> idx;     // Fermat passes: candidate index within the step (ascending)
+    std::vector<Nat> p;            //                 and their p = 2q + 1
+    std::vector<uint8_t> sprp;     // verdicts for sprp_q
+  };
+  StepOut safeprime_step(uint64_t seed, const uint8_t* raw, uint64_t stream_off, uint32_t count, uint32_t q_bits,
+                         const std::vector<Nat>& sprp_q);
   std::vector<uint8_t> strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases);
+  // mpcx_lucas_batch: strong Lucas test with parameters P (n < 2^1024)
+  std::vector<uint8_t> lucas(const std::vector<Nat>& n, const std::vector<uint32_t>& P);
 
  private:
   struct Mod {

@@ -9,6 +9,7 @@
 
 #include "bignum.hpp"
 #include "engine.hpp"
+#include "hostprof.hpp"
 
 namespace mpcx::host {
 
@@ -80,6 +81,7 @@ class ExpSet {
   };
   static constexpr size_t kFixedMin = 64;  // requests on one base before a comb table pays
   void launch_fixed(const std::vector<size_t>& idx) {
+    MPCX_PROF("expset.launch_fixed");
     std::vector<Nat> exps, muls;
     exps.reserve(idx.size());
     bool any_mul = false;
@@ -92,6 +94,7 @@ class ExpSet {
     for (size_t j = 0; j < idx.size(); ++j) *reqs_[idx[j]].out = std::move(r[j]);
   }
   void launch(const std::vector<size_t>& idx, bool shared) {
+    MPCX_PROF("expset.launch");
     std::vector<Nat> bases, exps, muls;
     bases.reserve(idx.size());
     bool any_mul = false;

@@ -1,0 +1,43 @@
+// hostprof.hpp -- opt-in host-side time accounting (MPCX_HOST_PROFILE=1):
+// scoped timers summed per label over all threads, to see where the host
+// share of a protocol batch goes (hashing, random draws, gcds, packing, ...).
+// Off by default: one relaxed load per scope.
+#pragma once
+
+#include <atomic>
+#include <chrono>
+#include <cstdint>
+#include <string>
+
+namespace mpcx::host::prof {
+
+bool enabled();
+void add(int slot, uint64_t ns);
+int slot_of(const char* label);  // registers the label on first use
+std::string report();            // "label: seconds (calls)" lines, largest first
+void reset();
+
+class Scope {
+ public:
+  explicit Scope(int slot) : slot_(enabled() ? slot : -1) {
+    if (slot_ >= 0) t0_ = std::chrono::steady_clock::now();
+  }
+  ~Scope() {
+    if (slot_ >= 0)
+      add(slot_, (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - t0_)
+                     .count());
+  }
+
+ private:
+  int slot_;
+  std::chrono::steady_clock::time_point t0_;
+};
+
+}  // namespace mpcx::host::prof
+
+#define MPCX_PROF_CAT2(a, b) a##b
+#define MPCX_PROF_CAT(a, b) MPCX_PROF_CAT2(a, b)
+// MPCX_PROF("label"): time the rest of the enclosing scope under `label`
+#define MPCX_PROF(label)                                                       \
+  static const int MPCX_PROF_CAT(mpcx_prof_slot_, __LINE__) = ::mpcx::host::prof::slot_of(label); \
+  ::mpcx::host::prof::Scope MPCX_PROF_CAT(mpcx_prof_scope_, __LINE__)(MPCX_PROF_CAT(mpcx_prof_slot_, __LINE__))

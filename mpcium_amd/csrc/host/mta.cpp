@@ -8,6 +8,7 @@
 
 #include "engine.hpp"
 #include "expset.hpp"
+#include "hostprof.hpp"
 
 namespace mpcx::host::mta {
 namespace {
@@ -103,6 +104,7 @@ std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const 
   std::vector<uint8_t> ok(n, 0);
   std::vector<Nat> e(n), gs1(n), L1(n), R1(n), t(n), L2(n), R2(n), cr(n);
   parallel_for(n, [&](size_t i) {
+    MPCX_PROF("mta.verify_range.checks");
     const auto& p = pf[i];
     if (!IsInInterval(p.Z, dln.NTilde) || !IsInInterval(p.U, N2) || !IsInInterval(p.W, dln.NTilde) ||
         !IsInInterval(p.S, pk.N))
@@ -243,6 +245,7 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
   std::vector<uint8_t> ok(n, 0);
   std::vector<Nat> e(n), gt1(n), p1(n), p2(n), r1(n), r2(n), q1(n), r3(n), l1(n), l2(n), l3(n);
   parallel_for(n, [&](size_t i) {
+    MPCX_PROF("mta.verify_bob.checks");
     const auto& p = pf[i];
     if (X && !secp::IsOnCurve(p.U)) return;
     const Nat& Nt = dln.NTilde;
@@ -347,6 +350,7 @@ void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& p
   std::vector<BobProveState> st(k);
   std::vector<Nat> cRand(k), gbp(k), cbp(k), gg(k);
   parallel_for(k, [&](size_t j) {
+    MPCX_PROF("mta.bob_mid.draws");
     const size_t i = idx[j];
     auto& o = (*out)[i];
     o.betaPrm = GetRandomPositiveInt(rand[i], pkA.N);                 // betaPrm < N

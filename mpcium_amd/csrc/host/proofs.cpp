@@ -5,6 +5,7 @@
 #include <stdexcept>
 
 #include "expset.hpp"
+#include "safeprime.hpp"
 #include "secp256k1.hpp"
 
 namespace mpcx::host::proofs {
@@ -21,26 +22,6 @@ int legendre_from(const Nat& r, const Nat& p) {
 }
 
 Nat mulmod(const Nat& a, const Nat& b, const Nat& m) { return (a * b) % m; }
-
-// x^(2^s d) base-2 strong probable prime test of odd n >= 5 (one GPU modexp)
-bool sprp_base2(const Nat& n) {
-  if (n < Nat(5)) return n == Nat(2) || n == Nat(3);
-  const Nat nm1 = n - Nat(1);
-  uint32_t s = 0;
-  while (!nm1.bit(s)) ++s;
-  const Nat d = nm1 >> s;
-  ExpSet e(n);
-  Nat x;
-  const Nat two(2);
-  e.add(two, d, &x);
-  e.run();
-  if (x == Nat(1) || x == nm1) return true;
-  for (uint32_t i = 1; i < s; ++i) {
-    x = mulmod(x, x, n);
-    if (x == nm1) return true;
-  }
-  return false;
-}
 
 std::vector<Nat> mod_challenges(const Bytes& session, const Nat& W, const Nat& N) {
   std::vector<Nat> Y;
@@ -237,7 +218,7 @@ std::vector<uint8_t> ModVerifyBatch(const std::vector<Bytes>& session, const Nat
   if (session.size() != n) throw std::invalid_argument("ModProof.Verify: sizes");
   std::vector<uint8_t> ok(n, 0);
   if (N.is_zero() || !N.is_odd()) return ok;
-  if (sprp_base2(N)) return ok;  // N.ProbablyPrime(30) (see proofs.hpp)
+  if (ProbablyPrimeBatch({N}, 30)[0]) return ok;  // Fig 16: N.ProbablyPrime(30) -> reject (see proofs.hpp)
   const Nat one(1);
   const Nat ref = one << kModIterations;
   std::vector<std::vector<Nat>> Y(n), ZN(n), X4(n);

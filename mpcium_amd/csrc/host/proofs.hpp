@@ -21,8 +21,11 @@
 // quadratic-residue tests of the Mod prover run as Euler-criterion Legendre
 // symbols mod P and Q on the GPU (equal to Go's Jacobi for prime moduli),
 // combined multiplicatively over the four candidates (-1)^a W^b Y; N's
-// compositeness in Mod verify (Go: !N.ProbablyPrime(30)) is a base-2 strong
-// probable-prime test (identical except for base-2 strong pseudoprimes).
+// compositeness in Mod verify (Go: N.ProbablyPrime(30) -> reject) is
+// ProbablyPrimeBatch(N, 30): Miller-Rabin with base 2 and 30 further bases on
+// the GPU (a 2048-bit N is beyond the Lucas kernel's class; a composite N
+// passing 31 rounds is the only divergence from Go, and would make the
+// verifier reject, never accept).
 #pragma once
 
 #include <cstdint>

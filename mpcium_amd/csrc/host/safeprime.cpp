@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <future>
 #include <thread>
 
 #include "engine.hpp"
@@ -102,14 +103,16 @@ bool passes_trial(const Nat& q) {
   return true;
 }
 
-// 20 deterministic Miller-Rabin bases in [2, q-2] for candidate q, plus base 2
-std::vector<Nat> mr_bases(const Nat& q) {
+// Miller-Rabin bases of ProbablyPrime(reps): base 2 (Go's forced last round)
+// first, then `reps` bases in [2, n-2] from a CounterDRBG seeded with the
+// candidate's low word (Go seeds math/rand with it; see safeprime.hpp)
+std::vector<Nat> mr_bases(const Nat& q, int reps) {
   std::vector<Nat> out{Nat(2)};
   CounterDRBG rng(q.low64() ^ 0x4d52u);
   const uint32_t bits = q.bit_len();
   const Nat lim = q - Nat(3);
   std::vector<uint8_t> buf((bits + 7) / 8);
-  while (out.size() < 21) {
+  while ((int)out.size() < reps + 1) {
     rng.read(buf.data(), buf.size());
     Nat v = Nat::from_bytes_be(buf.data(), buf.size()) % lim;
     out.push_back(v + Nat(2));
@@ -118,88 +121,175 @@ std::vector<Nat> mr_bases(const Nat& q) {
 }
 }  // namespace
 
+// ------------------------------------------------------------ Stream
+void Stream::read(uint8_t* out, size_t n) {
+  const size_t from_pb = std::min(n, pushback_.size() - pb_pos_);
+  if (from_pb) {
+    std::memcpy(out, pushback_.data() + pb_pos_, from_pb);
+    pb_pos_ += from_pb;
+    if (pb_pos_ == pushback_.size()) {
+      pushback_.clear();
+      pb_pos_ = 0;
+    }
+    out += from_pb;
+    n -= from_pb;
+  }
+  if (!n) return;
+  if (drbg_) drbg_->read(out, n);
+  else fn_(out, n);
+}
+
+void Stream::unread(const uint8_t* data, size_t n) {
+  if (!n) return;
+  if (drbg_ && pushback_.empty()) {  // a CounterDRBG just steps back
+    drbg_->seek(drbg_->position() - n);
+    return;
+  }
+  std::vector<uint8_t> nb(data, data + n);
+  nb.insert(nb.end(), pushback_.begin() + (long)pb_pos_, pushback_.end());
+  pushback_.swap(nb);
+  pb_pos_ = 0;
+}
+
+// ------------------------------------------------------------ ProbablyPrime
+int LucasParam(const Nat& n, uint32_t* P) {
+  // go:src/math/big/prime.go probablyPrimeLucas: smallest P >= 3 with
+  // Jacobi(P^2 - 4, n) = -1; Jacobi 0 means p + 2 | n; a square n never gets -1
+  for (uint32_t p = 3;; ++p) {
+    if (p > 10000) throw std::runtime_error("LucasParam: no D with (D/n) = -1");
+    const int j = jacobi(Nat((uint64_t)p * p - 4), n);
+    if (j == -1) {
+      *P = p;
+      return 1;
+    }
+    if (j == 0) return n == Nat(p + 2) ? 2 : 0;
+    if (p == 40) {
+      const Nat r = isqrt(n);
+      if (r * r == n) return 0;
+    }
+  }
+}
+
+std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, SafePrimeStats* stats) {
+  const size_t cnt = n.size();
+  std::vector<uint8_t> ok(cnt, 0);
+  static const uint32_t kSmall[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53};
+  const uint64_t mask = (1ull << 2) | (1ull << 3) | (1ull << 5) | (1ull << 7) | (1ull << 11) | (1ull << 13) |
+                        (1ull << 17) | (1ull << 19) | (1ull << 23) | (1ull << 29) | (1ull << 31) | (1ull << 37) |
+                        (1ull << 41) | (1ull << 43) | (1ull << 47) | (1ull << 53) | (1ull << 59) | (1ull << 61);
+  std::vector<size_t> live;
+  for (size_t i = 0; i < cnt; ++i) {
+    const Nat& x = n[i];
+    if (x.bit_len() <= 6) {  // x < 64
+      ok[i] = (uint8_t)((mask >> x.low64()) & 1u);
+      continue;
+    }
+    if (!x.is_odd()) continue;
+    bool div = false;
+    for (uint32_t p : kSmall) div |= x.mod_u32(p) == 0;
+    if (!div) live.push_back(i);
+  }
+  // Miller-Rabin: base 2 first; the other bases only for its survivors
+  std::vector<size_t> small, large;  // GPU thread-per-candidate class (< 2^1024) / wider
+  for (size_t i : live) (n[i].bit_len() <= 1024 ? small : large).push_back(i);
+  uint64_t mr = 0, lt = 0;
+  if (!small.empty()) {
+    std::vector<Nat> nn, aa;
+    for (size_t i : small) {
+      nn.push_back(n[i]);
+      aa.push_back(Nat(2));
+    }
+    auto r2 = Engine::get().strong_probable_prime(nn, aa);
+    mr += nn.size();
+    std::vector<size_t> s2;
+    for (size_t j = 0; j < small.size(); ++j)
+      if (r2[j]) s2.push_back(small[j]);
+    nn.clear();
+    aa.clear();
+    std::vector<size_t> owner;
+    for (size_t i : s2) {
+      const auto bs = mr_bases(n[i], reps);
+      for (size_t b = 1; b < bs.size(); ++b) {
+        nn.push_back(n[i]);
+        aa.push_back(bs[b]);
+        owner.push_back(i);
+      }
+    }
+    std::vector<uint8_t> pass(cnt, 0);
+    for (size_t i : s2) pass[i] = 1;
+    if (!nn.empty()) {
+      auto rr = Engine::get().strong_probable_prime(nn, aa);
+      mr += nn.size();
+      for (size_t j = 0; j < nn.size(); ++j)
+        if (!rr[j]) pass[owner[j]] = 0;
+    }
+    // strong Lucas test on the Miller-Rabin survivors
+    std::vector<Nat> ln;
+    std::vector<uint32_t> lp;
+    std::vector<size_t> lo;
+    for (size_t i : s2) {
+      if (!pass[i]) continue;
+      uint32_t P = 0;
+      const int lr = LucasParam(n[i], &P);
+      if (lr != 1) {
+        ok[i] = lr == 2;
+        continue;
+      }
+      ln.push_back(n[i]);
+      lp.push_back(P);
+      lo.push_back(i);
+    }
+    if (!ln.empty()) {
+      auto lr = Engine::get().lucas(ln, lp);
+      lt += ln.size();
+      for (size_t j = 0; j < ln.size(); ++j) ok[lo[j]] = lr[j];
+    }
+  }
+  for (size_t i : large) {
+    // > 1024 bits: base 2 + reps bases as one shared-exponent launch (x^d for
+    // every base), the squarings on the host; no Lucas step (see the header)
+    const Nat& x = n[i];
+    const Nat nm1 = x - Nat(1);
+    uint32_t s = 0;
+    while (!nm1.bit(s)) ++s;
+    const Nat d = nm1 >> s;
+    const auto bs = mr_bases(x, reps);
+    std::vector<Nat> ys = Engine::get().exp(x, bs, std::vector<Nat>{d});
+    mr += bs.size();
+    bool all = true;
+    for (Nat y : ys) {
+      if (y == Nat(1) || y == nm1) continue;
+      bool hit = false;
+      for (uint32_t j = 1; j < s && !hit; ++j) {
+        y = (y * y) % x;
+        if (y == Nat(1)) break;
+        hit = y == nm1;
+      }
+      if (!hit) {
+        all = false;
+        break;
+      }
+    }
+    ok[i] = all;
+  }
+  if (stats) {
+    stats->mr_tests += mr;
+    stats->lucas_tests += lt;
+  }
+  return ok;
+}
+
 namespace {
 void check_safe_prime_args(int bitLen) {
   if (bitLen < 6) throw std::invalid_argument("safe prime size must be at least 6 bits");
   if (bitLen > 1024) throw std::invalid_argument("GPU candidate class holds safe primes up to 1024 bits");
 }
 
-size_t default_batch(int bitLen) { return bitLen - 1 >= 63 ? 196608 : 16384; }
-
-// One batch of the candidate stream (raw = batch x nbytes of stream bytes whose
-// first candidate has stream index base_index): sieve, Pocklington, Miller-Rabin.
-// Appends the accepted safe primes in stream order, at most `limit` of them.
-void test_batch(int bitLen, const uint8_t* raw, size_t batch, uint64_t base_index, SafePrimeStats& st,
-                std::vector<GermainSafePrime>& out, size_t limit) {
-  const int qBitLen = bitLen - 1;
-  const size_t nbytes = (size_t)(qBitLen + 7) / 8;
-  // GPU sieve (mpcx_safeprime_sieve_fermat) for q of 63..1023 bits: candidate
-  // masks, delta walk, trial division and the Pocklington test all on the
-  // device; the host draws the stream and runs Miller-Rabin on the rare
-  // Fermat survivors. Smaller sizes keep the host sieve.
-  const bool gpu_sieve = qBitLen >= 63;
-  const unsigned nthreads = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
-  // Fermat survivors (stream order): candidate index in the batch and q
-  std::vector<size_t> fidx;
-  std::vector<Nat> fq;
-  if (gpu_sieve) {
-    const auto sv = Engine::get().safeprime_sieve_fermat(raw, (uint32_t)nbytes, (uint32_t)batch, (uint32_t)qBitLen);
-    st.sieved_out += batch - sv.size();
-    st.fermat_tests += sv.size();
-    for (const auto& [i, ok] : sv) {
-      if (!ok) continue;
-      fidx.push_back(i);
-      fq.push_back(CandidateFromBytes(raw + (size_t)i * nbytes, nbytes, qBitLen));
-    }
-  } else {
-    std::vector<Nat> qs(batch);
-    std::vector<uint8_t> keep(batch, 0);
-    auto work = [&](size_t lo, size_t hi) {
-      for (size_t i = lo; i < hi; ++i) {
-        qs[i] = CandidateFromBytes(raw + i * nbytes, nbytes, qBitLen);
-        keep[i] = (qs[i].bit_len() == (uint32_t)qBitLen) && (bitLen <= 12 || passes_trial(qs[i]));
-      }
-    };
-    std::vector<std::thread> th;
-    const size_t chunk = (batch + nthreads - 1) / nthreads;
-    for (unsigned t = 0; t < nthreads; ++t) {
-      const size_t lo = t * chunk, hi = std::min(batch, lo + chunk);
-      if (lo < hi) th.emplace_back(work, lo, hi);
-    }
-    for (auto& t : th) t.join();
-    std::vector<size_t> idx;
-    std::vector<Nat> ps;
-    for (size_t i = 0; i < batch; ++i) {
-      if (!keep[i]) continue;
-      idx.push_back(i);
-      ps.push_back((qs[i] << 1) + Nat(1));
-    }
-    st.sieved_out += batch - idx.size();
-    st.fermat_tests += ps.size();
-    // GPU: Pocklington criterion 2^(p-1) == 1 mod p on every survivor
-    std::vector<uint8_t> f = bitLen >= 4 ? Engine::get().fermat2(ps) : std::vector<uint8_t>(ps.size(), 1);
-    for (size_t j = 0; j < idx.size(); ++j) {
-      if (!f[j]) continue;
-      fidx.push_back(idx[j]);
-      fq.push_back(qs[idx[j]]);
-    }
-  }
-  st.candidates += batch;
-  // GPU: Miller-Rabin on q for the Fermat survivors, in stream order
-  std::vector<Nat> mr_n, mr_a;
-  for (const Nat& q : fq)
-    for (const Nat& a : mr_bases(q)) {
-      mr_n.push_back(q);
-      mr_a.push_back(a);
-    }
-  st.mr_tests += mr_n.size();
-  std::vector<uint8_t> mr = Engine::get().strong_probable_prime(mr_n, mr_a);
-  for (size_t s = 0; s < fq.size() && out.size() < limit; ++s) {
-    bool prime = true;
-    for (size_t r = 0; r < 21; ++r) prime &= mr[s * 21 + r] != 0;
-    if (!prime) continue;
-    out.push_back({(fq[s] << 1) + Nat(1), fq[s], base_index + fidx[s]});
-  }
+// candidates per batch: ~45K per 1024-bit safe prime, far fewer at small sizes
+size_t default_batch(int bitLen) {
+  if (bitLen > 512) return 262144;
+  if (bitLen > 256) return 65536;
+  return 16384;
 }
 
 void add_stats(SafePrimeStats* stats, const SafePrimeStats& st) {
@@ -208,53 +298,207 @@ void add_stats(SafePrimeStats* stats, const SafePrimeStats& st) {
   stats->sieved_out += st.sieved_out;
   stats->fermat_tests += st.fermat_tests;
   stats->mr_tests += st.mr_tests;
+  stats->lucas_tests += st.lucas_tests;
   stats->seconds += st.seconds;
 }
+
+// Host-sieve path for q below the GPU sieve's 63 bits: one batch of raw
+// stream bytes -> (candidate index, q) of its Fermat passes.
+void small_batch(int bitLen, const uint8_t* raw, size_t batch, SafePrimeStats& st, std::vector<uint32_t>* fidx,
+                 std::vector<Nat>* fq) {
+  const int qBitLen = bitLen - 1;
+  const size_t nbytes = (size_t)(qBitLen + 7) / 8;
+  std::vector<Nat> qs(batch), ps;
+  std::vector<uint8_t> keep(batch, 0);
+  parallel_for(batch, [&](size_t i) {
+    qs[i] = CandidateFromBytes(raw + i * nbytes, nbytes, qBitLen);
+    keep[i] = (qs[i].bit_len() == (uint32_t)qBitLen) && (bitLen <= 12 || passes_trial(qs[i]));
+  });
+  std::vector<uint32_t> idx;
+  for (size_t i = 0; i < batch; ++i) {
+    if (!keep[i]) continue;
+    idx.push_back((uint32_t)i);
+    ps.push_back((qs[i] << 1) + Nat(1));
+  }
+  st.sieved_out += batch - idx.size();
+  st.fermat_tests += ps.size();
+  std::vector<uint8_t> f = bitLen >= 4 ? Engine::get().fermat2(ps) : std::vector<uint8_t>(ps.size(), 1);
+  for (size_t j = 0; j < idx.size(); ++j)
+    if (f[j]) {
+      fidx->push_back(idx[j]);
+      fq->push_back(qs[idx[j]]);
+    }
+}
+
+// q (< 2^1023) that passed the base-2 Miller-Rabin round: the remaining
+// ProbablyPrime(20) rounds and the strong Lucas test
+std::vector<uint8_t> finish_q(const std::vector<Nat>& qs, SafePrimeStats& st) {
+  // ProbablyPrimeBatch redoes base 2 on these few survivors (negligible)
+  return ProbablyPrimeBatch(qs, 20, &st);
+}
 }  // namespace
+
+std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, Stream& src, SafePrimeStats* stats,
+                                                  size_t batch, uint64_t max_candidates) {
+  check_safe_prime_args(bitLen);
+  if (numPrimes < 1) throw std::invalid_argument("numPrimes should be > 0");
+  const auto t0 = std::chrono::steady_clock::now();
+  SafePrimeStats st;
+  const int qBitLen = bitLen - 1;
+  const size_t nbytes = (size_t)(qBitLen + 7) / 8;
+  if (batch == 0) batch = default_batch(bitLen);
+  const bool gpu = qBitLen >= 63;
+  CounterDRBG* dev = gpu ? src.device_stream() : nullptr;
+  const uint64_t off0 = dev ? dev->position() : 0;
+  std::vector<std::vector<uint8_t>> raws;  // host-read batches (given back past the last accepted candidate)
+  std::vector<GermainSafePrime> acc;        // accepted, stream order (decided candidates only)
+  // Pipeline (one step per batch): step k runs the sieve + Pocklington of
+  // batch k and the base-2 round of batch k-1's Fermat passes; batch k-1's
+  // base-2 survivors then finish (other rounds + Lucas) while step k+1 runs.
+  // Batches are decided in order, so `acc` only ever holds decided batches.
+  struct Cand {
+    uint64_t index;
+    Nat q;
+  };
+  std::vector<Cand> fermat_prev;  // Fermat passes of the previous batch
+  std::vector<Cand> running;      // stage B in flight
+  std::future<std::vector<uint8_t>> job;
+  SafePrimeStats stb;             // stage-B counters (joined before use)
+  auto absorb = [&](const std::vector<Cand>& c, const std::vector<uint8_t>& v) {
+    for (size_t j = 0; j < c.size(); ++j)
+      if (v[j]) acc.push_back({(c[j].q << 1) + Nat(1), c[j].q, c[j].index});
+  };
+  auto join = [&] {
+    if (job.valid()) absorb(running, job.get());
+    running.clear();
+  };
+  auto qs_of = [](const std::vector<Cand>& c) {
+    std::vector<Nat> qs;
+    for (const auto& x : c) qs.push_back(x.q);
+    return qs;
+  };
+  uint64_t next = 0;  // next candidate index to draw
+  for (;;) {
+    const bool more = next < max_candidates;
+    if (!more && fermat_prev.empty() && !job.valid()) break;
+    const uint64_t first = next;
+    const uint32_t count = more ? (uint32_t)batch : 0u;
+    const std::vector<Nat> ride = qs_of(fermat_prev);
+    std::vector<uint32_t> fidx;
+    std::vector<Nat> fq;
+    std::vector<uint8_t> sprp;
+    if (gpu) {
+      std::vector<uint8_t> raw;
+      if (count && !dev) {
+        raw.resize((size_t)count * nbytes);
+        src.read(raw.data(), raw.size());
+      }
+      const auto o = Engine::get().safeprime_step(dev ? dev->seed() : 0, raw.empty() ? nullptr : raw.data(),
+                                                  off0 + first * nbytes, count, (uint32_t)qBitLen, ride);
+      st.sieved_out += count - o.sieved;
+      st.fermat_tests += o.sieved;
+      fidx = o.idx;
+      for (const auto& p : o.p) fq.push_back(p >> 1);  // q = (p - 1) / 2
+      sprp = o.sprp;
+      if (!raw.empty()) raws.push_back(std::move(raw));
+    } else {
+      if (count) {
+        std::vector<uint8_t> raw((size_t)count * nbytes);
+        src.read(raw.data(), raw.size());
+        small_batch(bitLen, raw.data(), count, st, &fidx, &fq);
+        raws.push_back(std::move(raw));
+      }
+      const std::vector<Nat> two(ride.size(), Nat(2));
+      sprp = Engine::get().strong_probable_prime(ride, two);
+    }
+    st.mr_tests += ride.size();
+    st.candidates += count;
+    next += count;
+    std::vector<Cand> surv;  // previous batch's base-2 survivors
+    for (size_t j = 0; j < fermat_prev.size(); ++j)
+      if (sprp[j]) surv.push_back(fermat_prev[j]);
+    join();  // the batch before the previous one is decided
+    if (acc.size() >= (size_t)numPrimes) break;
+    if (acc.size() + surv.size() >= (size_t)numPrimes || !more) {
+      // its probable primes may suffice: finish them now rather than draw on
+      absorb(surv, finish_q(qs_of(surv), stb));
+      if (acc.size() >= (size_t)numPrimes) break;
+    } else {
+      running = std::move(surv);
+      job = std::async(std::launch::async, [qs = qs_of(running), &stb] { return finish_q(qs, stb); });
+    }
+    fermat_prev.clear();
+    for (size_t j = 0; j < fidx.size(); ++j) fermat_prev.push_back({first + fidx[j], fq[j]});
+  }
+  join();
+  st.mr_tests += stb.mr_tests;
+  st.lucas_tests += stb.lucas_tests;
+  std::sort(acc.begin(), acc.end(), [](const auto& a, const auto& b) { return a.index < b.index; });
+  if ((int)acc.size() < numPrimes) throw std::runtime_error("safe prime search exhausted max_candidates");
+  acc.resize((size_t)numPrimes);
+  // leave the stream right after the last accepted candidate
+  const uint64_t consumed = (acc.back().index + 1) * nbytes;
+  if (dev) {
+    dev->seek(off0 + consumed);
+  } else {
+    uint64_t pos = 0;
+    std::vector<uint8_t> back;
+    for (const auto& r : raws) {
+      const uint64_t lo = pos, hi = pos + r.size();
+      if (hi > consumed) {
+        const uint64_t from = consumed > lo ? consumed - lo : 0;
+        back.insert(back.end(), r.begin() + (long)from, r.end());
+      }
+      pos = hi;
+    }
+    src.unread(back.data(), back.size());
+  }
+  st.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  add_stats(stats, st);
+  return acc;
+}
+
+std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, const RandFn& rand,
+                                                  SafePrimeStats* stats, size_t batch, uint64_t max_candidates) {
+  Stream s(rand);
+  return GetRandomSafePrimes(bitLen, numPrimes, s, stats, batch, max_candidates);
+}
 
 std::vector<GermainSafePrime> SafePrimeBatch(int bitLen, uint64_t seed, uint64_t batch_no, size_t batch,
                                              SafePrimeStats* stats) {
   check_safe_prime_args(bitLen);
   const auto t0 = std::chrono::steady_clock::now();
   if (batch == 0) batch = default_batch(bitLen);
-  const size_t nbytes = (size_t)(bitLen - 1 + 7) / 8;
-  std::vector<uint8_t> raw(nbytes * batch);
-  CounterDRBG drbg(seed);
-  drbg.seek(batch_no * (uint64_t)raw.size());
-  drbg.read(raw.data(), raw.size());
+  const int qBitLen = bitLen - 1;
+  const size_t nbytes = (size_t)(qBitLen + 7) / 8;
   SafePrimeStats st;
-  std::vector<GermainSafePrime> out;
-  test_batch(bitLen, raw.data(), batch, batch_no * batch, st, out, SIZE_MAX);
-  st.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  add_stats(stats, st);
-  return out;
-}
-
-std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, const RandFn& rand,
-                                                  SafePrimeStats* stats, size_t batch, uint64_t max_candidates) {
-  check_safe_prime_args(bitLen);
-  if (numPrimes < 1) throw std::invalid_argument("numPrimes should be > 0");
-  const auto t0 = std::chrono::steady_clock::now();
-  SafePrimeStats st;
-  const size_t nbytes = (size_t)(bitLen - 1 + 7) / 8;
-  if (batch == 0) batch = default_batch(bitLen);
-  std::vector<GermainSafePrime> out;
-  std::vector<uint8_t> raw(nbytes * batch);
-  uint64_t index = 0;
-  while ((int)out.size() < numPrimes && index < max_candidates) {
-    // draw a batch from the stream: one read of batch candidates' bytes is the
-    // same byte stream as batch sequential reads (stream order is the contract)
-    rand(raw.data(), nbytes * batch);
-    test_batch(bitLen, raw.data(), batch, index, st, out, (size_t)numPrimes);
-    index += batch;
+  std::vector<uint32_t> fidx;
+  std::vector<Nat> fq;
+  if (qBitLen >= 63) {
+    const auto o = Engine::get().safeprime_step(seed, nullptr, batch_no * batch * nbytes, (uint32_t)batch,
+                                                (uint32_t)qBitLen, {});
+    st.sieved_out += batch - o.sieved;
+    st.fermat_tests += o.sieved;
+    fidx = o.idx;
+    for (const auto& p : o.p) fq.push_back(p >> 1);
+  } else {
+    std::vector<uint8_t> raw(nbytes * batch);
+    CounterDRBG drbg(seed);
+    drbg.seek(batch_no * (uint64_t)raw.size());
+    drbg.read(raw.data(), raw.size());
+    small_batch(bitLen, raw.data(), batch, st, &fidx, &fq);
   }
+  st.candidates += batch;
+  const auto pr = ProbablyPrimeBatch(fq, 20, &st);
+  std::vector<GermainSafePrime> out;
+  for (size_t j = 0; j < fq.size(); ++j)
+    if (pr[j]) out.push_back({(fq[j] << 1) + Nat(1), fq[j], batch_no * batch + fidx[j]});
   st.seconds = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   add_stats(stats, st);
-  if ((int)out.size() < numPrimes) throw std::runtime_error("safe prime search exhausted max_candidates");
   return out;
 }
 
-paillier::PrivateKey GenerateKeyPair(int modulusBitLen, const RandFn& rand, SafePrimeStats* stats) {
+paillier::PrivateKey GenerateKeyPair(int modulusBitLen, Stream& rand, SafePrimeStats* stats) {
   const int half = modulusBitLen / 2;
   Nat P, Q;
   for (;;) {
@@ -274,12 +518,13 @@ paillier::PrivateKey GenerateKeyPair(int modulusBitLen, const RandFn& rand, Safe
   return sk;
 }
 
-LocalPreParams GeneratePreParams(const RandFn& rand, SafePrimeStats* stats) {
+LocalPreParams GeneratePreParams(Stream& stream, SafePrimeStats* stats) {
+  const RandFn rand = stream.fn();
   LocalPreParams pp;
   // tss-lib runs these two searches concurrently on one reader (stream
   // interleaving is scheduling-defined); here they run in a fixed order.
-  pp.PaillierSK = GenerateKeyPair(2048, rand, stats);
-  auto sgps = GetRandomSafePrimes(1024, 2, rand, stats);
+  pp.PaillierSK = GenerateKeyPair(2048, stream, stats);
+  auto sgps = GetRandomSafePrimes(1024, 2, stream, stats);
   const Nat P = sgps[0].p, Q = sgps[1].p;
   pp.NTildei = P * Q;
   pp.P = sgps[0].q;

@@ -7,12 +7,26 @@
 // Candidate stream (per runGenPrimeRoutine): read (qBitLen+7)/8 bytes, mask to
 // qBitLen with the top two bits set, make odd, delta-walk until q is coprime to
 // the primes 3..53; p = 2q + 1. Accept iff bitlen(q) == qBitLen, 2^(p-1) == 1
-// mod p (Pocklington) and q passes Miller-Rabin (ProbablyPrime(20): base 2 plus
-// 20 further bases). The host sieves candidates (exact trial division, which
-// never changes which candidate is accepted first); the GPU runs the Fermat
-// test on every survivor in large batches, then Miller-Rabin on the rare
-// Fermat survivors. Output order = candidate-stream order, i.e. what tss-lib
-// returns at concurrency 1 (its concurrent output order is scheduling-defined).
+// mod p (Pocklington) and q.ProbablyPrime(20) (Go: 20 Miller-Rabin rounds with
+// pseudo-random bases plus base 2, then the strong Lucas test).
+//
+// GPU pipeline (q of 63..1023 bits), one mpcx_safeprime_step per batch of the
+// stream: candidates drawn on the device (CounterDRBG streams) or copied from
+// the host reader, sieved (exact trial division: never rejects a prime), the
+// Pocklington test on every survivor -- and, in the same launch, the base-2
+// Miller-Rabin round on the previous batch's Fermat passes. Their survivors
+// (in practice the primes) get the remaining 20 Miller-Rabin bases and the
+// strong Lucas test (mpcx_mr_batch, mpcx_lucas_batch) while the next batch's
+// step runs. Output order = candidate-stream order, i.e. what tss-lib returns
+// at concurrency 1 (its concurrent output order is scheduling-defined), and
+// the stream is left right after the last accepted candidate (Stream).
+//
+// ProbablyPrime decisions: Go draws its 20 bases from math/rand seeded with
+// the candidate's low word (go:src/math/big/prime.go), whose generator table
+// is not restated here; these 20 bases come from a CounterDRBG seeded the same
+// way. Base 2 and the strong Lucas test (together BPSW, no known
+// counterexample) are Go's exactly, so the accept decisions coincide except on
+// a composite passing BPSW, none of which is known.
 #pragma once
 
 #include <cstdint>
@@ -33,16 +47,57 @@ struct GermainSafePrime {
 
 struct SafePrimeStats {
   uint64_t candidates = 0;     // stream candidates drawn
-  uint64_t sieved_out = 0;     // rejected by host trial division
+  uint64_t sieved_out = 0;     // rejected by the sieve (masks, bit length, trial division)
   uint64_t fermat_tests = 0;   // GPU Pocklington/Fermat tests
-  uint64_t mr_tests = 0;       // GPU Miller-Rabin tests
+  uint64_t mr_tests = 0;       // GPU Miller-Rabin rounds (base 2 + further bases)
+  uint64_t lucas_tests = 0;    // GPU strong Lucas tests
   double seconds = 0;
 };
 
+// The io.Reader a search draws from, consumed exactly as tss-lib at
+// concurrency 1 consumes its reader: after GetRandomSafePrimes the stream
+// stands right after the last accepted candidate's bytes (the batches' extra
+// bytes are given back: a CounterDRBG seeks, a host reader's bytes are pushed
+// back and served first to the next draw). A CounterDRBG stream's candidate
+// bytes are drawn on the GPU.
+class Stream {
+ public:
+  explicit Stream(RandFn fn) : fn_(std::move(fn)) {}
+  explicit Stream(CounterDRBG* drbg) : drbg_(drbg) {}
+  void read(uint8_t* out, size_t n);
+  void unread(const uint8_t* data, size_t n);  // n bytes back in front of the stream
+  // the CounterDRBG the GPU may draw from at its current position (none while
+  // pushed-back bytes are pending)
+  CounterDRBG* device_stream() const { return pushback_.empty() ? drbg_ : nullptr; }
+  RandFn fn() {
+    return [this](uint8_t* b, size_t n) { read(b, n); };
+  }
+
+ private:
+  RandFn fn_;
+  CounterDRBG* drbg_ = nullptr;
+  std::vector<uint8_t> pushback_;  // served from the front
+  size_t pb_pos_ = 0;
+};
+
 // common.GetRandomSafePrimesConcurrent(ctx, bitLen, numPrimes, 1, rand)
+std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, Stream& rand,
+                                                  SafePrimeStats* stats = nullptr, size_t batch = 0,
+                                                  uint64_t max_candidates = (1ull << 40));
+// Same over a plain reader (the batches' extra bytes are consumed).
 std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, const RandFn& rand,
                                                   SafePrimeStats* stats = nullptr, size_t batch = 0,
                                                   uint64_t max_candidates = (1ull << 40));
+
+// Go (*Int).ProbablyPrime(reps) decisions for a batch of odd n (see the
+// header comment on the bases): small-prime exits, Miller-Rabin with base 2 +
+// `reps` further bases and, for n < 2^1024, the strong Lucas test, all on the
+// GPU. n >= 2^1024 (a 2048-bit Paillier N): Miller-Rabin only.
+std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, SafePrimeStats* stats = nullptr);
+// Baillie-OEIS method C for Go's probablyPrimeLucas: 1 with *P (run the test),
+// 0 (n composite: square, or Jacobi(P^2 - 4, n) = 0 with n != P + 2),
+// 2 (n == P + 2 is prime).
+int LucasParam(const Nat& n, uint32_t* P);
 
 // One batch of the CounterDRBG(seed) candidate stream: candidates
 // [batch_no*batch, (batch_no+1)*batch), drawn by seeking the stream to the
@@ -57,7 +112,7 @@ std::vector<GermainSafePrime> SafePrimeBatch(int bitLen, uint64_t seed, uint64_t
 Nat CandidateFromBytes(const uint8_t* bytes, size_t n, int qBitLen);
 
 // paillier.GenerateKeyPair(ctx, rand, modulusBitLen)
-paillier::PrivateKey GenerateKeyPair(int modulusBitLen, const RandFn& rand, SafePrimeStats* stats = nullptr);
+paillier::PrivateKey GenerateKeyPair(int modulusBitLen, Stream& rand, SafePrimeStats* stats = nullptr);
 
 struct LocalPreParams {
   paillier::PrivateKey PaillierSK;
@@ -65,7 +120,8 @@ struct LocalPreParams {
 };
 
 // keygen.GeneratePreParamsWithContextAndRandom (Paillier 2048 + N~ from two
-// 1024-bit safe primes, h1 = f^2, h2 = h1^alpha mod N~, beta = alpha^-1 mod pq)
-LocalPreParams GeneratePreParams(const RandFn& rand, SafePrimeStats* stats = nullptr);
+// 1024-bit safe primes, h1 = f^2, h2 = h1^alpha mod N~, beta = alpha^-1 mod pq),
+// the Paillier search first, then N~'s, then f and alpha, on one stream
+LocalPreParams GeneratePreParams(Stream& rand, SafePrimeStats* stats = nullptr);
 
 }  // namespace mpcx::host

@@ -2,6 +2,7 @@
 #include "signing.hpp"
 
 #include "engine.hpp"
+#include "hostprof.hpp"
 
 #include <atomic>
 #include <chrono>
@@ -189,6 +190,7 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
   std::vector<uint8_t> verified(Wn, 0);
   const double t4 = now();
   parallel_for(Wn, [&](size_t wi) {
+    MPCX_PROF("sign.finalize_verify");
     Nat delta, s_sum, sigma_sum;
     secp::Affine Gam, X;
     for (size_t i = 0; i < S; ++i) {

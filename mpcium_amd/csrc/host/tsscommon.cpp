@@ -1,6 +1,8 @@
 // tsscommon.cpp -- see tsscommon.hpp.
 #include "tsscommon.hpp"
 
+#include "hostprof.hpp"
+
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -225,6 +227,7 @@ std::vector<uint8_t> SHA512_256(const std::vector<std::vector<uint8_t>>& in) {
 }
 
 Nat SHA512_256i(const std::vector<const Nat*>& in) {
+  MPCX_PROF("hash.sha512_256i");
   if (in.empty()) return Nat();
   Sha512_256 s;
   frame(s, int_parts(in));
@@ -234,6 +237,7 @@ Nat SHA512_256i(const std::vector<const Nat*>& in) {
 }
 
 Nat SHA512_256i_TAGGED(const std::vector<uint8_t>& tag, const std::vector<const Nat*>& in) {
+  MPCX_PROF("hash.sha512_256i_tagged");
   const std::vector<uint8_t> tagBz = SHA512_256({tag});
   if (in.empty()) return Nat();
   Sha512_256 s;
@@ -271,6 +275,7 @@ Nat MustGetRandomInt(const RandFn& rand, uint32_t bits) {
 }
 
 Nat GetRandomPositiveInt(const RandFn& rand, const Nat& lessThan) {
+  MPCX_PROF("rand.positive_int");
   if (lessThan.is_zero()) throw std::invalid_argument("GetRandomPositiveInt: lessThan must be > 0");
   for (;;) {
     Nat t = MustGetRandomInt(rand, lessThan.bit_len());
@@ -279,6 +284,7 @@ Nat GetRandomPositiveInt(const RandFn& rand, const Nat& lessThan) {
 }
 
 Nat GetRandomPositiveRelativelyPrimeInt(const RandFn& rand, const Nat& n) {
+  MPCX_PROF("rand.relprime_int");
   if (n.is_zero()) throw std::invalid_argument("GetRandomPositiveRelativelyPrimeInt: n must be > 0");
   for (;;) {
     Nat t = MustGetRandomInt(rand, n.bit_len());

@@ -32,6 +32,9 @@ class CounterDRBG {
   // Position the stream at byte `offset` (block c depends only on (seed, c)):
   // a reader seeked to k bytes yields what a fresh reader yields after k bytes.
   void seek(uint64_t offset);
+  uint64_t seed() const { return seed_; }
+  // bytes read so far (the next byte's stream offset)
+  uint64_t position() const { return ctr_ * 32 - (buf_.size() - pos_); }
   RandFn fn() {
     return [this](uint8_t* b, size_t n) { read(b, n); };
   }

@@ -44,7 +44,9 @@
 static_assert(MPCX_NUM_GEOMS == 7, "update MPCX_FOR_EACH_GEOM and build.py GEOMS");
 extern "C" {
 MPCX_FOR_EACH_GEOM(MPCX_GEOM_DECL)
-hipError_t mpcx_launch_fermat2(const mpcx::FermatArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t mpcx_launch_prime2(const mpcx::Prime2Args* a, uint32_t blocks, hipStream_t st);
+hipError_t mpcx_launch_lucas(const mpcx::LucasArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t mpcx_launch_drbg(const mpcx::DrbgArgs* a, hipStream_t st);
 hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
@@ -108,7 +110,9 @@ struct Lane {
   uint32_t* ws = nullptr;    // exponentiation table workspace
   size_t ws_bytes = 0;
   Staging stage[4];  // bases, exps, out, misc
-  Staging sieve[3];  // survivors' p words, survivors' indices, trial-division tables + counter
+  // safe-prime step: survivors' p words, survivors' indices, trial-division
+  // tables + counters, Fermat passes' p words, their indices, ride-along q + verdicts
+  Staging sieve[6];
 };
 constexpr int kLanes = 4;
 
@@ -988,13 +992,14 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
     const size_t pb = (size_t)n * p_words * 4;
     if ((rc = ensure_buffer(l.stage[0], pb)) || (rc = ensure_buffer(l.stage[3], n))) return rc;
     if ((rc = h2d(l.stage[0].ptr, p + (size_t)first * p_words, pb, l.st))) return rc;
-    mpcx::FermatArgs a{};
-    a.p = (const uint32_t*)l.stage[0].ptr;
-    a.ok = (uint8_t*)l.stage[3].ptr;
-    a.count = n;
-    a.p_words = p_words;
-    hipError_t e = mpcx_launch_fermat2(&a, (n + 63) / 64, l.st);
-    if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
+    mpcx::Prime2Args a{};
+    a.nf = (const uint32_t*)l.stage[0].ptr;
+    a.count_f = n;
+    a.f_blocks = (n + 63) / 64;
+    a.ok_f = (uint8_t*)l.stage[3].ptr;
+    a.n_words = p_words;
+    hipError_t e = mpcx_launch_prime2(&a, a.f_blocks, l.st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_prime2");
     return d2h_sync(ok + first, l.stage[3].ptr, n, l.st);
   });
 }
@@ -1029,6 +1034,42 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
     a.n_words = n_words;
     hipError_t e = mpcx_launch_mr(&a, (cnt + 63) / 64, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_mr");
+    return d2h_sync(ok + first, l.stage[3].ptr, cnt, l.st);
+  });
+}
+
+int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* P, uint8_t* ok) {
+  if (count == 0) return MPCX_OK;
+  if (!n || !P || !ok || n_words == 0) return fail(MPCX_EINVAL, "null buffer");
+  if (n_words > (uint32_t)MPCX_CLASS_WORDS(0))
+    return fail(MPCX_EINVAL, "n_words %u > %d", n_words, MPCX_CLASS_WORDS(0));
+  for (uint32_t i = 0; i < count; ++i) {
+    const uint32_t* ni = n + (size_t)i * n_words;
+    const uint32_t bits = bit_length_words(ni, n_words);
+    if (bits < 3 || (ni[0] & 1u) == 0) return fail(MPCX_EINVAL, "candidate %u is not an odd integer >= 5", i);
+    if (bits > 1024) return fail(MPCX_EINVAL, "candidate %u has %u bits > 1024", i, bits);
+    if (P[i] < 3 || P[i] >= (1u << 14)) return fail(MPCX_EINVAL, "Lucas parameter P[%u] = %u outside [3, 2^14)", i, P[i]);
+  }
+  return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t cnt) {
+    std::unique_lock<std::mutex> lk;
+    Lane& l = acquire_lane(g_devs[di], lk);
+    int rc;
+    if ((rc = lane_stream(l))) return rc;
+    const size_t nb = (size_t)cnt * n_words * 4;
+    if ((rc = ensure_buffer(l.stage[0], nb)) || (rc = ensure_buffer(l.stage[1], (size_t)cnt * 4)) ||
+        (rc = ensure_buffer(l.stage[3], cnt)))
+      return rc;
+    if ((rc = h2d(l.stage[0].ptr, n + (size_t)first * n_words, nb, l.st)) ||
+        (rc = h2d(l.stage[1].ptr, P + first, (size_t)cnt * 4, l.st)))
+      return rc;
+    mpcx::LucasArgs a{};
+    a.n = (const uint32_t*)l.stage[0].ptr;
+    a.P = (const uint32_t*)l.stage[1].ptr;
+    a.ok = (uint8_t*)l.stage[3].ptr;
+    a.count = cnt;
+    a.n_words = n_words;
+    hipError_t e = mpcx_launch_lucas(&a, (cnt + 63) / 64, l.st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_lucas");
     return d2h_sync(ok + first, l.stage[3].ptr, cnt, l.st);
   });
 }
@@ -1333,42 +1374,54 @@ struct TrialTables {
 };
 }  // namespace
 
-int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t count, uint32_t q_bits,
-                                uint32_t* n_out, uint32_t* idx_out, uint8_t* ok_out) {
-  if (!n_out) return fail(MPCX_EINVAL, "null n_out");
-  *n_out = 0;
-  if (q_bits < 63 || q_bits > 1023) return fail(MPCX_EINVAL, "q_bits %u outside [63, 1023]", q_bits);
-  if (nbytes != (q_bits + 7) / 8) return fail(MPCX_EINVAL, "nbytes %u != (q_bits + 7) / 8", nbytes);
-  if (count == 0) return MPCX_OK;
-  if (!raw || !idx_out || !ok_out) return fail(MPCX_EINVAL, "null buffer");
+namespace {
+// One safe-prime step on lane l of device di (see mpcx_safeprime_step). With
+// all_idx / all_ok non-null, also every sieve survivor's index and Fermat
+// verdict (ascending index; the legacy mpcx_safeprime_sieve_fermat).
+int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream_off, uint32_t count, uint32_t q_bits,
+                      const uint32_t* sprp_q, uint32_t n_sprp, uint32_t max_pass, uint32_t* n_sieved,
+                      uint32_t* n_pass, uint32_t* pass_idx, uint32_t* pass_p, uint8_t* sprp_ok, uint32_t* all_idx,
+                      uint8_t* all_ok) {
   static const TrialTables tt;
-  // one device per candidate batch (round-robin): a search keeps several
-  // batches in flight on different GPUs (csrc/host/safeprime.cpp)
-  return run_sliced(count, 0, [&](int di, uint32_t, uint32_t) {
-    std::unique_lock<std::mutex> lk;
-    Lane& l = acquire_lane(g_devs[di], lk);
-    int rc;
-    if ((rc = lane_stream(l))) return rc;
-    Staging *sg = l.stage, *sv = l.sieve;
-    constexpr uint32_t W = MPCX_SIEVE_MAX_BYTES / 4;
-    const size_t ng = tt.prod.size();
-    // misc buffer: counter | prod | start | primes | inv (8-byte aligned)
-    const size_t off_prod = 2, off_start = off_prod + ng, off_primes = off_start + tt.start.size();
-    const size_t off_inv = (off_primes + tt.primes.size() + 1) / 2 * 2;
-    const size_t misc_words = off_inv + 2 * ng;
-    if ((rc = ensure_buffer(sg[0], (size_t)count * nbytes)) || (rc = ensure_buffer(sg[3], count)) ||
-        (rc = ensure_buffer(sv[0], (size_t)count * W * 4)) || (rc = ensure_buffer(sv[1], (size_t)count * 4)) ||
-        (rc = ensure_buffer(sv[2], misc_words * 4)))
-      return rc;
-    std::vector<uint32_t> misc(misc_words, 0);
-    std::copy(tt.prod.begin(), tt.prod.end(), misc.begin() + off_prod);
-    std::copy(tt.start.begin(), tt.start.end(), misc.begin() + off_start);
-    std::copy(tt.primes.begin(), tt.primes.end(), misc.begin() + off_primes);
-    std::memcpy(misc.data() + off_inv, tt.inv.data(), ng * 8);
-    if ((rc = h2d(sv[2].ptr, misc.data(), misc_words * 4, l.st)) ||
-        (rc = h2d(sg[0].ptr, raw, (size_t)count * nbytes, l.st)))
-      return rc;
-    uint32_t* dm = (uint32_t*)sv[2].ptr;
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(g_devs[di], lk);
+  int rc;
+  if ((rc = lane_stream(l))) return rc;
+  constexpr uint32_t W = MPCX_SIEVE_MAX_BYTES / 4;
+  const uint32_t nbytes = (q_bits + 7) / 8;
+  Staging *sg = l.stage, *sv = l.sieve;
+  const size_t ng = tt.prod.size();
+  // misc buffer: survivor counter | pass counter | prod | start | primes | inv (8-byte aligned)
+  const size_t off_prod = 2, off_start = off_prod + ng, off_primes = off_start + tt.start.size();
+  const size_t off_inv = (off_primes + tt.primes.size() + 1) / 2 * 2;
+  const size_t misc_words = off_inv + 2 * ng;
+  const size_t cap = std::max<uint32_t>(count, 1);
+  if ((rc = ensure_buffer(sg[0], cap * nbytes)) || (rc = ensure_buffer(sv[0], cap * W * 4)) ||
+      (rc = ensure_buffer(sv[1], cap * 4)) || (rc = ensure_buffer(sv[2], misc_words * 4)) ||
+      (rc = ensure_buffer(sv[3], (size_t)std::max<uint32_t>(max_pass, 1) * W * 4)) ||
+      (rc = ensure_buffer(sv[4], (size_t)std::max<uint32_t>(max_pass, 1) * 4)) ||
+      (rc = ensure_buffer(sv[5], (size_t)n_sprp * (W * 4 + 1) + 64)) || (all_ok && (rc = ensure_buffer(sg[3], cap))))
+    return rc;
+  std::vector<uint32_t> misc(misc_words, 0);
+  std::copy(tt.prod.begin(), tt.prod.end(), misc.begin() + off_prod);
+  std::copy(tt.start.begin(), tt.start.end(), misc.begin() + off_start);
+  std::copy(tt.primes.begin(), tt.primes.end(), misc.begin() + off_primes);
+  std::memcpy(misc.data() + off_inv, tt.inv.data(), ng * 8);
+  if ((rc = h2d(sv[2].ptr, misc.data(), misc_words * 4, l.st))) return rc;
+  uint32_t* dm = (uint32_t*)sv[2].ptr;
+  hipError_t e;
+  if (count) {
+    if (raw) {
+      if ((rc = h2d(sg[0].ptr, raw, (size_t)count * nbytes, l.st))) return rc;
+    } else {
+      mpcx::DrbgArgs da{};
+      da.seed = seed;
+      da.off = stream_off;
+      da.n = (uint64_t)count * nbytes;
+      da.out = (uint8_t*)sg[0].ptr;
+      e = mpcx_launch_drbg(&da, l.st);
+      if (e != hipSuccess) return hip_fail(e, "launch k_drbg");
+    }
     mpcx::SieveArgs sa{};
     sa.raw = (const uint8_t*)sg[0].ptr;
     sa.nbytes = nbytes;
@@ -1382,35 +1435,114 @@ int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t co
     sa.out_p = (uint32_t*)sv[0].ptr;
     sa.out_idx = (uint32_t*)sv[1].ptr;
     sa.out_count = dm;
-    hipError_t e = mpcx_launch_sieve(&sa, l.st);
+    e = mpcx_launch_sieve(&sa, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_sieve");
-    mpcx::FermatArgs fa{};
-    fa.p = sa.out_p;
-    fa.ok = (uint8_t*)sg[3].ptr;
-    fa.count = count;
-    fa.p_words = W;
-    fa.count_dev = dm;
-    e = mpcx_launch_fermat2(&fa, (count + 63) / 64, l.st);
-    if (e != hipSuccess) return hip_fail(e, "launch k_fermat2");
-    uint32_t n = 0;
-    if ((rc = d2h_sync(&n, dm, 4, l.st))) return rc;
-    if (n > count) return fail(MPCX_EHIP, "sieve survivor count %u > %u", n, count);
-    std::vector<uint32_t> idx(n);
-    std::vector<uint8_t> ok(n);
-    if (n) {
-      e = hipMemcpyAsync(idx.data(), sa.out_idx, (size_t)n * 4, hipMemcpyDeviceToHost, l.st);
-      if (e != hipSuccess) return hip_fail(e, "copy survivors");
-      if ((rc = d2h_sync(ok.data(), fa.ok, n, l.st))) return rc;
+  }
+  uint32_t* d_sq = (uint32_t*)sv[5].ptr;
+  uint8_t* d_sok = (uint8_t*)(d_sq + (size_t)n_sprp * W);
+  if (n_sprp && (rc = h2d(d_sq, sprp_q, (size_t)n_sprp * W * 4, l.st))) return rc;
+  mpcx::Prime2Args pa{};
+  pa.nf = (const uint32_t*)sv[0].ptr;
+  pa.count_f = count;
+  pa.count_dev = dm;
+  pa.f_blocks = (count + 63) / 64;
+  pa.ok_f = all_ok ? (uint8_t*)sg[3].ptr : nullptr;
+  pa.sieve_idx = (const uint32_t*)sv[1].ptr;
+  pa.pass_count = dm + 1;
+  pa.pass_idx = (uint32_t*)sv[4].ptr;
+  pa.pass_n = (uint32_t*)sv[3].ptr;
+  pa.ns = d_sq;
+  pa.count_s = n_sprp;
+  pa.ok_s = d_sok;
+  pa.n_words = W;
+  const uint32_t blocks = pa.f_blocks + (n_sprp + 63) / 64;
+  if (blocks) {
+    e = mpcx_launch_prime2(&pa, blocks, l.st);
+    if (e != hipSuccess) return hip_fail(e, "launch k_prime2");
+  }
+  uint32_t cnt2[2] = {0, 0};
+  if ((rc = d2h_sync(cnt2, dm, 8, l.st))) return rc;
+  const uint32_t ns = cnt2[0], np = cnt2[1];
+  if (ns > count || np > ns) return fail(MPCX_EHIP, "safe-prime step counters %u/%u out of range (%u)", ns, np, count);
+  if (np > max_pass) return fail(MPCX_ENOMEM, "%u Fermat passes > max_pass %u", np, max_pass);
+  std::vector<uint32_t> pidx(np), pp((size_t)np * W);
+  if (np) {
+    e = hipMemcpyAsync(pidx.data(), sv[4].ptr, (size_t)np * 4, hipMemcpyDeviceToHost, l.st);
+    if (e == hipSuccess) e = hipMemcpyAsync(pp.data(), sv[3].ptr, pp.size() * 4, hipMemcpyDeviceToHost, l.st);
+    if (e != hipSuccess) return hip_fail(e, "copy passes");
+  }
+  if (n_sprp) {
+    e = hipMemcpyAsync(sprp_ok, d_sok, n_sprp, hipMemcpyDeviceToHost, l.st);
+    if (e != hipSuccess) return hip_fail(e, "copy strong-test verdicts");
+  }
+  std::vector<uint32_t> aidx;
+  std::vector<uint8_t> aok;
+  if (all_ok && ns) {
+    aidx.resize(ns);
+    aok.resize(ns);
+    e = hipMemcpyAsync(aidx.data(), sv[1].ptr, (size_t)ns * 4, hipMemcpyDeviceToHost, l.st);
+    if (e == hipSuccess) e = hipMemcpyAsync(aok.data(), sg[3].ptr, ns, hipMemcpyDeviceToHost, l.st);
+    if (e != hipSuccess) return hip_fail(e, "copy survivors");
+  }
+  e = hipStreamSynchronize(l.st);
+  if (e != hipSuccess) return hip_fail(e, "safe-prime step");
+  // stream order
+  std::vector<uint32_t> ord(np);
+  for (uint32_t j = 0; j < np; ++j) ord[j] = j;
+  std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return pidx[x] < pidx[y]; });
+  for (uint32_t j = 0; j < np; ++j) {
+    if (pass_idx) pass_idx[j] = pidx[ord[j]];
+    if (pass_p) std::memcpy(pass_p + (size_t)j * W, &pp[(size_t)ord[j] * W], W * 4);
+  }
+  if (all_ok) {
+    std::vector<uint32_t> o2(ns);
+    for (uint32_t j = 0; j < ns; ++j) o2[j] = j;
+    std::sort(o2.begin(), o2.end(), [&](uint32_t x, uint32_t y) { return aidx[x] < aidx[y]; });
+    for (uint32_t j = 0; j < ns; ++j) {
+      all_idx[j] = aidx[o2[j]];
+      all_ok[j] = aok[o2[j]];
     }
-    // stream order
-    std::vector<uint32_t> ord(n);
-    for (uint32_t j = 0; j < n; ++j) ord[j] = j;
-    std::sort(ord.begin(), ord.end(), [&](uint32_t x, uint32_t y) { return idx[x] < idx[y]; });
-    for (uint32_t j = 0; j < n; ++j) {
-      idx_out[j] = idx[ord[j]];
-      ok_out[j] = ok[ord[j]];
-    }
-    *n_out = n;
-    return MPCX_OK;
+  }
+  if (n_sieved) *n_sieved = ns;
+  if (n_pass) *n_pass = np;
+  return MPCX_OK;
+}
+}  // namespace
+
+int mpcx_safeprime_step(uint64_t seed, const uint8_t* raw, uint64_t stream_off, uint32_t count, uint32_t q_bits,
+                        const uint32_t* sprp_q, uint32_t n_sprp, uint32_t max_pass, uint32_t* n_sieved,
+                        uint32_t* n_pass, uint32_t* pass_idx, uint32_t* pass_p, uint8_t* sprp_ok) {
+  if (!n_sieved || !n_pass) return fail(MPCX_EINVAL, "null counters");
+  *n_sieved = *n_pass = 0;
+  if (q_bits < 63 || q_bits > 1023) return fail(MPCX_EINVAL, "q_bits %u outside [63, 1023]", q_bits);
+  if (count && (!pass_idx || !pass_p)) return fail(MPCX_EINVAL, "null pass buffers");
+  if (n_sprp && (!sprp_q || !sprp_ok)) return fail(MPCX_EINVAL, "null strong-test buffers");
+  constexpr uint32_t W = MPCX_SIEVE_MAX_BYTES / 4;
+  for (uint32_t i = 0; i < n_sprp; ++i) {
+    const uint32_t* qi = sprp_q + (size_t)i * W;
+    if (bit_length_words(qi, W) < 3 || (qi[0] & 1u) == 0)
+      return fail(MPCX_EINVAL, "strong-test candidate %u is not an odd integer >= 5", i);
+  }
+  if (count == 0 && n_sprp == 0) return MPCX_OK;
+  return run_sliced(1, 0, [&](int di, uint32_t, uint32_t) {
+    return safeprime_step_on(di, seed, raw, stream_off, count, q_bits, sprp_q, n_sprp, max_pass, n_sieved, n_pass,
+                             pass_idx, pass_p, sprp_ok, nullptr, nullptr);
+  });
+}
+
+int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t count, uint32_t q_bits,
+                                uint32_t* n_out, uint32_t* idx_out, uint8_t* ok_out) {
+  if (!n_out) return fail(MPCX_EINVAL, "null n_out");
+  *n_out = 0;
+  if (q_bits < 63 || q_bits > 1023) return fail(MPCX_EINVAL, "q_bits %u outside [63, 1023]", q_bits);
+  if (nbytes != (q_bits + 7) / 8) return fail(MPCX_EINVAL, "nbytes %u != (q_bits + 7) / 8", nbytes);
+  if (count == 0) return MPCX_OK;
+  if (!raw || !idx_out || !ok_out) return fail(MPCX_EINVAL, "null buffer");
+  return run_sliced(1, 0, [&](int di, uint32_t, uint32_t) {
+    uint32_t np = 0;
+    std::vector<uint32_t> pidx(count);
+    std::vector<uint32_t> pp((size_t)count * (MPCX_SIEVE_MAX_BYTES / 4));
+    return safeprime_step_on(di, 0, raw, 0, count, q_bits, nullptr, 0, count, n_out, &np, pidx.data(), pp.data(),
+                             nullptr, idx_out, ok_out);
   });
 }

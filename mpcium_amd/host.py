@@ -64,10 +64,13 @@ SIGNATURES = [
     ("mpcxh_safe_prime_batch", _i, [_i, _u64, _u64, _u32, _u32, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("mpcxh_generate_preparams", _i, [_u64, _vp, _vp, _vp, _vp]),
     ("mpcxh_candidate_from_bytes", _i, [_vp, ctypes.c_size_t, _i, _vp, _u32]),
+    ("mpcxh_probably_prime_batch", _i, [_u32, _vp, _u32, _i, _vp]),
+    ("mpcxh_profile_report", _i, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
 ]
 
 ERR_OK, ERR_MESSAGE_TOO_LONG, ERR_MESSAGE_MALFORMED = 0, 1, 2
+STAT_KEYS = ["candidates", "sieved_out", "fermat_tests", "mr_tests", "usec", "lucas_tests"]
 _lib = None
 
 
@@ -190,11 +193,11 @@ def safe_primes(bit_len: int, num: int, seed: int = 0, rand_fn=None):
     P = np.zeros((num, words), dtype="<u4")
     Q = np.zeros((num, words), dtype="<u4")
     idx = np.zeros(num, dtype=np.uint64)
-    st = np.zeros(5, dtype=np.uint64)
+    st = np.zeros(6, dtype=np.uint64)
     cb = RAND_FN(rand_fn) if rand_fn else None
     _check(lib().mpcxh_safe_primes(bit_len, num, seed, ctypes.cast(cb, _vp) if cb else None, None, P.ctypes.data,
                                    Q.ctypes.data, words, idx.ctypes.data, st.ctypes.data))
-    stats = dict(zip(["candidates", "sieved_out", "fermat_tests", "mr_tests", "usec"], (int(x) for x in st)))
+    stats = dict(zip(STAT_KEYS, (int(x) for x in st)))
     return list(zip(words_to_ints(P), words_to_ints(Q), (int(i) for i in idx))), stats
 
 
@@ -205,25 +208,45 @@ def safe_prime_batch(bit_len: int, seed: int, batch_no: int, batch: int = 0, max
     P = np.zeros((max_out, words), dtype="<u4")
     Q = np.zeros((max_out, words), dtype="<u4")
     idx = np.zeros(max_out, dtype=np.uint64)
-    st = np.zeros(5, dtype=np.uint64)
+    st = np.zeros(6, dtype=np.uint64)
     n = ctypes.c_uint32(0)
     _check(lib().mpcxh_safe_prime_batch(bit_len, seed, batch_no, batch, max_out, P.ctypes.data, Q.ctypes.data, words,
                                         idx.ctypes.data, ctypes.byref(n), st.ctypes.data))
     k = n.value
-    stats = dict(zip(["candidates", "sieved_out", "fermat_tests", "mr_tests", "usec"], (int(x) for x in st)))
+    stats = dict(zip(STAT_KEYS, (int(x) for x in st)))
     return list(zip(words_to_ints(P[:k]), words_to_ints(Q[:k]), (int(i) for i in idx[:k]))), stats
 
 
 PREPARAM_FIELDS = ["N", "LambdaN", "PhiN", "P", "Q", "NTildei", "H1i", "H2i", "Alpha", "Beta", "p", "q"]
 
 
-def generate_preparams(seed: int = 0):
+def generate_preparams(seed: int = 0, rand_fn=None):
     out = np.zeros((len(PREPARAM_FIELDS), 64), dtype="<u4")
-    st = np.zeros(5, dtype=np.uint64)
-    _check(lib().mpcxh_generate_preparams(seed, None, None, out.ctypes.data, st.ctypes.data))
+    st = np.zeros(6, dtype=np.uint64)
+    cb = RAND_FN(rand_fn) if rand_fn else None
+    _check(lib().mpcxh_generate_preparams(seed, ctypes.cast(cb, _vp) if cb else None, None, out.ctypes.data,
+                                          st.ctypes.data))
     vals = dict(zip(PREPARAM_FIELDS, words_to_ints(out)))
-    stats = dict(zip(["candidates", "sieved_out", "fermat_tests", "mr_tests", "usec"], (int(x) for x in st)))
+    stats = dict(zip(STAT_KEYS, (int(x) for x in st)))
     return vals, stats
+
+
+def profile_report(reset: bool = False) -> str:
+    """Host-time profile (MPCX_HOST_PROFILE=1), '' when off."""
+    buf = ctypes.create_string_buffer(1 << 16)
+    _check(lib().mpcxh_profile_report(buf, len(buf), 1 if reset else 0))
+    return buf.value.decode()
+
+
+def probably_prime(ns: Sequence[int], reps: int = 20) -> List[bool]:
+    """Go (*Int).ProbablyPrime(reps) decisions (mpcxh_probably_prime_batch)."""
+    if len(ns) == 0:
+        return []
+    w = max(nwords(n) for n in ns)
+    Nw = ints_to_words(list(ns), w)
+    ok = np.zeros(len(ns), dtype=np.uint8)
+    _check(lib().mpcxh_probably_prime_batch(len(ns), Nw.ctypes.data, w, reps, ok.ctypes.data))
+    return [bool(x) for x in ok]
 
 
 def candidate_from_bytes(raw: bytes, q_bit_len: int) -> int:

@@ -60,6 +60,9 @@ SIGNATURES = [
     ("mpcx_fixedbase_exp_batch", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_vp), ctypes.c_uint32,
                                                 ctypes.POINTER(_vp), _u32p, _vp, ctypes.c_uint32, _vp,
                                                 ctypes.c_uint32]),
+    ("mpcx_lucas_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
+    ("mpcx_safeprime_step", ctypes.c_int, [ctypes.c_uint64, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                           _vp, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p, _vp, _vp, _vp]),
     ("mpcx_safeprime_sieve_fermat", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_uint32, _u32p,
                                                    _vp, _vp]),
     ("mpcx_dev_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
@@ -381,6 +384,41 @@ def mr_batch(ns: Sequence[int], bases: Sequence[int]) -> List[bool]:
     ok = np.zeros(len(ns), dtype=np.uint8)
     _check(lib().mpcx_mr_batch(len(ns), Nw.ctypes.data, w, A.ctypes.data, ok.ctypes.data))
     return [bool(x) for x in ok]
+
+
+def lucas_batch(ns: Sequence[int], Ps: Sequence[int]) -> List[bool]:
+    """[n passes the strong Lucas test with parameter P] (mpcx_lucas_batch)."""
+    if len(ns) != len(Ps):
+        raise ValueError("one P per candidate")
+    if len(ns) == 0:
+        return []
+    w = max(nwords(n) for n in ns)
+    Nw = ints_to_words(ns, w)
+    Pw = np.array(Ps, dtype="<u4")
+    ok = np.zeros(len(ns), dtype=np.uint8)
+    _check(lib().mpcx_lucas_batch(len(ns), Nw.ctypes.data, w, Pw.ctypes.data, ok.ctypes.data))
+    return [bool(x) for x in ok]
+
+
+def safeprime_step(seed: int, stream_off: int, count: int, q_bits: int, sprp_q: Sequence[int] = (),
+                   raw: Optional[bytes] = None, max_pass: int = 4096):
+    """mpcx_safeprime_step: (n_sieved, [(index in the step, p)] Fermat passes,
+    [strong-test verdicts of sprp_q]); candidates from stream byte stream_off."""
+    W = 32
+    Q = ints_to_words(list(sprp_q), W) if len(sprp_q) else np.zeros((0, W), dtype="<u4")
+    pidx = np.zeros(max(max_pass, 1), dtype=np.uint32)
+    pp = np.zeros((max(max_pass, 1), W), dtype="<u4")
+    sok = np.zeros(max(len(sprp_q), 1), dtype=np.uint8)
+    ns, npass = ctypes.c_uint32(), ctypes.c_uint32()
+    rb = None
+    if raw is not None:
+        rb = np.frombuffer(raw, dtype=np.uint8).copy()
+    _check(lib().mpcx_safeprime_step(seed, rb.ctypes.data if rb is not None else None, stream_off, count, q_bits,
+                                     Q.ctypes.data if len(sprp_q) else None, len(sprp_q), max_pass,
+                                     ctypes.byref(ns), ctypes.byref(npass), pidx.ctypes.data, pp.ctypes.data,
+                                     sok.ctypes.data))
+    k = npass.value
+    return ns.value, list(zip((int(i) for i in pidx[:k]), words_to_ints(pp[:k]))), [bool(x) for x in sok[:len(sprp_q)]]
 
 
 def safeprime_sieve_fermat(raw: bytes, q_bits: int):
