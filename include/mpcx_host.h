@@ -254,6 +254,8 @@ int mpcxh_sha512_256i(const uint8_t* tag, size_t tag_len, uint32_t count, const 
                       uint8_t* digest32);
 int mpcxh_secp_scalar_base_mult(const uint32_t* k, uint32_t w, uint32_t* out16);
 int mpcxh_secp_scalar_mult(const uint32_t* p16, const uint32_t* k, uint32_t w, uint32_t* out16);
+/* u1*G + u2*P (the ecdsa.Verify combination) */
+int mpcxh_secp_lincomb(const uint32_t* u1, const uint32_t* p16, const uint32_t* u2, uint32_t w, uint32_t* out16);
 int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int relprime, uint32_t count,
                        uint32_t* out);
 
@@ -263,6 +265,11 @@ int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int
  * the build's deterministic stream, not Go's math/rand one -- decisions agree
  * except on a composite passing BPSW). ok[i] = 1: probably prime. */
 int mpcxh_probably_prime_batch(uint32_t count, const uint32_t* n, uint32_t words, int reps, uint8_t* ok);
+/* ok[i] = gcd(x[i], m[i]) == 1 for odd m[i] (math/big GCD(nil, nil, x, m).Cmp(one)
+ * == 0, the coprimality test behind common.GetRandomPositiveRelativelyPrimeInt
+ * and the proof verifiers' gcd checks); host-side, count operands of `words`
+ * words each. MPCX_EINVAL for an even modulus. */
+int mpcxh_coprime_batch(uint32_t count, const uint32_t* x, const uint32_t* m, uint32_t words, uint8_t* ok);
 
 /* Host-time profile (environment MPCX_HOST_PROFILE=1 at process start, else
  * empty): "label: seconds (calls)" lines summed over threads, largest first,

@@ -73,7 +73,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> dict:
         hdeps = host_srcs + [os.path.join(CSRC, "host", h) for h in os.listdir(os.path.join(CSRC, "host"))
                              if h.endswith(".hpp")] + [os.path.join(ROOT, "include", "mpcx_host.h")]
         if force or _newer(hlib, hdeps + [lib]):
-            _run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-pthread",
+            _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-pthread",
                   "-I", os.path.join(ROOT, "include"), "-I", os.path.join(CSRC, "host"),
                   "-o", hlib] + host_srcs + ["-L", HERE, "-lmpcx", "-Wl,-rpath,$ORIGIN"])
         out["libmpcx_host"] = hlib

@@ -352,13 +352,49 @@ void sub_shift(V64& a, const V64& b) {
 
 }  // namespace
 
-bool coprime_odd(const Nat& x, const Nat& m) {
-  MPCX_PROF("gcd.coprime_odd");
-  if (m.is_zero() || !m.is_odd()) throw std::invalid_argument("coprime_odd: modulus must be odd");
-  if (m == Nat(1)) return true;
-  const Nat a = x >= m ? x % m : x;
-  if (a.is_zero()) return false;
-  V64 u = to64(a), v = to64(m);
+namespace {
+
+constexpr size_t kGcdMaxWords = 128;  // 8192-bit operands on the batched path
+
+size_t bitlen64(const uint64_t* a, size_t n) {
+  for (size_t i = n; i-- > 0;)
+    if (a[i]) return i * 64 + 64 - (size_t)__builtin_clzll(a[i]);
+  return 0;
+}
+
+// bits [nb-64, nb) of a (nb >= 64)
+uint64_t top64(const uint64_t* a, size_t nb) {
+  const size_t lo = nb - 64, w = lo / 64, s = lo % 64;
+  return s ? (a[w] >> s) | (a[w + 1] << (64 - s)) : a[w];
+}
+
+// out = |a f + b g| / 2^31 (the combination is divisible by 2^31 by
+// construction); n words in, n words out
+void lincomb_shift31(const uint64_t* a, const uint64_t* b, size_t n, int64_t f, int64_t g, uint64_t* out) {
+  uint64_t t[kGcdMaxWords + 1];
+  __int128 carry = 0;
+  for (size_t i = 0; i < n; ++i) {
+    const __int128 v = carry + (__int128)a[i] * f + (__int128)b[i] * g;
+    t[i] = (uint64_t)v;
+    carry = v >> 64;
+  }
+  t[n] = (uint64_t)carry;
+  if (carry < 0) {  // two's complement negate
+    unsigned __int128 c = 1;
+    for (size_t i = 0; i <= n; ++i) {
+      c += (uint64_t)~t[i];
+      t[i] = (uint64_t)c;
+      c >>= 64;
+    }
+  }
+  for (size_t i = 0; i < n; ++i) out[i] = (t[i] >> 31) | (t[i + 1] << 33);
+}
+
+// plain binary GCD of u and odd v (word arrays of n words): gcd == 1?
+bool coprime_binary(V64 u, V64 v) {
+  while (!u.empty() && u.back() == 0) u.pop_back();
+  while (!v.empty() && v.back() == 0) v.pop_back();
+  if (u.empty()) return v.size() == 1 && v[0] == 1;
   {
     size_t z = 0;
     while (u[z] == 0) ++z;
@@ -370,7 +406,6 @@ bool coprime_odd(const Nat& x, const Nat& m) {
     }
     while (!u.empty() && u.back() == 0) u.pop_back();
   }
-  // binary GCD of odd u, v (gcd(x, m) = gcd(x / 2^k, m) for odd m)
   for (;;) {
     if (u.size() == 1 && v.size() == 1) {
       uint64_t a64 = u[0], b64 = v[0];
@@ -390,6 +425,162 @@ bool coprime_odd(const Nat& x, const Nat& m) {
     if (c > 0) sub_shift(u, v);
     else sub_shift(v, u);
   }
+}
+
+}  // namespace
+
+bool coprime_odd(const Nat& x, const Nat& m) {
+  MPCX_PROF("gcd.coprime_odd");
+  if (m.is_zero() || !m.is_odd()) throw std::invalid_argument("coprime_odd: modulus must be odd");
+  if (m == Nat(1)) return true;
+  const Nat a = x >= m ? x % m : x;
+  if (a.is_zero()) return false;
+  V64 u = to64(a), v = to64(m);
+  const size_t n = v.size();
+  if (n > kGcdMaxWords) return coprime_binary(u, v);
+  u.resize(n, 0);
+  // Binary GCD with v odd throughout, 31 steps at a time: the steps' parity
+  // tests read the exact low 31 bits and their comparisons read the top 33
+  // bits, so they run on one 64-bit register per operand; the resulting
+  // transition matrix (entries < 2^31 in magnitude, determinant +-2^31) is
+  // then applied to the full operands. Every step keeps gcd(u, v) (v stays
+  // odd), an approximate comparison only costs a sign flip, and u reaches 0
+  // with v = gcd after about 2 * bits / 31 rounds.
+  std::vector<uint64_t> nu(n), nv(n);
+  const size_t bits = bitlen64(v.data(), n);
+  const size_t cap = 2 * (2 * bits / 31 + 8);
+  for (size_t round = 0;; ++round) {
+    const size_t nb = std::max(bitlen64(u.data(), n), bitlen64(v.data(), n));
+    if (bitlen64(u.data(), n) == 0) break;
+    if (round == cap) return coprime_binary(u, v);  // not reached in practice
+    uint64_t xa, xb;
+    if (nb <= 64) {
+      xa = u[0];
+      xb = v[0];
+    } else {
+      constexpr uint64_t lo31 = (1ull << 31) - 1;
+      xa = (top64(u.data(), nb) & ~lo31) | (u[0] & lo31);
+      xb = (top64(v.data(), nb) & ~lo31) | (v[0] & lo31);
+    }
+    int64_t f0 = 1, g0 = 0, f1 = 0, g1 = 1;
+    for (int i = 0; i < 31; ++i) {  // branch-free: odd -> (swap if xa < xb), xa -= xb; then xa /= 2
+      const uint64_t odd = 0 - (xa & 1);
+      const uint64_t sw = odd & (0 - (uint64_t)(xa < xb));
+      const uint64_t tx = (xa ^ xb) & sw;
+      xa ^= tx;
+      xb ^= tx;
+      const int64_t tf = (f0 ^ f1) & (int64_t)sw, tg = (g0 ^ g1) & (int64_t)sw;
+      f0 ^= tf;
+      f1 ^= tf;
+      g0 ^= tg;
+      g1 ^= tg;
+      xa -= xb & odd;
+      f0 -= f1 & (int64_t)odd;
+      g0 -= g1 & (int64_t)odd;
+      xa >>= 1;
+      f1 *= 2;
+      g1 *= 2;
+    }
+    lincomb_shift31(u.data(), v.data(), n, f0, g0, nu.data());
+    lincomb_shift31(u.data(), v.data(), n, f1, g1, nv.data());
+    u.swap(nu);
+    v.swap(nv);
+  }
+  // gcd = v
+  if (v[0] != 1) return false;
+  for (size_t i = 1; i < n; ++i)
+    if (v[i]) return false;
+  return true;
+}
+
+namespace {
+
+// t = a b R^-1 mod m (CIOS on 64-bit limbs, R = 2^(64 n)), result < m
+void mont_mul64(const uint64_t* a, const uint64_t* b, const uint64_t* m, size_t n, uint64_t minv, uint64_t* out) {
+  using u128 = unsigned __int128;
+  uint64_t t[kGcdMaxWords + 2] = {};
+  for (size_t i = 0; i < n; ++i) {
+    uint64_t c = 0;
+    for (size_t j = 0; j < n; ++j) {
+      const u128 v = (u128)a[j] * b[i] + t[j] + c;
+      t[j] = (uint64_t)v;
+      c = (uint64_t)(v >> 64);
+    }
+    u128 v = (u128)t[n] + c;
+    t[n] = (uint64_t)v;
+    t[n + 1] = (uint64_t)(v >> 64);
+    const uint64_t q = t[0] * minv;
+    v = (u128)q * m[0] + t[0];
+    c = (uint64_t)(v >> 64);
+    for (size_t j = 1; j < n; ++j) {
+      v = (u128)q * m[j] + t[j] + c;
+      t[j - 1] = (uint64_t)v;
+      c = (uint64_t)(v >> 64);
+    }
+    v = (u128)t[n] + c;
+    t[n - 1] = (uint64_t)v;
+    t[n] = t[n + 1] + (uint64_t)(v >> 64);
+  }
+  // t < 2m: one conditional subtraction
+  bool ge = t[n] != 0;
+  if (!ge) {
+    ge = true;
+    for (size_t j = n; j-- > 0;)
+      if (t[j] != m[j]) {
+        ge = t[j] > m[j];
+        break;
+      }
+  }
+  if (ge) {
+    uint64_t br = 0;
+    for (size_t j = 0; j < n; ++j) {
+      const u128 d = (u128)t[j] - m[j] - br;
+      t[j] = (uint64_t)d;
+      br = (uint64_t)(d >> 64) & 1;
+    }
+  }
+  for (size_t j = 0; j < n; ++j) out[j] = t[j];
+}
+
+}  // namespace
+
+bool coprime_product_odd(const Nat* const* xs, size_t k, const Nat& m) {
+  if (m.is_zero() || !m.is_odd()) throw std::invalid_argument("coprime_product_odd: modulus must be odd");
+  if (m == Nat(1) || k == 0) return true;
+  if (k == 1) return coprime_odd(*xs[0], m);
+  const V64 mv = to64(m);
+  const size_t n = mv.size();
+  if (n > kGcdMaxWords) {
+    for (size_t i = 0; i < k; ++i)
+      if (!coprime_odd(*xs[i], m)) return false;
+    return true;
+  }
+  uint64_t minv = 1;  // -m^-1 mod 2^64 by Newton iteration
+  for (int i = 0; i < 6; ++i) minv *= 2 - mv[0] * minv;
+  minv = 0 - minv;
+  // acc = prod x_i R^-(k-1) mod m; R is a unit mod odd m, so gcd(acc, m) ==
+  // gcd(prod x_i, m), which is 1 iff every x_i is coprime to m
+  auto load = [&](const Nat& x, V64* out) {
+    *out = to64(x < m ? x : x % m);
+    out->resize(n, 0);
+  };
+  V64 acc, xv, tmp(n);
+  load(*xs[0], &acc);
+  for (size_t i = 1; i < k; ++i) {
+    load(*xs[i], &xv);
+    mont_mul64(acc.data(), xv.data(), mv.data(), n, minv, tmp.data());
+    acc.swap(tmp);
+  }
+  Nat a;
+  {
+    std::vector<uint32_t> w(2 * n);
+    for (size_t i = 0; i < n; ++i) {
+      w[2 * i] = (uint32_t)acc[i];
+      w[2 * i + 1] = (uint32_t)(acc[i] >> 32);
+    }
+    a = Nat::from_words(w.data(), w.size());
+  }
+  return coprime_odd(a, m);
 }
 
 }  // namespace mpcx::host

@@ -58,6 +58,9 @@ Nat gcd(Nat a, Nat b);
 // gcd(x, m) == 1 for odd m > 0 (binary GCD on 64-bit limbs; the validity
 // checks of the MtA proofs and GetRandomPositiveRelativelyPrimeInt)
 bool coprime_odd(const Nat& x, const Nat& m);
+// gcd(x_0 * ... * x_{k-1}, m) == 1 for odd m, i.e. every x_i coprime to m: one
+// gcd of a Montgomery product (64-bit CIOS) instead of k gcds
+bool coprime_product_odd(const Nat* const* xs, size_t k, const Nat& m);
 // floor(sqrt(n)) (Go (*Int).Sqrt)
 Nat isqrt(const Nat& n);
 // Jacobi symbol (a | n) for odd n > 0 (Go big.Jacobi)

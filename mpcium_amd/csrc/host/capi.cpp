@@ -325,6 +325,16 @@ int mpcxh_probably_prime_batch(uint32_t count, const uint32_t* n, uint32_t words
   });
 }
 
+int mpcxh_coprime_batch(uint32_t count, const uint32_t* x, const uint32_t* m, uint32_t words, uint8_t* ok) {
+  return guard([&] {
+    const auto xs = nats(x, words, count), ms = nats(m, words, count);
+    parallel_for(count, [&](size_t i) {
+      if (!ms[i].is_odd()) throw std::invalid_argument("coprime_batch: even modulus");
+      ok[i] = coprime_odd(xs[i], ms[i]) ? 1 : 0;
+    });
+  });
+}
+
 int mpcxh_profile_report(char* buf, size_t cap, int reset) {
   return guard([&] {
     if (!buf || !cap) throw std::invalid_argument("null buffer");
@@ -469,6 +479,13 @@ int mpcxh_secp_scalar_mult(const uint32_t* p16, const uint32_t* k, uint32_t w, u
   return guard([&] {
     const auto P = points_from(p16, 1)[0];
     point_out(secp::ScalarMult(P, Nat::from_words(k, w)), out16);
+  });
+}
+
+int mpcxh_secp_lincomb(const uint32_t* u1, const uint32_t* p16, const uint32_t* u2, uint32_t w, uint32_t* out16) {
+  return guard([&] {
+    const auto P = points_from(p16, 1)[0];
+    point_out(secp::LinComb(Nat::from_words(u1, w), P, Nat::from_words(u2, w)), out16);
   });
 }
 

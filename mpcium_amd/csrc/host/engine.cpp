@@ -50,6 +50,15 @@ void Engine::leave_call() {
                                                                                busy_t0_).count();
 }
 
+double Engine::busy_seconds_now() {
+  std::lock_guard<std::mutex> lk(busy_mu_);
+  uint64_t ns = busy_ns_;
+  if (inflight_ > 0)
+    ns += (uint64_t)std::chrono::duration_cast<std::chrono::nanoseconds>(std::chrono::steady_clock::now() - busy_t0_)
+              .count();
+  return (double)ns * 1e-9;
+}
+
 void Engine::count_work(const Nat& m, const std::vector<Nat>& exps, size_t count) {
   const uint64_t L = m.words(), l2 = 2 * L * L;
   uint64_t w = 0;

@@ -60,6 +60,8 @@ class Engine {
   // (GPU + transfers) was in flight, since the last reset. Calls from
   // different threads run concurrently on libmpcx's lanes (streams).
   double busy_seconds() const { return (double)busy_ns_.load() * 1e-9; }
+  // the same, including a busy interval still open now
+  double busy_seconds_now();
   // Go-equivalent algorithmic work of the exponentiations sent to libmpcx
   // since the last reset: SURVEY.md 8(d) W = (E + ceil(E/4)) 2 L^2 32-bit
   // MACs per x^e mod m (E = bit length of e, L = 32-bit words of m), the

@@ -25,13 +25,6 @@ const Nat& q7() {
 // Gamma^k mod N^2 = (1 + N)^k = 1 + (k mod N) N  (binomial theorem; < N^2)
 Nat gamma_pow(const Nat& k, const Nat& N) { return Nat(1) + (k % N) * N; }
 
-// gcd(x, m) == 1 for odd m; with known factors P, Q (m = P*Q or m = P^2 Q^2 with
-// the same prime set): P !| x and Q !| x.
-bool coprime_to(const Nat& x, const Nat& m, const Nat& P, const Nat& Qf) {
-  if (!P.is_zero() && !Qf.is_zero()) return !(x % P).is_zero() && !(x % Qf).is_zero();
-  return coprime_odd(x, m);
-}
-
 Nat affine_x(const secp::Affine& p) { return secp::FeToNat(p.x); }
 Nat affine_y(const secp::Affine& p) { return secp::FeToNat(p.y); }
 
@@ -41,12 +34,26 @@ struct RangeProveState {
   Nat gam_alpha, t1, t2, e;
 };
 
-// steps 1-4: alpha < q^3, beta in Z*_N, gamma < q^3 N~, rho < q N~
-void range_draw(RangeProveState& s, const paillier::PublicKey& pk, const DLNParams& dln, const RandFn& rand) {
-  s.alpha = GetRandomPositiveInt(rand, q3());
-  s.beta = GetRandomPositiveRelativelyPrimeInt(rand, pk.N);
-  s.gamma = GetRandomPositiveInt(rand, q3() * dln.NTilde);
-  s.rho = GetRandomPositiveInt(rand, Q() * dln.NTilde);
+// steps 1-4 for every session, in each reader's draw order: alpha < q^3,
+// beta in Z*_N (the batch's gcd decisions taken together), gamma < q^3 N~,
+// rho < q N~; plus Gamma^alpha
+void range_draw(std::vector<RangeProveState>& st, const paillier::PublicKey& pk, const DLNParams& dln,
+                const std::vector<RandFn>& rand) {
+  const size_t n = st.size();
+  parallel_for(n, [&](size_t i) { st[i].alpha = GetRandomPositiveInt(rand[i], q3()); });
+  std::vector<const RandFn*> rd(n);
+  std::vector<Nat*> beta(n);
+  for (size_t i = 0; i < n; ++i) {
+    rd[i] = &rand[i];
+    beta[i] = &st[i].beta;
+  }
+  GetRandomPositiveRelativelyPrimeIntBatch(rd, pk.N, beta);
+  const Nat q3Nt = q3() * dln.NTilde, qNt = Q() * dln.NTilde;
+  parallel_for(n, [&](size_t i) {
+    st[i].gamma = GetRandomPositiveInt(rand[i], q3Nt);
+    st[i].rho = GetRandomPositiveInt(rand[i], qNt);
+    st[i].gam_alpha = gamma_pow(st[i].alpha, pk.N);
+  });
 }
 
 }  // namespace
@@ -62,10 +69,7 @@ void ProveRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln, c
   const Nat N2 = pk.NSquare();
   std::vector<RangeProveState> st(n);
   out->assign(n, RangeProofAlice{});
-  parallel_for(n, [&](size_t i) {
-    range_draw(st[i], pk, dln, rand[i]);
-    st[i].gam_alpha = gamma_pow(st[i].alpha, pk.N);
-  });
+  range_draw(st, pk, dln, rand);
   ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
   for (size_t i = 0; i < n; ++i) {
     auto& s = st[i];
@@ -109,19 +113,32 @@ std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const 
     if (!IsInInterval(p.Z, dln.NTilde) || !IsInInterval(p.U, N2) || !IsInInterval(p.W, dln.NTilde) ||
         !IsInInterval(p.S, pk.N))
       return;
-    if (!coprime_to(p.Z, dln.NTilde, dln.P, dln.Q) || !coprime_odd(p.U, pk.N) ||
-        !coprime_to(p.W, dln.NTilde, dln.P, dln.Q) || !coprime_odd(p.S, pk.N))
-      return;
     if (p.S1 > q3()) return;
     // Go's Exp(c, -e, N^2) accepts any c invertible mod N^2 (c >= N^2 is
     // reduced by ModInverse); a non-invertible c gives nil and the following
     // Mul panics -- reported here as a verification failure. The hash binds
     // the caller's c as given.
     cr[i] = c[i] < N2 ? c[i] : c[i] % N2;
-    if (!coprime_odd(cr[i], pk.N)) return;
+    ok[i] = 1;
+  });
+  {  // z, w in Z*_N~ and u, s, c in Z*_N: the batch's gcd decisions together
+    std::vector<size_t> sel;
+    std::vector<const Nat*> xt, xn;
+    for (size_t i = 0; i < n; ++i)
+      if (ok[i]) {
+        sel.push_back(i);
+        xt.insert(xt.end(), {&pf[i].Z, &pf[i].W});
+        xn.insert(xn.end(), {&pf[i].U, &pf[i].S, &cr[i]});
+      }
+    const std::vector<uint8_t> ct = CoprimeMany(xt, dln.NTilde), cn = CoprimeMany(xn, pk.N);
+    for (size_t j = 0; j < sel.size(); ++j)
+      ok[sel[j]] = ct[2 * j] && ct[2 * j + 1] && cn[3 * j] && cn[3 * j + 1] && cn[3 * j + 2];
+  }
+  parallel_for(n, [&](size_t i) {
+    if (!ok[i]) return;
+    const auto& p = pf[i];
     e[i] = RejectionSample(Q(), SHA512_256i({&pk.N, &gamma, &c[i], &p.Z, &p.U, &p.W}));
     gs1[i] = gamma_pow(p.S1, pk.N);
-    ok[i] = 1;
   });
   ExpSet eN2(N2), eNt(dln.NTilde);
   for (size_t i = 0; i < n; ++i) {
@@ -149,17 +166,30 @@ struct BobProveState {
   Nat bg, a1, a2, a3, a4, e;
 };
 
-// steps 1-4 (+5 for WC): draw order alpha, rho, sigma, tau, rhoPrm, beta, gamma
-void bob_draw(BobProveState& s, const paillier::PublicKey& pk, const DLNParams& dln, const RandFn& rand, bool wc) {
+// steps 1-4 (+5 for WC) for the sessions st[js[k]] with readers rd[k], in
+// each reader's draw order alpha, rho, sigma, tau, rhoPrm, beta, gamma (the
+// beta gcd decisions taken together)
+void bob_draw(std::vector<BobProveState>& st, const std::vector<size_t>& js, const std::vector<const RandFn*>& rd,
+              const paillier::PublicKey& pk, const DLNParams& dln, bool wc) {
+  const size_t n = js.size();
   const Nat qNt = Q() * dln.NTilde, q3Nt = q3() * dln.NTilde;
-  s.alpha = GetRandomPositiveInt(rand, q3());
-  s.rho = GetRandomPositiveInt(rand, qNt);
-  s.sigma = GetRandomPositiveInt(rand, qNt);
-  s.tau = GetRandomPositiveInt(rand, q3Nt);
-  s.rhoPrm = GetRandomPositiveInt(rand, q3Nt);
-  s.beta = GetRandomPositiveRelativelyPrimeInt(rand, pk.N);
-  s.gamma = GetRandomPositiveInt(rand, q7());
-  if (wc) s.u = secp::ScalarBaseMult(s.alpha);  // 5. u = alpha*G
+  parallel_for(n, [&](size_t k) {
+    BobProveState& s = st[js[k]];
+    const RandFn& rand = *rd[k];
+    s.alpha = GetRandomPositiveInt(rand, q3());
+    s.rho = GetRandomPositiveInt(rand, qNt);
+    s.sigma = GetRandomPositiveInt(rand, qNt);
+    s.tau = GetRandomPositiveInt(rand, q3Nt);
+    s.rhoPrm = GetRandomPositiveInt(rand, q3Nt);
+  });
+  std::vector<Nat*> beta(n);
+  for (size_t k = 0; k < n; ++k) beta[k] = &st[js[k]].beta;
+  GetRandomPositiveRelativelyPrimeIntBatch(rd, pk.N, beta);
+  parallel_for(n, [&](size_t k) {
+    BobProveState& s = st[js[k]];
+    s.gamma = GetRandomPositiveInt(*rd[k], q7());
+    if (wc) s.u = secp::ScalarBaseMult(s.alpha);  // 5. u = alpha*G
+  });
 }
 
 // stage A of ProveBob: N^2 -> bg = Gamma^gamma beta^N ; N~ -> h1^x, h1^alpha, h1^y, h1^gamma
@@ -214,7 +244,15 @@ void ProveBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey&
   std::vector<BobProveState> st(n);
   std::vector<Nat> gg(n);
   out->assign(n, ProofBob{});
-  parallel_for(n, [&](size_t i) { bob_draw(st[i], pk, dln, rand[i], X != nullptr); });
+  {
+    std::vector<size_t> js(n);
+    std::vector<const RandFn*> rd(n);
+    for (size_t i = 0; i < n; ++i) {
+      js[i] = i;
+      rd[i] = &rand[i];
+    }
+    bob_draw(st, js, rd, pk, dln, X != nullptr);
+  }
   ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
   for (size_t i = 0; i < n; ++i) bob_stage_a(st[i], pk, dln, x[i], y[i], eN2, eNt, &gg[i]);
   eN2.run();
@@ -239,9 +277,9 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
   if (session.size() != n || c2.size() != n || pf.size() != n || (X && X->size() != n))
     throw std::invalid_argument("ProofBob.Verify: sizes");
   const Nat N2 = pk.NSquare(), gamma = pk.Gamma();
-  const Nat zero;
-  const Nat& kP = own_sk ? own_sk->P : zero;
-  const Nat& kQ = own_sk ? own_sk->Q : zero;
+  // own_sk (the verifier's own key) does not change any decision: gcd(x, N)
+  // == 1 is decided for the whole batch at once below
+  (void)own_sk;
   std::vector<uint8_t> ok(n, 0);
   std::vector<Nat> e(n), gt1(n), p1(n), p2(n), r1(n), r2(n), q1(n), r3(n), l1(n), l2(n), l3(n);
   parallel_for(n, [&](size_t i) {
@@ -250,12 +288,30 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
     if (X && !secp::IsOnCurve(p.U)) return;
     const Nat& Nt = dln.NTilde;
     for (const Nat* v : {&p.Z, &p.ZPrm, &p.T, &p.W})
-      if (!IsInInterval(*v, Nt) || !coprime_to(*v, Nt, dln.P, dln.Q)) return;
-    if (!IsInInterval(p.V, N2) || !coprime_to(p.V, pk.N, kP, kQ)) return;
-    if (!IsInInterval(p.S, pk.N) || !coprime_to(p.S, pk.N, kP, kQ)) return;
+      if (!IsInInterval(*v, Nt)) return;
+    if (!IsInInterval(p.V, N2) || !IsInInterval(p.S, pk.N)) return;
     // 3. s1 <= q^3. No t1 bound: BobMid draws betaPrm < N, so an honest
     // t1 = e betaPrm + gamma has ~2300 bits (upstream, verify).
     if (p.S1 > q3()) return;
+    ok[i] = 1;
+  });
+  {  // z, z', t, w in Z*_N~ and v, s in Z*_N: the batch's gcd decisions together
+    std::vector<size_t> sel;
+    std::vector<const Nat*> xt, xn;
+    for (size_t i = 0; i < n; ++i)
+      if (ok[i]) {
+        sel.push_back(i);
+        xt.insert(xt.end(), {&pf[i].Z, &pf[i].ZPrm, &pf[i].T, &pf[i].W});
+        xn.insert(xn.end(), {&pf[i].V, &pf[i].S});
+      }
+    const std::vector<uint8_t> ct = CoprimeMany(xt, dln.NTilde), cn = CoprimeMany(xn, pk.N);
+    for (size_t j = 0; j < sel.size(); ++j)
+      ok[sel[j]] = ct[4 * j] && ct[4 * j + 1] && ct[4 * j + 2] && ct[4 * j + 3] && cn[2 * j] && cn[2 * j + 1];
+  }
+  parallel_for(n, [&](size_t i) {
+    if (!ok[i]) return;
+    ok[i] = 0;
+    const auto& p = pf[i];
     e[i] = bob_challenge(session[i], pk, gamma, X ? &(*X)[i] : nullptr, c1[i], c2[i], p);
     if (X) {  // 4. s1*G == e*X + u
       const secp::Affine gS1 = secp::ScalarBaseMult(p.S1 % Q());
@@ -307,10 +363,16 @@ void AliceInitBatch(const paillier::PublicKey& pkA, const std::vector<Nat>& a, c
   const size_t k = idx.size();
   std::vector<Nat> r(k), ga(k), c(k), m(k);
   std::vector<RandFn> rd(k);
-  parallel_for(k, [&](size_t j) {
-    r[j] = GetRandomPositiveRelativelyPrimeInt(rand[idx[j]], pkA.N);
-    ga[j] = gamma_pow(a[idx[j]], pkA.N);
-  });
+  {
+    std::vector<const RandFn*> rdr(k);
+    std::vector<Nat*> rp(k);
+    for (size_t j = 0; j < k; ++j) {
+      rdr[j] = &rand[idx[j]];
+      rp[j] = &r[j];
+    }
+    GetRandomPositiveRelativelyPrimeIntBatch(rdr, pkA.N, rp);
+  }
+  parallel_for(k, [&](size_t j) { ga[j] = gamma_pow(a[idx[j]], pkA.N); });
   ExpSet eN2(pkA.NSquare());
   for (size_t j = 0; j < k; ++j) {
     eN2.add(r[j], pkA.N, &c[j], &ga[j]);  // c = Gamma^a r^N mod N^2
@@ -349,19 +411,31 @@ void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& p
   const size_t k = idx.size();
   std::vector<BobProveState> st(k);
   std::vector<Nat> cRand(k), gbp(k), cbp(k), gg(k);
-  parallel_for(k, [&](size_t j) {
+  {
     MPCX_PROF("mta.bob_mid.draws");
-    const size_t i = idx[j];
-    auto& o = (*out)[i];
-    o.betaPrm = GetRandomPositiveInt(rand[i], pkA.N);                 // betaPrm < N
-    cRand[j] = GetRandomPositiveRelativelyPrimeInt(rand[i], pkA.N);   // Encrypt(betaPrm) randomness
-    gbp[j] = gamma_pow(o.betaPrm, pkA.N);
-    if (!(b[i] < pkA.N)) {  // HomoMult(b, cA) fails before ProveBob draws anything
-      (*err)[i] = ErrMessageTooLong;
-      return;
+    std::vector<const RandFn*> rd(k);
+    std::vector<Nat*> cr(k);
+    for (size_t j = 0; j < k; ++j) {
+      rd[j] = &rand[idx[j]];
+      cr[j] = &cRand[j];
     }
-    bob_draw(st[j], pkA, dlnA, rand[i], B != nullptr);                // ProveBob[WC] steps 1-5
-  });
+    // betaPrm < N, then the Encrypt(betaPrm) randomness in Z*_N
+    parallel_for(k, [&](size_t j) { (*out)[idx[j]].betaPrm = GetRandomPositiveInt(*rd[j], pkA.N); });
+    GetRandomPositiveRelativelyPrimeIntBatch(rd, pkA.N, cr);
+    std::vector<size_t> js;
+    std::vector<const RandFn*> rdj;
+    for (size_t j = 0; j < k; ++j) {
+      const size_t i = idx[j];
+      gbp[j] = gamma_pow((*out)[i].betaPrm, pkA.N);
+      if (!(b[i] < pkA.N)) {  // HomoMult(b, cA) fails before ProveBob draws anything
+        (*err)[i] = ErrMessageTooLong;
+        continue;
+      }
+      js.push_back(j);
+      rdj.push_back(rd[j]);
+    }
+    bob_draw(st, js, rdj, pkA, dlnA, B != nullptr);  // ProveBob[WC] steps 1-5
+  }
   ExpSet eN2(N2), eNt(dlnA.NTilde), eN(pkA.N);
   for (size_t j = 0; j < k; ++j) {
     const size_t i = idx[j];

@@ -1,9 +1,11 @@
 // secp256k1.hpp -- the curve arithmetic the MtAwc proofs need on the host
 // (tss.EC() = btcec/v2 S256, /root/reference/go.mod:29): u = alpha*G in
 // ProveBobWC and s1*G == e*X + u in (*ProofBobWC).Verify
-// (up:crypto/mta/proofs.go). Fixed-width 4x64-bit field arithmetic mod
-// p = 2^256 - 2^32 - 977, Jacobian coordinates, 4-bit fixed-window scalar
-// multiplication, and a precomputed 64 x 16 table for the base point.
+// (up:crypto/mta/proofs.go), and the signature + ecdsa.Verify of signing.cpp.
+// Fixed-width 4x64-bit field arithmetic mod p = 2^256 - 2^32 - 977 (dedicated
+// squaring, 255S + 15M inversion chain), Jacobian coordinates, a 32 x 255
+// affine table for the base point (k*G = at most 32 mixed additions), and
+// width-5 NAF for variable points.
 // ScalarBaseMult(k) = (k mod n)*G (crypto.ScalarBaseMult semantics under which
 // the MtAwc check holds for alpha < q^3).
 #pragma once
@@ -29,6 +31,8 @@ Affine ScalarBaseMult(const Nat& k);
 // k*P, k reduced mod n
 Affine ScalarMult(const Affine& P, const Nat& k);
 Affine Add(const Affine& P, const Affine& Q);
+// u1*G + u2*X (both scalars reduced mod n) with one affine conversion
+Affine LinComb(const Nat& u1, const Affine& X, const Nat& u2);
 bool IsOnCurve(const Affine& P);
 bool Equal(const Affine& P, const Affine& Q);
 

@@ -25,9 +25,11 @@
 // Schnorr proofs (round 5-9) check consistency without changing it and carry
 // no Paillier work, so they are not replayed here.
 // One process plays every signer of every wallet: each protocol step is one
-// batch per ordered signer pair across all wallets (the nodes' preparams are
-// shared by all wallets, /root/reference/pkg/mpc/node.go:69,109), so the
-// measured time is the cluster's whole signing work per signature on one GPU.
+// batch per ordered signer pair across a chunk of wallets (the nodes'
+// preparams are shared by all wallets, /root/reference/pkg/mpc/node.go:69,109),
+// so the measured time is the cluster's whole signing work per signature on
+// one GPU. Wallet chunks run as concurrent pipelines (rounds 1-3, then the
+// finalize), so one chunk's host work overlaps another's GPU batches.
 #pragma once
 
 #include <cstdint>
@@ -44,13 +46,13 @@ struct NodeKeys {
 };
 
 struct MtaStats {
-  double round1_s = 0, round2_s = 0, round3_s = 0, total_s = 0;
+  double round1_s = 0, round2_s = 0, round3_s = 0, total_s = 0;  // rounds: summed over chunks
   double engine_busy_s = 0;  // wall time with >= 1 libmpcx call in flight (GPU + transfers)
   double alg_macs = 0;       // Go-equivalent algorithmic work sent to the GPU (Engine::alg_macs)
   uint64_t wallets = 0, pairs = 0, sessions = 0;  // sessions = wallets x ordered pairs
   uint64_t errors = 0;                            // non-OK status codes
   uint64_t relation_failures = 0;                 // alpha + beta != k gamma (or mu + nu != k w)
-  double finalize_s = 0;                          // rounds 4-9 + ecdsa.Verify on the host
+  double finalize_s = 0;                          // rounds 4-9 + ecdsa.Verify on the host (summed over chunks)
   uint64_t signatures = 0, verified = 0;          // signatures produced / passing ecdsa.Verify
 };
 

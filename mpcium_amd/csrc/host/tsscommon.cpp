@@ -3,6 +3,9 @@
 
 #include "hostprof.hpp"
 
+#include <cpuid.h>
+#include <immintrin.h>
+
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
@@ -14,10 +17,67 @@ namespace mpcx::host {
 
 // ------------------------------------------------------------------ SHA-256 (CounterDRBG)
 namespace {
+// x86 SHA extensions (SHA-NI; every EPYC since Zen 1): one 64-byte block with
+// sha256rnds2 (2 rounds per instruction) and sha256msg1/msg2 for the message
+// schedule, W[4i..4i+3] = msg2(msg1(W[i-4], W[i-3]) + W[4i-7..4i-4], W[i-1]).
+// Selected at run time (CPUID.7.0:EBX bit 29); the scalar block is the
+// fallback, and tests/test_host_cpu.py checks the DRBG stream against hashlib.
+bool has_sha_ni() {
+  static const bool v = [] {
+    unsigned a = 0, b = 0, c = 0, d = 0;
+    if (!__get_cpuid_count(7, 0, &a, &b, &c, &d)) return false;
+    if (!((b >> 29) & 1u)) return false;
+    if (!__get_cpuid(1, &a, &b, &c, &d)) return false;
+    return ((c >> 19) & 1u) && ((c >> 9) & 1u);  // SSE4.1, SSSE3
+  }();
+  return v;
+}
+
+__attribute__((target("sha,sse4.1,ssse3"))) void sha256_block_ni(uint32_t h[8], const uint8_t* p) {
+  alignas(16) static const uint32_t K[64] = {
+      0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
+      0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
+      0xe49b69c1, 0xefbe4786, 0x0fc19dc6, 0x240ca1cc, 0x2de92c6f, 0x4a7484aa, 0x5cb0a9dc, 0x76f988da,
+      0x983e5152, 0xa831c66d, 0xb00327c8, 0xbf597fc7, 0xc6e00bf3, 0xd5a79147, 0x06ca6351, 0x14292967,
+      0x27b70a85, 0x2e1b2138, 0x4d2c6dfc, 0x53380d13, 0x650a7354, 0x766a0abb, 0x81c2c92e, 0x92722c85,
+      0xa2bfe8a1, 0xa81a664b, 0xc24b8b70, 0xc76c51a3, 0xd192e819, 0xd6990624, 0xf40e3585, 0x106aa070,
+      0x19a4c116, 0x1e376c08, 0x2748774c, 0x34b0bcb5, 0x391c0cb3, 0x4ed8aa4a, 0x5b9cca4f, 0x682e6ff3,
+      0x748f82ee, 0x78a5636f, 0x84c87814, 0x8cc70208, 0x90befffa, 0xa4506ceb, 0xbef9a3f7, 0xc67178f2};
+  const __m128i bswap = _mm_set_epi64x(0x0c0d0e0f08090a0bULL, 0x0405060700010203ULL);
+  // state as (A B E F), (C D G H)
+  __m128i t = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&h[0]), 0xB1);
+  __m128i s1 = _mm_shuffle_epi32(_mm_loadu_si128((const __m128i*)&h[4]), 0x1B);
+  __m128i s0 = _mm_alignr_epi8(t, s1, 8);
+  s1 = _mm_blend_epi16(s1, t, 0xF0);
+  const __m128i abef = s0, cdgh = s1;
+  __m128i w[16];
+  for (int i = 0; i < 16; ++i) {
+    if (i < 4) {
+      w[i] = _mm_shuffle_epi8(_mm_loadu_si128((const __m128i*)(p + 16 * i)), bswap);
+    } else {
+      __m128i x = _mm_sha256msg1_epu32(w[i - 4], w[i - 3]);
+      x = _mm_add_epi32(x, _mm_alignr_epi8(w[i - 1], w[i - 2], 4));
+      w[i] = _mm_sha256msg2_epu32(x, w[i - 1]);
+    }
+    __m128i m = _mm_add_epi32(w[i], _mm_load_si128((const __m128i*)&K[4 * i]));
+    s1 = _mm_sha256rnds2_epu32(s1, s0, m);
+    m = _mm_shuffle_epi32(m, 0x0E);
+    s0 = _mm_sha256rnds2_epu32(s0, s1, m);
+  }
+  s0 = _mm_add_epi32(s0, abef);
+  s1 = _mm_add_epi32(s1, cdgh);
+  t = _mm_shuffle_epi32(s0, 0x1B);   // F E B A
+  s1 = _mm_shuffle_epi32(s1, 0xB1);  // D C H G
+  s0 = _mm_blend_epi16(t, s1, 0xF0); // D C B A
+  s1 = _mm_alignr_epi8(s1, t, 8);    // H G F E
+  _mm_storeu_si128((__m128i*)&h[0], s0);
+  _mm_storeu_si128((__m128i*)&h[4], s1);
+}
+
 struct Sha256 {
   uint32_t h[8] = {0x6a09e667, 0xbb67ae85, 0x3c6ef372, 0xa54ff53a, 0x510e527f, 0x9b05688c, 0x1f83d9ab, 0x5be0cd19};
   static uint32_t ror(uint32_t x, int n) { return (x >> n) | (x << (32 - n)); }
-  void block(const uint8_t* p) {
+  void block_scalar(const uint8_t* p) {
     static const uint32_t k[64] = {
         0x428a2f98, 0x71374491, 0xb5c0fbcf, 0xe9b5dba5, 0x3956c25b, 0x59f111f1, 0x923f82a4, 0xab1c5ed5,
         0xd807aa98, 0x12835b01, 0x243185be, 0x550c7dc3, 0x72be5d74, 0x80deb1fe, 0x9bdc06a7, 0xc19bf174,
@@ -45,6 +105,10 @@ struct Sha256 {
       hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
     }
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
+  }
+  void block(const uint8_t* p) {
+    if (has_sha_ni()) sha256_block_ni(h, p);
+    else block_scalar(p);
   }
   // one-shot digest of a short message (< 56 bytes)
   static void digest_short(const uint8_t* msg, size_t n, uint8_t out[32]) {
@@ -290,6 +354,61 @@ Nat GetRandomPositiveRelativelyPrimeInt(const RandFn& rand, const Nat& n) {
     Nat t = MustGetRandomInt(rand, n.bit_len());
     if (t.is_zero() || !(t < n)) continue;
     if (n.is_odd() ? coprime_odd(t, n) : gcd(t, n) == Nat(1)) return t;
+  }
+}
+
+std::vector<uint8_t> CoprimeMany(const std::vector<const Nat*>& xs, const Nat& m) {
+  MPCX_PROF("gcd.coprime_many");
+  const size_t n = xs.size();
+  std::vector<uint8_t> ok(n, 0);
+  if (n == 0) return ok;
+  if (!m.is_odd()) {
+    parallel_for(n, [&](size_t i) { ok[i] = gcd(*xs[i], m) == Nat(1); });
+    return ok;
+  }
+  // one gcd per chunk of a product; a chunk holding a non-coprime x (never
+  // for honest inputs) is decided element by element
+  constexpr size_t kChunk = 48;
+  const size_t chunks = (n + kChunk - 1) / kChunk;
+  parallel_for(chunks, [&](size_t c) {
+    const size_t b = c * kChunk, e = std::min(n, b + kChunk);
+    if (coprime_product_odd(xs.data() + b, e - b, m)) {
+      for (size_t i = b; i < e; ++i) ok[i] = 1;
+    } else {
+      for (size_t i = b; i < e; ++i) ok[i] = coprime_odd(*xs[i], m);
+    }
+  });
+  return ok;
+}
+
+void GetRandomPositiveRelativelyPrimeIntBatch(const std::vector<const RandFn*>& rand, const Nat& n,
+                                              const std::vector<Nat*>& out) {
+  if (n.is_zero()) throw std::invalid_argument("GetRandomPositiveRelativelyPrimeInt: n must be > 0");
+  if (rand.size() != out.size()) throw std::invalid_argument("GetRandomPositiveRelativelyPrimeIntBatch: sizes");
+  // Each reader makes exactly the reads of its one-by-one call: a round draws
+  // one candidate t in [1, n) per pending reader (zero / out-of-range draws
+  // are redrawn on the spot, as in the scalar loop), the round's gcd
+  // decisions are batched, and only readers whose t shares a factor with n
+  // draw again.
+  std::vector<size_t> pending(rand.size());
+  for (size_t i = 0; i < pending.size(); ++i) pending[i] = i;
+  while (!pending.empty()) {
+    parallel_for(pending.size(), [&](size_t j) {
+      const size_t i = pending[j];
+      for (;;) {
+        Nat t = MustGetRandomInt(*rand[i], n.bit_len());
+        if (t.is_zero() || !(t < n)) continue;
+        *out[i] = std::move(t);
+        return;
+      }
+    });
+    std::vector<const Nat*> xs(pending.size());
+    for (size_t j = 0; j < pending.size(); ++j) xs[j] = out[pending[j]];
+    const std::vector<uint8_t> ok = CoprimeMany(xs, n);
+    std::vector<size_t> next;
+    for (size_t j = 0; j < pending.size(); ++j)
+      if (!ok[j]) next.push_back(pending[j]);
+    pending.swap(next);
   }
 }
 

@@ -53,6 +53,13 @@ Nat MustGetRandomInt(const RandFn& rand, uint32_t bits);
 Nat GetRandomPositiveInt(const RandFn& rand, const Nat& lessThan);
 // common.GetRandomPositiveRelativelyPrimeInt(rand, n), n odd
 Nat GetRandomPositiveRelativelyPrimeInt(const RandFn& rand, const Nat& n);
+// out[i] = GetRandomPositiveRelativelyPrimeInt(*rand[i], n) for every i; each
+// reader makes the same reads as the scalar call, the coprimality decisions of
+// each draw round are batched (CoprimeMany)
+void GetRandomPositiveRelativelyPrimeIntBatch(const std::vector<const RandFn*>& rand, const Nat& n,
+                                              const std::vector<Nat*>& out);
+// ok[i] = gcd(*xs[i], m) == 1 (one gcd per chunk of a Montgomery product for odd m)
+std::vector<uint8_t> CoprimeMany(const std::vector<const Nat*>& xs, const Nat& m);
 // common.IsInInterval(b, bound): 0 <= b < bound (b non-negative here)
 inline bool IsInInterval(const Nat& b, const Nat& bound) { return b < bound; }
 

@@ -65,6 +65,7 @@ SIGNATURES = [
     ("mpcxh_generate_preparams", _i, [_u64, _vp, _vp, _vp, _vp]),
     ("mpcxh_candidate_from_bytes", _i, [_vp, ctypes.c_size_t, _i, _vp, _u32]),
     ("mpcxh_probably_prime_batch", _i, [_u32, _vp, _u32, _i, _vp]),
+    ("mpcxh_coprime_batch", _i, [_u32, _vp, _vp, _u32, _vp]),
     ("mpcxh_profile_report", _i, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
 ]
@@ -247,6 +248,19 @@ def probably_prime(ns: Sequence[int], reps: int = 20) -> List[bool]:
     ok = np.zeros(len(ns), dtype=np.uint8)
     _check(lib().mpcxh_probably_prime_batch(len(ns), Nw.ctypes.data, w, reps, ok.ctypes.data))
     return [bool(x) for x in ok]
+
+
+def coprime(xs: Sequence[int], ms: Sequence[int]) -> List[bool]:
+    """gcd(x, m) == 1 for odd m (mpcxh_coprime_batch, host side)."""
+    if len(xs) != len(ms):
+        raise ValueError("coprime: sizes")
+    if len(xs) == 0:
+        return []
+    w = max(nwords(v) for v in list(xs) + list(ms))
+    X, M = ints_to_words(list(xs), w), ints_to_words(list(ms), w)
+    ok = np.zeros(len(xs), dtype=np.uint8)
+    _check(lib().mpcxh_coprime_batch(len(xs), X.ctypes.data, M.ctypes.data, w, ok.ctypes.data))
+    return [bool(v) for v in ok]
 
 
 def candidate_from_bytes(raw: bytes, q_bit_len: int) -> int:

@@ -44,6 +44,7 @@ SIGNATURES = [
     ("mpcxh_sha512_256i", _i, [_vp, _sz, _u32, _vp, _u32, _vp]),
     ("mpcxh_secp_scalar_base_mult", _i, [_vp, _u32, _vp]),
     ("mpcxh_secp_scalar_mult", _i, [_vp, _vp, _u32, _vp]),
+    ("mpcxh_secp_lincomb", _i, [_vp, _vp, _vp, _u32, _vp]),
     ("mpcxh_random_draws", _i, [_u64, _vp, _u32, _i, _u32, _vp]),
     ("mpcxh_bench_signing", _i, [_u32, _vp, _vp, _u32, _u32, _u32, _u64, _vp, _u32, _vp]),
 ]
@@ -254,6 +255,15 @@ def scalar_mult(P: Tuple[int, int], k_: int):
     Pp = _points([P])
     o = np.zeros(16, dtype="<u4")
     _check(lib().mpcxh_secp_scalar_mult(Pp.ctypes.data, K.ctypes.data, W, o.ctypes.data))
+    return _pt_out(o)
+
+
+def lincomb(u1: int, P: Tuple[int, int], u2: int):
+    """u1*G + u2*P on secp256k1 (mpcxh_secp_lincomb)."""
+    U1, U2 = _one(u1), _one(u2)
+    Pp = _points([P])
+    o = np.zeros(16, dtype="<u4")
+    _check(lib().mpcxh_secp_lincomb(U1.ctypes.data, Pp.ctypes.data, U2.ctypes.data, W, o.ctypes.data))
     return _pt_out(o)
 
 

@@ -150,8 +150,10 @@ def test_gpu_sieve_fermat_matches_oracle(gpu, q_bits):
 
 def test_safe_primes_1024_gpu_sieve(host):
     """One GeneratePreParams-size search through the GPU sieve path: p = 2q+1
-    with p, q prime (CPython pow Miller-Rabin spot check), the index's stream
-    bytes give q, and the GPU survivors before it are all rejected."""
+    with p, q passing Fermat spot checks and the index's stream bytes giving
+    q.  Bit-exact first indices at 1024 bits (every earlier candidate
+    rejected) are pinned by tests/test_gpu_primes.py against the golden
+    stream vector."""
     got, stats = host.safe_primes(1024, 2, seed=0x5AFE)
     nb = 128
     for p, q, idx in got:

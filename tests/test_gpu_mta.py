@@ -49,8 +49,19 @@ def bob_pf(d, wc):
     return p
 
 
-def test_golden_sessions_bit_exact(mta, nodes, vec):
-    A, B = nodes[0], nodes[1]
+def by_pair(vec):
+    """Golden sessions grouped by (Alice node, Bob node): one batch per pair."""
+    out = {}
+    for v in vec:
+        out.setdefault((v["alice_node"], v["bob_node"]), []).append(v)
+    return out
+
+
+@pytest.mark.parametrize("pair", [(0, 1), (1, 0), (1, 2), (2, 1), (2, 0), (0, 2)])
+def test_golden_sessions_bit_exact(mta, nodes, vec, pair):
+    """39 golden sessions over all 6 ordered node pairs, every field bit-exact."""
+    vec = by_pair(vec)[pair]
+    A, B = nodes[pair[0]], nodes[pair[1]]
     n = len(vec)
     a = [H(v["a"]) for v in vec]
     cA, pfA, err = mta.alice_init(A["N"], a, dln(B), [v["seed_a"] for v in vec])
@@ -167,12 +178,14 @@ def test_random_batch_relations(mta, nodes):
         assert [(x + y) % q for x, y in zip(alpha, beta)] == [x * y % q for x, y in zip(a, b)]
 
 
-def test_golden_sessions_through_reader_callbacks(mta, nodes, vec):
+@pytest.mark.parametrize("pair", [(0, 1), (2, 0)])
+def test_golden_sessions_through_reader_callbacks(mta, nodes, vec, pair):
     """The same golden sessions with every random draw made through the
     io.Reader callback (mpcxh_reader_t.fn -> a Python reader object called from
     libmpcx_host's worker threads), as a Go integration threads tss-lib's
     party reader through the batch entry points."""
-    A, B = nodes[0], nodes[1]
+    vec = by_pair(vec)[pair]
+    A, B = nodes[pair[0]], nodes[pair[1]]
     n = len(vec)
     a = [H(v["a"]) for v in vec]
     cA, pfA, err = mta.alice_init(A["N"], a, dln(B), [T.Reader(v["seed_a"]) for v in vec])

@@ -23,7 +23,8 @@ def mta(gpu):
 
 
 def test_wire_batches_through_gpu(mta):
-    vec = json.load(open(os.path.join(GOLDEN, "mta_vectors.json")))["sessions"]
+    vec = [v for v in json.load(open(os.path.join(GOLDEN, "mta_vectors.json")))["sessions"]
+           if (v["alice_node"], v["bob_node"]) == (0, 1)]
     d = json.load(open(os.path.join(GOLDEN, "node_preparams.json")))
     nodes = [{k: int(v, 16) for k, v in n.items() if isinstance(v, str) and k != "paillier_source"}
              for n in d["nodes"]]

@@ -59,9 +59,15 @@ def test_oracle_reproduces_golden_alice_init(nodes, vectors):
     assert not M.verify_range_alice(pf, A["N"], B["NTildei"], B["H1i"], B["H2i"], cA)
 
 
-def test_oracle_golden_relations(vectors):
+def test_oracle_golden_relations(nodes, vectors):
+    """Every golden session (6 ordered node pairs): the MtA relations, and
+    Alice's range proof verifies under Bob's DLN parameters (oracle verifier)."""
     q = M.Q
+    assert len({(v["alice_node"], v["bob_node"]) for v in vectors}) == 6 and len(vectors) >= 32
     for v in vectors:
+        A, B = nodes[v["alice_node"]], nodes[v["bob_node"]]
+        pf = M.RangeProofAlice(**{k: H(x) for k, x in v["pfA"].items()})
+        assert M.verify_range_alice(pf, A["N"], B["NTildei"], B["H1i"], B["H2i"], H(v["cA"]))
         assert (H(v["alpha"]) + H(v["bob"]["beta"])) % q == H(v["a"]) * H(v["b"]) % q
         assert (H(v["alpha_wc"]) + H(v["bob_wc"]["beta"])) % q == H(v["a"]) * H(v["wB"]) % q
         assert T.scalar_base_mult(H(v["wB"])) == (H(v["Bx"]), H(v["By"]))
@@ -77,12 +83,23 @@ def test_sha512_256_framing_matches_oracle(mta):
 
 
 def test_secp256k1_matches_oracle(mta):
-    for k in (1, 2, 3, T.SECP_N - 1, T.SECP_N, T.SECP_N + 5, 2 ** 255 + 12345, M.Q ** 3 - 1, 0xDEADBEEF ** 9):
+    import random
+    rng = random.Random(5)
+    ks = [1, 2, 3, 15, 16, 17, 31, 32, 255, 256, 257, 2 ** 64 - 1, 2 ** 64, T.SECP_N - 1, T.SECP_N, T.SECP_N + 5,
+          2 ** 255 + 12345, 2 ** 256 - 1, M.Q ** 3 - 1, 0xDEADBEEF ** 9, (T.SECP_N - 1) // 2, (T.SECP_N + 1) // 2]
+    ks += [rng.getrandbits(256) for _ in range(24)] + [rng.getrandbits(rng.randrange(1, 300)) for _ in range(24)]
+    for k in ks:
         assert mta.scalar_base_mult(k) == T.scalar_base_mult(k), k
     P = T.scalar_base_mult(0x1234567)
-    for k in (1, 7, T.SECP_N - 2, 2 ** 200 + 1):
+    for k in [1, 7, T.SECP_N - 2, 2 ** 200 + 1] + ks[::3]:
         assert mta.scalar_mult(P, k) == T.ec_mul(k, P), k
     assert mta.scalar_base_mult(T.SECP_N) is None
+    assert mta.scalar_mult(P, T.SECP_N) is None and mta.scalar_mult(P, 0) is None
+    # u1*G + u2*P, including results at infinity and doublings inside the sum
+    cases = [(rng.getrandbits(256), rng.getrandbits(256)) for _ in range(16)]
+    cases += [(0x1234567, T.SECP_N - 1), (0x1234567, 1), (0, 5), (7, 0), (T.SECP_N - 0x1234567, 1)]
+    for u1, u2 in cases:
+        assert mta.lincomb(u1, P, u2) == T.ec_add(T.scalar_base_mult(u1), T.ec_mul(u2, P)), (u1, u2)
 
 
 def test_random_draws_match_oracle(mta, nodes):
