@@ -5,6 +5,7 @@
 #include <chrono>
 #include <cstdint>
 #include <cstring>
+#include <cstdlib>
 #include <future>
 #include <thread>
 
@@ -170,7 +171,8 @@ int LucasParam(const Nat& n, uint32_t* P) {
   }
 }
 
-std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, SafePrimeStats* stats) {
+std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, SafePrimeStats* stats,
+                                        bool base2_passed) {
   const size_t cnt = n.size();
   std::vector<uint8_t> ok(cnt, 0);
   static const uint32_t kSmall[] = {3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53};
@@ -195,17 +197,21 @@ std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, Saf
   uint64_t mr = 0, lt = 0;
   if (!small.empty()) {
     std::vector<Nat> nn, aa;
-    for (size_t i : small) {
-      nn.push_back(n[i]);
-      aa.push_back(Nat(2));
+    std::vector<size_t> s2;  // base-2 survivors
+    if (base2_passed) {
+      s2 = small;
+    } else {
+      for (size_t i : small) {
+        nn.push_back(n[i]);
+        aa.push_back(Nat(2));
+      }
+      auto r2 = Engine::get().strong_probable_prime(nn, aa);
+      mr += nn.size();
+      for (size_t j = 0; j < small.size(); ++j)
+        if (r2[j]) s2.push_back(small[j]);
+      nn.clear();
+      aa.clear();
     }
-    auto r2 = Engine::get().strong_probable_prime(nn, aa);
-    mr += nn.size();
-    std::vector<size_t> s2;
-    for (size_t j = 0; j < small.size(); ++j)
-      if (r2[j]) s2.push_back(small[j]);
-    nn.clear();
-    aa.clear();
     std::vector<size_t> owner;
     for (size_t i : s2) {
       const auto bs = mr_bases(n[i], reps);
@@ -215,35 +221,45 @@ std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, Saf
         owner.push_back(i);
       }
     }
-    std::vector<uint8_t> pass(cnt, 0);
-    for (size_t i : s2) pass[i] = 1;
-    if (!nn.empty()) {
-      auto rr = Engine::get().strong_probable_prime(nn, aa);
-      mr += nn.size();
-      for (size_t j = 0; j < nn.size(); ++j)
-        if (!rr[j]) pass[owner[j]] = 0;
-    }
-    // strong Lucas test on the Miller-Rabin survivors
+    // strong Lucas test on the base-2 survivors, concurrently with their
+    // further Miller-Rabin bases (two latency-bound batches on two lanes)
     std::vector<Nat> ln;
     std::vector<uint32_t> lp;
     std::vector<size_t> lo;
+    std::vector<uint8_t> lucas_ok(cnt, 0);
     for (size_t i : s2) {
-      if (!pass[i]) continue;
       uint32_t P = 0;
       const int lr = LucasParam(n[i], &P);
       if (lr != 1) {
-        ok[i] = lr == 2;
+        lucas_ok[i] = lr == 2;
         continue;
       }
       ln.push_back(n[i]);
       lp.push_back(P);
       lo.push_back(i);
     }
-    if (!ln.empty()) {
-      auto lr = Engine::get().lucas(ln, lp);
-      lt += ln.size();
-      for (size_t j = 0; j < ln.size(); ++j) ok[lo[j]] = lr[j];
+    std::future<std::vector<uint8_t>> lucas;
+    if (!ln.empty()) lucas = std::async(std::launch::async, [&] { return Engine::get().lucas(ln, lp); });
+    std::vector<uint8_t> pass(cnt, 0);
+    for (size_t i : s2) pass[i] = 1;
+    std::exception_ptr mr_err;
+    try {
+      if (!nn.empty()) {
+        auto rr = Engine::get().strong_probable_prime(nn, aa);
+        mr += nn.size();
+        for (size_t j = 0; j < nn.size(); ++j)
+          if (!rr[j]) pass[owner[j]] = 0;
+      }
+    } catch (...) {
+      mr_err = std::current_exception();
     }
+    if (lucas.valid()) {
+      const auto lr = lucas.get();  // joined before any rethrow
+      lt += ln.size();
+      for (size_t j = 0; j < ln.size(); ++j) lucas_ok[lo[j]] = lr[j];
+    }
+    if (mr_err) std::rethrow_exception(mr_err);
+    for (size_t i : s2) ok[i] = pass[i] && lucas_ok[i];
   }
   for (size_t i : large) {
     // > 1024 bits: base 2 + reps bases as one shared-exponent launch (x^d for
@@ -286,8 +302,18 @@ void check_safe_prime_args(int bitLen) {
 }
 
 // candidates per batch: ~45K per 1024-bit safe prime, far fewer at small sizes
+// (environment MPCX_SAFEPRIME_BATCH overrides it above 512 bits; the output
+// and the stream consumption do not depend on the batch size)
 size_t default_batch(int bitLen) {
-  if (bitLen > 512) return 262144;
+  if (bitLen > 512) {
+    static const size_t env = [] {
+      const char* e = std::getenv("MPCX_SAFEPRIME_BATCH");
+      const long v = e ? std::atol(e) : 0;
+      return v >= 1024 && v <= (1l << 22) ? (size_t)v : (size_t)0;
+    }();
+    if (env) return env;
+    return 262144;
+  }
   if (bitLen > 256) return 65536;
   return 16384;
 }
@@ -333,8 +359,7 @@ void small_batch(int bitLen, const uint8_t* raw, size_t batch, SafePrimeStats& s
 // q (< 2^1023) that passed the base-2 Miller-Rabin round: the remaining
 // ProbablyPrime(20) rounds and the strong Lucas test
 std::vector<uint8_t> finish_q(const std::vector<Nat>& qs, SafePrimeStats& st) {
-  // ProbablyPrimeBatch redoes base 2 on these few survivors (negligible)
-  return ProbablyPrimeBatch(qs, 20, &st);
+  return ProbablyPrimeBatch(qs, 20, &st, /*base2_passed=*/true);
 }
 }  // namespace
 

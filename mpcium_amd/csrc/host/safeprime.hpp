@@ -93,7 +93,12 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, con
 // header comment on the bases): small-prime exits, Miller-Rabin with base 2 +
 // `reps` further bases and, for n < 2^1024, the strong Lucas test, all on the
 // GPU. n >= 2^1024 (a 2048-bit Paillier N): Miller-Rabin only.
-std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, SafePrimeStats* stats = nullptr);
+// base2_passed: every n is already known to pass the base-2 round (the safe-
+// prime step decided it), which is then not repeated. The further bases and
+// the Lucas test run as two concurrent GPU batches; the decision is their
+// conjunction, as in Go.
+std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, SafePrimeStats* stats = nullptr,
+                                        bool base2_passed = false);
 // Baillie-OEIS method C for Go's probablyPrimeLucas: 1 with *P (run the test),
 // 0 (n composite: square, or Jacobi(P^2 - 4, n) = 0 with n != P + 2),
 // 2 (n == P + 2 is prime).

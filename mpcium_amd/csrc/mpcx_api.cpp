@@ -48,6 +48,9 @@ hipError_t mpcx_launch_prime2(const mpcx::Prime2Args* a, uint32_t blocks, hipStr
 hipError_t mpcx_launch_lucas(const mpcx::LucasArgs* a, uint32_t blocks, hipStream_t st);
 hipError_t mpcx_launch_drbg(const mpcx::DrbgArgs* a, hipStream_t st);
 hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st);
+hipError_t mpcx_launch_prime2c(const mpcx::Prime2Args* a, hipStream_t st);
+hipError_t mpcx_launch_mrc(const mpcx::MrArgs* a, hipStream_t st);
+hipError_t mpcx_launch_lucasc(const mpcx::LucasArgs* a, hipStream_t st);
 hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g1(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
@@ -93,6 +96,7 @@ double g_narrow_rounds = 0.15;           // mpcx_set_option("narrow_rounds", 100
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
+bool g_prime_coop = true;                // mpcx_set_option("prime_coop", 0): thread-per-candidate prime kernels
 struct Staging {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -111,8 +115,9 @@ struct Lane {
   size_t ws_bytes = 0;
   Staging stage[4];  // bases, exps, out, misc
   // safe-prime step: survivors' p words, survivors' indices, trial-division
-  // tables + counters, Fermat passes' p words, their indices, ride-along q + verdicts
-  Staging sieve[6];
+  // tables + counters, Fermat passes' p words, their indices, ride-along q +
+  // verdicts, per-item constants of the cooperative kernels (R mod n, meta)
+  Staging sieve[8];
 };
 constexpr int kLanes = 4;
 
@@ -533,6 +538,9 @@ int mpcx_set_option(const char* key, int value) {
     // main (throughput) geometry of the geometry's class
     if (value < 0 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "main_geom %d out of range", value);
     g_main_geom[MPCX_GEOM_CLASS(value)] = value;
+  } else if (std::strcmp(key, "prime_coop") == 0) {
+    // 1: cooperative base-2 / Miller-Rabin kernels (k_prime2c, k_mrc); 0: thread per candidate
+    g_prime_coop = value != 0;
   } else if (std::strcmp(key, "device_split_min") == 0) {
     // smallest per-device slice of a host-buffer batch split across the bound GPUs (0: never split)
     if (value < 0) return fail(MPCX_EINVAL, "device_split_min %d < 0", value);
@@ -990,15 +998,27 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
     int rc;
     if ((rc = lane_stream(l))) return rc;
     const size_t pb = (size_t)n * p_words * 4;
-    if ((rc = ensure_buffer(l.stage[0], pb)) || (rc = ensure_buffer(l.stage[3], n))) return rc;
+    if ((rc = ensure_buffer(l.stage[0], pb)) || (rc = ensure_buffer(l.stage[3], n)) ||
+        (g_prime_coop && ((rc = ensure_buffer(l.stage[1], (size_t)n * MPCX_PRIME_L * 4)) ||
+                          (rc = ensure_buffer(l.stage[2], (size_t)n * 8)))))
+      return rc;
     if ((rc = h2d(l.stage[0].ptr, p + (size_t)first * p_words, pb, l.st))) return rc;
     mpcx::Prime2Args a{};
     a.nf = (const uint32_t*)l.stage[0].ptr;
     a.count_f = n;
-    a.f_blocks = (n + 63) / 64;
     a.ok_f = (uint8_t*)l.stage[3].ptr;
     a.n_words = p_words;
-    hipError_t e = mpcx_launch_prime2(&a, a.f_blocks, l.st);
+    hipError_t e;
+    if (g_prime_coop) {
+      a.f_blocks = (n + 64 / MPCX_PRIME_P - 1) / (64 / MPCX_PRIME_P);
+      a.fp_blocks = (n + 63) / 64;
+      a.r1 = (uint32_t*)l.stage[1].ptr;
+      a.meta = (uint32_t*)l.stage[2].ptr;
+      e = mpcx_launch_prime2c(&a, l.st);
+    } else {
+      a.f_blocks = (n + 63) / 64;
+      e = mpcx_launch_prime2(&a, a.f_blocks, l.st);
+    }
     if (e != hipSuccess) return hip_fail(e, "launch k_prime2");
     return d2h_sync(ok + first, l.stage[3].ptr, n, l.st);
   });
@@ -1021,7 +1041,8 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
     if ((rc = lane_stream(l))) return rc;
     const size_t nb = (size_t)cnt * n_words * 4;
     if ((rc = ensure_buffer(l.stage[0], nb)) || (rc = ensure_buffer(l.stage[1], nb)) ||
-        (rc = ensure_buffer(l.stage[3], cnt)))
+        (rc = ensure_buffer(l.stage[3], cnt)) ||
+        (g_prime_coop && (rc = ensure_buffer(l.stage[2], (size_t)cnt * (MPCX_MR_L + 2) * 4))))
       return rc;
     if ((rc = h2d(l.stage[0].ptr, n + (size_t)first * n_words, nb, l.st)) ||
         (rc = h2d(l.stage[1].ptr, bases + (size_t)first * n_words, nb, l.st)))
@@ -1032,7 +1053,14 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
     a.ok = (uint8_t*)l.stage[3].ptr;
     a.count = cnt;
     a.n_words = n_words;
-    hipError_t e = mpcx_launch_mr(&a, (cnt + 63) / 64, l.st);
+    hipError_t e;
+    if (g_prime_coop) {
+      a.r1 = (uint32_t*)l.stage[2].ptr;
+      a.meta = a.r1 + (size_t)cnt * MPCX_MR_L;
+      e = mpcx_launch_mrc(&a, l.st);
+    } else {
+      e = mpcx_launch_mr(&a, (cnt + 63) / 64, l.st);
+    }
     if (e != hipSuccess) return hip_fail(e, "launch k_mr");
     return d2h_sync(ok + first, l.stage[3].ptr, cnt, l.st);
   });
@@ -1057,7 +1085,8 @@ int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const 
     if ((rc = lane_stream(l))) return rc;
     const size_t nb = (size_t)cnt * n_words * 4;
     if ((rc = ensure_buffer(l.stage[0], nb)) || (rc = ensure_buffer(l.stage[1], (size_t)cnt * 4)) ||
-        (rc = ensure_buffer(l.stage[3], cnt)))
+        (rc = ensure_buffer(l.stage[3], cnt)) ||
+        (g_prime_coop && (rc = ensure_buffer(l.stage[2], (size_t)cnt * (4 * MPCX_MR_L + 2) * 4))))
       return rc;
     if ((rc = h2d(l.stage[0].ptr, n + (size_t)first * n_words, nb, l.st)) ||
         (rc = h2d(l.stage[1].ptr, P + first, (size_t)cnt * 4, l.st)))
@@ -1068,7 +1097,14 @@ int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const 
     a.ok = (uint8_t*)l.stage[3].ptr;
     a.count = cnt;
     a.n_words = n_words;
-    hipError_t e = mpcx_launch_lucas(&a, (cnt + 63) / 64, l.st);
+    hipError_t e;
+    if (g_prime_coop) {
+      a.consts = (uint32_t*)l.stage[2].ptr;
+      a.meta = a.consts + (size_t)cnt * 4 * MPCX_MR_L;
+      e = mpcx_launch_lucasc(&a, l.st);
+    } else {
+      e = mpcx_launch_lucas(&a, (cnt + 63) / 64, l.st);
+    }
     if (e != hipSuccess) return hip_fail(e, "launch k_lucas");
     return d2h_sync(ok + first, l.stage[3].ptr, cnt, l.st);
   });
@@ -1400,7 +1436,9 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
       (rc = ensure_buffer(sv[1], cap * 4)) || (rc = ensure_buffer(sv[2], misc_words * 4)) ||
       (rc = ensure_buffer(sv[3], (size_t)std::max<uint32_t>(max_pass, 1) * W * 4)) ||
       (rc = ensure_buffer(sv[4], (size_t)std::max<uint32_t>(max_pass, 1) * 4)) ||
-      (rc = ensure_buffer(sv[5], (size_t)n_sprp * (W * 4 + 1) + 64)) || (all_ok && (rc = ensure_buffer(sg[3], cap))))
+      (rc = ensure_buffer(sv[5], (size_t)n_sprp * (W * 4 + 1) + 64)) || (all_ok && (rc = ensure_buffer(sg[3], cap))) ||
+      (g_prime_coop && ((rc = ensure_buffer(sv[6], (cap + n_sprp) * MPCX_PRIME_L * 4)) ||
+                        (rc = ensure_buffer(sv[7], (cap + n_sprp) * 8)))))
     return rc;
   std::vector<uint32_t> misc(misc_words, 0);
   std::copy(tt.prod.begin(), tt.prod.end(), misc.begin() + off_prod);
@@ -1455,10 +1493,21 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
   pa.count_s = n_sprp;
   pa.ok_s = d_sok;
   pa.n_words = W;
-  const uint32_t blocks = pa.f_blocks + (n_sprp + 63) / 64;
-  if (blocks) {
-    e = mpcx_launch_prime2(&pa, blocks, l.st);
-    if (e != hipSuccess) return hip_fail(e, "launch k_prime2");
+  if (g_prime_coop) {
+    pa.f_blocks = (count + 64 / MPCX_PRIME_P - 1) / (64 / MPCX_PRIME_P);
+    pa.fp_blocks = (count + 63) / 64;
+    pa.r1 = (uint32_t*)sv[6].ptr;
+    pa.meta = (uint32_t*)sv[7].ptr;
+    if (count || n_sprp) {
+      e = mpcx_launch_prime2c(&pa, l.st);
+      if (e != hipSuccess) return hip_fail(e, "launch k_prime2c");
+    }
+  } else {
+    const uint32_t blocks = pa.f_blocks + (n_sprp + 63) / 64;
+    if (blocks) {
+      e = mpcx_launch_prime2(&pa, blocks, l.st);
+      if (e != hipSuccess) return hip_fail(e, "launch k_prime2");
+    }
   }
   uint32_t cnt2[2] = {0, 0};
   if ((rc = d2h_sync(cnt2, dm, 8, l.st))) return rc;

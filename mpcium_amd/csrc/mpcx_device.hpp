@@ -45,11 +45,20 @@
 #ifndef MPCX_SQR_OPT
 #define MPCX_SQR_OPT 1  // half-product squarings (montmul<..., true>)
 #endif
+#ifndef MPCX_PREFETCH2_KMAX
+#define MPCX_PREFETCH2_KMAX 24  // montmul reads b two digits ahead for K below this
+#endif
 #ifndef MPCX_PREFETCH_B
 #define MPCX_PREFETCH_B 1
 #endif
 #ifndef MPCX_WAVES_PER_EU_FERMAT
 #define MPCX_WAVES_PER_EU_FERMAT 1
+#endif
+#ifndef MPCX_WAVES_PER_EU_PRIME2C
+#define MPCX_WAVES_PER_EU_PRIME2C 3
+#endif
+#ifndef MPCX_WAVES_PER_EU_MRC
+#define MPCX_WAVES_PER_EU_MRC 3
 #endif
 #ifndef MPCX_WAVES_PER_EU_MR
 #define MPCX_WAVES_PER_EU_MR 1
@@ -165,7 +174,13 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
   uint64_t acc[K];
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
+  // b digits are read from LDS ahead of use: one iteration ahead, or two for
+  // short iterations (K < MPCX_PREFETCH2_KMAX: half an iteration of a K = 19
+  // squaring is ~60 cycles, under the LDS read latency). Rows carry 2 digits
+  // of padding for the reads past their end.
+  constexpr bool PF2 = K < MPCX_PREFETCH2_KMAX;
   uint32_t bnext = bl[0];
+  uint32_t bnext2 = PF2 ? bl[1] : 0u;
   for (int o = 0; o < P; ++o) {
     const uint32_t* bo = bl + o * K;
     // diagonal-register factor of this lane for the whole block (2 above the
@@ -176,6 +191,10 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
     static_for<0, K>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
       const uint32_t bi = bnext;
+      if constexpr (PF2) {
+        bnext = bnext2;
+        bnext2 = bo[u + 2];
+      }
       const uint32_t b2 = bi << 1;
       const uint32_t bd = b2 >> dsh;
       auto ab = [&](auto kc) __attribute__((always_inline)) {
@@ -198,11 +217,11 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
 #if MPCX_PREFETCH_B
       // next digit of b, in flight behind the bpermute and the a*b_i mads
       // (the last read of the last block touches the neighbour row: unused)
-      bnext = bo[u + 1];
+      if constexpr (!PF2) bnext = bo[u + 1];
 #endif
       static_for<1, K>(ab);
 #if !MPCX_PREFETCH_B
-      bnext = bo[u + 1];
+      if constexpr (!PF2) bnext = bo[u + 1];
 #endif
       static_for<0, K>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
@@ -297,7 +316,7 @@ __device__ __forceinline__ void store_result(uint32_t (&A)[K], const uint32_t (&
 template <int P, int K, int G, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp(const ModexpArgs a) {
   constexpr int L = P * K;
-  __shared__ uint32_t lds[(G + 1) * L + 1];  // +1: the b prefetch reads one past a row
+  __shared__ uint32_t lds[(G + 1) * L + 2];  // +2: the b prefetch reads up to two past a row
   const int lane = threadIdx.x;
   const int g_raw = lane / P;
   const bool idle = g_raw >= G;  // lanes beyond G*P carry zeros
@@ -539,7 +558,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 template <int P, int K, int G, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase(const FixedBaseArgs a) {
   constexpr int L = P * K;
-  __shared__ uint32_t lds[(G + 1) * L + 1];
+  __shared__ uint32_t lds[(G + 1) * L + 2];
   const int lane = threadIdx.x;
   const int g_raw = lane / P;
   const bool idle = g_raw >= G;
@@ -737,7 +756,7 @@ __device__ __forceinline__ uint32_t word_bit(const uint32_t* w, int j) { return 
 template <int K, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_prime2(const Prime2Args a) {
   constexpr int L = K;
-  __shared__ uint32_t lds[65 * L + 1];
+  __shared__ uint32_t lds[65 * L + 2];
   const int lane = threadIdx.x;
   const bool strong = blockIdx.x >= a.f_blocks;
   uint32_t op, cnt;
@@ -827,7 +846,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 template <int K, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_lucas(const LucasArgs a) {
   constexpr int L = K;
-  __shared__ uint32_t lds[65 * L + 1];
+  __shared__ uint32_t lds[65 * L + 2];
   const int lane = threadIdx.x;
   const uint32_t op = blockIdx.x * 64u + lane;
   if (blockIdx.x * 64u >= a.count) return;
@@ -960,7 +979,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 template <int K, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_mr(const MrArgs a) {
   constexpr int L = K;
-  __shared__ uint32_t lds[2 * 65 * L + 1];
+  __shared__ uint32_t lds[2 * 65 * L + 2];
   const int lane = threadIdx.x;
   const uint32_t op = blockIdx.x * 64u + lane;
   const bool active = op < a.count;
@@ -1087,6 +1106,544 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     pass = eq(A, NR1);
   }
   if (active) a.ok[op] = pass ? 1 : 0;
+}
+
+// ------------------------------------ cooperative per-candidate kernels
+// The thread-per-candidate kernels above hold K = 37 digits per lane and run
+// one wavefront per SIMD, where a lone wave issues v_mad_u64_u32 at ~45% of
+// the SIMD peak (profiles/r01): a Fermat launch is capped there, and a small
+// Miller-Rabin or Lucas batch is one thread's full serial latency. The
+// kernels below give each candidate P lanes (K digits each, the k_modexp
+// montmul with a per-group modulus and -n^-1): P = 2 x K = 19 for the base-2
+// throughput tests (32 candidates and 3 waves per SIMD), P = 16 x K = 3 for
+// general-base Miller-Rabin (4 tests per wave, 1/8 of the serial chain).
+// Per-item constants come from a thread-per-item prep kernel.
+
+// R mod n (canonical, L digits), -n^-1 mod 2^28 and nbits | s << 16
+// (s = v2(n - 1)) of one odd n >= 5 for R = 2^(28 L): 28 L - nbits doublings,
+// a few % of the exponentiation that follows.
+template <int L>
+__device__ __forceinline__ void pprep_item(const uint32_t* nw, uint32_t n_words, uint32_t* r1_out, uint32_t* meta_out) {
+  uint32_t Nd[L], R1[L];
+  load_candidate<L>(nw, n_words, true, Nd);
+  const int nbits = bitlen_digits<L>(Nd);
+  r_mod<L>(Nd, nbits, R1);
+  int s = 1;
+  while (s < nbits && !word_bit(nw, s)) ++s;
+#pragma unroll
+  for (int d = 0; d < L; ++d) r1_out[d] = R1[d];
+  meta_out[0] = neg_inv28(Nd[0]);
+  meta_out[1] = (uint32_t)nbits | ((uint32_t)s << 16);
+}
+
+template <int L>
+__global__ __launch_bounds__(64) void k_pprep_prime2(const Prime2Args a) {
+  const bool strong = blockIdx.x >= a.fp_blocks;
+  uint32_t cnt, i;
+  const uint32_t* src;
+  size_t base;
+  if (!strong) {
+    cnt = a.count_dev ? min(a.count_f, *a.count_dev) : a.count_f;
+    i = blockIdx.x * 64u + threadIdx.x;
+    src = a.nf;
+    base = 0;
+  } else {
+    cnt = a.count_s;
+    i = (blockIdx.x - a.fp_blocks) * 64u + threadIdx.x;
+    src = a.ns;
+    base = a.count_f;
+  }
+  if (i >= cnt) return;
+  pprep_item<L>(src + (size_t)i * a.n_words, a.n_words, a.r1 + (base + i) * L, a.meta + (base + i) * 2);
+}
+
+template <int L>
+__global__ __launch_bounds__(64) void k_pprep_mr(const MrArgs a) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  if (i >= a.count) return;
+  pprep_item<L>(a.n + (size_t)i * a.n_words, a.n_words, a.r1 + (size_t)i * L, a.meta + (size_t)i * 2);
+}
+
+// digits p*K .. p*K+K-1 of a little-endian word array (radix 2^28)
+template <int K>
+__device__ __forceinline__ void load_group_digits(const uint32_t* w, uint32_t words, int p, uint32_t (&D)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const uint32_t bit = (uint32_t)(p * K + k) * DB, wi = bit >> 5, sh = bit & 31u;
+    const uint64_t v = ((uint64_t)((wi + 1) < words ? w[wi + 1] : 0u) << 32) | (wi < words ? w[wi] : 0u);
+    D[k] = (uint32_t)(v >> sh) & M28;
+  }
+}
+
+__device__ __forceinline__ int wave_max(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
+  return v;
+}
+
+// all P lanes of this lane's group have v set
+template <int P>
+__device__ __forceinline__ bool group_all(bool v, int g) {
+  const uint64_t bal = __ballot(v);
+  const uint64_t gmask = (P == 64 ? ~0ull : (((1ull << P) - 1ull) << (g * P)));
+  return (bal & gmask) == gmask;
+}
+
+// Leave the Montgomery domain on a copy and compare with 1 and n - 1:
+// Y = mont(X, 1) <= n, canonical digits (uses the group's LDS row bl).
+template <int P, int K>
+__device__ __forceinline__ void exit_compare(const uint32_t (&X)[K], const uint32_t (&Nd)[K], uint32_t n0inv,
+                                             uint32_t* bl, int p, int g, bool* is_one, bool* is_nm1) {
+  uint32_t Y[K], one[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    Y[k] = X[k];
+    one[k] = (p == 0 && k == 0) ? 1u : 0u;
+  }
+  wave_lds_fence();
+  lds_store_digits<K>(bl, p, one);
+  wave_lds_fence();
+  montmul<P, K, false>(Y, bl, Nd, n0inv, 0, p);
+  wave_lds_fence();
+  canonicalize<P, K>(Y);
+  bool e1 = true, em = true;
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    const bool d0 = p == 0 && k == 0;
+    e1 &= Y[k] == (d0 ? 1u : 0u);
+    em &= Y[k] == (d0 ? Nd[0] - 1u : Nd[k]);  // n odd: n - 1 only changes digit 0
+  }
+  *is_one = group_all<P>(e1, g);
+  *is_nm1 = group_all<P>(em, g);
+}
+
+// x <- 2x (digits doubled, one carry pass; values stay < R / 4)
+template <int P, int K>
+__device__ __forceinline__ void double_digits(uint32_t (&A)[K], bool on) {
+  const uint32_t sh = on ? 1u : 0u;
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] <<= sh;
+  carry_pass32<P, K>(A);
+}
+
+// Base-2 tests of k_prime2, P lanes per candidate: Fermat items
+// (2^(n-1) == 1) in blocks [0, f_blocks), strong items (n - 1 = 2^s d:
+// 2^d == 1, or 2^(2^j d) == n - 1 for some j < s) after them. Square and
+// double as in k_prime2 (values < 4n, R > 16n); the exponent bits differ per
+// candidate, so the doubling is a per-lane shift by 0 or 1.
+template <int P, int K, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_prime2c(const Prime2Args a) {
+  constexpr int L = P * K, G = 64 / P;
+  __shared__ uint32_t lds[2 * G * L + 2];  // per group: work row, saved-x row
+  const int lane = threadIdx.x, g = lane / P, p = lane - g * P;
+  const bool strong = blockIdx.x >= a.f_blocks;
+  uint32_t cnt, item;
+  const uint32_t* src;
+  size_t base;
+  if (!strong) {
+    cnt = a.count_dev ? min(a.count_f, *a.count_dev) : a.count_f;
+    if (blockIdx.x * (uint32_t)G >= cnt) return;  // whole wave beyond the sieve's survivors
+    item = blockIdx.x * G + g;
+    src = a.nf;
+    base = 0;
+  } else {
+    cnt = a.count_s;
+    if ((blockIdx.x - a.f_blocks) * (uint32_t)G >= cnt) return;
+    item = (blockIdx.x - a.f_blocks) * G + g;
+    src = a.ns;
+    base = a.count_f;
+  }
+  const bool active = item < cnt;
+  const uint32_t it = active ? item : item - g;  // idle groups recompute the block's first item
+  uint32_t* bl = lds + 2 * g * L;
+  uint32_t* sv = bl + L;
+  const uint32_t* nw = src + (size_t)it * a.n_words;
+  uint32_t Nd[K], A[K];
+  load_group_digits<K>(nw, a.n_words, p, Nd);
+  {
+    const uint32_t* r1 = a.r1 + (base + it) * L + p * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) A[k] = r1[k];  // Montgomery 1
+  }
+  const uint32_t n0inv = a.meta[(base + it) * 2];
+  const uint32_t mt = a.meta[(base + it) * 2 + 1];
+  const int nbits = (int)(mt & 0xFFFFu), s = (int)(mt >> 16);
+  const int sh = strong ? s : 0;  // strong: e = (n - 1) >> s; Fermat: e = n - 1
+  // Left to right from the wave's highest exponent bit, starting at
+  // Montgomery 1: above a candidate's own top bit its exponent bits are 0 and
+  // squaring 1 changes nothing, so no lane needs a predicated select.
+  // Two montmul call sites (squaring, exit product) as in k_modexp: states
+  //   SQ : x <- x^2, then x <- 2x on an exponent bit
+  //   EX : y = mont(x, 1) <= n (x saved in the group's second row), compare
+  //        y with 1 and n - 1, restore x
+  //   SS : strong-test squaring x <- x^2, then EX again
+  enum { SQ, EX, SS };
+  int st = SQ;
+  int i = wave_max(nbits - sh - 1), j = 0;
+  const int smax = strong ? wave_max(s) : 1;
+  bool pass = false, done = false;
+  for (;;) {
+    wave_lds_fence();
+    if (st == EX) {
+      uint32_t one[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0) ? 1u : 0u;
+      lds_store_digits<K>(sv, p, A);
+      lds_store_digits<K>(bl, p, one);
+    } else {
+      lds_store_digits<K>(bl, p, A);
+    }
+    wave_lds_fence();
+    if (st == EX) {
+      montmul<P, K, false>(A, bl, Nd, n0inv, 0, p);
+    } else {
+      montmul<P, K, true>(A, bl, Nd, n0inv, 0, p);
+    }
+    if (st == SQ) {
+      const int jb = i + sh;  // bit jb of n - 1: bit jb of n except bit 0 (n odd)
+      double_digits<P, K>(A, jb > 0 && jb < nbits && word_bit(nw, jb));
+      if (--i < 0) st = EX;
+    } else if (st == SS) {
+      st = EX;
+    } else {
+      canonicalize<P, K>(A);
+      bool e1 = true, em = true;
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        const bool d0 = p == 0 && k == 0;
+        e1 &= A[k] == (d0 ? 1u : 0u);
+        em &= A[k] == (d0 ? Nd[0] - 1u : Nd[k]);  // n odd: n - 1 only changes digit 0
+      }
+      const bool one = group_all<P>(e1, g), nm1 = group_all<P>(em, g);
+      if (j == 0) {
+        pass = one || (strong && nm1);
+        done = pass;
+      } else if (!done && j < s) {
+        if (one) {
+          done = true;  // nontrivial square root of 1: composite
+        } else if (nm1) {
+          pass = true;
+          done = true;
+        }
+      }
+      if (++j >= smax) break;
+      wave_lds_fence();
+#pragma unroll
+      for (int k = 0; k < K; ++k) A[k] = sv[p * K + k];
+      st = SS;
+    }
+  }
+  if (!active || p != 0) return;
+  if (strong) {
+    a.ok_s[item] = pass ? 1 : 0;
+    return;
+  }
+  if (a.ok_f) a.ok_f[item] = pass ? 1 : 0;
+  if (pass && a.pass_count) {
+    const uint32_t slot = atomicAdd(a.pass_count, 1u);
+    a.pass_idx[slot] = a.sieve_idx ? a.sieve_idx[item] : item;
+    for (uint32_t w = 0; w < a.n_words; ++w) a.pass_n[(size_t)slot * a.n_words + w] = nw[w];
+  }
+}
+
+// Miller-Rabin to arbitrary bases, P lanes per test: R^2 mod n by
+// square-and-double from Mont(2), a R = mont(a, R^2), a 16-entry table
+// T[v] = a^v R in the group's LDS rows, then x = a^d by Go's 4-bit fixed
+// window (4 squarings and one table product per window for every lane: the
+// wave never diverges) and the strong check. ok[i] as k_mr.
+template <int P, int K, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_mrc(const MrArgs a) {
+  constexpr int L = P * K, G = 64 / P, ROWS = 17;  // table rows 0..15, work row 16
+  __shared__ uint32_t lds[G * ROWS * L + 2];
+  const int lane = threadIdx.x, g = lane / P, p = lane - g * P;
+  if (blockIdx.x * (uint32_t)G >= a.count) return;
+  const uint32_t item = blockIdx.x * G + g;
+  const bool active = item < a.count;
+  const uint32_t it = active ? item : item - g;
+  uint32_t* rows = lds + g * ROWS * L;
+  uint32_t* wl = rows + 16 * L;
+  const uint32_t* nw = a.n + (size_t)it * a.n_words;
+  uint32_t Nd[K], R1[K], A[K], X[K];
+  load_group_digits<K>(nw, a.n_words, p, Nd);
+  load_group_digits<K>(a.a + (size_t)it * a.n_words, a.n_words, p, X);
+  const uint32_t* r1 = a.r1 + (size_t)it * L + p * K;
+#pragma unroll
+  for (int k = 0; k < K; ++k) R1[k] = r1[k];
+  const uint32_t n0inv = a.meta[(size_t)it * 2];
+  const uint32_t mt = a.meta[(size_t)it * 2 + 1];
+  const int nbits = (int)(mt & 0xFFFFu), s = (int)(mt >> 16);
+  auto sqr = [&] __attribute__((always_inline))() {
+    wave_lds_fence();
+    lds_store_digits<K>(wl, p, A);
+    wave_lds_fence();
+    montmul<P, K, true>(A, wl, Nd, n0inv, 0, p);
+  };
+  // R^2 mod n = Mont(2^(28 L)): square-and-double over E = 28 L from Mont(2)
+  constexpr int E = DB * L;
+  constexpr int ETOP = 31 - __builtin_clz((unsigned)E);
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] = R1[k];
+  double_digits<P, K>(A, true);
+  for (int i = ETOP - 1; i >= 0; --i) {
+    sqr();
+    double_digits<P, K>(A, ((E >> i) & 1) != 0);
+  }
+  // T[1] = a R = mont(a, R^2); T[0] = R mod n; T[v] = mont(T[v-1], T[1])
+  wave_lds_fence();
+  lds_store_digits<K>(wl, p, A);
+  wave_lds_fence();
+  montmul<P, K, false>(X, wl, Nd, n0inv, 0, p);
+  wave_lds_fence();
+  lds_store_digits<K>(rows, p, R1);
+  lds_store_digits<K>(rows + L, p, X);
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] = X[k];
+  for (int v = 2; v < 16; ++v) {
+    wave_lds_fence();
+    montmul<P, K, false>(A, rows + L, Nd, n0inv, 0, p);
+    wave_lds_fence();
+    lds_store_digits<K>(rows + v * L, p, A);
+  }
+  // x = a^d, d = (n - 1) >> s = bits [s, nbits) of n, 4-bit windows from the top
+  const int dbits = nbits - s;
+  const int nwin = (dbits + 3) / 4;
+#pragma unroll
+  for (int k = 0; k < K; ++k) A[k] = R1[k];  // Montgomery one: leading zero windows keep it
+  for (int w = wave_max(nwin) - 1; w >= 0; --w) {
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) sqr();
+    uint32_t v = 0;
+#pragma unroll
+    for (int b = 3; b >= 0; --b) {
+      const int j = s + 4 * w + b;
+      v = (v << 1) | ((j < nbits) ? word_bit(nw, j) : 0u);
+    }
+    wave_lds_fence();
+    montmul<P, K, false>(A, rows + v * L, Nd, n0inv, 0, p);
+  }
+  bool one, nm1;
+  exit_compare<P, K>(A, Nd, n0inv, wl, p, g, &one, &nm1);
+  bool pass = one || nm1, done = pass;
+  const int smax = wave_max(s);
+  for (int j = 1; j < smax; ++j) {
+    sqr();
+    exit_compare<P, K>(A, Nd, n0inv, wl, p, g, &one, &nm1);
+    const bool live = !done && j < s;
+    if (live && one) done = true;  // nontrivial square root of 1: composite
+    else if (live && nm1) {
+      pass = true;
+      done = true;
+    }
+  }
+  if (active && p == 0) a.ok[item] = pass ? 1 : 0;
+}
+
+// Strong Lucas test (k_lucas's ladder and checks), P lanes per candidate.
+// Per-item Montgomery constants from a thread-per-item prep (the serial
+// Horner / doubling steps), then the V ladder: every bit is one product and
+// one squaring for every lane; bits above a candidate's own top keep
+// (V_0, V_1) = (2, P) fixed (2^2 - 2 = 2, 2P - P = P), so the wave needs no
+// predication. The checks compare canonical values after leaving the
+// Montgomery domain.
+template <int L>
+__global__ __launch_bounds__(64) void k_pprep_lucas(const LucasArgs a) {
+  const uint32_t i = blockIdx.x * 64u + threadIdx.x;
+  if (i >= a.count) return;
+  const uint32_t* nw = a.n + (size_t)i * a.n_words;
+  uint32_t Nd[L], R1[L], PR[L], T[L];
+  load_candidate<L>(nw, a.n_words, true, Nd);
+  const int nbits = bitlen_digits<L>(Nd);
+  r_mod<L>(Nd, nbits, R1);
+  const uint32_t P = a.P[i];
+#pragma unroll
+  for (int k = 0; k < L; ++k) PR[k] = 0;
+  for (int b = 13; b >= 0; --b) {  // P R mod n, Horner over P's bits
+#pragma unroll
+    for (int k = 0; k < L; ++k) PR[k] <<= 1;
+    norm_serial<L>(PR);
+    if (ge_digits<L>(PR, Nd)) sub_digits<L>(PR, Nd);
+    if ((P >> b) & 1u) {
+      add_digits<L>(PR, R1);
+      if (ge_digits<L>(PR, Nd)) sub_digits<L>(PR, Nd);
+    }
+  }
+  uint32_t* c = a.consts + (size_t)i * 4 * L;
+  // [0] P R, [1] 2 R, [2] 2n - P R, [3] 2n - 2 R (all canonical, < 2n)
+#pragma unroll
+  for (int k = 0; k < L; ++k) c[k] = PR[k];
+#pragma unroll
+  for (int k = 0; k < L; ++k) T[k] = R1[k] << 1;
+  norm_serial<L>(T);
+  if (ge_digits<L>(T, Nd)) sub_digits<L>(T, Nd);
+#pragma unroll
+  for (int k = 0; k < L; ++k) c[L + k] = T[k];
+  uint32_t N2[L];
+#pragma unroll
+  for (int k = 0; k < L; ++k) N2[k] = Nd[k] << 1;
+  norm_serial<L>(N2);
+  {
+    uint32_t X[L];
+#pragma unroll
+    for (int k = 0; k < L; ++k) X[k] = N2[k];
+    sub_digits<L>(X, PR);
+#pragma unroll
+    for (int k = 0; k < L; ++k) c[2 * L + k] = X[k];
+#pragma unroll
+    for (int k = 0; k < L; ++k) X[k] = N2[k];
+    sub_digits<L>(X, T);
+#pragma unroll
+    for (int k = 0; k < L; ++k) c[3 * L + k] = X[k];
+  }
+  int r = 0;  // n + 1 = 2^r s: r = trailing ones of n
+  while (r < nbits && word_bit(nw, r)) ++r;
+  a.meta[(size_t)i * 2] = neg_inv28(Nd[0]);
+  a.meta[(size_t)i * 2 + 1] = (uint32_t)nbits | ((uint32_t)r << 16);
+}
+
+// canonical value of Montgomery-form X in [0, n): y = mont(X, 1) <= n, with
+// n mapped to 0
+template <int P, int K>
+__device__ __forceinline__ void exit_canonical(const uint32_t (&X)[K], const uint32_t (&Nd)[K], uint32_t n0inv,
+                                               uint32_t* bl, int p, int g, uint32_t (&Y)[K]) {
+  uint32_t one[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) {
+    Y[k] = X[k];
+    one[k] = (p == 0 && k == 0) ? 1u : 0u;
+  }
+  wave_lds_fence();
+  lds_store_digits<K>(bl, p, one);
+  wave_lds_fence();
+  montmul<P, K, false>(Y, bl, Nd, n0inv, 0, p);
+  wave_lds_fence();
+  canonicalize<P, K>(Y);
+  bool en = true;
+#pragma unroll
+  for (int k = 0; k < K; ++k) en &= Y[k] == Nd[k];
+  if (group_all<P>(en, g)) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) Y[k] = 0;
+  }
+}
+
+// canonical Y equals the small constant c
+template <int P, int K>
+__device__ __forceinline__ bool group_eq_small(const uint32_t (&Y)[K], uint32_t c, int p, int g) {
+  bool e = true;
+#pragma unroll
+  for (int k = 0; k < K; ++k) e &= Y[k] == ((p == 0 && k == 0) ? c : 0u);
+  return group_all<P>(e, g);
+}
+
+template <int P, int K, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_lucasc(const LucasArgs a) {
+  constexpr int L = P * K, G = 64 / P;
+  __shared__ uint32_t lds[G * L + 2];
+  const int lane = threadIdx.x, g = lane / P, p = lane - g * P;
+  if (blockIdx.x * (uint32_t)G >= a.count) return;
+  const uint32_t item = blockIdx.x * G + g;
+  const bool active = item < a.count;
+  const uint32_t it = active ? item : item - g;
+  uint32_t* bl = lds + g * L;
+  const uint32_t* nw = a.n + (size_t)it * a.n_words;
+  uint32_t Nd[K], PR[K], CP[K], C2[K], vk[K], vk1[K];
+  load_group_digits<K>(nw, a.n_words, p, Nd);
+  {
+    const uint32_t* c = a.consts + (size_t)it * 4 * L + p * K;
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      PR[k] = c[k];
+      vk[k] = c[L + k];  // V_0 = 2
+      CP[k] = c[2 * L + k];
+      C2[k] = c[3 * L + k];
+      vk1[k] = PR[k];  // V_1 = P
+    }
+  }
+  const uint32_t n0inv = a.meta[(size_t)it * 2];
+  const uint32_t mt = a.meta[(size_t)it * 2 + 1];
+  const int nbits = (int)(mt & 0xFFFFu), r = (int)(mt >> 16);
+  const int sbits = (r == nbits) ? 1 : nbits - r;  // bit length of s = (n + 1) >> r
+  auto add_const = [&](uint32_t (&X)[K], const uint32_t (&C)[K]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < K; ++k) X[k] += C[k];
+    carry_pass32<P, K>(X);  // < 4n < R: no carry leaves the group
+  };
+  for (int i = wave_max(sbits) - 1; i >= 0; --i) {
+    const int j = i + r;  // bit i of s = bit j of n + 1: 1 at j == r, n's bit above
+    const bool bit = i < sbits && (j == r || (j < nbits && word_bit(nw, j)));
+    // X = V_k V_k+1 - P; Y = (bit ? V_k+1 : V_k)^2 - 2
+    uint32_t X[K], Y[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      X[k] = vk[k];
+      Y[k] = bit ? vk1[k] : vk[k];
+    }
+    wave_lds_fence();
+    lds_store_digits<K>(bl, p, vk1);
+    wave_lds_fence();
+    montmul<P, K, false>(X, bl, Nd, n0inv, 0, p);
+    add_const(X, CP);
+    wave_lds_fence();
+    lds_store_digits<K>(bl, p, Y);
+    wave_lds_fence();
+    montmul<P, K, true>(Y, bl, Nd, n0inv, 0, p);
+    add_const(Y, C2);
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      vk[k] = bit ? X[k] : Y[k];
+      vk1[k] = bit ? Y[k] : X[k];
+    }
+  }
+  // V_s == +-2 and U_s == 0 (P V_s == 2 V_s+1), or V_(2^t s) == 0, t < r - 1
+  uint32_t Y[K];
+  exit_canonical<P, K>(vk, Nd, n0inv, bl, p, g, Y);
+  bool pass = false;
+  {
+    const bool is2 = group_eq_small<P, K>(Y, 2u, p, g);
+    uint32_t Z[K];  // Y + 2 == n  <=>  V_s == n - 2
+#pragma unroll
+    for (int k = 0; k < K; ++k) Z[k] = Y[k] + ((p == 0 && k == 0) ? 2u : 0u);
+    carry_pass32<P, K>(Z);
+    bool en = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) en &= Z[k] == Nd[k];
+    const bool isn2 = group_all<P>(en, g);
+    uint32_t U1[K], U2[K], A1[K], A2[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      U1[k] = vk[k];
+      U2[k] = vk1[k] << 1;  // 2 V_s+1 R (< 4n)
+    }
+    carry_pass32<P, K>(U2);
+    wave_lds_fence();
+    lds_store_digits<K>(bl, p, PR);
+    wave_lds_fence();
+    montmul<P, K, false>(U1, bl, Nd, n0inv, 0, p);  // P V_s R
+    exit_canonical<P, K>(U1, Nd, n0inv, bl, p, g, A1);
+    exit_canonical<P, K>(U2, Nd, n0inv, bl, p, g, A2);
+    bool eu = true;
+#pragma unroll
+    for (int k = 0; k < K; ++k) eu &= A1[k] == A2[k];
+    pass = (is2 || isn2) && group_all<P>(eu, g);
+  }
+  bool done = pass;
+  const int tmax = wave_max(r - 1);
+  for (int t = 0; t < tmax; ++t) {
+    const bool live = !done && t < r - 1;
+    exit_canonical<P, K>(vk, Nd, n0inv, bl, p, g, Y);
+    if (live && group_eq_small<P, K>(Y, 0u, p, g)) {
+      pass = true;
+      done = true;
+    } else if (live && group_eq_small<P, K>(Y, 2u, p, g)) {
+      done = true;  // V = 2 is a fixed point of V^2 - 2: never 0
+    }
+    wave_lds_fence();
+    lds_store_digits<K>(bl, p, vk);
+    wave_lds_fence();
+    montmul<P, K, true>(vk, bl, Nd, n0inv, 0, p);
+    add_const(vk, C2);
+  }
+  if (active && p == 0) a.ok[item] = pass ? 1 : 0;
 }
 
 }  // namespace mpcx

@@ -156,7 +156,23 @@ struct Prime2Args {
   uint32_t count_s;
   uint8_t* ok_s;
   uint32_t n_words;
+  // cooperative kernels (k_pprep_prime2 + k_prime2c): per-item constants for
+  // the Fermat items [0, count_f) then the strong items (offset count_f)
+  uint32_t* r1;        // (count_f + count_s) x MPCX_PRIME_L digits: R mod n
+  uint32_t* meta;      // (count_f + count_s) x 2: -n^-1 mod 2^28, nbits | s << 16
+  uint32_t fp_blocks;  // prep blocks (64 items) of the Fermat segment
 };
+
+// Cooperative per-candidate geometries (P lanes x K digits per candidate,
+// L = P K digits, R = 2^(28 L) > 16 n for n < 2^1024): the base-2 tests of
+// the safe-prime step, and Miller-Rabin with arbitrary bases (latency-bound
+// batches: 16 lanes per test).
+#define MPCX_PRIME_P 2
+#define MPCX_PRIME_K 19
+#define MPCX_PRIME_L (MPCX_PRIME_P * MPCX_PRIME_K)
+#define MPCX_MR_P 16
+#define MPCX_MR_K 3
+#define MPCX_MR_L (MPCX_MR_P * MPCX_MR_K)
 
 // Strong Lucas probable-prime test (Go math/big probablyPrimeLucas, the
 // "extra strong" test with Baillie-OEIS method C parameters P, Q = 1,
@@ -167,6 +183,10 @@ struct LucasArgs {
   uint8_t* ok;
   uint32_t count;
   uint32_t n_words;
+  // cooperative kernel (k_pprep_lucas + k_lucasc, MPCX_MR_L digits): per item
+  // P R, 2 R, 2n - P R, 2n - 2 R (Montgomery forms) and n0inv, nbits | r << 16
+  uint32_t* consts;  // count x 4 x MPCX_MR_L digits
+  uint32_t* meta;    // count x 2
 };
 
 // The build's CounterDRBG stream on the device: block c (32 bytes) =
@@ -185,6 +205,8 @@ struct MrArgs {
   uint8_t* ok;
   uint32_t count;
   uint32_t n_words;
+  uint32_t* r1;    // cooperative kernel: count x MPCX_MR_L digits (k_pprep_mr)
+  uint32_t* meta;  // count x 2
 };
 
 }  // namespace mpcx

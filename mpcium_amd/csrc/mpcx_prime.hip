@@ -300,6 +300,38 @@ __attribute__((visibility("hidden"))) hipError_t mpcx_launch_prime2(const mpcx::
   return hipGetLastError();
 }
 
+// cooperative base-2 tests: per-item constants, then P lanes per candidate
+// (the caller sets f_blocks = ceil(count_f / (64 / MPCX_PRIME_P)) and
+// fp_blocks = ceil(count_f / 64))
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_prime2c(const mpcx::Prime2Args* a, hipStream_t st) {
+  constexpr uint32_t G = 64 / MPCX_PRIME_P;
+  const uint32_t pb = a->fp_blocks + (a->count_s + 63) / 64;
+  const uint32_t cb = a->f_blocks + (a->count_s + G - 1) / G;
+  if (pb) hipLaunchKernelGGL((mpcx::k_pprep_prime2<MPCX_PRIME_L>), dim3(pb), dim3(64), 0, st, *a);
+  if (cb)
+    hipLaunchKernelGGL((mpcx::k_prime2c<MPCX_PRIME_P, MPCX_PRIME_K, MPCX_WAVES_PER_EU_PRIME2C>), dim3(cb), dim3(64), 0,
+                       st, *a);
+  return hipGetLastError();
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_mrc(const mpcx::MrArgs* a, hipStream_t st) {
+  constexpr uint32_t G = 64 / MPCX_MR_P;
+  if (a->count == 0) return hipSuccess;
+  hipLaunchKernelGGL((mpcx::k_pprep_mr<MPCX_MR_L>), dim3((a->count + 63) / 64), dim3(64), 0, st, *a);
+  hipLaunchKernelGGL((mpcx::k_mrc<MPCX_MR_P, MPCX_MR_K, MPCX_WAVES_PER_EU_MRC>), dim3((a->count + G - 1) / G), dim3(64),
+                     0, st, *a);
+  return hipGetLastError();
+}
+
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_lucasc(const mpcx::LucasArgs* a, hipStream_t st) {
+  constexpr uint32_t G = 64 / MPCX_MR_P;
+  if (a->count == 0) return hipSuccess;
+  hipLaunchKernelGGL((mpcx::k_pprep_lucas<MPCX_MR_L>), dim3((a->count + 63) / 64), dim3(64), 0, st, *a);
+  hipLaunchKernelGGL((mpcx::k_lucasc<MPCX_MR_P, MPCX_MR_K, MPCX_WAVES_PER_EU_MRC>), dim3((a->count + G - 1) / G),
+                     dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
 __attribute__((visibility("hidden"))) hipError_t mpcx_launch_lucas(const mpcx::LucasArgs* a, uint32_t blocks,
                                                                   hipStream_t st) {
   hipLaunchKernelGGL((mpcx::k_lucas<MPCX_C0_K, MPCX_WAVES_PER_EU_MR>), dim3(blocks), dim3(64), 0, st, *a);

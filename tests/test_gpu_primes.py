@@ -59,18 +59,54 @@ def test_mr_base2_pseudoprimes(gpu):
     assert all(got[:len(A001262)])
 
 
-def test_lucas_kernel(gpu):
+@pytest.mark.parametrize("coop", [1, 0])
+def test_fermat_and_mr_kernels_both_geometries(gpu, coop):
+    """The cooperative kernels (k_prime2c: 2 lanes per candidate; k_mrc: 16
+    lanes per test, 4-bit window) and the thread-per-candidate ones give the
+    same decisions as CPython pow on primes, pseudoprimes, Carmichael numbers
+    and random odd candidates of 3..1024 bits (bit lengths mixed in one wave)."""
     import random
-    rng = random.Random(3)
+    rng = random.Random(11 + coop)
+    ns = A001262 + CARMICHAEL + [5, 7, 9, 15, 101, 7919, 3825123056546413051, (1 << 521) - 1, (1 << 607) - 1]
+    ns += [rng.getrandbits(rng.randrange(3, 1025)) | 1 for _ in range(150)]
+    ns += [(rng.getrandbits(1023) | (1 << 1023) | 1) for _ in range(50)]
+    ns = [n for n in ns if n >= 5]
+    key = load_golden("paillier_key_2048.json")
+    ns += [int(key["P"], 16), int(key["Q"], 16)]
+    gpu.set_option("prime_coop", coop)
+    try:
+        assert gpu.fermat2_batch(ns) == [pow(2, n - 1, n) == 1 for n in ns]
+        bases = [rng.randrange(2, n - 1) if n > 4 else 2 for n in ns]
+        assert gpu.mr_batch(ns, bases) == [S.strong_probable_prime(n, a) for n, a in zip(ns, bases)]
+        assert gpu.mr_batch(ns, [2] * len(ns)) == [S.strong_probable_prime(n, 2) for n in ns]
+    finally:
+        gpu.set_option("prime_coop", 1)
+
+
+@pytest.mark.parametrize("coop", [1, 0])
+def test_lucas_kernel(gpu, coop):
+    """k_lucasc (16 lanes per candidate) and k_lucas (thread per candidate)
+    against the oracle: the extra strong Lucas pseudoprimes pass (as in Go),
+    primes pass, composites of mixed sizes fail."""
+    import random
+    rng = random.Random(3 + coop)
     ns = A217719 + [3825123056546413051, (1 << 521) - 1, (1 << 607) - 1, 1000003, 999983 * 1000003]
     ns += [rng.getrandbits(1023) | (1 << 1022) | 1 for _ in range(40)]
+    ns += [rng.getrandbits(rng.randrange(5, 1024)) | 1 for _ in range(40)]
+    ns += [(1 << 89) - 1, (1 << 127) - 1, 2 ** 64 - 59]
     runs, Ps = [], []
     for n in ns:
+        if n < 5:
+            continue
         r, P = S.lucas_param(n)
         if r == 1:
             runs.append(n)
             Ps.append(P)
-    got = gpu.lucas_batch(runs, Ps)
+    gpu.set_option("prime_coop", coop)
+    try:
+        got = gpu.lucas_batch(runs, Ps)
+    finally:
+        gpu.set_option("prime_coop", 1)
     assert got == [S.probably_prime_lucas(n) for n in runs]
     assert all(got[:len(A217719)])  # the pseudoprimes pass, as in Go
 
