@@ -312,7 +312,10 @@ size_t default_batch(int bitLen) {
       return v >= 1024 && v <= (1l << 22) ? (size_t)v : (size_t)0;
     }();
     if (env) return env;
-    return 262144;
+    // 2^19: the ~132K sieve survivors fill whole resident rounds of k_prime2c
+    // (MI355X sweep, profiles/r02/pmc2: 2^18 -> 353, 2^19 -> 416, 3 * 2^18
+    // -> 393 safe primes/s)
+    return 524288;
   }
   if (bitLen > 256) return 65536;
   return 16384;
