@@ -711,6 +711,65 @@ def main():
         if bad:
             raise SystemExit(f"rank {rank}: GPU results differ from pow() at operands {bad[:5]}")
 
+    # whole-batch digest of rank 0's default batch against the C restatement
+    # (tests/golden/batch_digest.json, untimed)
+    digest = None
+    gd_path = os.path.join(ROOT, "tests", "golden", "batch_digest.json")
+    if rank == 0 and args.modbits == 4096 and args.steps + args.warmup > 0 and os.path.exists(gd_path):
+        gd = json.load(open(gd_path))
+        if gd["count"] == count and gd["words"] == words:
+            import hashlib
+            got = hashlib.sha256(d_out.cpu().numpy().astype("<u4").tobytes()).hexdigest()
+            digest = {"sha256": got, "expected": gd["sha256"], "match": got == gd["sha256"],
+                      "scope": f"all {count} outputs of rank 0 vs oracle/gomodexp.c (tests/golden/batch_digest.json)"}
+            if not digest["match"]:
+                raise SystemExit(f"rank 0: batch digest {got} != C restatement {gd['sha256']}")
+
+    def per_operand(E: int) -> dict:
+        """Config-2 secondary shape: the same 65,536 bases with per-operand
+        uniform E-bit exponents (Go's 4-bit fixed window per operand; no
+        shared sliding-window schedule), one launch, HIP events."""
+        rng = np.random.default_rng(0x70657230 + E)
+        ew = (E + 31) // 32
+        ex = rng.integers(0, 1 << 32, size=(count, ew), dtype=np.uint64).astype(np.uint32)
+        tb = (E - 1) % 32
+        ex[:, ew - 1] &= np.uint32((1 << (tb + 1)) - 1 if tb < 31 else 0xFFFFFFFF)
+        ex[:, ew - 1] |= np.uint32(1 << tb)
+        d_e = torch.from_numpy(ex.view(np.int32)).to(dev)
+        d_o = torch.zeros((count, words), dtype=torch.int32, device=dev)
+
+        def st():
+            rc = L.mpcx_modexp_batch_device(mod.handle, count, d_bases.data_ptr(), words, d_e.data_ptr(), ew, 0, E,
+                                            d_o.data_ptr(), words, stream.cuda_stream)
+            if rc != 0:
+                raise mpcx.MpcxError(rc, L.mpcx_last_error().decode())
+        st()
+        torch.cuda.synchronize()
+        reps = 3
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(reps):
+            st()
+        e1.record(stream)
+        torch.cuda.synchronize()
+        kms = e0.elapsed_time(e1) / reps
+        out = d_o.cpu().numpy().view(np.uint32)
+        idx = np.linspace(0, count - 1, 8).astype(int)
+        xs, zs = mpcx.words_to_ints(bases[idx]), mpcx.words_to_ints(out[idx])
+        es = mpcx.words_to_ints(ex[idx])
+        if any(pow(x, e, N2) != z for x, e, z in zip(xs, es, zs)):
+            raise SystemExit(f"per-operand {E}-bit exponents: GPU results differ from pow()")
+        Wp = alg_macs(N2.bit_length(), E)
+        ach = Wp * count / (kms * 1e-3)
+        return {"exp_bits": E, "value": count / (kms * 1e-3), "unit": "modexp/s", "kernel_ms": kms,
+                "roofline": {"bound": "valu", "achieved": ach / 1e12, "peak": PEAK_INT32_NOMINAL / 1e12,
+                             "unit": "TOP/s", "frac": ach / PEAK_INT32_NOMINAL, "alg_ops_per_modexp": Wp},
+                "checked": "8 sampled operands vs pow()"}
+
+    sub_lines = None
+    if rank == 0 and args.extra_lines and args.modbits == 4096:
+        sub_lines = [per_operand(2048), per_operand(4096)]
+
     from mpcium_amd.shard import max_over_ranks
     elapsed, kernel_ms = max_over_ranks([elapsed, kernel_ms], world)
 
@@ -747,6 +806,10 @@ def main():
         "cpu_baseline": None,
     }
     result["roofline"].update(pmc_traffic(count, args.modbits, mod))
+    if digest:
+        result["batch_digest"] = digest
+    if sub_lines:
+        result["config2_per_operand_exponents"] = sub_lines
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, info)
     if args.wallets > 0:

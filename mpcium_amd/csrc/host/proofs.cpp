@@ -341,10 +341,18 @@ std::vector<uint8_t> FacVerifyBatch(const std::vector<Bytes>& session, const Nat
   std::vector<uint8_t> ok(n, 0);
   if (N0.is_zero() || NCap.is_zero()) return ok;
   const Nat& Q_ = q();
+  // z1, z2 range (CGGMP Fig. 28: z1, z2 in +-sqrt(N0) 2^(l+eps)), checked
+  // before any exponentiation: an honest z = e N0p + alpha has alpha <
+  // q^3 isqrt(N0) and e N0p < 2 q isqrt(N0) (N0p < sqrt(2 N0) for a balanced
+  // N0), so z <= (q^3 + 2q) isqrt(N0); a prover hiding a small factor of N0
+  // needs z ~ e N0/small far above it. The exact expression tss-lib uses is
+  // not in this image: parity of this bound is unpinned.
+  const Nat zbound = (Q_ * Q_ * Q_ + Q_ + Q_) * isqrt(N0);
   std::vector<Nat> e(n);
   bool any_neg = false;
   parallel_for(n, [&](size_t i) {
     const auto& p = pf[i];
+    if (p.Z1 > zbound || p.Z2 > zbound) return;
     for (const Nat* v : {&p.P, &p.Q, &p.A, &p.B, &p.T})
       if (!IsInInterval(*v, NCap)) return;
     e[i] = RejectionSample(Q_, SHA512_256i_TAGGED(session[i], {&N0, &NCap, &s, &t, &p.P, &p.Q, &p.A, &p.B, &p.T,

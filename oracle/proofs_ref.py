@@ -260,6 +260,12 @@ def fac_verify(pf: FacProof, session: bytes, N0: int, NCap: int, s: int, t: int)
     """(*ProofFac).Verify(Session, ec, N0, NCap, s, t)."""
     if pf is None or N0 <= 0 or NCap <= 0:
         return False
+    # z1, z2 range, CGGMP Fig. 28 form (+-sqrt(N0) 2^(l+eps) with 2^(l+eps) ->
+    # q^3 plus the e*N0p slack of an honest response); tss-lib's exact
+    # expression is not in this image: parity of the bound is unpinned
+    zbound = (Q ** 3 + 2 * Q) * math.isqrt(N0)
+    if not (0 <= pf.Z1 <= zbound and 0 <= pf.Z2 <= zbound):
+        return False
     for v in (pf.P, pf.Q, pf.A, pf.B, pf.T):
         if not T.is_in_interval(v, NCap):
             return False

@@ -75,6 +75,30 @@ def test_shared_exponent_N_config2_sample(gpu, paillier_key):
         assert g == pow(x, N, N2)
 
 
+def test_config2_full_batch_digest(gpu, paillier_key):
+    """The whole config-2 batch (bench.py's 65,536 synthetic bases, x^N mod
+    N^2) through the host-buffer entry: SHA-256 of all outputs equals the
+    digest computed by the oracle's C restatement of Go's expNN
+    (tests/golden/batch_digest.json, tests/golden/gen_batch_digest.py)."""
+    import hashlib
+    import json
+    import os
+    from conftest import GOLDEN
+    gd = json.load(open(os.path.join(GOLDEN, "batch_digest.json")))
+    N = paillier_key["N"]
+    N2 = N * N
+    mod = gpu.Modulus(N2)
+    words = gd["words"]
+    rng = np.random.default_rng(gd["seed"])  # bench.synth_bases
+    x = rng.integers(0, 1 << 32, size=(gd["count"], words), dtype=np.uint64).astype(np.uint32)
+    top = (N2 >> (32 * (words - 1))) & 0xFFFFFFFF
+    x[:, words - 1] = x[:, words - 1] % max(top, 1)
+    e = gpu.int_to_words(N, gpu.nwords(N))
+    out = mod.exp_words(x, e, shared=True, out_words=words)
+    assert int.from_bytes(out[0].astype("<u4").tobytes(), "little") == int(gd["first_output"], 16)
+    assert hashlib.sha256(out.astype("<u4").tobytes()).hexdigest() == gd["sha256"]
+
+
 def test_per_operand_exponents_mixed_lengths(gpu, paillier_key):
     N = paillier_key["N"]
     N2 = N * N

@@ -87,6 +87,14 @@ def test_fac_golden_and_rejections(pr, nodes, vec):
     neg = dict(got[1])
     neg["V"] = -neg["V"]  # exercises the negative-exponent path (must fail)
     cases.append(neg)
+    # z1 / z2 shifted by the order of the QR subgroup mod N~: the equations
+    # hold, only the z range check rejects (tests/test_proofs_cpu.py)
+    order = n1["p"] * n1["q"]
+    for dz1, dz2 in ((order, 0), (0, order), (2 * order, order)):
+        c = dict(got[0])
+        c["Z1"] += dz1
+        c["Z2"] += dz2
+        cases.append(c)
     ok = pr.fac_verify([ss] * len(cases), *args, cases)
     assert ok == [True, True] + [False] * (len(cases) - 2)
     for c, o in zip(cases, ok):

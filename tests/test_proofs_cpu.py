@@ -42,6 +42,44 @@ def test_fac_oracle_reproduces_golden(nodes, vec):
     assert not PR.fac_verify(pf, ss, n0["N"], n1["NTildei"], n1["H1i"], n1["H2i"])
 
 
+def fac_equations_hold(pf, ss, N0, NCap, s, t):
+    """The three verification equations of (*ProofFac).Verify, without the
+    range checks."""
+    e = T.rejection_sample(PR.Q, T.sha512_256i_tagged(ss, N0, NCap, s, t, pf.P, pf.Q, pf.A, pf.B, pf.T, pf.Sigma))
+    M = NCap
+    tv = pow(t, pf.V, M) if pf.V >= 0 else pow(pow(t, -1, M), -pf.V, M)
+    R = pow(s, N0, M) * pow(t, pf.Sigma, M) % M
+    return (pow(s, pf.Z1, M) * pow(t, pf.W1, M) % M == pf.A * pow(pf.P, e, M) % M and
+            pow(s, pf.Z2, M) * pow(t, pf.W2, M) % M == pf.B * pow(pf.Q, e, M) % M and
+            pow(pf.Q, pf.Z1, M) * tv % M == pf.T * pow(R, e, M) % M)
+
+
+def shifted_fac_proofs(pf, nodes):
+    """z1 or z2 moved by the order p'q' of the quadratic residues mod N~ =
+    (2p'+1)(2q'+1), where s, t, P, Q, A, B, T all live: every equation still
+    holds, and only the z range check can reject the proof (the
+    bound that makes the no-small-factor proof sound)."""
+    import dataclasses
+    order = nodes[1]["p"] * nodes[1]["q"]
+    return [dataclasses.replace(pf, Z1=pf.Z1 + order), dataclasses.replace(pf, Z2=pf.Z2 + order),
+            dataclasses.replace(pf, Z1=pf.Z1 + 2 * order, Z2=pf.Z2 + order)]
+
+
+def test_fac_z_range_rejects_shifted_responses(nodes, vec):
+    n0, n1 = nodes[0], nodes[1]
+    ss = bytes.fromhex(vec["session"])
+    g = vec["fac"]
+    args = (n0["N"], n1["NTildei"], n1["H1i"], n1["H2i"])
+    pf = PR.fac_prove(ss, *args[:4], n0["P"], n0["Q"], T.Reader(g["seed"]))
+    assert fac_equations_hold(pf, ss, *args) and PR.fac_verify(pf, ss, *args)
+    import math
+    bound = (PR.Q ** 3 + 2 * PR.Q) * math.isqrt(n0["N"])
+    assert pf.Z1 <= bound and pf.Z2 <= bound
+    for bad in shifted_fac_proofs(pf, nodes):
+        assert fac_equations_hold(bad, ss, *args)
+        assert not PR.fac_verify(bad, ss, *args)
+
+
 def test_mod_and_dln_golden_verify(nodes, vec):
     n0 = nodes[0]
     ss = bytes.fromhex(vec["session"])
