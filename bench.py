@@ -571,9 +571,13 @@ def signing_line(args, world, rank, signers: int):
         dist.barrier()
     torch.cuda.synchronize()
     mhost.profile_report(reset=True)
+    import resource
+    ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
     st = mta.bench_signing(nodes, signers, args.wallets, seed=0x5168 + 7919 * rank)
     torch.cuda.synchronize()
+    ru1 = resource.getrusage(resource.RUSAGE_SELF)
+    host_cpu_s = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
@@ -589,6 +593,7 @@ def signing_line(args, world, rank, signers: int):
             "rounds_s": {"round1_alice_init": r1, "round2_bob_mid": r2, "round3_alice_end": r3,
                          "rounds4_9_finalize_verify": fin},
             "engine_busy_s": st["engine_busy_s"], "host_share": 1.0 - st["engine_busy_s"] / max(el, 1e-9),
+            "host_cpu_s": host_cpu_s,
             "sessions_per_gpu": int(st["sessions"]),
             "checked": "alpha+beta == k*gamma, mu+nu == k*w (mod q) on every session; ecdsa.Verify on every "
                        "signature",

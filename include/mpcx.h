@@ -269,6 +269,11 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
 /* Device memory helpers for callers without their own HIP allocator. */
 int mpcx_dev_alloc(size_t bytes, void** out_ptr);
 int mpcx_dev_free(void* ptr);
+/* Page-locked host memory (portable across the bound devices): host-buffer
+ * batches staged here are copied by DMA, without the runtime's CPU bounce
+ * copy of pageable memory. */
+int mpcx_host_alloc(size_t bytes, void** out_ptr);
+int mpcx_host_free(void* ptr);
 int mpcx_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes);
 int mpcx_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes);
 int mpcx_stream_create(void** out_stream);

@@ -75,7 +75,7 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> dict:
         if force or _newer(hlib, hdeps + [lib]):
             _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-pthread",
                   "-I", os.path.join(ROOT, "include"), "-I", os.path.join(CSRC, "host"),
-                  "-o", hlib] + host_srcs + ["-L", HERE, "-lmpcx", "-Wl,-rpath,$ORIGIN"])
+                  "-o", hlib] + host_srcs + ["-L", HERE, "-lmpcx", "-lcrypto", "-Wl,-rpath,$ORIGIN"])
         out["libmpcx_host"] = hlib
     return out
 

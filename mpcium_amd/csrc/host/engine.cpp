@@ -2,8 +2,10 @@
 #include "engine.hpp"
 
 #include "hostprof.hpp"
+#include "tsscommon.hpp"
 
 #include <algorithm>
+#include <functional>
 #include <chrono>
 #include <cstdlib>
 
@@ -86,15 +88,99 @@ Engine::Mod& Engine::modulus(const Nat& m) {
   return mods_.emplace(m.limbs(), md).first->second;
 }
 
+// fn(lo, hi) over [0, n) in chunks of 2048 on the host pool (packing and
+// unpacking a 40K-operand batch serially sat on its task's critical path)
+static void par_chunks(size_t n, const std::function<void(size_t, size_t)>& fn) {
+  constexpr size_t kChunk = 2048;
+  if (n <= kChunk) {
+    fn(0, n);
+    return;
+  }
+  parallel_for((n + kChunk - 1) / kChunk, [&](size_t c) { fn(c * kChunk, std::min(n, (c + 1) * kChunk)); });
+}
+
+namespace {
+// Pool of page-locked host buffers (mpcx_host_alloc) for the batches' inputs
+// and outputs: copies from pageable memory go through the runtime's CPU
+// bounce buffer in the calling thread, which a signing run's concurrent tasks
+// then also contend for. Buffers are reused across calls (size classes of
+// powers of two) and never returned to the system.
+class PinnedPool {
+ public:
+  static PinnedPool& get() {
+    static PinnedPool p;
+    return p;
+  }
+  uint32_t* acquire(size_t words) {
+    size_t cls = 1u << 16;  // 256 KB minimum
+    while (cls < words) cls <<= 1;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      auto& fl = free_[cls];
+      if (!fl.empty()) {
+        uint32_t* p = fl.back();
+        fl.pop_back();
+        return p;
+      }
+    }
+    void* p = nullptr;
+    if (mpcx_host_alloc(cls * 4, &p) != MPCX_OK) return nullptr;
+    std::lock_guard<std::mutex> lk(mu_);
+    size_of_[(uint32_t*)p] = cls;
+    return (uint32_t*)p;
+  }
+  void release(uint32_t* p) {
+    if (!p) return;
+    std::lock_guard<std::mutex> lk(mu_);
+    free_[size_of_.at(p)].push_back(p);
+  }
+
+ private:
+  std::mutex mu_;
+  std::map<size_t, std::vector<uint32_t*>> free_;
+  std::map<uint32_t*, size_t> size_of_;
+};
+
+// a pinned buffer of `words` words (pageable fallback if pinning fails)
+struct HostBuf {
+  uint32_t* p = nullptr;
+  std::vector<uint32_t> fallback;
+  explicit HostBuf(size_t words) {
+    p = PinnedPool::get().acquire(words);
+    if (!p) {
+      fallback.resize(words);
+      p = fallback.data();
+    } else {
+      pinned = true;
+    }
+  }
+  ~HostBuf() {
+    if (pinned) PinnedPool::get().release(p);
+  }
+  HostBuf(const HostBuf&) = delete;
+  HostBuf& operator=(const HostBuf&) = delete;
+  bool pinned = false;
+};
+}  // namespace
+
+static void pack_into(const std::vector<Nat>& v, uint32_t w, uint32_t* out) {
+  par_chunks(v.size(), [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) v[i].to_words(out + i * w, w);
+  });
+}
+
 static std::vector<uint32_t> pack(const std::vector<Nat>& v, uint32_t w) {
   std::vector<uint32_t> out((size_t)v.size() * w);
-  for (size_t i = 0; i < v.size(); ++i) v[i].to_words(out.data() + i * w, w);
+  pack_into(v, w, out.data());
   return out;
 }
 
-static std::vector<Nat> unpack(const std::vector<uint32_t>& buf, size_t count, uint32_t w) {
+static std::vector<Nat> unpack(const uint32_t* buf, size_t count, uint32_t w) {
+  MPCX_PROF("engine.unpack");
   std::vector<Nat> out(count);
-  for (size_t i = 0; i < count; ++i) out[i] = Nat::from_words(buf.data() + i * w, w);
+  par_chunks(count, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) out[i] = Nat::from_words(buf + i * w, w);
+  });
   return out;
 }
 
@@ -112,42 +198,43 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
   // use the GPU meanwhile. math/big reduces x mod m first when
   // len(x) > len(m) (nat.expNNMontgomery); here: only when x does not fit
   // the kernel class width.
-  auto packed = [&](const std::vector<Nat>& v) {
-    std::vector<uint32_t> out((size_t)v.size() * md.class_words);
-    for (size_t i = 0; i < v.size(); ++i) {
-      if (v[i].words() > md.class_words) {
-        (v[i] % m).to_words(out.data() + i * md.class_words, md.class_words);
-      } else {
-        v[i].to_words(out.data() + i * md.class_words, md.class_words);
+  auto packed = [&](const std::vector<Nat>& v, uint32_t* out) {
+    par_chunks(v.size(), [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        if (v[i].words() > md.class_words) {
+          (v[i] % m).to_words(out + i * md.class_words, md.class_words);
+        } else {
+          v[i].to_words(out + i * md.class_words, md.class_words);
+        }
       }
-    }
-    return out;
+    });
   };
   const bool shared = exps.size() == 1;
   uint32_t ew = 1;
   for (const auto& e : exps) ew = std::max<uint32_t>(ew, (uint32_t)e.words());
-  std::vector<uint32_t> B, E, M;
+  const size_t n = bases.size();
+  HostBuf B(n * md.class_words), E(exps.size() * ew), M(muls ? n * md.class_words : 1), out(n * md.words);
   {
     MPCX_PROF("engine.exp.pack");
-    B = packed(bases);
-    E = pack(exps, ew);
-    if (muls) M = packed(*muls);
+    packed(bases, B.p);
+    pack_into(exps, ew, E.p);
+    if (muls) packed(*muls, M.p);
   }
-  std::vector<uint32_t> out((size_t)bases.size() * md.words);
-  count_work(m, exps, bases.size());
+  count_work(m, exps, n);
   int rc;
-  MPCX_PROF("engine.exp.gpu+unpack");
-  enter_call();
-  if (muls) {
-    rc = mpcx_modexp_mul_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
-                               M.data(), md.class_words, out.data(), md.words);
-  } else {
-    rc = mpcx_modexp_batch(md.h, (uint32_t)bases.size(), B.data(), md.class_words, E.data(), ew, shared ? 1 : 0,
-                           out.data(), md.words);
+  {
+    MPCX_PROF("engine.exp.gpu");
+    enter_call();
+    if (muls) {
+      rc = mpcx_modexp_mul_batch(md.h, (uint32_t)n, B.p, md.class_words, E.p, ew, shared ? 1 : 0, M.p,
+                                 md.class_words, out.p, md.words);
+    } else {
+      rc = mpcx_modexp_batch(md.h, (uint32_t)n, B.p, md.class_words, E.p, ew, shared ? 1 : 0, out.p, md.words);
+    }
+    leave_call();
   }
-  leave_call();
   if (rc) throw_last(rc, "mpcx_modexp_batch");
-  return unpack(out, bases.size(), md.words);
+  return unpack(out.p, n, md.words);
 }
 
 bool Engine::fixed_base_ok(const Nat& m) const {
@@ -189,16 +276,17 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
     need = std::max<uint32_t>(need, e.bit_len());
   }
   const Nat b = base.words() > md.class_words || base >= m ? base % m : base;
-  auto E = pack(exps, ew);
-  std::vector<uint32_t> Mw;
+  const size_t n = exps.size();
+  HostBuf E(n * ew), Mw(muls ? n * md.class_words : 1), out(n * md.words);
+  pack_into(exps, ew, E.p);
   if (muls) {
-    Mw.assign((size_t)muls->size() * md.class_words, 0);
-    for (size_t i = 0; i < muls->size(); ++i) {
-      const Nat& x = (*muls)[i];
-      (x.words() > md.class_words ? x % m : x).to_words(Mw.data() + i * md.class_words, md.class_words);
-    }
+    par_chunks(n, [&](size_t lo, size_t hi) {
+      for (size_t i = lo; i < hi; ++i) {
+        const Nat& x = (*muls)[i];
+        (x.words() > md.class_words ? x % m : x).to_words(Mw.p + i * md.class_words, md.class_words);
+      }
+    });
   }
-  std::vector<uint32_t> out((size_t)exps.size() * md.words);
   Fixed f;
   {
     // look up (or build) under the lock; the shared handle keeps the table
@@ -206,15 +294,18 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
     std::lock_guard<std::mutex> lk(mu_);
     f = fixed(m, b, need);
   }
-  const uint32_t* ep = E.data();
-  count_work(m, exps, exps.size());
-  MPCX_PROF("engine.fixed.gpu+unpack");
-  enter_call();
-  int rc = mpcx_fixedbase_exp_batch(1, &f->h, (uint32_t)exps.size(), &ep, &ew, muls ? Mw.data() : nullptr,
-                                    muls ? md.class_words : 0, out.data(), md.words);
-  leave_call();
+  const uint32_t* ep = E.p;
+  count_work(m, exps, n);
+  int rc;
+  {
+    MPCX_PROF("engine.fixed.gpu");
+    enter_call();
+    rc = mpcx_fixedbase_exp_batch(1, &f->h, (uint32_t)n, &ep, &ew, muls ? Mw.p : nullptr, muls ? md.class_words : 0,
+                                  out.p, md.words);
+    leave_call();
+  }
   if (rc) throw_last(rc, "mpcx_fixedbase_exp_batch");
-  return unpack(out, exps.size(), md.words);
+  return unpack(out.p, n, md.words);
 }
 
 std::vector<Nat> Engine::mulmod(const Nat& m, const std::vector<Nat>& a, const std::vector<Nat>& b) {

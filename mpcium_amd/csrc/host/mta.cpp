@@ -23,7 +23,10 @@ const Nat& q7() {
 }
 
 // Gamma^k mod N^2 = (1 + N)^k = 1 + (k mod N) N  (binomial theorem; < N^2)
-Nat gamma_pow(const Nat& k, const Nat& N) { return Nat(1) + (k % N) * N; }
+Nat gamma_pow(const Nat& k, const Nat& N) {
+  MPCX_PROF("paillier.gamma_pow");
+  return Nat(1) + (k % N) * N;
+}
 
 Nat affine_x(const secp::Affine& p) { return secp::FeToNat(p.x); }
 Nat affine_y(const secp::Affine& p) { return secp::FeToNat(p.y); }

@@ -1,6 +1,8 @@
 // secp256k1.cpp -- see secp256k1.hpp.
 #include "secp256k1.hpp"
 
+#include "hostprof.hpp"
+
 #include <algorithm>
 #include <vector>
 
@@ -477,11 +479,18 @@ Affine Add(const Affine& a, const Affine& b) {
   return to_affine(jac_madd(to_jac(a), b));
 }
 
-Affine ScalarBaseMult(const Nat& k) { return to_affine(add_base_mult(Jac{}, scalar_limbs(k))); }
+Affine ScalarBaseMult(const Nat& k) {
+  MPCX_PROF("ec.base_mult");
+  return to_affine(add_base_mult(Jac{}, scalar_limbs(k)));
+}
 
-Affine ScalarMult(const Affine& p, const Nat& k) { return to_affine(var_mult(p, scalar_limbs(k))); }
+Affine ScalarMult(const Affine& p, const Nat& k) {
+  MPCX_PROF("ec.var_mult");
+  return to_affine(var_mult(p, scalar_limbs(k)));
+}
 
 Affine LinComb(const Nat& u1, const Affine& X, const Nat& u2) {
+  MPCX_PROF("ec.lincomb");
   return to_affine(add_base_mult(var_mult(X, scalar_limbs(u2)), scalar_limbs(u1)));
 }
 

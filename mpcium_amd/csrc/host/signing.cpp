@@ -152,12 +152,14 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
   std::mutex tm;
   double r1 = 0, r2 = 0, r3 = 0, r4 = 0;  // per-round seconds summed over chunks
 
-  // Wallets [lo, hi) through rounds 1-3 and the finalize. Within a round the
-  // ordered pairs (and a pair's MtA / MtAwc halves) are independent tasks;
-  // chunks run as concurrent pipelines, so one chunk's host work (draws,
-  // hashing, gcds, finalize + ecdsa.Verify) overlaps another chunk's GPU
-  // batches. Every session's reader is its own CounterDRBG(mix(seed, wallet,
+  // Wallets [lo, hi) through rounds 1-3 and the finalize. The ordered pairs
+  // (and a pair's MtA / MtAwc halves) are independent tasks; chunks can run as
+  // concurrent pipelines, so one chunk's host work (draws, hashing, gcds,
+  // finalize + ecdsa.Verify) overlaps another chunk's GPU batches. Every session's reader is its own CounterDRBG(mix(seed, wallet,
   // pair, role)), so the split changes no value.
+  // MPCX_SIGN_CHAINS=0: rounds with a barrier between them (A/B)
+  const char* ce = std::getenv("MPCX_SIGN_CHAINS");
+  const bool chains = !(ce && ce[0] == '0');
   auto run_chunk = [&](size_t lo, size_t hi) {
     const size_t n = hi - lo;
     const std::vector<mta::Bytes> cs(sess.begin() + (long)lo, sess.begin() + (long)hi);
@@ -192,63 +194,83 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
       }
     }
     const double c0 = now(), b0 = Engine::get().busy_seconds_now();
-    {  // round 1: AliceInit(pk_i, k_i, N~_j, h1_j, h2_j)
-      std::vector<std::function<void()>> tasks;
-      for (size_t pi = 0; pi < pairs.size(); ++pi)
-        tasks.push_back([&, pi] {
-          const Pair& p = pairs[pi];
-          std::vector<uint8_t> err;
-          mta::AliceInitBatch(nodes[p.i].sk.pub, sl(k[p.i]), public_dln(nodes[p.j].dln), L[pi].ra, &L[pi].cA,
-                              &L[pi].pfA, &err);
-          count_err(err);
-        });
-      run_tasks(tasks);
-    }
-    const double b1 = Engine::get().busy_seconds_now(), cj = now();
-    join_ec();
-    const double c1 = now();
-    {  // round 2: Bob j -- BobMid(gamma_j), BobMidWC(w_j, W_j)
-      std::vector<std::function<void()>> tasks;
-      for (size_t pi = 0; pi < pairs.size(); ++pi) {
-        tasks.push_back([&, pi] {
-          const Pair& p = pairs[pi];
-          std::vector<uint8_t> err;
-          mta::BobMidBatch(cs, nodes[p.i].sk.pub, L[pi].pfA, sl(g[p.j]), L[pi].cA, public_dln(nodes[p.i].dln),
-                           nodes[p.j].dln, nullptr, L[pi].rb, &L[pi].bob, &err);
-          count_err(err);
-        });
-        tasks.push_back([&, pi] {
-          const Pair& p = pairs[pi];
-          std::vector<uint8_t> err;
-          const std::vector<secp::Affine> Wj = slp(Wp[p.j]);
-          mta::BobMidBatch(cs, nodes[p.i].sk.pub, L[pi].pfA, sl(w[p.j]), L[pi].cA, public_dln(nodes[p.i].dln),
-                           nodes[p.j].dln, &Wj, L[pi].rbwc, &L[pi].bobwc, &err);
-          count_err(err);
-        });
+    // One pair's protocol steps (Alice i, Bob j)
+    auto alice_init = [&](size_t pi) {
+      const Pair& p = pairs[pi];
+      std::vector<uint8_t> err;
+      mta::AliceInitBatch(nodes[p.i].sk.pub, sl(k[p.i]), public_dln(nodes[p.j].dln), L[pi].ra, &L[pi].cA, &L[pi].pfA,
+                          &err);
+      count_err(err);
+    };
+    auto bob_mid = [&](size_t pi, bool wc) {  // BobMid(gamma_j) / BobMidWC(w_j, W_j)
+      const Pair& p = pairs[pi];
+      std::vector<uint8_t> err;
+      std::vector<secp::Affine> Wj;
+      if (wc) {
+        join_ec();
+        Wj = slp(Wp[p.j]);
       }
-      run_tasks(tasks);
-    }
-    const double c2 = now(), b2 = Engine::get().busy_seconds_now();
-    {  // round 3: Alice i -- AliceEnd, AliceEndWC
+      mta::BobMidBatch(cs, nodes[p.i].sk.pub, L[pi].pfA, sl(wc ? w[p.j] : g[p.j]), L[pi].cA,
+                       public_dln(nodes[p.i].dln), nodes[p.j].dln, wc ? &Wj : nullptr, wc ? L[pi].rbwc : L[pi].rb,
+                       wc ? &L[pi].bobwc : &L[pi].bob, &err);
+      count_err(err);
+    };
+    auto alice_end = [&](size_t pi, bool wc) {  // AliceEnd / AliceEndWC
+      const Pair& p = pairs[pi];
+      const auto& bm = wc ? L[pi].bobwc : L[pi].bob;
+      std::vector<mta::ProofBob> pf(n);
+      std::vector<Nat> cB(n);
+      for (size_t x = 0; x < n; ++x) {
+        pf[x] = bm[x].pf;
+        cB[x] = bm[x].cB;
+      }
+      std::vector<uint8_t> err;
+      const std::vector<secp::Affine> Wj = wc ? slp(Wp[p.j]) : std::vector<secp::Affine>{};
+      mta::AliceEndBatch(cs, nodes[p.i].sk, pf, nodes[p.i].dln, L[pi].cA, cB, wc ? &Wj : nullptr,
+                         wc ? &L[pi].mu : &L[pi].alpha, &err);
+      count_err(err);
+    };
+    const size_t np = pairs.size();
+    std::vector<double> st1(np), st2(np), st3(np);
+    if (chains) {
+      // Each ordered pair's chain -- AliceInit, then BobMid || BobMidWC, then
+      // AliceEnd || AliceEndWC -- depends only on its own outputs: the chains
+      // run concurrently with no barrier between rounds, so one chain's host
+      // phases (draws, hashing, gcd batches, packing) overlap another chain's
+      // GPU batches instead of every task reaching its host phase in lockstep.
       std::vector<std::function<void()>> tasks;
-      for (size_t pi = 0; pi < pairs.size(); ++pi)
-        for (int wc = 0; wc < 2; ++wc)
-          tasks.push_back([&, pi, wc] {
-            const Pair& p = pairs[pi];
-            const auto& bm = wc ? L[pi].bobwc : L[pi].bob;
-            std::vector<mta::ProofBob> pf(n);
-            std::vector<Nat> cB(n);
-            for (size_t x = 0; x < n; ++x) {
-              pf[x] = bm[x].pf;
-              cB[x] = bm[x].cB;
-            }
-            std::vector<uint8_t> err;
-            const std::vector<secp::Affine> Wj = slp(Wp[p.j]);
-            mta::AliceEndBatch(cs, nodes[p.i].sk, pf, nodes[p.i].dln, L[pi].cA, cB, wc ? &Wj : nullptr,
-                               wc ? &L[pi].mu : &L[pi].alpha, &err);
-            count_err(err);
-          });
+      for (size_t pi = 0; pi < np; ++pi)
+        tasks.push_back([&, pi] {
+          const double a0 = now();
+          alice_init(pi);
+          const double a1 = now();
+          run_tasks({[&] { bob_mid(pi, false); }, [&] { bob_mid(pi, true); }});
+          const double a2 = now();
+          run_tasks({[&] { alice_end(pi, false); }, [&] { alice_end(pi, true); }});
+          st1[pi] = a1 - a0;
+          st2[pi] = a2 - a1;
+          st3[pi] = now() - a2;
+        });
       run_tasks(tasks);
+    } else {  // rounds with a barrier between them (A/B: MPCX_SIGN_CHAINS=0)
+      std::vector<std::function<void()>> t1, t2, t3;
+      for (size_t pi = 0; pi < np; ++pi) {
+        t1.push_back([&, pi] { alice_init(pi); });
+        t2.push_back([&, pi] { bob_mid(pi, false); });
+        t2.push_back([&, pi] { bob_mid(pi, true); });
+        t3.push_back([&, pi] { alice_end(pi, false); });
+        t3.push_back([&, pi] { alice_end(pi, true); });
+      }
+      const double a0 = now();
+      run_tasks(t1);
+      const double a1 = now();
+      run_tasks(t2);
+      const double a2 = now();
+      run_tasks(t3);
+      const double a3 = now();
+      std::fill(st1.begin(), st1.end(), a1 - a0);
+      std::fill(st2.begin(), st2.end(), a2 - a1);
+      std::fill(st3.begin(), st3.end(), a3 - a2);
     }
     const double c3 = now(), b3 = Engine::get().busy_seconds_now();
     for (size_t pi = 0; pi < pairs.size(); ++pi) {
@@ -314,18 +336,20 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
       verified[wi] = !P.inf && secp::FeToNat(P.x) % q == r;
     });
     const double c4 = now();
-    if (prof::enabled()) {  // seconds of each round with no libmpcx call in flight (one chunk: exact)
-      static const int s1 = prof::slot_of("sign.gpu_idle.round1"), s2 = prof::slot_of("sign.gpu_idle.round2"),
-                       s3 = prof::slot_of("sign.gpu_idle.round3"), sj = prof::slot_of("sign.ec_join_wait");
-      prof::add(s1, (uint64_t)(std::max(0.0, (cj - c0) - (b1 - b0)) * 1e9));
-      prof::add(sj, (uint64_t)((c1 - cj) * 1e9));
-      prof::add(s2, (uint64_t)(std::max(0.0, (c2 - c1) - (b2 - b1)) * 1e9));
-      prof::add(s3, (uint64_t)(std::max(0.0, (c3 - c2) - (b3 - b2)) * 1e9));
+    if (prof::enabled()) {  // seconds with no libmpcx call in flight (one chunk: exact)
+      static const int s13 = prof::slot_of("sign.gpu_idle.rounds1_3"), s4 = prof::slot_of("sign.gpu_idle.finalize");
+      prof::add(s13, (uint64_t)(std::max(0.0, (c3 - c0) - (b3 - b0)) * 1e9));
+      prof::add(s4, (uint64_t)((c4 - c3) * 1e9));
     }
+    auto mean = [&](const std::vector<double>& v) {
+      double t = 0;
+      for (double x : v) t += x;
+      return v.empty() ? 0.0 : t / (double)v.size();
+    };
     std::lock_guard<std::mutex> lk(tm);
-    r1 += c1 - c0;
-    r2 += c2 - c1;
-    r3 += c3 - c2;
+    r1 += mean(st1);  // per pair chain, averaged over the pairs
+    r2 += mean(st2);
+    r3 += mean(st3);
     r4 += c4 - c3;
   };
 

@@ -46,7 +46,7 @@ struct NodeKeys {
 };
 
 struct MtaStats {
-  double round1_s = 0, round2_s = 0, round3_s = 0, total_s = 0;  // rounds: summed over chunks
+  double round1_s = 0, round2_s = 0, round3_s = 0, total_s = 0;  // rounds: per pair chain (mean over pairs), summed over chunks
   double engine_busy_s = 0;  // wall time with >= 1 libmpcx call in flight (GPU + transfers)
   double alg_macs = 0;       // Go-equivalent algorithmic work sent to the GPU (Engine::alg_macs)
   uint64_t wallets = 0, pairs = 0, sessions = 0;  // sessions = wallets x ordered pairs

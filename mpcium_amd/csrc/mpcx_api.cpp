@@ -111,6 +111,10 @@ struct Lane {
   std::mutex mu;
   hipStream_t st = nullptr;  // created on first use (non-blocking); or a caller's stream (own_stream false)
   bool own_stream = true;
+  // completion event for host waits, created with hipEventBlockingSync: a
+  // waiting host thread sleeps instead of spinning a core (a signing run has
+  // 4-12 tasks waiting on their launches while others need the CPU)
+  hipEvent_t ev = nullptr;
   uint32_t* ws = nullptr;    // exponentiation table workspace
   size_t ws_bytes = 0;
   Staging stage[4];  // bases, exps, out, misc
@@ -286,13 +290,28 @@ Lane& acquire_lane(Device& d, std::unique_lock<std::mutex>& lk) {
 }
 
 int lane_stream(Lane& l) {
-  if (l.st || !l.own_stream) return MPCX_OK;
-  hipError_t e = hipStreamCreateWithFlags(&l.st, hipStreamNonBlocking);
-  if (e != hipSuccess) {
-    l.st = nullptr;
-    return hip_fail(e, "hipStreamCreate(lane)");
+  if (!l.st && l.own_stream) {
+    hipError_t e = hipStreamCreateWithFlags(&l.st, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      l.st = nullptr;
+      return hip_fail(e, "hipStreamCreate(lane)");
+    }
+  }
+  if (!l.ev) {
+    hipError_t e = hipEventCreateWithFlags(&l.ev, hipEventBlockingSync | hipEventDisableTiming);
+    if (e != hipSuccess) {
+      l.ev = nullptr;
+      return hip_fail(e, "hipEventCreate(lane)");
+    }
   }
   return MPCX_OK;
+}
+
+// wait (sleeping) until the lane's stream has drained
+int lane_wait(Lane& l) {
+  hipError_t e = hipEventRecord(l.ev, l.st);
+  if (e == hipSuccess) e = hipEventSynchronize(l.ev);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "lane wait");
 }
 
 int h2d(void* d, const void* h, size_t bytes, hipStream_t st) {
@@ -301,10 +320,10 @@ int h2d(void* d, const void* h, size_t bytes, hipStream_t st) {
   return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy inputs");
 }
 
-int d2h_sync(void* h, const void* d, size_t bytes, hipStream_t st) {
-  hipError_t e = bytes ? hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, st) : hipSuccess;
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy results");
+int d2h_sync(void* h, const void* d, size_t bytes, Lane& l) {
+  hipError_t e = bytes ? hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, l.st) : hipSuccess;
+  if (e != hipSuccess) return hip_fail(e, "copy results");
+  return lane_wait(l);
 }
 
 int ensure_buffer(Staging& s, size_t bytes) {
@@ -341,6 +360,8 @@ void drop_lane(Lane& l) {
     if (l.own_stream) (void)hipStreamDestroy(l.st);
   }
   l.st = nullptr;
+  if (l.ev) (void)hipEventDestroy(l.ev);
+  l.ev = nullptr;
   if (l.ws) (void)hipFree(l.ws);
   l.ws = nullptr;
   l.ws_bytes = 0;
@@ -825,7 +846,7 @@ static int modexp_host_range(int di, mpcx_mod_t mod, uint32_t count, const uint3
                       exp_words, exp_shared, exp_bits, muls ? (const uint32_t*)sg[3].ptr : nullptr, mul_words,
                       (uint32_t*)sg[2].ptr, out_words);
   if (rc) return rc;
-  return d2h_sync(out, sg[2].ptr, ob, l.st);
+  return d2h_sync(out, sg[2].ptr, ob, l);
 }
 
 static int modexp_host(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
@@ -1020,7 +1041,7 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
       e = mpcx_launch_prime2(&a, a.f_blocks, l.st);
     }
     if (e != hipSuccess) return hip_fail(e, "launch k_prime2");
-    return d2h_sync(ok + first, l.stage[3].ptr, n, l.st);
+    return d2h_sync(ok + first, l.stage[3].ptr, n, l);
   });
 }
 
@@ -1062,7 +1083,7 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
       e = mpcx_launch_mr(&a, (cnt + 63) / 64, l.st);
     }
     if (e != hipSuccess) return hip_fail(e, "launch k_mr");
-    return d2h_sync(ok + first, l.stage[3].ptr, cnt, l.st);
+    return d2h_sync(ok + first, l.stage[3].ptr, cnt, l);
   });
 }
 
@@ -1106,7 +1127,7 @@ int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const 
       e = mpcx_launch_lucas(&a, (cnt + 63) / 64, l.st);
     }
     if (e != hipSuccess) return hip_fail(e, "launch k_lucas");
-    return d2h_sync(ok + first, l.stage[3].ptr, cnt, l.st);
+    return d2h_sync(ok + first, l.stage[3].ptr, cnt, l);
   });
 }
 
@@ -1122,6 +1143,21 @@ int mpcx_dev_alloc(size_t bytes, void** out_ptr) {
 int mpcx_dev_free(void* ptr) {
   hipError_t e = hipFree(ptr);
   return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipFree");
+}
+
+int mpcx_host_alloc(size_t bytes, void** out_ptr) {
+  if (!out_ptr) return fail(MPCX_EINVAL, "null out_ptr");
+  Device* dev = nullptr;
+  if (int rc = selected(&dev)) return rc;
+  hipError_t e = hipHostMalloc(out_ptr, std::max<size_t>(bytes, 1), hipHostMallocPortable);
+  if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  return MPCX_OK;
+}
+
+int mpcx_host_free(void* ptr) {
+  if (!ptr) return MPCX_OK;
+  hipError_t e = hipHostFree(ptr);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipHostFree");
 }
 
 int mpcx_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes) {
@@ -1240,7 +1276,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
                       d_bj, cw);
   // T(j, v) = R * b_j^v: operand i = j*255 + (v-1) takes base b_j -> replicate b_j rows
   std::vector<uint32_t> hbj((size_t)nwin * cw), hb2;
-  if (!rc) rc = d2h_sync(hbj.data(), d_bj, hbj.size() * 4, bl.st);
+  if (!rc) rc = d2h_sync(hbj.data(), d_bj, hbj.size() * 4, bl);
   if (!rc) {
     hb2.resize(n2 * cw);
     for (size_t i = 0; i < n2; ++i) std::memcpy(&hb2[i * cw], &hbj[(i / nv) * cw], cw * 4);
@@ -1253,7 +1289,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     rc = modexp_enqueue(di, bl, mod, (uint32_t)n2, d_b, cw, d_e2, 1, 0, MPCX_FB_WINDOW_BITS, d_m, mod->words, d_t,
                         cw);
   std::vector<uint32_t> ht(n2 * cw);
-  if (!rc) rc = d2h_sync(ht.data(), d_t, ht.size() * 4, bl.st);
+  if (!rc) rc = d2h_sync(ht.data(), d_t, ht.size() * 4, bl);
   cleanup();
   if (rc) return rc;
   auto* fb = new mpcx_fixedbase_s();
@@ -1370,7 +1406,7 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     hipError_t e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
                                              : mpcx_launch_fixedbase_g1(&a, waves, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
-    return d2h_sync(out + (size_t)first * out_words, sg[2].ptr, ob, l.st);
+    return d2h_sync(out + (size_t)first * out_words, sg[2].ptr, ob, l);
   });
 }
 
@@ -1510,7 +1546,7 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
     }
   }
   uint32_t cnt2[2] = {0, 0};
-  if ((rc = d2h_sync(cnt2, dm, 8, l.st))) return rc;
+  if ((rc = d2h_sync(cnt2, dm, 8, l))) return rc;
   const uint32_t ns = cnt2[0], np = cnt2[1];
   if (ns > count || np > ns) return fail(MPCX_EHIP, "safe-prime step counters %u/%u out of range (%u)", ns, np, count);
   if (np > max_pass) return fail(MPCX_ENOMEM, "%u Fermat passes > max_pass %u", np, max_pass);
@@ -1533,8 +1569,7 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
     if (e == hipSuccess) e = hipMemcpyAsync(aok.data(), sg[3].ptr, ns, hipMemcpyDeviceToHost, l.st);
     if (e != hipSuccess) return hip_fail(e, "copy survivors");
   }
-  e = hipStreamSynchronize(l.st);
-  if (e != hipSuccess) return hip_fail(e, "safe-prime step");
+  if ((rc = lane_wait(l))) return rc;
   // stream order
   std::vector<uint32_t> ord(np);
   for (uint32_t j = 0; j < np; ++j) ord[j] = j;

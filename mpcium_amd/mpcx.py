@@ -67,6 +67,8 @@ SIGNATURES = [
                                                    _vp, _vp]),
     ("mpcx_dev_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(_vp)]),
     ("mpcx_dev_free", ctypes.c_int, [_vp]),
+    ("mpcx_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
+    ("mpcx_host_free", ctypes.c_int, [_vp]),
     ("mpcx_memcpy_h2d", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
     ("mpcx_memcpy_d2h", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
     ("mpcx_stream_create", ctypes.c_int, [ctypes.POINTER(_vp)]),
