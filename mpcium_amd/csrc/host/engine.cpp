@@ -146,7 +146,11 @@ struct HostBuf {
   uint32_t* p = nullptr;
   std::vector<uint32_t> fallback;
   explicit HostBuf(size_t words) {
-    p = PinnedPool::get().acquire(words);
+    static const bool off = [] {  // MPCX_PINNED=0: pageable staging (A/B runs)
+      const char* e = std::getenv("MPCX_PINNED");
+      return e && e[0] == '0';
+    }();
+    p = off ? nullptr : PinnedPool::get().acquire(words);
     if (!p) {
       fallback.resize(words);
       p = fallback.data();

@@ -2,7 +2,9 @@
 #include "keygenload.hpp"
 
 #include <atomic>
+#include <mutex>
 #include <chrono>
+#include <cstdlib>
 #include <functional>
 #include <memory>
 #include <stdexcept>
@@ -95,68 +97,89 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
       if (j != i) r_fac[i][j] = &stream(i, 16 + j);
   }
   const size_t width = 8;
-  Engine::get().reset_busy();
-  const double t0 = now();
-  {  // every party's proofs, for all sessions
-    std::vector<std::function<void()>> tasks;
-    for (size_t i = 0; i < n; ++i) {
-      tasks.push_back([&, i] {
-        const PartyKeys& P = parties[i];
-        dln1[i] = proofs::DLNProveBatch(P.h1, P.h2, P.alpha, P.p, P.q, P.NTilde, *r_dln1[i]);
-      });
-      tasks.push_back([&, i] {
-        const PartyKeys& P = parties[i];
-        dln2[i] = proofs::DLNProveBatch(P.h2, P.h1, P.beta, P.p, P.q, P.NTilde, *r_dln2[i]);
-      });
-      tasks.push_back([&, i] {
-        const PartyKeys& P = parties[i];
-        mod[i] = proofs::ModProveBatch(sess, P.sk.pub.N, P.sk.P, P.sk.Q, *r_mod[i]);
-      });
-      for (size_t j = 0; j < n; ++j) {
-        if (j == i) continue;
-        tasks.push_back([&, i, j] {
-          const PartyKeys& P = parties[i];
-          const PartyKeys& V = parties[j];
-          fac[i][j] = proofs::FacProveBatch(sess, P.sk.pub.N, V.NTilde, V.h1, V.h2, P.sk.P, P.sk.Q, *r_fac[i][j]);
-        });
-      }
-    }
-    st.proofs = (uint64_t)sessions * n * (3 + (n - 1));
-    run_bounded(tasks, width);
-  }
-  const double t1 = now();
+  const char* ce = std::getenv("MPCX_KEYGEN_CHAINS");
+  const bool chains = !(ce && ce[0] == '0');
   std::atomic<uint64_t> fails{0};
   auto count = [&](const std::vector<uint8_t>& ok) {
     uint64_t f = 0;
     for (auto v : ok) f += v == 0;
     fails += f;
   };
-  {  // every party verifies every peer's proofs
+  st.proofs = (uint64_t)sessions * n * (3 + (n - 1));
+  st.verifications = (uint64_t)sessions * n * (n - 1) * 4;
+  // One chain per proof batch: prove, then every peer's verification of it.
+  // A verification depends only on its proof, so the chains run with no
+  // barrier between proving and verifying: one chain's host steps overlap
+  // another's GPU batches.
+  std::mutex tm;
+  double last_prove = 0;
+  auto proved = [&] {
+    std::lock_guard<std::mutex> lk(tm);
+    last_prove = std::max(last_prove, now());
+  };
+  Engine::get().reset_busy();
+  const double t0 = now();
+  {
     std::vector<std::function<void()>> tasks;
-    for (size_t j = 0; j < n; ++j)
-      for (size_t i = 0; i < n; ++i) {
-        if (i == j) continue;
-        tasks.push_back([&, i] {
-          const PartyKeys& P = parties[i];
-          count(proofs::DLNVerifyBatch(P.h1, P.h2, P.NTilde, dln1[i]));
-        });
-        tasks.push_back([&, i] {
-          const PartyKeys& P = parties[i];
-          count(proofs::DLNVerifyBatch(P.h2, P.h1, P.NTilde, dln2[i]));
-        });
-        tasks.push_back([&, i] { count(proofs::ModVerifyBatch(sess, parties[i].sk.pub.N, mod[i])); });
+    for (size_t i = 0; i < n; ++i) {
+      const PartyKeys& P = parties[i];
+      tasks.push_back([&, i] {
+        dln1[i] = proofs::DLNProveBatch(P.h1, P.h2, P.alpha, P.p, P.q, P.NTilde, *r_dln1[i]);
+        proved();
+        for (size_t j = 0; j < n; ++j)
+          if (j != i) count(proofs::DLNVerifyBatch(P.h1, P.h2, P.NTilde, dln1[i]));
+      });
+      tasks.push_back([&, i] {
+        dln2[i] = proofs::DLNProveBatch(P.h2, P.h1, P.beta, P.p, P.q, P.NTilde, *r_dln2[i]);
+        proved();
+        for (size_t j = 0; j < n; ++j)
+          if (j != i) count(proofs::DLNVerifyBatch(P.h2, P.h1, P.NTilde, dln2[i]));
+      });
+      tasks.push_back([&, i] {
+        mod[i] = proofs::ModProveBatch(sess, P.sk.pub.N, P.sk.P, P.sk.Q, *r_mod[i]);
+        proved();
+        for (size_t j = 0; j < n; ++j)
+          if (j != i) count(proofs::ModVerifyBatch(sess, P.sk.pub.N, mod[i]));
+      });
+      for (size_t j = 0; j < n; ++j) {
+        if (j == i) continue;
         tasks.push_back([&, i, j] {
-          const PartyKeys& P = parties[i];
           const PartyKeys& V = parties[j];
+          fac[i][j] = proofs::FacProveBatch(sess, P.sk.pub.N, V.NTilde, V.h1, V.h2, P.sk.P, P.sk.Q, *r_fac[i][j]);
+          proved();
           count(proofs::FacVerifyBatch(sess, P.sk.pub.N, V.NTilde, V.h1, V.h2, fac[i][j]));
         });
       }
-    st.verifications = (uint64_t)sessions * n * (n - 1) * 4;
-    run_bounded(tasks, width);
+    }
+    if (chains) {
+      run_bounded(tasks, width);
+    } else {  // every proof first, then every verification (MPCX_KEYGEN_CHAINS=0)
+      std::vector<std::function<void()>> prove, verify;
+      for (size_t i = 0; i < n; ++i) {
+        const PartyKeys& P = parties[i];
+        prove.push_back([&, i] { dln1[i] = proofs::DLNProveBatch(P.h1, P.h2, P.alpha, P.p, P.q, P.NTilde, *r_dln1[i]); });
+        prove.push_back([&, i] { dln2[i] = proofs::DLNProveBatch(P.h2, P.h1, P.beta, P.p, P.q, P.NTilde, *r_dln2[i]); });
+        prove.push_back([&, i] { mod[i] = proofs::ModProveBatch(sess, P.sk.pub.N, P.sk.P, P.sk.Q, *r_mod[i]); });
+        for (size_t j = 0; j < n; ++j) {
+          if (j == i) continue;
+          const PartyKeys& V = parties[j];
+          prove.push_back([&, i, j] {
+            fac[i][j] = proofs::FacProveBatch(sess, P.sk.pub.N, V.NTilde, V.h1, V.h2, P.sk.P, P.sk.Q, *r_fac[i][j]);
+          });
+          verify.push_back([&, i] { count(proofs::DLNVerifyBatch(P.h1, P.h2, P.NTilde, dln1[i])); });
+          verify.push_back([&, i] { count(proofs::DLNVerifyBatch(P.h2, P.h1, P.NTilde, dln2[i])); });
+          verify.push_back([&, i] { count(proofs::ModVerifyBatch(sess, P.sk.pub.N, mod[i])); });
+          verify.push_back([&, i, j] { count(proofs::FacVerifyBatch(sess, P.sk.pub.N, V.NTilde, V.h1, V.h2, fac[i][j])); });
+        }
+      }
+      run_bounded(prove, width);
+      proved();
+      run_bounded(verify, width);
+    }
   }
   const double t2 = now();
-  st.prove_s = t1 - t0;
-  st.verify_s = t2 - t1;
+  st.prove_s = last_prove - t0;  // until the last proof batch was done
+  st.verify_s = t2 - last_prove;  // verification tail after it
   st.total_s = t2 - t0;
   st.failures = fails.load();
   st.engine_busy_s = Engine::get().busy_seconds();

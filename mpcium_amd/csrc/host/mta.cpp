@@ -316,10 +316,18 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
     ok[i] = 0;
     const auto& p = pf[i];
     e[i] = bob_challenge(session[i], pk, gamma, X ? &(*X)[i] : nullptr, c1[i], c2[i], p);
-    if (X) {  // 4. s1*G == e*X + u
-      const secp::Affine gS1 = secp::ScalarBaseMult(p.S1 % Q());
-      const secp::Affine xEU = secp::Add(secp::ScalarMult((*X)[i], e[i]), p.U);
-      if (xEU.inf || !secp::Equal(gS1, xEU)) return;
+    if (X) {
+      // 4. s1*G == e*X + u, rejected when e*X + u is the point at infinity
+      // (Go: xEU nil). Evaluated as one combination T = s1*G + (q - e)*X
+      // compared with u: T == u  <=>  s1*G == e*X + u as group elements, and
+      // when that holds, e*X + u = infinity  <=>  s1*G = infinity  <=>
+      // s1 == 0 (mod q). Same decision as two scalar multiplications, an
+      // addition and three affine conversions, for one chain and one.
+      const Nat s1q = p.S1 % Q();
+      if (s1q.is_zero()) return;
+      const Nat eq = e[i] % Q();
+      const secp::Affine T = secp::LinComb(s1q, (*X)[i], eq.is_zero() ? eq : Q() - eq);
+      if (!secp::Equal(T, p.U)) return;
     }
     gt1[i] = gamma_pow(p.T1, pk.N);
     ok[i] = 1;

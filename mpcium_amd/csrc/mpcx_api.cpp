@@ -307,10 +307,20 @@ int lane_stream(Lane& l) {
   return MPCX_OK;
 }
 
-// wait (sleeping) until the lane's stream has drained
+// wait (sleeping) until the lane's stream has drained; MPCX_SPIN_WAIT=1:
+// hipStreamSynchronize (the runtime's default spin) for A/B runs
 int lane_wait(Lane& l) {
-  hipError_t e = hipEventRecord(l.ev, l.st);
-  if (e == hipSuccess) e = hipEventSynchronize(l.ev);
+  static const bool spin = [] {
+    const char* e = std::getenv("MPCX_SPIN_WAIT");
+    return e && e[0] == '1';
+  }();
+  hipError_t e;
+  if (spin) {
+    e = hipStreamSynchronize(l.st);
+  } else {
+    e = hipEventRecord(l.ev, l.st);
+    if (e == hipSuccess) e = hipEventSynchronize(l.ev);
+  }
   return e == hipSuccess ? MPCX_OK : hip_fail(e, "lane wait");
 }
 
