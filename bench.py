@@ -652,7 +652,17 @@ def main():
         keygen_cpu = cpu_baseline_keygen(16.0, info, args.parties)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("gloo", rank=rank, world_size=world)
+        # gloo prints its connection messages to stdout from C++: keep stdout
+        # for the one JSON result line by pointing fd 1 at stderr meanwhile
+        sys.stdout.flush()
+        saved = os.dup(1)
+        os.dup2(2, 1)
+        try:
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        finally:
+            sys.stdout.flush()
+            os.dup2(saved, 1)
+            os.close(saved)
     torch.cuda.set_device(local)
 
     from mpcium_amd import build, mpcx

@@ -160,6 +160,9 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
   // MPCX_SIGN_CHAINS=0: rounds with a barrier between them (A/B)
   const char* ce = std::getenv("MPCX_SIGN_CHAINS");
   const bool chains = !(ce && ce[0] == '0');
+  // MPCX_SIGN_STAGGER_MS: chain k starts k times this late (A/B runs)
+  const char* se = std::getenv("MPCX_SIGN_STAGGER_MS");
+  const double stagger_ms = se ? std::atof(se) : 0.0;
   auto run_chunk = [&](size_t lo, size_t hi) {
     const size_t n = hi - lo;
     const std::vector<mta::Bytes> cs(sess.begin() + (long)lo, sess.begin() + (long)hi);
@@ -241,6 +244,7 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
       std::vector<std::function<void()>> tasks;
       for (size_t pi = 0; pi < np; ++pi)
         tasks.push_back([&, pi] {
+          if (stagger_ms > 0 && pi) std::this_thread::sleep_for(std::chrono::microseconds((long)(stagger_ms * 1000 * pi)));
           const double a0 = now();
           alice_init(pi);
           const double a1 = now();
