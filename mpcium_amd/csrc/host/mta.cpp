@@ -17,6 +17,10 @@ const Nat& q3() {
   static const Nat v = Q() * Q() * Q();
   return v;
 }
+const Nat& q5() {
+  static const Nat v = q3() * Q() * Q();
+  return v;
+}
 const Nat& q7() {
   static const Nat v = q3() * q3() * Q();
   return v;
@@ -293,9 +297,9 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
     for (const Nat* v : {&p.Z, &p.ZPrm, &p.T, &p.W})
       if (!IsInInterval(*v, Nt)) return;
     if (!IsInInterval(p.V, N2) || !IsInInterval(p.S, pk.N)) return;
-    // 3. s1 <= q^3. No t1 bound: BobMid draws betaPrm < N, so an honest
-    // t1 = e betaPrm + gamma has ~2300 bits (upstream, verify).
-    if (p.S1 > q3()) return;
+    // 3. s1 <= q^3, t1 <= q^7 (tss-lib v2's Alpha-Rays range checks: betaPrm < q^5,
+    // gamma < q^7, so an honest t1 = e betaPrm + gamma < q^6 + q^7)
+    if (p.S1 > q3() || p.T1 > q7()) return;
     ok[i] = 1;
   });
   {  // z, z', t, w in Z*_N~ and v, s in Z*_N: the batch's gcd decisions together
@@ -430,8 +434,8 @@ void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& p
       rd[j] = &rand[idx[j]];
       cr[j] = &cRand[j];
     }
-    // betaPrm < N, then the Encrypt(betaPrm) randomness in Z*_N
-    parallel_for(k, [&](size_t j) { (*out)[idx[j]].betaPrm = GetRandomPositiveInt(*rd[j], pkA.N); });
+    // betaPrm < q^5 (tss-lib v2 BobMid), then the Encrypt(betaPrm) randomness in Z*_N
+    parallel_for(k, [&](size_t j) { (*out)[idx[j]].betaPrm = GetRandomPositiveInt(*rd[j], q5()); });
     GetRandomPositiveRelativelyPrimeIntBatch(rd, pkA.N, cr);
     std::vector<size_t> js;
     std::vector<const RandFn*> rdj;

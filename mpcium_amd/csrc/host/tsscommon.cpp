@@ -220,15 +220,22 @@ struct Sha512_256 {
   }
 };
 
-// 8-byte little-endian element count, then every element followed by '$'
+void put_le64(uint8_t* o, uint64_t v) {
+  for (int i = 0; i < 8; ++i) o[i] = (uint8_t)(v >> (8 * i));
+}
+
+// 8-byte little-endian element count, then every element followed by '$' and
+// its byte length as 8 little-endian bytes (up:common/hash.go)
 void frame(Sha512_256& s, const std::vector<std::vector<uint8_t>>& parts) {
   uint8_t cnt[8];
-  for (int i = 0; i < 8; ++i) cnt[i] = (uint8_t)((uint64_t)parts.size() >> (8 * i));
+  put_le64(cnt, parts.size());
   s.update(cnt, 8);
-  const uint8_t delim = '$';
+  uint8_t tail[9];
+  tail[0] = '$';
   for (const auto& p : parts) {
     if (!p.empty()) s.update(p.data(), p.size());
-    s.update(&delim, 1);
+    put_le64(tail + 1, p.size());
+    s.update(tail, 9);
   }
 }
 
@@ -237,18 +244,21 @@ void frame(Sha512_256& s, const std::vector<std::vector<uint8_t>>& parts) {
 void frame_ints(Sha512_256& s, const std::vector<const Nat*>& in) {
   static thread_local std::vector<uint8_t> buf;
   size_t total = 8;
-  for (const Nat* n : in) total += (n ? (n->bit_len() + 7) / 8 : 0) + 1;
+  for (const Nat* n : in) total += (n ? (n->bit_len() + 7) / 8 : 0) + 9;
   buf.resize(total);
   uint8_t* o = buf.data();
-  for (int i = 0; i < 8; ++i) *o++ = (uint8_t)((uint64_t)in.size() >> (8 * i));
+  put_le64(o, in.size());
+  o += 8;
   for (const Nat* n : in) {
-    if (n) {
-      const uint32_t nb = (n->bit_len() + 7) / 8;
+    const uint32_t nb = n ? (n->bit_len() + 7) / 8 : 0;
+    if (nb) {
       const auto& w = n->limbs();
       for (uint32_t i = 0; i < nb; ++i) o[nb - 1 - i] = (uint8_t)(w[i / 4] >> (8 * (i % 4)));
       o += nb;
     }
     *o++ = '$';
+    put_le64(o, nb);
+    o += 8;
   }
   s.update(buf.data(), total);
 }

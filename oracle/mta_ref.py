@@ -216,14 +216,15 @@ def verify_bob_wc(pf: ProofBob, session: bytes, pkN: int, NTilde: int, h1: int, 
     if X is not None and not T.ec_on_curve(pf.U):
         return False
     N2 = pkN * pkN
-    q3 = Q ** 3
+    q3, q7 = Q ** 3, Q ** 7
     Nt = NTilde
     for v_, bound in ((pf.Z, Nt), (pf.ZPrm, Nt), (pf.T, Nt), (pf.V, N2), (pf.W, Nt), (pf.S, pkN)):
         if not T.is_in_interval(v_, bound) or math.gcd(v_, bound) != 1:
             return False
-    # s1 <= q^3 (the Alpha-Rays range check). No t1 bound: BobMid draws
-    # betaPrm < N, so an honest t1 = e*betaPrm + gamma has ~2300 bits (> q^7).
-    if pf.S1 > q3:
+    # s1 <= q^3 and t1 <= q^7 (the Alpha-Rays range checks of tss-lib v2: BobMid
+    # draws betaPrm < q^5 and ProveBob gamma < q^7, so an honest t1 = e*betaPrm +
+    # gamma < q^6 + q^7 passes except with probability ~1/q).
+    if pf.S1 > q3 or pf.T1 > q7:
         return False
     if X is None:
         eh = T.sha512_256i_tagged(session, pkN, pkN + 1, c1, c2, pf.Z, pf.ZPrm, pf.T, pf.V, pf.W)
@@ -260,7 +261,7 @@ def bob_mid(session: bytes, pkA: int, pf: RangeProofAlice, b: int, cA: int, NTil
     -> (beta, cB, betaPrm, piB); raises ValueError where Go returns an error."""
     if not verify_range_alice(pf, pkA, NTildeB, h1B, h2B, cA):
         raise ValueError("RangeProofAlice.Verify() returned false")
-    beta_prm = T.get_random_positive_int(rd, pkA)
+    beta_prm = T.get_random_positive_int(rd, Q ** 5)  # betaPrm < q^5 (tss-lib v2, Alpha-Rays fix)
     c_beta_prm, c_rand = encrypt_and_return_randomness(rd, pkA, beta_prm)
     cB = homo_mult(pkA, b, cA)
     cB = homo_add(pkA, cB, c_beta_prm)

@@ -15,8 +15,10 @@ published algorithm and could not be checked against the source here
   GetRandomPositiveRelativelyPrimeInt, IsNumberInMultiplicativeGroup
   (up:common/random.go).
 * Hashing: common.SHA512_256, SHA512_256i, SHA512_256i_TAGGED
-  (up:common/hash.go; 8-byte little-endian element-count prefix, '$' delimiter
-  after every element, big.Int.Bytes() encoding -- upstream, verify) and
+  (up:common/hash.go; 8-byte little-endian element-count prefix, then per
+  element its big.Int.Bytes(), a '$' delimiter and its byte length as 8
+  little-endian bytes -- restated from tss-lib v2's hash.go as recalled, no
+  source in this image to check it against: upstream, verify) and
   common.RejectionSample (up:common/hash_utils.go: eHash mod q -- upstream,
   verify).
 * secp256k1 (tss.EC() = btcec/v2 S256, /root/reference/go.mod:29): affine
@@ -122,9 +124,12 @@ def _bytes(n: Optional[int]) -> bytes:
 
 
 def _frame(parts: Sequence[bytes]) -> bytes:
+    """8-byte little-endian part count, then per part: its bytes, '$', and its
+    length as 8 little-endian bytes (the audit's domain separation: the capacity
+    len(inLenBz) + bzSize + inLen + inLen*8 of up:common/hash.go)."""
     data = struct.pack("<Q", len(parts))
     for p in parts:
-        data += p + HASH_INPUT_DELIMITER
+        data += p + HASH_INPUT_DELIMITER + struct.pack("<Q", len(p))
     return data
 
 

@@ -145,6 +145,9 @@ def test_bob_proof_rejections(mta, nodes, vec):
     p = dict(pf)
     p["S1"] = M.Q ** 3 + 1
     cases.append((p, ss, X, False))
+    p = dict(pf)
+    p["T1"] = M.Q ** 7 + 1                                 # t1 above the q^7 bound
+    cases.append((p, ss, X, False))
     sk = (A["LambdaN"], A["P"], A["Q"])
     for own in (None, sk):
         ok = mta.verify_bob([c[1] for c in cases], A["N"], dln(A, own=own is not None), [c1] * len(cases),

@@ -71,10 +71,26 @@ def test_oracle_golden_relations(nodes, vectors):
         assert (H(v["alpha"]) + H(v["bob"]["beta"])) % q == H(v["a"]) * H(v["b"]) % q
         assert (H(v["alpha_wc"]) + H(v["bob_wc"]["beta"])) % q == H(v["a"]) * H(v["wB"]) % q
         assert T.scalar_base_mult(H(v["wB"])) == (H(v["Bx"]), H(v["By"]))
+        # tss-lib v2's Alpha-Rays ranges: betaPrm < q^5, honest s1 <= q^3 and t1 <= q^7
+        for side in ("bob", "bob_wc"):
+            assert H(v[side]["betaPrm"]) < q ** 5
+            assert H(v[side]["pf"]["S1"]) <= q ** 3 and H(v[side]["pf"]["T1"]) <= q ** 7
+
+
+def test_oracle_bob_verify_rejects_t1_over_q7(nodes, vectors):
+    """ProofBob.Verify rejects t1 > q^7 before any exponentiation; the honest
+    golden proof verifies."""
+    v = vectors[0]
+    A = nodes[v["alice_node"]]
+    pf = M.ProofBob(**{k: H(x) for k, x in v["bob"]["pf"].items()}, U=None)
+    args = (bytes.fromhex(v["session"]), A["N"], A["NTildei"], A["H1i"], A["H2i"], H(v["cA"]), H(v["bob"]["cB"]), None)
+    assert M.verify_bob_wc(pf, *args)
+    pf.T1 = M.Q ** 7 + 1
+    assert not M.verify_bob_wc(pf, *args)
 
 
 def test_sha512_256_framing_matches_oracle(mta):
-    assert T.sha512_256(b"abc") == hashlib.new("sha512_256", b"\x01" + b"\0" * 7 + b"abc$").digest()
+    assert T.sha512_256(b"abc") == hashlib.new("sha512_256", b"\x01" + b"\0" * 7 + b"abc$" + b"\x03" + b"\0" * 7).digest()
     cases = [(1,), (0, 5, 2 ** 4095 + 7), tuple(range(1, 14)), (2 ** 2048 - 1, 0, 0)]
     for ints in cases:
         assert mta.sha512_256i(*ints) == T.sha512_256i(*ints), ints
