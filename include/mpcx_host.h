@@ -168,6 +168,26 @@ int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t sess
                               const mpcxh_dln_t* dlnA, uint32_t count, const uint32_t* pfB, const uint32_t* cA,
                               const uint32_t* cB, const uint32_t* B, uint32_t* alpha, uint8_t* err);
 
+/* Signing round 2 runs BobMid and BobMidWC on every peer's round-1 message
+ * (up:ecdsa/signing/round_2.go): both halves of each session in one call,
+ * RangeProofAlice.Verify once for both, shared launches. b / readers / beta /
+ * cB / betaPrm / pfB / err: the BobMid half; bwc, Bwc, readers_wc, *_wc: the
+ * BobMidWC half. Every output equals the two separate calls'. */
+int mpcxh_mta_bob_mid_pair_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len,
+                                 const mpcxh_paillier_t* pkA, const mpcxh_dln_t* dlnA, const mpcxh_dln_t* dlnB,
+                                 uint32_t count, const uint32_t* pfA, const uint32_t* cA, const uint32_t* b,
+                                 const mpcxh_reader_t* readers, const uint32_t* bwc, const uint32_t* Bwc,
+                                 const mpcxh_reader_t* readers_wc, uint32_t* beta, uint32_t* cB, uint32_t* betaPrm,
+                                 uint32_t* pfB, uint8_t* err, uint32_t* beta_wc, uint32_t* cB_wc,
+                                 uint32_t* betaPrm_wc, uint32_t* pfB_wc, uint8_t* err_wc);
+/* Signing round 3's AliceEnd and AliceEndWC per peer (up:ecdsa/signing/round_3.go)
+ * in one call: one verification batch and one Decrypt batch for both halves. */
+int mpcxh_mta_alice_end_pair_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len,
+                                   const mpcxh_paillier_t* skA, const mpcxh_dln_t* dlnA, uint32_t count,
+                                   const uint32_t* cA, const uint32_t* pfB, const uint32_t* cB,
+                                   const uint32_t* pfB_wc, const uint32_t* cB_wc, const uint32_t* Bwc,
+                                   uint32_t* alpha, uint8_t* err, uint32_t* mu, uint8_t* err_wc);
+
 /* ---------------------------------------------------------------- keygen proofs
  * Batched mirror of tss-lib v2.0.2's DLN (up:crypto/dlnproof, 128 iterations),
  * Paillier-Blum modulus (up:crypto/modproof, 80 iterations) and no-small-factor

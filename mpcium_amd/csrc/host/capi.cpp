@@ -450,6 +450,67 @@ int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t sess
   });
 }
 
+static void bob_results_out(const std::vector<mta::BobMidResult>& out, uint32_t w, uint32_t* beta, uint32_t* cB,
+                            uint32_t* betaPrm, uint32_t* pfB) {
+  std::vector<mta::ProofBob> pfs(out.size());
+  for (size_t i = 0; i < out.size(); ++i) {
+    put(out[i].beta, beta + i * w, w);
+    put(out[i].cB, cB + i * w, w);
+    put(out[i].betaPrm, betaPrm + i * w, w);
+    pfs[i] = out[i].pf;
+  }
+  bob_to(pfs, pfB, w);
+}
+
+int mpcxh_mta_bob_mid_pair_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len,
+                                 const mpcxh_paillier_t* pkA, const mpcxh_dln_t* dlnA, const mpcxh_dln_t* dlnB,
+                                 uint32_t count, const uint32_t* pfA, const uint32_t* cA, const uint32_t* b,
+                                 const mpcxh_reader_t* rdr, const uint32_t* bwc, const uint32_t* Bwc,
+                                 const mpcxh_reader_t* rdr_wc, uint32_t* beta, uint32_t* cB, uint32_t* betaPrm,
+                                 uint32_t* pfB, uint8_t* err, uint32_t* beta_wc, uint32_t* cB_wc,
+                                 uint32_t* betaPrm_wc, uint32_t* pfB_wc, uint8_t* err_wc) {
+  return guard([&] {
+    check_width(w);
+    if (!Bwc) throw std::invalid_argument("BobMidPair: Bwc is required");
+    const auto sk = paillier_from(pkA, w);
+    std::vector<CounterDRBG> d1, d2;
+    const auto rd = readers(rdr, count, &d1);
+    const auto rdwc = readers(rdr_wc, count, &d2);
+    std::vector<mta::BobMidResult> out, outwc;
+    std::vector<uint8_t> e, ewc;
+    mta::BobMidPairBatch(sessions_from(sessions, session_len, count), sk.pub, range_from(pfA, count, w),
+                         nats(b, w, count), nats(bwc, w, count), nats(cA, w, count), dln_from(dlnA, w),
+                         dln_from(dlnB, w), points_from(Bwc, count), rd, rdwc, &out, &outwc, &e, &ewc);
+    bob_results_out(out, w, beta, cB, betaPrm, pfB);
+    bob_results_out(outwc, w, beta_wc, cB_wc, betaPrm_wc, pfB_wc);
+    std::memcpy(err, e.data(), count);
+    std::memcpy(err_wc, ewc.data(), count);
+  });
+}
+
+int mpcxh_mta_alice_end_pair_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len,
+                                   const mpcxh_paillier_t* skA, const mpcxh_dln_t* dlnA, uint32_t count,
+                                   const uint32_t* cA, const uint32_t* pfB, const uint32_t* cB,
+                                   const uint32_t* pfB_wc, const uint32_t* cB_wc, const uint32_t* Bwc,
+                                   uint32_t* alpha, uint8_t* err, uint32_t* mu, uint8_t* err_wc) {
+  return guard([&] {
+    check_width(w);
+    if (!Bwc) throw std::invalid_argument("AliceEndPair: Bwc is required");
+    const auto sk = paillier_from(skA, w);
+    if (sk.LambdaN.is_zero() || sk.P.is_zero() || sk.Q.is_zero())
+      throw std::invalid_argument("AliceEnd needs the private key (LambdaN, P, Q)");
+    std::vector<Nat> al, m;
+    std::vector<uint8_t> e, ewc;
+    mta::AliceEndPairBatch(sessions_from(sessions, session_len, count), sk, bob_from(pfB, count, w, false),
+                           bob_from(pfB_wc, count, w, true), dln_from(dlnA, w), nats(cA, w, count),
+                           nats(cB, w, count), nats(cB_wc, w, count), points_from(Bwc, count), &al, &m, &e, &ewc);
+    store(al, alpha, w);
+    store(m, mu, w);
+    std::memcpy(err, e.data(), count);
+    std::memcpy(err_wc, ewc.data(), count);
+  });
+}
+
 // ------------------------------------------------------------------ test hooks
 int mpcxh_sha512_256i(const uint8_t* tag, size_t tag_len, uint32_t count, const uint32_t* ints, uint32_t w,
                       uint8_t* digest32) {

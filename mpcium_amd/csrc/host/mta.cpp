@@ -171,13 +171,14 @@ struct BobProveState {
   Nat alpha, rho, sigma, tau, rhoPrm, beta, gamma;
   secp::Affine u;
   Nat bg, a1, a2, a3, a4, e;
+  bool wc = false;  // ProveBobWC (u = alpha*G)
 };
 
-// steps 1-4 (+5 for WC) for the sessions st[js[k]] with readers rd[k], in
-// each reader's draw order alpha, rho, sigma, tau, rhoPrm, beta, gamma (the
+// steps 1-4 (+5 for WC states) for the sessions st[js[k]] with readers rd[k],
+// in each reader's draw order alpha, rho, sigma, tau, rhoPrm, beta, gamma (the
 // beta gcd decisions taken together)
 void bob_draw(std::vector<BobProveState>& st, const std::vector<size_t>& js, const std::vector<const RandFn*>& rd,
-              const paillier::PublicKey& pk, const DLNParams& dln, bool wc) {
+              const paillier::PublicKey& pk, const DLNParams& dln) {
   const size_t n = js.size();
   const Nat qNt = Q() * dln.NTilde, q3Nt = q3() * dln.NTilde;
   parallel_for(n, [&](size_t k) {
@@ -195,7 +196,7 @@ void bob_draw(std::vector<BobProveState>& st, const std::vector<size_t>& js, con
   parallel_for(n, [&](size_t k) {
     BobProveState& s = st[js[k]];
     s.gamma = GetRandomPositiveInt(*rd[k], q7());
-    if (wc) s.u = secp::ScalarBaseMult(s.alpha);  // 5. u = alpha*G
+    if (s.wc) s.u = secp::ScalarBaseMult(s.alpha);  // 5. u = alpha*G
   });
 }
 
@@ -257,8 +258,9 @@ void ProveBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey&
     for (size_t i = 0; i < n; ++i) {
       js[i] = i;
       rd[i] = &rand[i];
+      st[i].wc = X != nullptr;
     }
-    bob_draw(st, js, rd, pk, dln, X != nullptr);
+    bob_draw(st, js, rd, pk, dln);
   }
   ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
   for (size_t i = 0; i < n; ++i) bob_stage_a(st[i], pk, dln, x[i], y[i], eN2, eNt, &gg[i]);
@@ -276,23 +278,22 @@ void ProveBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey&
   parallel_for(n, [&](size_t i) { bob_responses(st[i], x[i], y[i], (*out)[i]); });
 }
 
-std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pk,
-                                    const DLNParams& dln, const std::vector<Nat>& c1, const std::vector<Nat>& c2,
-                                    const std::vector<ProofBob>& pf, const std::vector<secp::Affine>* X,
-                                    const paillier::PrivateKey* own_sk) {
+namespace {
+// ProofBob[WC].Verify of session i's proof *pfp[i], X[i] == nullptr for a
+// plain ProofBob: one batch may mix both kinds (AliceEnd and AliceEndWC of one
+// pair share every modulus).
+std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, const paillier::PublicKey& pk,
+                                     const DLNParams& dln, const std::vector<const Nat*>& c1,
+                                     const std::vector<const Nat*>& c2, const std::vector<const ProofBob*>& pfp,
+                                     const std::vector<const secp::Affine*>& X) {
   const size_t n = c1.size();
-  if (session.size() != n || c2.size() != n || pf.size() != n || (X && X->size() != n))
-    throw std::invalid_argument("ProofBob.Verify: sizes");
   const Nat N2 = pk.NSquare(), gamma = pk.Gamma();
-  // own_sk (the verifier's own key) does not change any decision: gcd(x, N)
-  // == 1 is decided for the whole batch at once below
-  (void)own_sk;
   std::vector<uint8_t> ok(n, 0);
   std::vector<Nat> e(n), gt1(n), p1(n), p2(n), r1(n), r2(n), q1(n), r3(n), l1(n), l2(n), l3(n);
   parallel_for(n, [&](size_t i) {
     MPCX_PROF("mta.verify_bob.checks");
-    const auto& p = pf[i];
-    if (X && !secp::IsOnCurve(p.U)) return;
+    const auto& p = *pfp[i];
+    if (X[i] && !secp::IsOnCurve(p.U)) return;
     const Nat& Nt = dln.NTilde;
     for (const Nat* v : {&p.Z, &p.ZPrm, &p.T, &p.W})
       if (!IsInInterval(*v, Nt)) return;
@@ -308,8 +309,8 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
     for (size_t i = 0; i < n; ++i)
       if (ok[i]) {
         sel.push_back(i);
-        xt.insert(xt.end(), {&pf[i].Z, &pf[i].ZPrm, &pf[i].T, &pf[i].W});
-        xn.insert(xn.end(), {&pf[i].V, &pf[i].S});
+        xt.insert(xt.end(), {&pfp[i]->Z, &pfp[i]->ZPrm, &pfp[i]->T, &pfp[i]->W});
+        xn.insert(xn.end(), {&pfp[i]->V, &pfp[i]->S});
       }
     const std::vector<uint8_t> ct = CoprimeMany(xt, dln.NTilde), cn = CoprimeMany(xn, pk.N);
     for (size_t j = 0; j < sel.size(); ++j)
@@ -318,9 +319,9 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
   parallel_for(n, [&](size_t i) {
     if (!ok[i]) return;
     ok[i] = 0;
-    const auto& p = pf[i];
-    e[i] = bob_challenge(session[i], pk, gamma, X ? &(*X)[i] : nullptr, c1[i], c2[i], p);
-    if (X) {
+    const auto& p = *pfp[i];
+    e[i] = bob_challenge(*session[i], pk, gamma, X[i], *c1[i], *c2[i], p);
+    if (X[i]) {
       // 4. s1*G == e*X + u, rejected when e*X + u is the point at infinity
       // (Go: xEU nil). Evaluated as one combination T = s1*G + (q - e)*X
       // compared with u: T == u  <=>  s1*G == e*X + u as group elements, and
@@ -330,7 +331,7 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
       const Nat s1q = p.S1 % Q();
       if (s1q.is_zero()) return;
       const Nat eq = e[i] % Q();
-      const secp::Affine T = secp::LinComb(s1q, (*X)[i], eq.is_zero() ? eq : Q() - eq);
+      const secp::Affine T = secp::LinComb(s1q, *X[i], eq.is_zero() ? eq : Q() - eq);
       if (!secp::Equal(T, p.U)) return;
     }
     gt1[i] = gamma_pow(p.T1, pk.N);
@@ -339,26 +340,51 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
   ExpSet eN2(N2), eNt(dln.NTilde);
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
-    const auto& p = pf[i];
+    const auto& p = *pfp[i];
     eNt.add(dln.h1, p.S1, &p1[i]);          // 5. h1^s1
     eNt.add(dln.h1, p.T1, &p2[i]);          // 6. h1^t1
     eNt.add(p.Z, e[i], &r1[i], &p.ZPrm);    // 5. z^e z'
     eNt.add(p.T, e[i], &r2[i], &p.W);       // 6. t^e w
     eN2.add(p.S, pk.N, &q1[i], &gt1[i]);    // 7. s^N Gamma^t1
-    eN2.add(c2[i], e[i], &r3[i], &p.V);     // 7. c2^e v
+    eN2.add(*c2[i], e[i], &r3[i], &p.V);    // 7. c2^e v
   }
   eN2.run();
   eNt.run();
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
-    eNt.add(dln.h2, pf[i].S2, &l1[i], &p1[i]);  // 5. h1^s1 h2^s2
-    eNt.add(dln.h2, pf[i].T2, &l2[i], &p2[i]);  // 6. h1^t1 h2^t2
-    eN2.add(c1[i], pf[i].S1, &l3[i], &q1[i]);   // 7. c1^s1 s^N Gamma^t1
+    eNt.add(dln.h2, pfp[i]->S2, &l1[i], &p1[i]);  // 5. h1^s1 h2^s2
+    eNt.add(dln.h2, pfp[i]->T2, &l2[i], &p2[i]);  // 6. h1^t1 h2^t2
+    eN2.add(*c1[i], pfp[i]->S1, &l3[i], &q1[i]);  // 7. c1^s1 s^N Gamma^t1
   }
   eN2.run();
   eNt.run();
   for (size_t i = 0; i < n; ++i) ok[i] = ok[i] && l1[i] == r1[i] && l2[i] == r2[i] && l3[i] == r3[i];
   return ok;
+}
+}  // namespace
+
+std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pk,
+                                    const DLNParams& dln, const std::vector<Nat>& c1, const std::vector<Nat>& c2,
+                                    const std::vector<ProofBob>& pf, const std::vector<secp::Affine>* X,
+                                    const paillier::PrivateKey* own_sk) {
+  const size_t n = c1.size();
+  if (session.size() != n || c2.size() != n || pf.size() != n || (X && X->size() != n))
+    throw std::invalid_argument("ProofBob.Verify: sizes");
+  // own_sk (the verifier's own key) does not change any decision: gcd(x, N)
+  // == 1 is decided for the whole batch at once
+  (void)own_sk;
+  std::vector<const Bytes*> sp(n);
+  std::vector<const Nat*> c1p(n), c2p(n);
+  std::vector<const ProofBob*> pfp(n);
+  std::vector<const secp::Affine*> Xp(n, nullptr);
+  for (size_t i = 0; i < n; ++i) {
+    sp[i] = &session[i];
+    c1p[i] = &c1[i];
+    c2p[i] = &c2[i];
+    pfp[i] = &pf[i];
+    if (X) Xp[i] = &(*X)[i];
+  }
+  return verify_bob_core(sp, pk, dln, c1p, c2p, pfp, Xp);
 }
 
 // ================================================================ protocol
@@ -404,6 +430,86 @@ void AliceInitBatch(const paillier::PublicKey& pkA, const std::vector<Nat>& a, c
   }
 }
 
+namespace {
+// One BobMid[WC] half of a session whose RangeProofAlice verified: its b, its
+// point B (nullptr: plain BobMid), its reader and its result slots.
+struct BobHalf {
+  size_t i;  // session index (session id, cA)
+  const Nat* b;
+  const secp::Affine* B;
+  const RandFn* rd;
+  BobMidResult* out;
+  uint8_t* err;
+};
+
+// Everything of BobMid[WC] after pf.Verify, for any mix of plain and WC halves
+// on one Alice key: every half's draws in its own reader's order, and each
+// step's exponentiations of all halves in shared launches.
+void bob_mid_halves(const std::vector<Bytes>& session, const paillier::PublicKey& pkA, const DLNParams& dlnA,
+                    const std::vector<Nat>& cA, const std::vector<BobHalf>& h) {
+  const size_t k = h.size();
+  const Nat N2 = pkA.NSquare(), gamma = pkA.Gamma();
+  std::vector<BobProveState> st(k);
+  std::vector<Nat> cRand(k), gbp(k), cbp(k), gg(k);
+  std::vector<uint8_t> live(k, 0);
+  {
+    MPCX_PROF("mta.bob_mid.draws");
+    std::vector<const RandFn*> rd(k);
+    std::vector<Nat*> cr(k);
+    for (size_t j = 0; j < k; ++j) {
+      rd[j] = h[j].rd;
+      cr[j] = &cRand[j];
+    }
+    // betaPrm < q^5 (tss-lib v2 BobMid), then the Encrypt(betaPrm) randomness in Z*_N
+    parallel_for(k, [&](size_t j) { h[j].out->betaPrm = GetRandomPositiveInt(*rd[j], q5()); });
+    GetRandomPositiveRelativelyPrimeIntBatch(rd, pkA.N, cr);
+    std::vector<size_t> js;
+    std::vector<const RandFn*> rdj;
+    for (size_t j = 0; j < k; ++j) {
+      gbp[j] = gamma_pow(h[j].out->betaPrm, pkA.N);
+      if (!(*h[j].b < pkA.N)) {  // HomoMult(b, cA) fails before ProveBob draws anything
+        *h[j].err = ErrMessageTooLong;
+        continue;
+      }
+      live[j] = 1;
+      st[j].wc = h[j].B != nullptr;
+      js.push_back(j);
+      rdj.push_back(rd[j]);
+    }
+    bob_draw(st, js, rdj, pkA, dlnA);  // ProveBob[WC] steps 1-5
+  }
+  ExpSet eN2(N2), eNt(dlnA.NTilde), eN(pkA.N);
+  for (size_t j = 0; j < k; ++j) {
+    if (!live[j]) continue;
+    eN2.add(cRand[j], pkA.N, &cbp[j], &gbp[j]);  // cBetaPrm = Gamma^betaPrm r^N
+    bob_stage_a(st[j], pkA, dlnA, *h[j].b, h[j].out->betaPrm, eN2, eNt, &gg[j]);
+  }
+  eN2.run();
+  eNt.run();
+  for (size_t j = 0; j < k; ++j) {
+    if (!live[j]) continue;
+    const Nat& c = cA[h[j].i];
+    eN2.add(c, *h[j].b, &h[j].out->cB, &cbp[j]);  // cB = HomoAdd(HomoMult(b, cA), cBetaPrm)
+    bob_stage_b(st[j], dlnA, c, eN2, eNt, h[j].out->pf);
+  }
+  eN2.run();
+  eNt.run();
+  parallel_for(k, [&](size_t j) {
+    if (!live[j]) return;
+    auto& o = *h[j].out;
+    o.beta = (Q() - o.betaPrm % Q()) % Q();  // beta = ModInt(q).Sub(0, betaPrm)
+    o.pf.U = st[j].u;
+    st[j].e = bob_challenge(session[h[j].i], pkA, gamma, h[j].B, cA[h[j].i], o.cB, o.pf);
+  });
+  for (size_t j = 0; j < k; ++j)
+    if (live[j]) eN.add(cRand[j], st[j].e, &h[j].out->pf.S, &st[j].beta);  // s = r^e beta mod N
+  eN.run();
+  parallel_for(k, [&](size_t j) {
+    if (live[j]) bob_responses(st[j], *h[j].b, h[j].out->betaPrm, h[j].out->pf);
+  });
+}
+}  // namespace
+
 void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pkA,
                  const std::vector<RangeProofAlice>& pf, const std::vector<Nat>& b, const std::vector<Nat>& cA,
                  const DLNParams& dlnA, const DLNParams& dlnB, const std::vector<secp::Affine>* B,
@@ -411,81 +517,73 @@ void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& p
   const size_t n = cA.size();
   if (session.size() != n || pf.size() != n || b.size() != n || rand.size() != n || (B && B->size() != n))
     throw std::invalid_argument("BobMid: sizes");
-  const Nat N2 = pkA.NSquare(), gamma = pkA.Gamma();
   out->assign(n, BobMidResult{});
   err->assign(n, OK);
   // RangeProofAlice.Verify(ec, pkA, NTildeB, h1B, h2B, cA)
   const std::vector<uint8_t> ok = VerifyRangeAliceBatch(pkA, dlnB, cA, pf);
   // HomoMult's range checks: cA < N^2 holds for every verified session; b < N
   // is checked after betaPrm and the Encrypt randomness are drawn, as in Go.
-  std::vector<size_t> idx;
+  std::vector<BobHalf> h;
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) (*err)[i] = ErrProofVerify;
-    else idx.push_back(i);
+    else h.push_back({i, &b[i], B ? &(*B)[i] : nullptr, &rand[i], &(*out)[i], &(*err)[i]});
   }
-  const size_t k = idx.size();
-  std::vector<BobProveState> st(k);
-  std::vector<Nat> cRand(k), gbp(k), cbp(k), gg(k);
-  {
-    MPCX_PROF("mta.bob_mid.draws");
-    std::vector<const RandFn*> rd(k);
-    std::vector<Nat*> cr(k);
-    for (size_t j = 0; j < k; ++j) {
-      rd[j] = &rand[idx[j]];
-      cr[j] = &cRand[j];
-    }
-    // betaPrm < q^5 (tss-lib v2 BobMid), then the Encrypt(betaPrm) randomness in Z*_N
-    parallel_for(k, [&](size_t j) { (*out)[idx[j]].betaPrm = GetRandomPositiveInt(*rd[j], q5()); });
-    GetRandomPositiveRelativelyPrimeIntBatch(rd, pkA.N, cr);
-    std::vector<size_t> js;
-    std::vector<const RandFn*> rdj;
-    for (size_t j = 0; j < k; ++j) {
-      const size_t i = idx[j];
-      gbp[j] = gamma_pow((*out)[i].betaPrm, pkA.N);
-      if (!(b[i] < pkA.N)) {  // HomoMult(b, cA) fails before ProveBob draws anything
-        (*err)[i] = ErrMessageTooLong;
-        continue;
-      }
-      js.push_back(j);
-      rdj.push_back(rd[j]);
-    }
-    bob_draw(st, js, rdj, pkA, dlnA, B != nullptr);  // ProveBob[WC] steps 1-5
-  }
-  ExpSet eN2(N2), eNt(dlnA.NTilde), eN(pkA.N);
-  for (size_t j = 0; j < k; ++j) {
-    const size_t i = idx[j];
-    if ((*err)[i]) continue;
-    eN2.add(cRand[j], pkA.N, &cbp[j], &gbp[j]);  // cBetaPrm = Gamma^betaPrm r^N
-    bob_stage_a(st[j], pkA, dlnA, b[i], (*out)[i].betaPrm, eN2, eNt, &gg[j]);
-  }
-  eN2.run();
-  eNt.run();
-  for (size_t j = 0; j < k; ++j) {
-    const size_t i = idx[j];
-    if ((*err)[i]) continue;
-    eN2.add(cA[i], b[i], &(*out)[i].cB, &cbp[j]);  // cB = HomoAdd(HomoMult(b, cA), cBetaPrm)
-    bob_stage_b(st[j], dlnA, cA[i], eN2, eNt, (*out)[i].pf);
-  }
-  eN2.run();
-  eNt.run();
-  parallel_for(k, [&](size_t j) {
-    const size_t i = idx[j];
-    if ((*err)[i]) return;
-    auto& o = (*out)[i];
-    o.beta = (Q() - o.betaPrm % Q()) % Q();  // beta = ModInt(q).Sub(0, betaPrm)
-    o.pf.U = st[j].u;
-    st[j].e = bob_challenge(session[i], pkA, gamma, B ? &(*B)[i] : nullptr, cA[i], o.cB, o.pf);
-  });
-  for (size_t j = 0; j < k; ++j) {
-    const size_t i = idx[j];
-    if (!(*err)[i]) eN.add(cRand[j], st[j].e, &(*out)[i].pf.S, &st[j].beta);  // s = r^e beta mod N
-  }
-  eN.run();
-  parallel_for(k, [&](size_t j) {
-    const size_t i = idx[j];
-    if (!(*err)[i]) bob_responses(st[j], b[i], (*out)[i].betaPrm, (*out)[i].pf);
-  });
+  bob_mid_halves(session, pkA, dlnA, cA, h);
 }
+
+void BobMidPairBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pkA,
+                     const std::vector<RangeProofAlice>& pf, const std::vector<Nat>& b, const std::vector<Nat>& bwc,
+                     const std::vector<Nat>& cA, const DLNParams& dlnA, const DLNParams& dlnB,
+                     const std::vector<secp::Affine>& Bwc, const std::vector<RandFn>& rand,
+                     const std::vector<RandFn>& randwc, std::vector<BobMidResult>* out,
+                     std::vector<BobMidResult>* outwc, std::vector<uint8_t>* err, std::vector<uint8_t>* errwc) {
+  const size_t n = cA.size();
+  if (session.size() != n || pf.size() != n || b.size() != n || bwc.size() != n || Bwc.size() != n ||
+      rand.size() != n || randwc.size() != n)
+    throw std::invalid_argument("BobMidPair: sizes");
+  out->assign(n, BobMidResult{});
+  outwc->assign(n, BobMidResult{});
+  err->assign(n, OK);
+  errwc->assign(n, OK);
+  // Both halves verify the same (cA, pf) under the same key: one verification
+  // decides both (Verify is a pure function of its inputs)
+  const std::vector<uint8_t> ok = VerifyRangeAliceBatch(pkA, dlnB, cA, pf);
+  std::vector<BobHalf> h;
+  h.reserve(2 * n);
+  for (size_t i = 0; i < n; ++i) {
+    if (!ok[i]) {
+      (*err)[i] = (*errwc)[i] = ErrProofVerify;
+      continue;
+    }
+    h.push_back({i, &b[i], nullptr, &rand[i], &(*out)[i], &(*err)[i]});
+    h.push_back({i, &bwc[i], &Bwc[i], &randwc[i], &(*outwc)[i], &(*errwc)[i]});
+  }
+  bob_mid_halves(session, pkA, dlnA, cA, h);
+}
+
+namespace {
+// Decrypt(cB) mod q of every session whose proof verified
+void alice_decrypt(const paillier::PrivateKey& skA, const std::vector<const Nat*>& cB, const std::vector<uint8_t>& ok,
+                   const std::vector<Nat*>& alpha, const std::vector<uint8_t*>& err) {
+  std::vector<Int> cs;
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < cB.size(); ++i) {
+    if (!ok[i]) {
+      *err[i] = ErrProofVerify;
+      continue;
+    }
+    idx.push_back(i);
+    cs.push_back(Int(*cB[i]));
+  }
+  std::vector<Nat> m;
+  std::vector<uint8_t> derr;
+  skA.DecryptBatch(cs, &m, &derr);
+  for (size_t j = 0; j < idx.size(); ++j) {
+    if (derr[j]) *err[idx[j]] = derr[j];
+    else *alpha[idx[j]] = m[j] % Q();
+  }
+}
+}  // namespace
 
 void AliceEndBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,
                    const std::vector<ProofBob>& pf, const DLNParams& dlnA, const std::vector<Nat>& cA,
@@ -495,26 +593,53 @@ void AliceEndBatch(const std::vector<Bytes>& session, const paillier::PrivateKey
   const std::vector<uint8_t> ok = VerifyBobBatch(session, skA.pub, dlnA, cA, cB, pf, B, &skA);
   alpha->assign(n, Nat());
   err->assign(n, OK);
-  std::vector<Int> cs;
-  std::vector<size_t> idx;
+  std::vector<const Nat*> c(n);
+  std::vector<Nat*> a(n);
+  std::vector<uint8_t*> e(n);
   for (size_t i = 0; i < n; ++i) {
-    if (!ok[i]) {
-      (*err)[i] = ErrProofVerify;
-      continue;
-    }
-    idx.push_back(i);
-    cs.push_back(Int(cB[i]));
+    c[i] = &cB[i];
+    a[i] = &(*alpha)[i];
+    e[i] = &(*err)[i];
   }
-  std::vector<Nat> m;
-  std::vector<uint8_t> derr;
-  skA.DecryptBatch(cs, &m, &derr);
-  for (size_t j = 0; j < idx.size(); ++j) {
-    if (derr[j]) {
-      (*err)[idx[j]] = derr[j];
-      continue;
-    }
-    (*alpha)[idx[j]] = m[j] % Q();
+  alice_decrypt(skA, c, ok, a, e);
+}
+
+void AliceEndPairBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,
+                       const std::vector<ProofBob>& pf, const std::vector<ProofBob>& pfwc, const DLNParams& dlnA,
+                       const std::vector<Nat>& cA, const std::vector<Nat>& cB, const std::vector<Nat>& cBwc,
+                       const std::vector<secp::Affine>& Bwc, std::vector<Nat>* alpha, std::vector<Nat>* mu,
+                       std::vector<uint8_t>* err, std::vector<uint8_t>* errwc) {
+  const size_t n = cA.size();
+  if (session.size() != n || pf.size() != n || pfwc.size() != n || cB.size() != n || cBwc.size() != n ||
+      Bwc.size() != n)
+    throw std::invalid_argument("AliceEndPair: sizes");
+  alpha->assign(n, Nat());
+  mu->assign(n, Nat());
+  err->assign(n, OK);
+  errwc->assign(n, OK);
+  // session i's ProofBob at 2i, its ProofBobWC at 2i+1: one verification batch
+  // and one Decrypt batch for both halves
+  std::vector<const Bytes*> sp(2 * n);
+  std::vector<const Nat*> c1(2 * n), c2(2 * n);
+  std::vector<const ProofBob*> pp(2 * n);
+  std::vector<const secp::Affine*> Xp(2 * n, nullptr);
+  std::vector<Nat*> a(2 * n);
+  std::vector<uint8_t*> e(2 * n);
+  for (size_t i = 0; i < n; ++i) {
+    sp[2 * i] = sp[2 * i + 1] = &session[i];
+    c1[2 * i] = c1[2 * i + 1] = &cA[i];
+    c2[2 * i] = &cB[i];
+    c2[2 * i + 1] = &cBwc[i];
+    pp[2 * i] = &pf[i];
+    pp[2 * i + 1] = &pfwc[i];
+    Xp[2 * i + 1] = &Bwc[i];
+    a[2 * i] = &(*alpha)[i];
+    a[2 * i + 1] = &(*mu)[i];
+    e[2 * i] = &(*err)[i];
+    e[2 * i + 1] = &(*errwc)[i];
   }
+  const std::vector<uint8_t> ok = verify_bob_core(sp, skA.pub, dlnA, c1, c2, pp, Xp);
+  alice_decrypt(skA, c2, ok, a, e);
 }
 
 }  // namespace mpcx::host::mta

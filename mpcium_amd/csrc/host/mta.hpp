@@ -101,11 +101,32 @@ void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& p
                  const DLNParams& dlnA, const DLNParams& dlnB, const std::vector<secp::Affine>* B,
                  const std::vector<RandFn>& rand, std::vector<BobMidResult>* out, std::vector<uint8_t>* err);
 
+// BobMid (b, rand) and BobMidWC (bwc, Bwc, randwc) on the same Alice message,
+// as tss-lib's signing round 2 runs both per peer (up:ecdsa/signing/round_2.go):
+// RangeProofAlice.Verify once for both (the same pure decision twice in Go),
+// both halves' exponentiations in shared launches; every output equals the two
+// separate calls'.
+void BobMidPairBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pkA,
+                     const std::vector<RangeProofAlice>& pf, const std::vector<Nat>& b, const std::vector<Nat>& bwc,
+                     const std::vector<Nat>& cA, const DLNParams& dlnA, const DLNParams& dlnB,
+                     const std::vector<secp::Affine>& Bwc, const std::vector<RandFn>& rand,
+                     const std::vector<RandFn>& randwc, std::vector<BobMidResult>* out,
+                     std::vector<BobMidResult>* outwc, std::vector<uint8_t>* err, std::vector<uint8_t>* errwc);
+
 // AliceEnd (B == nullptr) / AliceEndWC -> alpha = Decrypt(cB) mod q
 void AliceEndBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,
                    const std::vector<ProofBob>& pf, const DLNParams& dlnA, const std::vector<Nat>& cA,
                    const std::vector<Nat>& cB, const std::vector<secp::Affine>* B, std::vector<Nat>* alpha,
                    std::vector<uint8_t>* err);
+
+// AliceEnd (pf, cB -> alpha) and AliceEndWC (pfwc, cBwc, Bwc -> mu) of one
+// pair, as signing round 3 runs both per peer (up:ecdsa/signing/round_3.go):
+// one verification batch and one Decrypt batch for both halves.
+void AliceEndPairBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,
+                       const std::vector<ProofBob>& pf, const std::vector<ProofBob>& pfwc, const DLNParams& dlnA,
+                       const std::vector<Nat>& cA, const std::vector<Nat>& cB, const std::vector<Nat>& cBwc,
+                       const std::vector<secp::Affine>& Bwc, std::vector<Nat>* alpha, std::vector<Nat>* mu,
+                       std::vector<uint8_t>* err, std::vector<uint8_t>* errwc);
 
 // q = secp256k1 group order (ec.Params().N)
 const Nat& Q();

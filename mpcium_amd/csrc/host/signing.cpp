@@ -163,6 +163,10 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
   // MPCX_SIGN_STAGGER_MS: chain k starts k times this late (A/B runs)
   const char* se = std::getenv("MPCX_SIGN_STAGGER_MS");
   const double stagger_ms = se ? std::atof(se) : 0.0;
+  // MPCX_SIGN_PAIRED=0: BobMid / BobMidWC (AliceEnd / AliceEndWC) as two
+  // concurrent batches instead of one paired batch (A/B)
+  const char* pe = std::getenv("MPCX_SIGN_PAIRED");
+  const bool paired = !(pe && pe[0] == '0');
   auto run_chunk = [&](size_t lo, size_t hi) {
     const size_t n = hi - lo;
     const std::vector<mta::Bytes> cs(sess.begin() + (long)lo, sess.begin() + (long)hi);
@@ -233,6 +237,36 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
                          wc ? &L[pi].mu : &L[pi].alpha, &err);
       count_err(err);
     };
+    // BobMid + BobMidWC (and AliceEnd + AliceEndWC) of a pair as one paired
+    // batch: one RangeProofAlice verification, launches twice as large
+    auto bob_mid_pair = [&](size_t pi) {
+      const Pair& p = pairs[pi];
+      std::vector<uint8_t> err, errwc;
+      join_ec();
+      const std::vector<secp::Affine> Wj = slp(Wp[p.j]);
+      mta::BobMidPairBatch(cs, nodes[p.i].sk.pub, L[pi].pfA, sl(g[p.j]), sl(w[p.j]), L[pi].cA,
+                           public_dln(nodes[p.i].dln), nodes[p.j].dln, Wj, L[pi].rb, L[pi].rbwc, &L[pi].bob,
+                           &L[pi].bobwc, &err, &errwc);
+      count_err(err);
+      count_err(errwc);
+    };
+    auto alice_end_pair = [&](size_t pi) {
+      const Pair& p = pairs[pi];
+      std::vector<mta::ProofBob> pf(n), pfwc(n);
+      std::vector<Nat> cB(n), cBwc(n);
+      for (size_t x = 0; x < n; ++x) {
+        pf[x] = L[pi].bob[x].pf;
+        cB[x] = L[pi].bob[x].cB;
+        pfwc[x] = L[pi].bobwc[x].pf;
+        cBwc[x] = L[pi].bobwc[x].cB;
+      }
+      std::vector<uint8_t> err, errwc;
+      const std::vector<secp::Affine> Wj = slp(Wp[p.j]);
+      mta::AliceEndPairBatch(cs, nodes[p.i].sk, pf, pfwc, nodes[p.i].dln, L[pi].cA, cB, cBwc, Wj, &L[pi].alpha,
+                             &L[pi].mu, &err, &errwc);
+      count_err(err);
+      count_err(errwc);
+    };
     const size_t np = pairs.size();
     std::vector<double> st1(np), st2(np), st3(np);
     if (chains) {
@@ -248,9 +282,11 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
           const double a0 = now();
           alice_init(pi);
           const double a1 = now();
-          run_tasks({[&] { bob_mid(pi, false); }, [&] { bob_mid(pi, true); }});
+          if (paired) bob_mid_pair(pi);
+          else run_tasks({[&] { bob_mid(pi, false); }, [&] { bob_mid(pi, true); }});
           const double a2 = now();
-          run_tasks({[&] { alice_end(pi, false); }, [&] { alice_end(pi, true); }});
+          if (paired) alice_end_pair(pi);
+          else run_tasks({[&] { alice_end(pi, false); }, [&] { alice_end(pi, true); }});
           st1[pi] = a1 - a0;
           st2[pi] = a2 - a1;
           st3[pi] = now() - a2;
@@ -260,6 +296,11 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
       std::vector<std::function<void()>> t1, t2, t3;
       for (size_t pi = 0; pi < np; ++pi) {
         t1.push_back([&, pi] { alice_init(pi); });
+        if (paired) {
+          t2.push_back([&, pi] { bob_mid_pair(pi); });
+          t3.push_back([&, pi] { alice_end_pair(pi); });
+          continue;
+        }
         t2.push_back([&, pi] { bob_mid(pi, false); });
         t2.push_back([&, pi] { bob_mid(pi, true); });
         t3.push_back([&, pi] { alice_end(pi, false); });

@@ -41,6 +41,8 @@ SIGNATURES = [
                                      _vp, _vp]),
     ("mpcxh_mta_verify_bob_batch", _i, [_u32, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp]),
     ("mpcxh_mta_alice_end_batch", _i, [_u32, _vp, _u32, _vp, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("mpcxh_mta_bob_mid_pair_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _u32] + [_vp] * 17),
+    ("mpcxh_mta_alice_end_pair_batch", _i, [_u32, _vp, _u32, _vp, _vp, _u32] + [_vp] * 10),
     ("mpcxh_sha512_256i", _i, [_vp, _sz, _u32, _vp, _u32, _vp]),
     ("mpcxh_secp_scalar_base_mult", _i, [_vp, _u32, _vp]),
     ("mpcxh_secp_scalar_mult", _i, [_vp, _vp, _u32, _vp]),
@@ -226,6 +228,54 @@ def alice_end(sessions: Sequence[bytes], skA: Tuple[int, int, int, int], pfB: Se
                                            P.ctypes.data, CA.ctypes.data, CB.ctypes.data, _ptr(Bp), alpha.ctypes.data,
                                            err.ctypes.data))
     return words_to_ints(alpha), [int(e) for e in err]
+
+
+def bob_mid_pair(sessions: Sequence[bytes], pkA_N: int, pfA: Sequence[dict], b: Sequence[int], cA: Sequence[int],
+                 dlnA: Dict[str, int], dlnB: Dict[str, int], seeds: Sequence, bwc: Sequence[int],
+                 Bwc: Sequence[Tuple[int, int]], seeds_wc: Sequence):
+    """BobMid (b, seeds) and BobMidWC (bwc, Bwc, seeds_wc) on the same Alice
+    messages in one call -> ((beta, cB, betaPrm, ProofBob, err), (the WC half))."""
+    k = _Keep()
+    pk, da, db = _paillier(k, pkA_N), _dln(k, dlnA), _dln(k, dlnB)
+    n = len(b)
+    ss, sl = _sessions(sessions)
+    PA, Bw, Bwcw, CA = _proof_buf(pfA, RANGE_FIELDS, 6), _col(b), _col(bwc), _col(cA)
+    Bp = _points(Bwc)
+    S, Swc = _host.Readers(seeds), _host.Readers(seeds_wc)
+    outs = []
+    for _ in range(2):
+        outs.append([np.zeros((n, W), dtype="<u4") for _ in range(3)] + [np.zeros((n, 12 * W), dtype="<u4"),
+                                                                         np.zeros(n, dtype=np.uint8)])
+    (b1, c1, p1, f1, e1), (b2, c2, p2, f2, e2) = outs
+    _check(lib().mpcxh_mta_bob_mid_pair_batch(
+        W, ss.ctypes.data, sl, ctypes.byref(pk), ctypes.byref(da), ctypes.byref(db), n, PA.ctypes.data,
+        CA.ctypes.data, Bw.ctypes.data, S.ptr, Bwcw.ctypes.data, Bp.ctypes.data, Swc.ptr,
+        b1.ctypes.data, c1.ctypes.data, p1.ctypes.data, f1.ctypes.data, e1.ctypes.data,
+        b2.ctypes.data, c2.ctypes.data, p2.ctypes.data, f2.ctypes.data, e2.ctypes.data))
+    return tuple((words_to_ints(bb), words_to_ints(cc), words_to_ints(pp), _proofs(ff, BOB_FIELDS, n, wc),
+                  [int(x) for x in ee]) for (bb, cc, pp, ff, ee), wc in zip(outs, (False, True)))
+
+
+def alice_end_pair(sessions: Sequence[bytes], skA: Tuple[int, int, int, int], dlnA: Dict[str, int],
+                   cA: Sequence[int], pfB: Sequence[dict], cB: Sequence[int], pfB_wc: Sequence[dict],
+                   cB_wc: Sequence[int], Bwc: Sequence[Tuple[int, int]]):
+    """AliceEnd and AliceEndWC of the same sessions in one call ->
+    (alpha list, err list, mu list, err_wc list)."""
+    k = _Keep()
+    sk = _paillier(k, *skA)
+    dln = _dln(k, dlnA)
+    n = len(cA)
+    ss, sl = _sessions(sessions)
+    P1, P2 = _proof_buf(pfB, BOB_FIELDS, 12), _proof_buf(pfB_wc, BOB_FIELDS, 12)
+    CA, CB, CBw = _col(cA), _col(cB), _col(cB_wc)
+    Bp = _points(Bwc)
+    alpha, mu = np.zeros((n, W), dtype="<u4"), np.zeros((n, W), dtype="<u4")
+    e1, e2 = np.zeros(n, dtype=np.uint8), np.zeros(n, dtype=np.uint8)
+    _check(lib().mpcxh_mta_alice_end_pair_batch(
+        W, ss.ctypes.data, sl, ctypes.byref(sk), ctypes.byref(dln), n, CA.ctypes.data, P1.ctypes.data,
+        CB.ctypes.data, P2.ctypes.data, CBw.ctypes.data, Bp.ctypes.data, alpha.ctypes.data, e1.ctypes.data,
+        mu.ctypes.data, e2.ctypes.data))
+    return words_to_ints(alpha), [int(x) for x in e1], words_to_ints(mu), [int(x) for x in e2]
 
 
 # ---------------------------------------------------------------- test hooks

@@ -85,6 +85,41 @@ def test_golden_sessions_bit_exact(mta, nodes, vec, pair):
         assert alpha == [H(v["alpha_wc" if wc else "alpha"]) for v in vec], key
 
 
+@pytest.mark.parametrize("pair", [(0, 1), (2, 0)])
+def test_golden_sessions_paired_entries(mta, nodes, vec, pair):
+    """BobMid + BobMidWC and AliceEnd + AliceEndWC as one paired call each
+    (signing rounds 2 and 3): every field equals the golden sessions; a tampered
+    range proof fails both halves, a tampered ProofBobWC only its own half."""
+    vec = by_pair(vec)[pair]
+    A, B = nodes[pair[0]], nodes[pair[1]]
+    n = len(vec)
+    ss = [bytes.fromhex(v["session"]) for v in vec]
+    Bpts = [(H(v["Bx"]), H(v["By"])) for v in vec]
+    pfA = [hx(v["pfA"]) for v in vec]
+    bad = dict(pfA[0])
+    bad["S2"] += 1
+    pfA_in = [bad] + pfA[1:]
+    cA = [H(v["cA"]) for v in vec]
+    plain, wc = mta.bob_mid_pair(ss, A["N"], pfA_in, [H(v["b"]) for v in vec], cA, dln(A), dln(B, own=True),
+                                 [v["seed_b"] for v in vec], [H(v["wB"]) for v in vec], Bpts,
+                                 [v["seed_bwc"] for v in vec])
+    for (beta, cB, bp, pfB, err), key, is_wc in ((plain, "bob", False), (wc, "bob_wc", True)):
+        assert err == [mta.ERR_PROOF_VERIFY] + [0] * (n - 1), key
+        assert beta[1:] == [H(v[key]["beta"]) for v in vec[1:]], key
+        assert cB[1:] == [H(v[key]["cB"]) for v in vec[1:]], key
+        assert bp[1:] == [H(v[key]["betaPrm"]) for v in vec[1:]], key
+        assert pfB[1:] == [bob_pf(v[key]["pf"], is_wc) for v in vec[1:]], key
+    sk = (A["N"], A["LambdaN"], A["P"], A["Q"])
+    pf1 = [bob_pf(v["bob"]["pf"], False) for v in vec]
+    pf2 = [bob_pf(v["bob_wc"]["pf"], True) for v in vec]
+    pf2[-1] = dict(pf2[-1], T2=pf2[-1]["T2"] + 1)
+    alpha, e1, mu, e2 = mta.alice_end_pair(ss, sk, dln(A, own=True), cA, pf1, [H(v["bob"]["cB"]) for v in vec], pf2,
+                                           [H(v["bob_wc"]["cB"]) for v in vec], Bpts)
+    assert e1 == [0] * n and e2 == [0] * (n - 1) + [mta.ERR_PROOF_VERIFY]
+    assert alpha == [H(v["alpha"]) for v in vec]
+    assert mu[:-1] == [H(v["alpha_wc"]) for v in vec[:-1]]
+
+
 def test_range_proof_rejections(mta, nodes, vec):
     A, B = nodes[0], nodes[1]
     v = vec[0]
