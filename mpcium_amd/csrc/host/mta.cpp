@@ -3,8 +3,11 @@
 #include "mta.hpp"
 
 #include <algorithm>
+#include <exception>
+#include <functional>
 #include <map>
 #include <stdexcept>
+#include <thread>
 
 #include "engine.hpp"
 #include "expset.hpp"
@@ -431,6 +434,26 @@ void AliceInitBatch(const paillier::PublicKey& pkA, const std::vector<Nat>& a, c
 }
 
 namespace {
+// f and g on two threads; rethrows the first failure
+void both(const std::function<void()>& f, const std::function<void()>& g) {
+  std::exception_ptr ef, eg;
+  std::thread t([&] {
+    try {
+      g();
+    } catch (...) {
+      eg = std::current_exception();
+    }
+  });
+  try {
+    f();
+  } catch (...) {
+    ef = std::current_exception();
+  }
+  t.join();
+  if (ef) std::rethrow_exception(ef);
+  if (eg) std::rethrow_exception(eg);
+}
+
 // One BobMid[WC] half of a session whose RangeProofAlice verified: its b, its
 // point B (nullptr: plain BobMid), its reader and its result slots.
 struct BobHalf {
@@ -548,17 +571,19 @@ void BobMidPairBatch(const std::vector<Bytes>& session, const paillier::PublicKe
   // Both halves verify the same (cA, pf) under the same key: one verification
   // decides both (Verify is a pure function of its inputs)
   const std::vector<uint8_t> ok = VerifyRangeAliceBatch(pkA, dlnB, cA, pf);
-  std::vector<BobHalf> h;
-  h.reserve(2 * n);
+  std::vector<BobHalf> h, hwc;
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) {
       (*err)[i] = (*errwc)[i] = ErrProofVerify;
       continue;
     }
     h.push_back({i, &b[i], nullptr, &rand[i], &(*out)[i], &(*err)[i]});
-    h.push_back({i, &bwc[i], &Bwc[i], &randwc[i], &(*outwc)[i], &(*errwc)[i]});
+    hwc.push_back({i, &bwc[i], &Bwc[i], &randwc[i], &(*outwc)[i], &(*errwc)[i]});
   }
-  bob_mid_halves(session, pkA, dlnA, cA, h);
+  // the two halves as concurrent tasks: one half's host phases (draws, hashing,
+  // gcd batches) overlap the other's launches (measured faster on MI355X than
+  // one merged batch of both halves, whose host and GPU phases alternate)
+  both([&] { bob_mid_halves(session, pkA, dlnA, cA, h); }, [&] { bob_mid_halves(session, pkA, dlnA, cA, hwc); });
 }
 
 namespace {
@@ -617,29 +642,29 @@ void AliceEndPairBatch(const std::vector<Bytes>& session, const paillier::Privat
   mu->assign(n, Nat());
   err->assign(n, OK);
   errwc->assign(n, OK);
-  // session i's ProofBob at 2i, its ProofBobWC at 2i+1: one verification batch
-  // and one Decrypt batch for both halves
-  std::vector<const Bytes*> sp(2 * n);
-  std::vector<const Nat*> c1(2 * n), c2(2 * n);
-  std::vector<const ProofBob*> pp(2 * n);
-  std::vector<const secp::Affine*> Xp(2 * n, nullptr);
-  std::vector<Nat*> a(2 * n);
-  std::vector<uint8_t*> e(2 * n);
-  for (size_t i = 0; i < n; ++i) {
-    sp[2 * i] = sp[2 * i + 1] = &session[i];
-    c1[2 * i] = c1[2 * i + 1] = &cA[i];
-    c2[2 * i] = &cB[i];
-    c2[2 * i + 1] = &cBwc[i];
-    pp[2 * i] = &pf[i];
-    pp[2 * i + 1] = &pfwc[i];
-    Xp[2 * i + 1] = &Bwc[i];
-    a[2 * i] = &(*alpha)[i];
-    a[2 * i + 1] = &(*mu)[i];
-    e[2 * i] = &(*err)[i];
-    e[2 * i + 1] = &(*errwc)[i];
-  }
-  const std::vector<uint8_t> ok = verify_bob_core(sp, skA.pub, dlnA, c1, c2, pp, Xp);
-  alice_decrypt(skA, c2, ok, a, e);
+  // each half verified and decrypted as its own batch, the two halves as
+  // concurrent tasks (host phases of one overlap the other's launches)
+  auto half = [&](const std::vector<ProofBob>& p, const std::vector<Nat>& c, const secp::Affine* X0,
+                  std::vector<Nat>* res, std::vector<uint8_t>* er) {
+    std::vector<const Bytes*> sp(n);
+    std::vector<const Nat*> c1(n), c2(n);
+    std::vector<const ProofBob*> pp(n);
+    std::vector<const secp::Affine*> Xp(n, nullptr);
+    std::vector<Nat*> a(n);
+    std::vector<uint8_t*> e(n);
+    for (size_t i = 0; i < n; ++i) {
+      sp[i] = &session[i];
+      c1[i] = &cA[i];
+      c2[i] = &c[i];
+      pp[i] = &p[i];
+      if (X0) Xp[i] = X0 + i;
+      a[i] = &(*res)[i];
+      e[i] = &(*er)[i];
+    }
+    const std::vector<uint8_t> ok = verify_bob_core(sp, skA.pub, dlnA, c1, c2, pp, Xp);
+    alice_decrypt(skA, c2, ok, a, e);
+  };
+  both([&] { half(pf, cB, nullptr, alpha, err); }, [&] { half(pfwc, cBwc, Bwc.data(), mu, errwc); });
 }
 
 }  // namespace mpcx::host::mta

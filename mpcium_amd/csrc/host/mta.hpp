@@ -104,7 +104,7 @@ void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& p
 // BobMid (b, rand) and BobMidWC (bwc, Bwc, randwc) on the same Alice message,
 // as tss-lib's signing round 2 runs both per peer (up:ecdsa/signing/round_2.go):
 // RangeProofAlice.Verify once for both (the same pure decision twice in Go),
-// both halves' exponentiations in shared launches; every output equals the two
+// then the two halves as concurrent tasks; every output equals the two
 // separate calls'.
 void BobMidPairBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pkA,
                      const std::vector<RangeProofAlice>& pf, const std::vector<Nat>& b, const std::vector<Nat>& bwc,
@@ -121,7 +121,7 @@ void AliceEndBatch(const std::vector<Bytes>& session, const paillier::PrivateKey
 
 // AliceEnd (pf, cB -> alpha) and AliceEndWC (pfwc, cBwc, Bwc -> mu) of one
 // pair, as signing round 3 runs both per peer (up:ecdsa/signing/round_3.go):
-// one verification batch and one Decrypt batch for both halves.
+// the two halves as concurrent tasks.
 void AliceEndPairBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,
                        const std::vector<ProofBob>& pf, const std::vector<ProofBob>& pfwc, const DLNParams& dlnA,
                        const std::vector<Nat>& cA, const std::vector<Nat>& cB, const std::vector<Nat>& cBwc,
