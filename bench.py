@@ -496,7 +496,10 @@ def keygen_line(args):
         pp, _ = mhost.generate_preparams(seed=seed)
         parties.append(pp)
     parties = parties[:args.parties]
-    warm = mproofs.bench_keygen_proofs(parties, 4, seed=0x6B66)
+    # warm-up at the timed size: the node-lifetime fixed-base comb tables (h1, h2
+    # of every party's N~ and their inverses) are built on first use, as a node
+    # builds them once for its peers' preparams, not per session
+    warm = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B66)
     if warm["failures"]:
         raise SystemExit(f"keygen proofs warmup: {warm}")
     st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67)

@@ -4,7 +4,12 @@
 #pragma once
 
 #include <algorithm>
+#include <cstdlib>
+#include <exception>
+#include <functional>
+#include <initializer_list>
 #include <map>
+#include <thread>
 #include <vector>
 
 #include "bignum.hpp"
@@ -12,6 +17,40 @@
 #include "hostprof.hpp"
 
 namespace mpcx::host {
+
+// Runs every closure concurrently (the last one on the calling thread) and
+// rethrows the first failure once all have finished. libmpcx runs calls from
+// different threads on different execution lanes (streams), so independent
+// launches of one protocol step overlap on the GPU instead of queueing.
+inline void run_concurrently(const std::vector<std::function<void()>>& fs) {
+  if (fs.empty()) return;
+  static const bool serial = [] {  // MPCX_EXPSET_SERIAL=1: one launch after another (A/B runs)
+    const char* e = std::getenv("MPCX_EXPSET_SERIAL");
+    return e && e[0] == '1';
+  }();
+  if (serial) {
+    for (const auto& f : fs) f();
+    return;
+  }
+  std::vector<std::exception_ptr> errs(fs.size());
+  std::vector<std::thread> th;
+  for (size_t i = 0; i + 1 < fs.size(); ++i)
+    th.emplace_back([&, i] {
+      try {
+        fs[i]();
+      } catch (...) {
+        errs[i] = std::current_exception();
+      }
+    });
+  try {
+    fs.back()();
+  } catch (...) {
+    errs.back() = std::current_exception();
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : errs)
+    if (e) std::rethrow_exception(e);
+}
 
 // ------------------------------------------------------------------ ExpSet
 // Modexp requests against one modulus, issued as few GPU launches: large
@@ -26,7 +65,16 @@ class ExpSet {
     reqs_.push_back({&base, &e, mul, out});
   }
   size_t size() const { return reqs_.size(); }
+  // Every launch of the pending requests, concurrently; the set is empty after.
   void run() {
+    std::vector<std::function<void()>> fs;
+    collect(fs);
+    run_concurrently(fs);
+    clear();
+  }
+  // Appends one closure per launch of the pending requests (run them, e.g. with
+  // run_concurrently together with other sets' launches, then clear()).
+  void collect(std::vector<std::function<void()>>& fs) {
     if (reqs_.empty()) return;
     // A base recurring across many requests (h1, h2 of N~ in every session's
     // range proof) goes to the fixed-base comb path: no squarings, one
@@ -39,11 +87,11 @@ class ExpSet {
         if (reqs_[i].e->bit_len() <= Engine::kFixedMaxBits) by_b[reqs_[i].b].push_back(i);
       for (auto& kv : by_b) {
         if (kv.second.size() < kFixedMin) continue;
-        auto& idx = kv.second;
+        auto idx = kv.second;
         std::stable_sort(idx.begin(), idx.end(),
                          [&](size_t a, size_t b) { return reqs_[a].e->bit_len() < reqs_[b].e->bit_len(); });
-        launch_fixed(idx);
         for (size_t i : idx) done[i] = 1;
+        fs.push_back([this, idx] { launch_fixed(idx); });
       }
     }
     std::map<const Nat*, std::vector<size_t>> by_e;
@@ -54,7 +102,8 @@ class ExpSet {
       // a shared-exponent launch only for a large group (y = N, y = lambda);
       // a session's own e used by two requests stays in the per-operand groups
       if (kv.second.size() >= 64 || kv.second.size() == reqs_.size()) {
-        launch(kv.second, true);
+        auto idx = kv.second;
+        fs.push_back([this, idx] { launch(idx, true); });
       } else {
         rest.insert(rest.end(), kv.second.begin(), kv.second.end());
       }
@@ -66,11 +115,12 @@ class ExpSet {
       const uint32_t lo = reqs_[rest[g0]].e->bit_len();
       size_t g1 = g0 + 1;
       while (g1 < rest.size() && reqs_[rest[g1]].e->bit_len() <= lo + lo / 8 + 32) ++g1;
-      launch(std::vector<size_t>(rest.begin() + (long)g0, rest.begin() + (long)g1), false);
+      std::vector<size_t> idx(rest.begin() + (long)g0, rest.begin() + (long)g1);
+      fs.push_back([this, idx] { launch(idx, false); });
       g0 = g1;
     }
-    reqs_.clear();
   }
+  void clear() { reqs_.clear(); }
 
  private:
   struct Req {
@@ -111,5 +161,13 @@ class ExpSet {
   const Nat m_;  // by value: callers pass temporaries (pk.NSquare())
   std::vector<Req> reqs_;
 };
+
+// Every launch of several sets (one protocol step's moduli: N^2, N~, N) at once.
+inline void run_all(std::initializer_list<ExpSet*> sets) {
+  std::vector<std::function<void()>> fs;
+  for (ExpSet* s : sets) s->collect(fs);
+  run_concurrently(fs);
+  for (ExpSet* s : sets) s->clear();
+}
 
 }  // namespace mpcx::host

@@ -71,16 +71,17 @@ void range_draw(std::vector<RangeProveState>& st, const paillier::PublicKey& pk,
 const Nat& Q() { return secp::CurveN(); }
 
 // ================================================================ RangeProofAlice
-void ProveRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln, const std::vector<Nat>& c,
-                          const std::vector<Nat>& m, const std::vector<Nat>& r, const std::vector<RandFn>& rand,
-                          std::vector<RangeProofAlice>* out) {
-  const size_t n = c.size();
-  if (m.size() != n || r.size() != n || rand.size() != n) throw std::invalid_argument("ProveRangeAlice: sizes");
-  const Nat N2 = pk.NSquare();
-  std::vector<RangeProveState> st(n);
+namespace {
+// Steps 5-11 of ProveRangeAlice for drawn states st (range_draw), c[i] the
+// ciphertext session i proves. eN2 may already hold the caller's own requests
+// (AliceInit's Encrypt): they run in the proof's first launches, and c[i] is
+// read only after them (the challenge hashes it).
+void range_prove_core(const paillier::PublicKey& pk, const DLNParams& dln, const std::vector<const Nat*>& c,
+                      const std::vector<Nat>& m, const std::vector<Nat>& r, std::vector<RangeProveState>& st,
+                      ExpSet& eN2, std::vector<RangeProofAlice>* out) {
+  const size_t n = st.size();
   out->assign(n, RangeProofAlice{});
-  range_draw(st, pk, dln, rand);
-  ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
+  ExpSet eNt(dln.NTilde), eN(pk.N);
   for (size_t i = 0; i < n; ++i) {
     auto& s = st[i];
     auto& o = (*out)[i];
@@ -88,8 +89,7 @@ void ProveRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln, c
     eNt.add(dln.h1, m[i], &s.t1);               // 5. h1^m
     eNt.add(dln.h1, s.alpha, &s.t2);            // 7. h1^alpha
   }
-  eN2.run();
-  eNt.run();
+  run_all({&eN2, &eNt});
   for (size_t i = 0; i < n; ++i) {
     eNt.add(dln.h2, st[i].rho, &(*out)[i].Z, &st[i].t1);    // 5. z = h1^m h2^rho mod N~
     eNt.add(dln.h2, st[i].gamma, &(*out)[i].W, &st[i].t2);  // 7. w = h1^alpha h2^gamma mod N~
@@ -98,7 +98,7 @@ void ProveRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln, c
   const Nat gamma = pk.Gamma();
   parallel_for(n, [&](size_t i) {  // 8-9. e = RejectionSample(q, SHA512_256i(N, Gamma, c, z, u, w))
     auto& o = (*out)[i];
-    st[i].e = RejectionSample(Q(), SHA512_256i({&pk.N, &gamma, &c[i], &o.Z, &o.U, &o.W}));
+    st[i].e = RejectionSample(Q(), SHA512_256i({&pk.N, &gamma, c[i], &o.Z, &o.U, &o.W}));
   });
   for (size_t i = 0; i < n; ++i) eN.add(r[i], st[i].e, &(*out)[i].S, &st[i].beta);  // s = r^e beta mod N
   eN.run();
@@ -107,6 +107,20 @@ void ProveRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln, c
     o.S1 = st[i].e * m[i] + st[i].alpha;    // s1 = e m + alpha
     o.S2 = st[i].e * st[i].rho + st[i].gamma;  // s2 = e rho + gamma
   });
+}
+}  // namespace
+
+void ProveRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln, const std::vector<Nat>& c,
+                          const std::vector<Nat>& m, const std::vector<Nat>& r, const std::vector<RandFn>& rand,
+                          std::vector<RangeProofAlice>* out) {
+  const size_t n = c.size();
+  if (m.size() != n || r.size() != n || rand.size() != n) throw std::invalid_argument("ProveRangeAlice: sizes");
+  std::vector<RangeProveState> st(n);
+  range_draw(st, pk, dln, rand);
+  std::vector<const Nat*> cp(n);
+  for (size_t i = 0; i < n; ++i) cp[i] = &c[i];
+  ExpSet eN2(pk.NSquare());
+  range_prove_core(pk, dln, cp, m, r, st, eN2, out);
 }
 
 std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln,
@@ -159,8 +173,7 @@ std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const 
     eNt.add(dln.h1, p.S1, &t[i]);           // h1^s1
     eNt.add(p.Z, e[i], &L2[i], &p.W);       // w z^e
   }
-  eN2.run();
-  eNt.run();
+  run_all({&eN2, &eNt});
   for (size_t i = 0; i < n; ++i)
     if (ok[i]) eNt.add(dln.h2, pf[i].S2, &R2[i], &t[i]);  // h1^s1 h2^s2
   eNt.run();
@@ -267,11 +280,9 @@ void ProveBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey&
   }
   ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
   for (size_t i = 0; i < n; ++i) bob_stage_a(st[i], pk, dln, x[i], y[i], eN2, eNt, &gg[i]);
-  eN2.run();
-  eNt.run();
+  run_all({&eN2, &eNt});
   for (size_t i = 0; i < n; ++i) bob_stage_b(st[i], dln, c1[i], eN2, eNt, (*out)[i]);
-  eN2.run();
-  eNt.run();
+  run_all({&eN2, &eNt});
   parallel_for(n, [&](size_t i) {
     (*out)[i].U = st[i].u;
     st[i].e = bob_challenge(session[i], pk, gamma, X ? &(*X)[i] : nullptr, c1[i], c2[i], (*out)[i]);
@@ -351,16 +362,14 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
     eN2.add(p.S, pk.N, &q1[i], &gt1[i]);    // 7. s^N Gamma^t1
     eN2.add(*c2[i], e[i], &r3[i], &p.V);    // 7. c2^e v
   }
-  eN2.run();
-  eNt.run();
+  run_all({&eN2, &eNt});
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
     eNt.add(dln.h2, pfp[i]->S2, &l1[i], &p1[i]);  // 5. h1^s1 h2^s2
     eNt.add(dln.h2, pfp[i]->T2, &l2[i], &p2[i]);  // 6. h1^t1 h2^t2
     eN2.add(*c1[i], pfp[i]->S1, &l3[i], &q1[i]);  // 7. c1^s1 s^N Gamma^t1
   }
-  eN2.run();
-  eNt.run();
+  run_all({&eN2, &eNt});
   for (size_t i = 0; i < n; ++i) ok[i] = ok[i] && l1[i] == r1[i] && l2[i] == r2[i] && l3[i] == r3[i];
   return ok;
 }
@@ -413,19 +422,25 @@ void AliceInitBatch(const paillier::PublicKey& pkA, const std::vector<Nat>& a, c
     for (size_t j = 0; j < k; ++j) {
       rdr[j] = &rand[idx[j]];
       rp[j] = &r[j];
+      m[j] = a[idx[j]];
+      rd[j] = rand[idx[j]];
     }
     GetRandomPositiveRelativelyPrimeIntBatch(rdr, pkA.N, rp);
   }
-  parallel_for(k, [&](size_t j) { ga[j] = gamma_pow(a[idx[j]], pkA.N); });
+  // every reader's ProveRangeAlice draws follow its Encrypt draw, so all are
+  // taken before the first launch: c = Gamma^a r^N then runs in the proof's
+  // first launches (same modulus and exponent as its u = Gamma^alpha beta^N)
+  std::vector<RangeProveState> st(k);
+  range_draw(st, pkA, dlnB, rd);
+  parallel_for(k, [&](size_t j) { ga[j] = gamma_pow(m[j], pkA.N); });
   ExpSet eN2(pkA.NSquare());
+  std::vector<const Nat*> cp(k);
   for (size_t j = 0; j < k; ++j) {
     eN2.add(r[j], pkA.N, &c[j], &ga[j]);  // c = Gamma^a r^N mod N^2
-    m[j] = a[idx[j]];
-    rd[j] = rand[idx[j]];
+    cp[j] = &c[j];
   }
-  eN2.run();
   std::vector<RangeProofAlice> p;
-  ProveRangeAliceBatch(pkA, dlnB, c, m, r, rd, &p);
+  range_prove_core(pkA, dlnB, cp, m, r, st, eN2, &p);
   pf->assign(n, RangeProofAlice{});
   for (size_t j = 0; j < k; ++j) {
     (*cA)[idx[j]] = c[j];
@@ -507,16 +522,14 @@ void bob_mid_halves(const std::vector<Bytes>& session, const paillier::PublicKey
     eN2.add(cRand[j], pkA.N, &cbp[j], &gbp[j]);  // cBetaPrm = Gamma^betaPrm r^N
     bob_stage_a(st[j], pkA, dlnA, *h[j].b, h[j].out->betaPrm, eN2, eNt, &gg[j]);
   }
-  eN2.run();
-  eNt.run();
+  run_all({&eN2, &eNt});
   for (size_t j = 0; j < k; ++j) {
     if (!live[j]) continue;
     const Nat& c = cA[h[j].i];
     eN2.add(c, *h[j].b, &h[j].out->cB, &cbp[j]);  // cB = HomoAdd(HomoMult(b, cA), cBetaPrm)
     bob_stage_b(st[j], dlnA, c, eN2, eNt, h[j].out->pf);
   }
-  eN2.run();
-  eNt.run();
+  run_all({&eN2, &eNt});
   parallel_for(k, [&](size_t j) {
     if (!live[j]) return;
     auto& o = *h[j].out;

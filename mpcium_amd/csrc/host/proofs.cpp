@@ -146,8 +146,7 @@ std::vector<ModProof> ModProveBatch(const std::vector<Bytes>& session, const Nat
         eQ_.add(Y[i][k], eQ, &yQ[i][k]);
       }
     }
-    eP_.run();
-    eQ_.run();
+    run_all({&eP_, &eQ_});
   }
   const int lmP = P.bit(1) ? -1 : 1, lmQ = Q.bit(1) ? -1 : 1;  // (-1 | p) = (-1)^((p-1)/2)
   std::vector<std::vector<Nat>> Yp(n, std::vector<Nat>(kModIterations));
@@ -193,8 +192,7 @@ std::vector<ModProof> ModProveBatch(const std::vector<Bytes>& session, const Nat
         sP.add(Y[i][k], zP, &rP[i][2 * k + 1]);
         sQ.add(Y[i][k], zQ, &rQ[i][2 * k + 1]);
       }
-    sP.run();
-    sQ.run();
+    run_all({&sP, &sQ});
   }
   Nat qinv;
   if (!mod_inverse(Int(Q % P), P, &qinv)) throw std::invalid_argument("ModProof: P, Q not coprime");

@@ -93,6 +93,8 @@ std::mutex g_mu;  // options, device binding, shutdown
 bool g_split = false;                    // narrow-geometry tail launch (measured slower: off)
 int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): one geometry for everything
 double g_narrow_rounds = 0.15;           // mpcx_set_option("narrow_rounds", 100x): narrow-geometry threshold
+double g_mid_rounds = 0.0;               // mpcx_set_option("mid_rounds", 100x): mid-geometry threshold
+int g_geom_policy = 1;                   // 1: 4096-bit class by the launch-time model; 0: thresholds only
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
@@ -565,6 +567,15 @@ int mpcx_set_option(const char* key, int value) {
     // batches below value/100 of a resident round run in the narrow geometry
     if (value < 0 || value > 100) return fail(MPCX_EINVAL, "narrow_rounds %d out of range", value);
     g_narrow_rounds = value / 100.0;
+  } else if (std::strcmp(key, "mid_rounds") == 0) {
+    // batches from narrow_rounds up to value/100 of a main-geometry round run in
+    // the class's mid geometry (twice the wavefronts per operand count)
+    if (value < 0 || value > 400) return fail(MPCX_EINVAL, "mid_rounds %d out of range", value);
+    g_mid_rounds = value / 100.0;
+  } else if (std::strcmp(key, "geom_policy") == 0) {
+    // 1: the 4096-bit class picks main / mid / narrow by the launch-time model; 0: thresholds
+    if (value < 0 || value > 1) return fail(MPCX_EINVAL, "geom_policy %d out of range", value);
+    g_geom_policy = value;
   } else if (std::strcmp(key, "main_geom") == 0) {
     // main (throughput) geometry of the geometry's class
     if (value < 0 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "main_geom %d out of range", value);
@@ -593,15 +604,25 @@ int mpcx_device_count(int* out_count) {
   return MPCX_OK;
 }
 
-int mpcx_init(int device) {
-  std::lock_guard<std::mutex> lk(g_mu);
+// launch-policy overrides from the environment (A/B runs of whole drivers)
+static void read_env_options() {
   const char* sp = std::getenv("MPCX_SPLIT");
   if (sp) g_split = sp[0] != '0';
+  const char* mr = std::getenv("MPCX_MID_ROUNDS");  // percent of a main round
+  if (mr) g_mid_rounds = std::max(0, std::min(400, std::atoi(mr))) / 100.0;
+  const char* gp = std::getenv("MPCX_GEOM_POLICY");
+  if (gp) g_geom_policy = gp[0] == '0' ? 0 : 1;
+}
+
+int mpcx_init(int device) {
+  std::lock_guard<std::mutex> lk(g_mu);
+  read_env_options();
   return bind_new_device(device);
 }
 
 int mpcx_init_devices(int n_gpus) {
   std::lock_guard<std::mutex> lk(g_mu);
+  read_env_options();
   int vis = 0;
   hipError_t e = hipGetDeviceCount(&vis);
   if (e != hipSuccess || vis <= 0) return fail(MPCX_ENODEV, "no HIP device visible");
@@ -728,6 +749,38 @@ int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K,
 
 // Enqueue one batch on lane `lane` of device `di` (lane locked by the caller;
 // its stream is lane.st).
+//
+// Launch-time model of the 4096-bit class's geometries, measured on MI355X
+// (tools/geom_sweep.py, profiles/r02/geom_sweep/): a launch of W wavefronts
+// takes about c0 + s * k with k = ceil(W / SIMDs) wavefronts per SIMD, in units
+// of the main geometry's time per wavefront-per-SIMD step. Per operand the main
+// geometry does the least work, but its 16 operands per wavefront leave most
+// SIMDs idle or one wave short on batches of a fraction of a round; the mid
+// geometry (8 operands per wavefront, 3 resident per SIMD) and the narrow one (2
+// per wavefront) trade per-operand work for a finer split. x^N mod N^2 for
+// 1.25K / 5K / 10K / 20K / 30K / 40K operands: main 49 / 49 / 50 / 91 / 93 / 135 ms,
+// mid 32 / 32 / 55 / 83 / 107 / 134 ms, narrow 20 / 41 / 65 / 119 / 175 / 230 ms.
+static int fastest_geom(int cls, uint32_t count, int nsimd) {
+  struct M {
+    int g;
+    double c0, s;
+  };
+  const M ms[3] = {{MPCX_MAIN_GEOM(cls), 0.10, 1.0}, {MPCX_MID_GEOM(cls), 0.12, 0.585},
+                   {MPCX_NARROW_GEOM(cls), 0.20, 0.245}};
+  int best = ms[0].g;
+  double tb = 1e300;
+  for (const M& m : ms) {
+    const uint32_t G = (uint32_t)MPCX_GEOM_G(m.g);
+    const double waves = (double)((count + G - 1) / G);
+    const double t = m.c0 + m.s * std::ceil(waves / (double)std::max(1, nsimd));
+    if (t < tb) {
+      tb = t;
+      best = m.g;
+    }
+  }
+  return best;
+}
+
 static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases,
                           uint32_t base_words, const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
                           uint32_t exp_bits, const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out,
@@ -764,8 +817,13 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     // at ~45% of SIMD peak, so tiny batches (< 0.15 of a round) finish sooner
     // spread over the narrow geometry's 3x more wavefronts; from ~0.3 rounds up
     // the main geometry wins, and a narrow tail launch did not pay.
-    if (gn >= 0 && rounds < g_narrow_rounds) {
+    const int gmid = MPCX_MID_GEOM(mod->cls);
+    if (g_geom_policy == 1 && gmid >= 0 && gn >= 0) {
+      parts[nparts++] = {fastest_geom(mod->cls, count, dev.num_cus * 4), 0, count};
+    } else if (gn >= 0 && rounds < g_narrow_rounds) {
       parts[nparts++] = {gn, 0, count};
+    } else if (gmid >= 0 && rounds < g_mid_rounds) {
+      parts[nparts++] = {gmid, 0, count};
     } else if (!g_split || gn < 0 || rounds < 1.0 || frac == 0.0 || frac > 0.75) {
       parts[nparts++] = {gm, 0, count};
     } else {

@@ -90,7 +90,8 @@ __device__ __forceinline__ uint32_t from_prev_lane(uint32_t v) {
 }
 
 // Broadcast lane 0 of each P-lane operand group to the whole group. Quads
-// (P = 4) and pairs (P = 2) use a DPP quad_perm, 16-lane groups (one DPP row)
+// (P = 4) and pairs (P = 2) use a DPP quad_perm, 8-lane groups a quad_perm plus
+// row_shr:4 into the upper quad, 16-lane groups (one DPP row)
 // DPP row_newbcast, 32-lane groups row_newbcast + row_bcast:15 -- a VALU move with a few cycles of latency on the
 // per-iteration serial path; other group widths go through the LDS crossbar
 // (ds_bpermute, ~100+ cycles of latency).
@@ -100,6 +101,11 @@ __device__ __forceinline__ uint32_t group_bcast(uint32_t v, int src_addr) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);  // quad_perm [0,0,0,0]
   } else if constexpr (P == 2) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xA0, 0xF, 0xF, false);  // quad_perm [0,0,2,2]
+  } else if constexpr (P == 8) {
+    // each quad takes its lane 0, then the upper quad of every 8-lane group
+    // (DPP banks 1 and 3) takes the lower quad's value by row_shr:4
+    const int t = __builtin_amdgcn_mov_dpp((int)v, 0x00, 0xF, 0xF, false);
+    return (uint32_t)__builtin_amdgcn_update_dpp(t, t, 0x114, 0xF, 0xA, false);
   } else if constexpr (P == 16) {
     return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0x150, 0xF, 0xF, false);  // row_newbcast:0
   } else if constexpr (P == 32) {

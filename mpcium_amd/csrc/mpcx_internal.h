@@ -12,7 +12,8 @@
 // for the class's largest modulus, and its own Montgomery constants (R mod m,
 // R^2 mod m depend on L), uploaded at registration.
 #define MPCX_NUM_CLASSES 3
-// class L_min: the smallest digit count of the class's geometries
+// class L_min: sets the class's operand width (every geometry of the class has
+// L >= L_min digits; 147 is the round-1 7 x 21 geometry's, kept as the width)
 #define MPCX_CLASS_LMIN(c) ((c) == 0 ? 37 : (c) == 1 ? 75 : 147)
 // operand width in 32-bit words (bases and moduli)
 #define MPCX_CLASS_WORDS(c) ((28 * MPCX_CLASS_LMIN(c)) / 32)
@@ -26,16 +27,18 @@
 //                           m_i broadcast by DPP row_newbcast
 //   4: 32 x 5,  2, class 2  narrow; two DPP rows per operand, m_i by row_newbcast + row_bcast:15
 //   5: 3 x 25, 21, class 1  7-lane/3-lane groups, m_i by ds_bpermute (round-1 main)
-//   6: 7 x 21,  9, class 2  (round-1 main)
+//   6: 8 x 19,  8, class 2  mid: batches of a fraction of a main round (twice the main
+//                           geometry's wavefronts, 3 per SIMD); m_i by quad_perm + row_shr:4
 #define MPCX_NUM_GEOMS 7
-#define MPCX_GEOM_P(g) ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 16 : (g) == 4 ? 32 : (g) == 5 ? 3 : 7)
-#define MPCX_GEOM_K(g) ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 5 : (g) == 5 ? 25 : 21)
-#define MPCX_GEOM_G(g) ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 2 : (g) == 5 ? 21 : 9)
+#define MPCX_GEOM_P(g) ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 16 : (g) == 4 ? 32 : (g) == 5 ? 3 : 8)
+#define MPCX_GEOM_K(g) ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 5 : (g) == 5 ? 25 : 19)
+#define MPCX_GEOM_G(g) ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 2 : (g) == 5 ? 21 : 8)
 #define MPCX_GEOM_CLASS(g) ((g) == 0 ? 0 : ((g) == 1 || (g) == 3 || (g) == 5) ? 1 : 2)
 #define MPCX_GEOM_L(g) (MPCX_GEOM_P(g) * MPCX_GEOM_K(g))
 // default main (throughput) and narrow geometry of each class
 #define MPCX_MAIN_GEOM(c) ((c) == 0 ? 0 : (c) == 1 ? 1 : 2)
 #define MPCX_NARROW_GEOM(c) ((c) == 1 ? 3 : (c) == 2 ? 4 : -1)
+#define MPCX_MID_GEOM(c) ((c) == 2 ? 6 : -1)
 // 1024-bit class used by the Fermat / Miller-Rabin kernels (thread per operand)
 #define MPCX_C0_K 37
 
