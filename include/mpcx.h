@@ -205,8 +205,9 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
  * (go:src/math/big/prime.go probablyPrimeLucas, the "extra strong" test):
  * ok[i] = n_i passes with parameters P[i], Q = 1 (Baillie-OEIS method C: the
  * caller supplies the smallest P >= 3 with Jacobi(P^2 - 4, n_i) = -1 and
- * handles the Jacobi = 0 / perfect-square exits). 5 <= n_i < 2^1024 odd,
- * 3 <= P[i] < 2^14. Each candidate is its own modulus. */
+ * handles the Jacobi = 0 / perfect-square exits). 5 <= n_i < 2^2048 odd
+ * (n_words <= 64; a batch with a candidate above 1024 bits runs in the wide
+ * 16 x 5-digit geometry), 3 <= P[i] < 2^14. Each candidate is its own modulus. */
 int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* P, uint8_t* ok);
 
 /* One pipelined step of the safe-prime search (up:common/safe_prime.go

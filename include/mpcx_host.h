@@ -302,6 +302,12 @@ int mpcxh_candidate_from_bytes(const uint8_t* bytes, size_t n, int q_bit_len, ui
 /* n bytes of the CounterDRBG stream for `seed` (test hook). */
 int mpcxh_drbg_read(uint64_t seed, uint8_t* out, size_t n);
 
+/* Go math/rand (test hooks): count Int63() values of rand.New(rand.NewSource(seed)),
+ * and the `reps` Miller-Rabin bases big.Int.ProbablyPrime(reps) draws for the odd
+ * n (w words, n > 3), in Go's order, w words each (go:src/math/big/prime.go). */
+int mpcxh_go_rand_int63(int64_t seed, uint32_t count, int64_t* out);
+int mpcxh_go_mr_bases(const uint32_t* n, uint32_t w, uint32_t reps, uint32_t* out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,6 +11,7 @@
 #include <vector>
 
 #include "engine.hpp"
+#include "gorand.hpp"
 #include "hostprof.hpp"
 #include "modint.hpp"
 #include "paillier.hpp"
@@ -348,6 +349,23 @@ int mpcxh_profile_report(char* buf, size_t cap, int reset) {
 
 int mpcxh_candidate_from_bytes(const uint8_t* bytes, size_t n, int q_bit_len, uint32_t* q_out, uint32_t words) {
   return guard([&] { CandidateFromBytes(bytes, n, q_bit_len).to_words(q_out, words); });
+}
+
+int mpcxh_go_rand_int63(int64_t seed, uint32_t count, int64_t* out) {
+  return guard([&] {
+    if (!out && count) throw std::invalid_argument("null out");
+    GoRand r(seed);
+    for (uint32_t i = 0; i < count; ++i) out[i] = r.Int63();
+  });
+}
+
+int mpcxh_go_mr_bases(const uint32_t* n, uint32_t w, uint32_t reps, uint32_t* out) {
+  return guard([&] {
+    const Nat x = Nat::from_words(n, w);
+    if (!x.is_odd() || x.bit_len() < 3 || x == Nat(3)) throw std::invalid_argument("need odd n > 3");
+    const auto bs = GoMillerRabinBases(x, (int)reps);
+    for (uint32_t i = 0; i < reps; ++i) bs[i].to_words(out + (size_t)i * w, w);
+  });
 }
 
 int mpcxh_drbg_read(uint64_t seed, uint8_t* out, size_t n) {

@@ -87,7 +87,7 @@ class Engine {
   StepOut safeprime_step(uint64_t seed, const uint8_t* raw, uint64_t stream_off, uint32_t count, uint32_t q_bits,
                          const std::vector<Nat>& sprp_q);
   std::vector<uint8_t> strong_probable_prime(const std::vector<Nat>& n, const std::vector<Nat>& bases);
-  // mpcx_lucas_batch: strong Lucas test with parameters P (n < 2^1024)
+  // mpcx_lucas_batch: strong Lucas test with parameters P (n < 2^2048)
   std::vector<uint8_t> lucas(const std::vector<Nat>& n, const std::vector<uint32_t>& P);
 
  private:

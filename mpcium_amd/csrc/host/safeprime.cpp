@@ -10,6 +10,7 @@
 #include <thread>
 
 #include "engine.hpp"
+#include "gorand.hpp"
 #include "modint.hpp"
 
 namespace mpcx::host {
@@ -104,20 +105,12 @@ bool passes_trial(const Nat& q) {
   return true;
 }
 
-// Miller-Rabin bases of ProbablyPrime(reps): base 2 (Go's forced last round)
-// first, then `reps` bases in [2, n-2] from a CounterDRBG seeded with the
-// candidate's low word (Go seeds math/rand with it; see safeprime.hpp)
+// Miller-Rabin bases of ProbablyPrime(reps): base 2 (Go's forced last round;
+// the decision does not depend on the order) first, then Go's `reps` bases in
+// [2, n-2] from math/rand seeded with the candidate's low word (gorand.hpp)
 std::vector<Nat> mr_bases(const Nat& q, int reps) {
   std::vector<Nat> out{Nat(2)};
-  CounterDRBG rng(q.low64() ^ 0x4d52u);
-  const uint32_t bits = q.bit_len();
-  const Nat lim = q - Nat(3);
-  std::vector<uint8_t> buf((bits + 7) / 8);
-  while ((int)out.size() < reps + 1) {
-    rng.read(buf.data(), buf.size());
-    Nat v = Nat::from_bytes_be(buf.data(), buf.size()) % lim;
-    out.push_back(v + Nat(2));
-  }
+  for (auto& b : GoMillerRabinBases(q, reps)) out.push_back(std::move(b));
   return out;
 }
 }  // namespace
@@ -261,9 +254,12 @@ std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, Saf
     if (mr_err) std::rethrow_exception(mr_err);
     for (size_t i : s2) ok[i] = pass[i] && lucas_ok[i];
   }
+  std::vector<Nat> wl;  // > 1024 bits passing every Miller-Rabin base: Lucas next
+  std::vector<uint32_t> wp;
+  std::vector<size_t> wo;
   for (size_t i : large) {
     // > 1024 bits: base 2 + reps bases as one shared-exponent launch (x^d for
-    // every base), the squarings on the host; no Lucas step (see the header)
+    // every base), the s - 1 squarings on the host, then the strong Lucas test
     const Nat& x = n[i];
     const Nat nm1 = x - Nat(1);
     uint32_t s = 0;
@@ -286,7 +282,21 @@ std::vector<uint8_t> ProbablyPrimeBatch(const std::vector<Nat>& n, int reps, Saf
         break;
       }
     }
-    ok[i] = all;
+    if (!all) continue;
+    uint32_t P = 0;
+    const int lr = LucasParam(x, &P);
+    if (lr != 1) {
+      ok[i] = lr == 2;
+      continue;
+    }
+    wl.push_back(x);
+    wp.push_back(P);
+    wo.push_back(i);
+  }
+  if (!wl.empty()) {
+    const auto lr = Engine::get().lucas(wl, wp);
+    lt += wl.size();
+    for (size_t j = 0; j < wl.size(); ++j) ok[wo[j]] = lr[j];
   }
   if (stats) {
     stats->mr_tests += mr;

@@ -21,12 +21,9 @@
 // at concurrency 1 (its concurrent output order is scheduling-defined), and
 // the stream is left right after the last accepted candidate (Stream).
 //
-// ProbablyPrime decisions: Go draws its 20 bases from math/rand seeded with
-// the candidate's low word (go:src/math/big/prime.go), whose generator table
-// is not restated here; these 20 bases come from a CounterDRBG seeded the same
-// way. Base 2 and the strong Lucas test (together BPSW, no known
-// counterexample) are Go's exactly, so the accept decisions coincide except on
-// a composite passing BPSW, none of which is known.
+// ProbablyPrime decisions are Go's: the n Miller-Rabin bases come from Go's
+// math/rand seeded with the candidate's low word (gorand.hpp, as
+// go:src/math/big/prime.go draws them), plus base 2 and the strong Lucas test.
 #pragma once
 
 #include <cstdint>
@@ -91,8 +88,8 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, con
 
 // Go (*Int).ProbablyPrime(reps) decisions for a batch of odd n (see the
 // header comment on the bases): small-prime exits, Miller-Rabin with base 2 +
-// `reps` further bases and, for n < 2^1024, the strong Lucas test, all on the
-// GPU. n >= 2^1024 (a 2048-bit Paillier N): Miller-Rabin only.
+// `reps` further bases (Go's), and the strong Lucas test, on the GPU (n up to
+// 2^2048: a 2048-bit Paillier N takes the wide Lucas geometry).
 // base2_passed: every n is already known to pass the base-2 round (the safe-
 // prime step decided it), which is then not repeated. The further bases and
 // the Lucas test run as two concurrent GPU batches; the decision is their

@@ -51,6 +51,7 @@ hipError_t mpcx_launch_mr(const mpcx::MrArgs* a, uint32_t blocks, hipStream_t st
 hipError_t mpcx_launch_prime2c(const mpcx::Prime2Args* a, hipStream_t st);
 hipError_t mpcx_launch_mrc(const mpcx::MrArgs* a, hipStream_t st);
 hipError_t mpcx_launch_lucasc(const mpcx::LucasArgs* a, hipStream_t st);
+hipError_t mpcx_launch_lucasc_wide(const mpcx::LucasArgs* a, hipStream_t st);
 hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g1(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
@@ -108,7 +109,7 @@ struct Staging {
 // on different lanes concurrently, so small or partial-round batches (a
 // latency-bound Fac-proof group, a 10k-wallet MtA step that fills 40% of the
 // wavefront slots) overlap on the GPU instead of queueing behind one lock.
-// kLanes matches the HW queues HIP gives a process by default.
+// g_lanes (default 4) matches the HW queues HIP gives a process by default.
 struct Lane {
   std::mutex mu;
   hipStream_t st = nullptr;  // created on first use (non-blocking); or a caller's stream (own_stream false)
@@ -125,14 +126,16 @@ struct Lane {
   // verdicts, per-item constants of the cooperative kernels (R mod n, meta)
   Staging sieve[8];
 };
-constexpr int kLanes = 4;
+constexpr int kMaxLanes = 8;
+// lanes in use per device: MPCX_LANES (1..8, read at init), default 4
+int g_lanes = 4;
 
 // One bound GPU.
 struct Device {
   int ordinal = -1;
   int num_cus = 0;
   int geom_slots[MPCX_NUM_GEOMS] = {0};  // resident wavefronts per geometry
-  Lane lanes[kLanes];
+  Lane lanes[kMaxLanes];
   std::atomic<unsigned> lane_rr{0};
   // Workspaces of the device-buffer entry points, one per caller stream: two
   // asynchronous calls on different streams never share a window table or a
@@ -278,15 +281,15 @@ int selected(Device** out) {
 // A free lane of device d (round-robin start, first one not in use), else wait for one.
 Lane& acquire_lane(Device& d, std::unique_lock<std::mutex>& lk) {
   const unsigned start = d.lane_rr.fetch_add(1, std::memory_order_relaxed);
-  for (int i = 0; i < kLanes; ++i) {
-    Lane& l = d.lanes[(start + i) % kLanes];
+  for (int i = 0; i < g_lanes; ++i) {
+    Lane& l = d.lanes[(start + i) % g_lanes];
     std::unique_lock<std::mutex> t(l.mu, std::try_to_lock);
     if (t.owns_lock()) {
       lk = std::move(t);
       return l;
     }
   }
-  Lane& l = d.lanes[start % kLanes];
+  Lane& l = d.lanes[start % g_lanes];
   lk = std::unique_lock<std::mutex>(l.mu);
   return l;
 }
@@ -612,6 +615,8 @@ static void read_env_options() {
   if (mr) g_mid_rounds = std::max(0, std::min(400, std::atoi(mr))) / 100.0;
   const char* gp = std::getenv("MPCX_GEOM_POLICY");
   if (gp) g_geom_policy = gp[0] == '0' ? 0 : 1;
+  const char* ln = std::getenv("MPCX_LANES");
+  if (ln && g_ndev.load() == 0) g_lanes = std::max(1, std::min(kMaxLanes, std::atoi(ln)));
 }
 
 int mpcx_init(int device) {
@@ -1034,7 +1039,7 @@ int mpcx_modexp_submit(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, ui
   JobPool& p = job_pool();
   {
     std::lock_guard<std::mutex> lk(p.mu);
-    p.start((size_t)n * kLanes);
+    p.start((size_t)n * g_lanes);
     p.q.push_back(j);
   }
   p.cv.notify_one();
@@ -1158,15 +1163,19 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
 int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uint32_t* P, uint8_t* ok) {
   if (count == 0) return MPCX_OK;
   if (!n || !P || !ok || n_words == 0) return fail(MPCX_EINVAL, "null buffer");
-  if (n_words > (uint32_t)MPCX_CLASS_WORDS(0))
-    return fail(MPCX_EINVAL, "n_words %u > %d", n_words, MPCX_CLASS_WORDS(0));
+  if (n_words > 64u) return fail(MPCX_EINVAL, "n_words %u > 64", n_words);
+  uint32_t maxbits = 0;
   for (uint32_t i = 0; i < count; ++i) {
     const uint32_t* ni = n + (size_t)i * n_words;
     const uint32_t bits = bit_length_words(ni, n_words);
     if (bits < 3 || (ni[0] & 1u) == 0) return fail(MPCX_EINVAL, "candidate %u is not an odd integer >= 5", i);
-    if (bits > 1024) return fail(MPCX_EINVAL, "candidate %u has %u bits > 1024", i, bits);
+    if (bits > 2048) return fail(MPCX_EINVAL, "candidate %u has %u bits > 2048", i, bits);
     if (P[i] < 3 || P[i] >= (1u << 14)) return fail(MPCX_EINVAL, "Lucas parameter P[%u] = %u outside [3, 2^14)", i, P[i]);
+    maxbits = std::max(maxbits, bits);
   }
+  // candidates above 1024 bits: the wide cooperative geometry (16 x 5 digits)
+  const bool wide = maxbits > 1024;
+  const uint32_t cl = wide ? (uint32_t)MPCX_LUCASW_L : (uint32_t)MPCX_MR_L;
   return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t cnt) {
     std::unique_lock<std::mutex> lk;
     Lane& l = acquire_lane(g_devs[di], lk);
@@ -1175,7 +1184,7 @@ int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const 
     const size_t nb = (size_t)cnt * n_words * 4;
     if ((rc = ensure_buffer(l.stage[0], nb)) || (rc = ensure_buffer(l.stage[1], (size_t)cnt * 4)) ||
         (rc = ensure_buffer(l.stage[3], cnt)) ||
-        (g_prime_coop && (rc = ensure_buffer(l.stage[2], (size_t)cnt * (4 * MPCX_MR_L + 2) * 4))))
+        ((g_prime_coop || wide) && (rc = ensure_buffer(l.stage[2], (size_t)cnt * (4 * cl + 2) * 4))))
       return rc;
     if ((rc = h2d(l.stage[0].ptr, n + (size_t)first * n_words, nb, l.st)) ||
         (rc = h2d(l.stage[1].ptr, P + first, (size_t)cnt * 4, l.st)))
@@ -1187,10 +1196,10 @@ int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const 
     a.count = cnt;
     a.n_words = n_words;
     hipError_t e;
-    if (g_prime_coop) {
+    if (g_prime_coop || wide) {
       a.consts = (uint32_t*)l.stage[2].ptr;
-      a.meta = a.consts + (size_t)cnt * 4 * MPCX_MR_L;
-      e = mpcx_launch_lucasc(&a, l.st);
+      a.meta = a.consts + (size_t)cnt * 4 * cl;
+      e = wide ? mpcx_launch_lucasc_wide(&a, l.st) : mpcx_launch_lucasc(&a, l.st);
     } else {
       e = mpcx_launch_lucas(&a, (cnt + 63) / 64, l.st);
     }

@@ -176,6 +176,10 @@ struct Prime2Args {
 #define MPCX_MR_P 16
 #define MPCX_MR_K 3
 #define MPCX_MR_L (MPCX_MR_P * MPCX_MR_K)
+// the strong Lucas test of wider candidates (2^1024 <= n < 2^2048: ModProof's
+// N.ProbablyPrime): 16 lanes x 5 digits, R = 2^(28 * 80) > 16 n
+#define MPCX_LUCASW_K 5
+#define MPCX_LUCASW_L (MPCX_MR_P * MPCX_LUCASW_K)
 
 // Strong Lucas probable-prime test (Go math/big probablyPrimeLucas, the
 // "extra strong" test with Baillie-OEIS method C parameters P, Q = 1,

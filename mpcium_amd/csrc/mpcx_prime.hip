@@ -332,6 +332,16 @@ __attribute__((visibility("hidden"))) hipError_t mpcx_launch_lucasc(const mpcx::
   return hipGetLastError();
 }
 
+// candidates of 1025..2048 bits (consts: count x 4 x MPCX_LUCASW_L digits)
+__attribute__((visibility("hidden"))) hipError_t mpcx_launch_lucasc_wide(const mpcx::LucasArgs* a, hipStream_t st) {
+  constexpr uint32_t G = 64 / MPCX_MR_P;
+  if (a->count == 0) return hipSuccess;
+  hipLaunchKernelGGL((mpcx::k_pprep_lucas<MPCX_LUCASW_L>), dim3((a->count + 63) / 64), dim3(64), 0, st, *a);
+  hipLaunchKernelGGL((mpcx::k_lucasc<MPCX_MR_P, MPCX_LUCASW_K, MPCX_WAVES_PER_EU_MRC>), dim3((a->count + G - 1) / G),
+                     dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
 __attribute__((visibility("hidden"))) hipError_t mpcx_launch_lucas(const mpcx::LucasArgs* a, uint32_t blocks,
                                                                   hipStream_t st) {
   hipLaunchKernelGGL((mpcx::k_lucas<MPCX_C0_K, MPCX_WAVES_PER_EU_MR>), dim3(blocks), dim3(64), 0, st, *a);

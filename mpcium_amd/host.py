@@ -68,6 +68,8 @@ SIGNATURES = [
     ("mpcxh_coprime_batch", _i, [_u32, _vp, _vp, _u32, _vp]),
     ("mpcxh_profile_report", _i, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
+    ("mpcxh_go_rand_int63", _i, [ctypes.c_int64, _u32, _vp]),
+    ("mpcxh_go_mr_bases", _i, [_vp, _u32, _u32, _vp]),
 ]
 
 ERR_OK, ERR_MESSAGE_TOO_LONG, ERR_MESSAGE_MALFORMED = 0, 1, 2
@@ -275,3 +277,19 @@ def drbg_read(seed: int, n: int) -> bytes:
     buf = (ctypes.c_uint8 * n)()
     _check(lib().mpcxh_drbg_read(seed, buf, n))
     return bytes(buf)
+
+
+def go_rand_int63(seed: int, count: int) -> list:
+    """Go math/rand: the first `count` Int63() of rand.New(rand.NewSource(seed)) (test hook)."""
+    out = np.zeros(count, dtype=np.int64)
+    _check(lib().mpcxh_go_rand_int63(seed, count, out.ctypes.data))
+    return [int(v) for v in out]
+
+
+def go_mr_bases(n: int, reps: int) -> list:
+    """The `reps` Miller-Rabin bases Go's ProbablyPrime(reps) draws for odd n > 3 (test hook)."""
+    w = (n.bit_length() + 31) // 32
+    src = ints_to_words([n], w)
+    out = np.zeros((reps, w), dtype="<u4")
+    _check(lib().mpcxh_go_mr_bases(src.ctypes.data, w, reps, out.ctypes.data))
+    return words_to_ints(out)

@@ -21,12 +21,9 @@ Go (*Int).ProbablyPrime(n) (go:src/math/big/prime.go, go1.23.5 per
 /root/reference/go.mod:5) is restated as: the x < 64 bitmask, the even and
 small-prime (3..53) exits, Miller-Rabin with n+1 rounds whose last base is 2,
 then probablyPrimeLucas -- the "extra strong" Lucas test with Baillie-OEIS
-method C parameters (P = 3, 4, ... until Jacobi(P^2-4, x) = -1, Q = 1). Go
-draws the other n Miller-Rabin bases from math/rand seeded with x's low word;
-that generator's table is not restated, so these n bases come from a
-CounterDRBG seeded with x mod 2^64 XOR 0x4d52 (the C++ mirror's
-csrc/host/safeprime.cpp mr_bases). Base 2 + the Lucas test is BPSW: decisions
-agree with Go on every input except a composite passing BPSW (none known).
+method C parameters (P = 3, 4, ... until Jacobi(P^2-4, x) = -1, Q = 1). The
+other n Miller-Rabin bases are Go's: math/rand seeded with x's low word
+(oracle/gorand.py, pinned by Go's documented seed-1 outputs).
 
 generate_preparams: keygen.GeneratePreParams on ONE stream, searches in a
 fixed order (Paillier's 2 safe primes, retried until |P - Q| has >= 1021 bits;
@@ -37,6 +34,7 @@ h1 = f^2 mod N~, h2 = h1^alpha mod N~.
 """
 from __future__ import annotations
 
+from . import gorand
 from .gomath import CounterDRBG
 
 SMALL_PRIMES = [3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 41, 43, 47, 53]
@@ -49,10 +47,9 @@ _SMALL_MASK = sum(1 << p for p in (2, 3, 5, 7, 11, 13, 17, 19, 23, 29, 31, 37, 4
 
 
 def mr_bases(n: int, reps: int):
-    """Base 2, then `reps` bases in [2, n-2] (csrc/host/safeprime.cpp mr_bases)."""
-    rng = CounterDRBG((n & 0xFFFFFFFFFFFFFFFF) ^ 0x4D52)
-    nb = (n.bit_length() + 7) // 8
-    return [2] + [int.from_bytes(rng.read(nb), "big") % (n - 3) + 2 for _ in range(reps)]
+    """Base 2, then Go's `reps` bases in [2, n-2] (oracle/gorand.py; Go runs
+    base 2 last, the decision does not depend on the order)."""
+    return [2] + gorand.mr_bases(n, reps)[:-1]
 
 
 def strong_probable_prime(n: int, a: int) -> bool:

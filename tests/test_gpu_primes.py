@@ -111,6 +111,40 @@ def test_lucas_kernel(gpu, coop):
     assert all(got[:len(A217719)])  # the pseudoprimes pass, as in Go
 
 
+def _prime_near(rng, bits):
+    small = [p for p in range(3, 2000, 2) if all(p % d for d in range(3, int(p ** 0.5) + 1, 2))]
+    n = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+    while any(n % p == 0 for p in small) or not S.probably_prime(n, 5):
+        n += 2
+    return n
+
+
+def test_lucas_kernel_wide(gpu):
+    """The wide Lucas geometry (16 x 5 digits, candidates up to 2048 bits):
+    a batch with a candidate above 1024 bits runs every candidate there --
+    the extra strong Lucas pseudoprimes, 1024-bit and 2048-bit composites,
+    Mersenne prime 2^1279 - 1 and generated 1536/2048-bit primes, against the
+    oracle."""
+    import random
+    rng = random.Random(11)
+    key = load_golden("paillier_key_2048.json")
+    ns = A217719 + [(1 << 1279) - 1, int(key["N"], 16), int(key["P"], 16), _prime_near(rng, 1536),
+                    _prime_near(rng, 2048), _prime_near(rng, 1025)]
+    ns += [rng.getrandbits(2048) | (1 << 2047) | 1 for _ in range(12)]
+    ns += [rng.getrandbits(rng.randrange(1025, 2049)) | 1 for _ in range(12)]
+    ns += [rng.getrandbits(1024) | 1 for _ in range(8)]
+    runs, Ps = [], []
+    for n in ns:
+        r, P = S.lucas_param(n)
+        if r == 1:
+            runs.append(n)
+            Ps.append(P)
+    got = gpu.lucas_batch(runs, Ps)
+    want = [S.probably_prime_lucas(n) for n in runs]
+    assert got == want
+    assert sum(want) >= len(A217719) + 4  # pseudoprimes and primes pass
+
+
 def test_probably_prime_decisions(h):
     import random
     rng = random.Random(4)
@@ -118,7 +152,8 @@ def test_probably_prime_decisions(h):
     ns += [(1 << 521) - 1, (1 << 607) - 1, ((1 << 89) - 1) * ((1 << 107) - 1)]
     ns += [rng.getrandbits(512) | 1 for _ in range(30)]
     key = load_golden("paillier_key_2048.json")
-    ns += [int(key["N"], 16), int(key["P"], 16)]  # 2048-bit composite (MR only) and a 1024-bit prime
+    ns += [int(key["N"], 16), int(key["P"], 16)]  # 2048-bit composite and a 1024-bit prime
+    ns += [(1 << 1279) - 1, _prime_near(random.Random(12), 2048)]  # wide: MR with Go's bases, then Lucas
     got = h.probably_prime(ns, 20)
     assert got == [S.probably_prime(n, 20) for n in ns]
 

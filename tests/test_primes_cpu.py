@@ -55,3 +55,36 @@ def test_lucas_param_exits():
     assert S.lucas_param(25) == (0, None)   # (5/25) = 0, 25 != 5
     assert S.lucas_param(9) == (0, None)    # (5/9) = 1, (12/9) = 0
     assert S.lucas_param(10007 ** 2) == (0, None)  # square: caught at P = 40
+
+
+# Go's documented math/rand outputs for rand.New(rand.NewSource(1)): the first
+# Int63() values, and the Go tour's rand.Intn(100) sequence.
+GO_SEED1_INT63 = [5577006791947779410, 8674665223082153551, 6129484611666145821]
+GO_TOUR_INTN100 = [81, 87, 47, 59, 81, 18, 25, 40, 56, 0]
+
+
+def test_go_rand_oracle_pinned_by_documented_outputs():
+    from oracle import gorand as G
+    r = G.Rand(1)
+    assert [r.int63() for _ in range(3)] == GO_SEED1_INT63
+    r = G.Rand(1)
+    assert [r.intn(100) for _ in range(10)] == GO_TOUR_INTN100
+
+
+def test_go_rand_product_matches_oracle():
+    """libmpcx_host's Go math/rand (csrc/host/gorand.cpp): the documented
+    seed-1 outputs, other seeds (negative, 0, above 2^31) and ProbablyPrime's
+    Miller-Rabin bases against the oracle."""
+    import random
+    from mpcium_amd import host
+    from oracle import gorand as G
+    assert host.go_rand_int63(1, 3) == GO_SEED1_INT63
+    for seed in (0, -1, 7, 2 ** 31 - 1, 2 ** 31, -(2 ** 63), 2 ** 63 - 1, 0x5DEECE66D):
+        r = G.Rand(seed)
+        assert host.go_rand_int63(seed, 700) == [r.int63() for _ in range(700)], seed
+    rng = random.Random(5)
+    for bits in (67, 128, 1024, 1025, 2048):
+        for _ in range(3):
+            n = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+            assert host.go_mr_bases(n, 20) == G.mr_bases(n, 20)[:-1], (bits, n)
+            assert all(2 <= b <= n - 2 for b in G.mr_bases(n, 20))
