@@ -96,6 +96,7 @@ int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): on
 double g_narrow_rounds = 0.15;           // mpcx_set_option("narrow_rounds", 100x): narrow-geometry threshold
 double g_mid_rounds = 0.0;               // mpcx_set_option("mid_rounds", 100x): mid-geometry threshold
 int g_geom_policy = 1;                   // 1: 4096-bit class by the launch-time model; 0: thresholds only
+int g_fixed_win = 5;                     // widest fixed window for per-operand exponents (4 or 5)
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
@@ -575,6 +576,10 @@ int mpcx_set_option(const char* key, int value) {
     // the class's mid geometry (twice the wavefronts per operand count)
     if (value < 0 || value > 400) return fail(MPCX_EINVAL, "mid_rounds %d out of range", value);
     g_mid_rounds = value / 100.0;
+  } else if (std::strcmp(key, "fixed_window") == 0) {
+    // widest fixed window of per-operand exponents: 4 (Go's) or 5 (above 320 bits)
+    if (value != 4 && value != 5) return fail(MPCX_EINVAL, "fixed_window %d not 4 or 5", value);
+    g_fixed_win = value;
   } else if (std::strcmp(key, "geom_policy") == 0) {
     // 1: the 4096-bit class picks main / mid / narrow by the launch-time model; 0: thresholds
     if (value < 0 || value > 1) return fail(MPCX_EINVAL, "geom_policy %d out of range", value);
@@ -877,6 +882,10 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     a.exp_words = exp_words;
     a.mul_words = d_muls ? mul_words : 0;
     a.exp_bits = exp_words ? exp_bits : 0;
+    // fixed window: 5 bits for per-operand exponents above 1024 bits (E/5 + 31
+    // table products < E/4 + 15 from 320 bits on; measured +2.4-2.6% on 2048- and
+    // 4096-bit exponents, profiles/r02/win_ab/), Go's 4 bits otherwise
+    a.win_bits = (!exp_shared && a.exp_bits > 1024u && g_fixed_win >= 5) ? 5u : 4u;
     a.out_words = out_words;
     a.n0inv = mod->n0inv;
     a.exp_shared = exp_shared ? 1 : 0;

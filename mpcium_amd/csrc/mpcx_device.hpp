@@ -278,8 +278,13 @@ __device__ __forceinline__ void lds_store_digits(uint32_t* bl, int p, const uint
   for (int k = 0; k < K; ++k) bl[p * K + k] = A[k];
 }
 
-__device__ __forceinline__ uint32_t window_of(const uint32_t* e, uint32_t j) {
-  return (e[(4u * j) >> 5] >> ((4u * j) & 31u)) & 15u;
+// bits [wb*j, wb*j + wb) of the ew-word exponent e (wb <= 8; bits past the
+// top word read as 0)
+__device__ __forceinline__ uint32_t window_of(const uint32_t* e, uint32_t j, uint32_t wb, uint32_t ew) {
+  const uint32_t bit = wb * j, w = bit >> 5, sh = bit & 31u;
+  uint32_t v = e[w] >> sh;
+  if (sh + wb > 32u && w + 1u < ew) v |= e[w + 1u] << (32u - sh);
+  return v & ((1u << wb) - 1u);
 }
 
 // Leaves A (<= m after the Montgomery-domain exit mont(z R, 1)) canonical,
@@ -360,7 +365,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     }
   };
 
-  const uint32_t nw = (a.exp_bits + 3u) / 4u;
+  // fixed window of wb bits (4, or 5 for long per-operand exponents): a step is
+  // wb squarings and one multiply by the operand's own window's table entry
+  const uint32_t wb = a.win_bits;
+  const uint32_t nw = (a.exp_bits + wb - 1u) / wb;
   const uint32_t* ex = a.exp_shared ? a.exps : a.exps + (size_t)(active ? op : 0) * a.exp_words;
   // Per-wavefront table of MPCX_TABLE_ENTRIES entries x K digit-slots x 64 lanes, accessed
   // through a buffer descriptor: lane offset in one VGPR, entry/slot offset
@@ -416,14 +424,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   // per entry s squarings and one multiply by an odd power. Windows of up to
   // 6 bits cost ~E/7 multiplies against Go's E/4 * 15/16; every decision
   // depends on e only, so the wave stays uniform. Per-operand exponents (and
-  // e = 0) keep Go's 4-bit fixed window: their sequences would diverge.
+  // e = 0) keep a fixed window (wb bits, every operand multiplies every step):
+  // sliding windows would diverge.
   const bool sched = a.exp_shared != 0 && a.sched != nullptr &&
                      __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_TOP]) != MPCX_SCHED_NONE;
-  const uint32_t wt = nw > 0 ? window_of(ex, nw - 1u) : 0u;
-  // table entries built: fixed window p_1..p_T (a shared e < 16 needs p_1..p_e only)
+  const uint32_t wt = nw > 0 ? window_of(ex, nw - 1u, wb, a.exp_words) : 0u;
+  // table entries built: fixed window p_1..p_T (a shared e < 2^wb needs p_1..p_e only)
   const uint32_t wt_u = __builtin_amdgcn_readfirstlane(wt);
   const uint32_t T = sched ? __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_TN])
-                           : (a.exp_shared && nw <= 1u ? (wt_u > 1u ? wt_u : 1u) : 15u);
+                           : (a.exp_shared && nw <= 1u ? (wt_u > 1u ? wt_u : 1u) : (1u << wb) - 1u);
   // exponent steps: schedule entries, or windows below the top one
   const uint32_t nsteps = sched ? __builtin_amdgcn_readfirstlane(a.sched[MPCX_SCHED_N]) : (nw > 0 ? nw - 1u : 0u);
 
@@ -464,7 +473,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       }
       if (pend >= 0) {
         // fixed window: the operand's window of the step just scheduled (idx - 1)
-        lds_from_table(pend == 0x100 ? window_of(ex, nw - 1u - idx) : (uint32_t)pend);
+        lds_from_table(pend == 0x100 ? window_of(ex, nw - 1u - idx, wb, a.exp_words) : (uint32_t)pend);
         pend = -1;
         return;
       }
@@ -483,7 +492,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         sq_left = s >> 8;
         pend = (s & 0xFFu) == 0xFFu ? -1 : (int)(s & 0xFFu);
       } else {
-        sq_left = 4;
+        sq_left = wb;
         pend = 0x100;
       }
       ++idx;

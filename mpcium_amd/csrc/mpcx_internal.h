@@ -81,7 +81,8 @@ struct ModexpArgs {
   uint32_t base_words;
   uint32_t exp_words;
   uint32_t mul_words;
-  uint32_t exp_bits;    // windows processed = ceil(exp_bits / 4)
+  uint32_t exp_bits;    // fixed window: windows processed = ceil(exp_bits / win_bits)
+  uint32_t win_bits;    // fixed-window width (4 or 5): table p_0..p_(2^win_bits - 1)
   uint32_t out_words;
   uint32_t n0inv;       // -m^-1 mod 2^28
   int exp_shared;

@@ -166,6 +166,30 @@ def test_each_geometry_forced(gpu, paillier_key, geom):
         gpu.set_option("force_geom", -1)
 
 
+@pytest.mark.parametrize("m_kind", ["N2", "N", "p"])
+def test_fixed_window_widths_agree(gpu, paillier_key, m_kind):
+    """Per-operand exponents above 1024 bits take a 5-bit fixed window (Go's is
+    4 bits): both widths give pow's results on exponents around the window
+    and word boundaries, with and without the fused multiplier."""
+    N = paillier_key["N"]
+    m = {"N2": N * N, "N": N, "p": paillier_key["P"]}[m_kind]
+    rng = random.Random(77)
+    lens = [320, 321, 1023, 1024, 1025, 1026, 1029, 1030, 2047, 2048, 2049, 2050, 3000, 4095, 4096, 4100]
+    xs = [rng.randrange(m) for _ in lens * 2]
+    es = [rng.getrandbits(b) | (1 << (b - 1)) for b in lens] + [(1 << b) - 1 for b in lens]
+    cs = [rng.randrange(m) for _ in xs]
+    want = [pow(x, e, m) for x, e in zip(xs, es)]
+    mod = gpu.Modulus(m)
+    try:
+        for w in (4, 5):
+            gpu.set_option("fixed_window", w)
+            assert mod.exp(xs, es) == want, w
+            assert mod.exp_mul(xs, es, cs) == [c * v % m for c, v in zip(cs, want)], w
+    finally:
+        gpu.set_option("fixed_window", 5)
+        mod.release()
+
+
 def test_split_plan_large_batch(gpu, paillier_key):
     """A batch that spans >1 round of resident wavefronts takes the main +
     narrow split; spot-check results across the split point."""
