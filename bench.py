@@ -287,6 +287,13 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict):
             "note": "host-buffer API end to end (Python ints -> words -> PCIe -> GPU -> back); Encrypt's Gamma^m "
                     "is the bit-exact 1 + mN shortcut, r^N a shared-exponent GPU batch, c^b per-operand",
             "cpu_baseline": None}
+    # Go-equivalent work per op (SURVEY.md 8(d) W = (E + E/4) 2 L^2, L = 128 words of N^2): r^N (E = 2048) + c^b
+    # (E = bit length of b < q); a 1,024-op batch is a small latency-bound launch pair, not a throughput shape
+    L2 = 2 * 128 * 128
+    alg = sum((2048 + 512) * L2 + (b.bit_length() + (b.bit_length() + 3) // 4) * L2 for b in bs) * reps
+    line["roofline"] = _job_roofline(alg, el)
+    line["roofline"]["scope"] = "end to end (host buffers, Python conversions); batch of 1,024 = latency-bound"
+    line["alg_ops_per_op"] = alg / (batch * reps)
     if cpu:
         line["cpu_baseline"] = cpu_baseline_paillier(N, 12.0, info)
     return line
