@@ -342,12 +342,20 @@ int d2h_sync(void* h, const void* d, size_t bytes, Lane& l) {
   return lane_wait(l);
 }
 
+// Buffers grow with headroom: hipFree waits for the whole device, so a size
+// that creeps up call by call (a safe-prime step's candidates plus a varying
+// ride-along count, a lane's workspace across batch sizes) must not reallocate
+// -- and stall every other lane -- on each new maximum.
+size_t grown(size_t old_bytes, size_t bytes) {
+  return std::max<size_t>({bytes + bytes / 4, old_bytes + old_bytes / 2, (size_t)1 << 20});
+}
+
 int ensure_buffer(Staging& s, size_t bytes) {
   if (s.bytes >= bytes && s.ptr) return MPCX_OK;
+  const size_t want = grown(s.bytes, bytes);
   if (s.ptr) (void)hipFree(s.ptr);
   s.ptr = nullptr;
   s.bytes = 0;
-  size_t want = std::max<size_t>(bytes, 1 << 20);
   hipError_t e = hipMalloc(&s.ptr, want);
   if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(%zu): %s", want, hipGetErrorString(e));
   s.bytes = want;
@@ -361,11 +369,12 @@ int ensure_workspace(Lane& l, size_t bytes) {
     (void)hipStreamSynchronize(l.st);
     (void)hipFree(l.ws);
   }
+  const size_t want = grown(l.ws_bytes, bytes);
   l.ws = nullptr;
   l.ws_bytes = 0;
-  hipError_t e = hipMalloc((void**)&l.ws, bytes);
-  if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(workspace %zu): %s", bytes, hipGetErrorString(e));
-  l.ws_bytes = bytes;
+  hipError_t e = hipMalloc((void**)&l.ws, want);
+  if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(workspace %zu): %s", want, hipGetErrorString(e));
+  l.ws_bytes = want;
   return MPCX_OK;
 }
 
