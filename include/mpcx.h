@@ -298,7 +298,20 @@ int mpcx_sync(void* stream);
  *                shared exponents; 0 selects Go's 4-bit fixed window.
  *   "device_split_min" operands (default 4096): smallest per-device slice
  *                of a host-buffer batch split across the bound devices
- *                (0: never split). */
+ *                (0: never split).
+ *   "geom_policy" 1 (default): 4096-bit batches pick the main, mid (8 x 19)
+ *                or narrow geometry by a measured launch-time model of
+ *                wavefronts per SIMD; 0: the "narrow_rounds" / "mid_rounds"
+ *                thresholds only.
+ *   "mid_rounds" 0..400 (default 0): with geom_policy 0, 4096-bit batches
+ *                under mid_rounds/100 of a main round run in the mid geometry.
+ *   "fixed_window" 4 or 5 (default 5): widest fixed window for per-operand
+ *                exponents (5 bits above 1024-bit exponents, else Go's 4).
+ *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
+ *                thread per candidate.
+ * Environment, read at mpcx_init / mpcx_init_devices: MPCX_LANES (1..8,
+ * default 4: execution lanes per device), MPCX_GEOM_POLICY, MPCX_MID_ROUNDS,
+ * MPCX_SPLIT. */
 int mpcx_set_option(const char* key, int value);
 
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):
