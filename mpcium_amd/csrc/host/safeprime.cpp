@@ -11,6 +11,7 @@
 
 #include "engine.hpp"
 #include "gorand.hpp"
+#include "hostprof.hpp"
 #include "modint.hpp"
 
 namespace mpcx::host {
@@ -322,10 +323,12 @@ size_t default_batch(int bitLen) {
       return v >= 1024 && v <= (1l << 22) ? (size_t)v : (size_t)0;
     }();
     if (env) return env;
-    // 2^19: the ~132K sieve survivors fill whole resident rounds of k_prime2c
-    // (MI355X sweep, profiles/r02/pmc2: 2^18 -> 353, 2^19 -> 416, 3 * 2^18
-    // -> 393 safe primes/s)
-    return 524288;
+    // 3 * 2^18: ~228K sieve survivors per step, 2.3 resident rounds of
+    // k_prime2c (MI355X, profiles/r02/sp_sweep: 256 safe primes at 2^19 /
+    // 3 * 2^18 / 3.5 * 2^18 / 2^20 -> 486 / 518 / 514 / 499 per s; the bench's
+    // 64 primes measure the same 400-412 per s for 2^19 .. 3 * 2^18, where the
+    // last step's overshoot offsets the fuller rounds)
+    return 786432;
   }
   if (bitLen > 256) return 65536;
   return 16384;
@@ -372,6 +375,7 @@ void small_batch(int bitLen, const uint8_t* raw, size_t batch, SafePrimeStats& s
 // q (< 2^1023) that passed the base-2 Miller-Rabin round: the remaining
 // ProbablyPrime(20) rounds and the strong Lucas test
 std::vector<uint8_t> finish_q(const std::vector<Nat>& qs, SafePrimeStats& st) {
+  MPCX_PROF("sp.stage_b");
   return ProbablyPrimeBatch(qs, 20, &st, /*base2_passed=*/true);
 }
 }  // namespace
@@ -407,6 +411,7 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, Str
       if (v[j]) acc.push_back({(c[j].q << 1) + Nat(1), c[j].q, c[j].index});
   };
   auto join = [&] {
+    MPCX_PROF("sp.join_wait");
     if (job.valid()) absorb(running, job.get());
     running.clear();
   };
@@ -431,6 +436,7 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, Str
         raw.resize((size_t)count * nbytes);
         src.read(raw.data(), raw.size());
       }
+      MPCX_PROF("sp.step");
       const auto o = Engine::get().safeprime_step(dev ? dev->seed() : 0, raw.empty() ? nullptr : raw.data(),
                                                   off0 + first * nbytes, count, (uint32_t)qBitLen, ride);
       st.sieved_out += count - o.sieved;
@@ -459,6 +465,7 @@ std::vector<GermainSafePrime> GetRandomSafePrimes(int bitLen, int numPrimes, Str
     if (acc.size() >= (size_t)numPrimes) break;
     if (acc.size() + surv.size() >= (size_t)numPrimes || !more) {
       // its probable primes may suffice: finish them now rather than draw on
+      MPCX_PROF("sp.finish_sync");
       absorb(surv, finish_q(qs_of(surv), stb));
       if (acc.size() >= (size_t)numPrimes) break;
     } else {

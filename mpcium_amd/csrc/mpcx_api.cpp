@@ -627,6 +627,8 @@ static void read_env_options() {
   if (sp) g_split = sp[0] != '0';
   const char* mr = std::getenv("MPCX_MID_ROUNDS");  // percent of a main round
   if (mr) g_mid_rounds = std::max(0, std::min(400, std::atoi(mr))) / 100.0;
+  const char* pc = std::getenv("MPCX_PRIME_COOP");
+  if (pc) g_prime_coop = pc[0] != '0';
   const char* gp = std::getenv("MPCX_GEOM_POLICY");
   if (gp) g_geom_policy = gp[0] == '0' ? 0 : 1;
   const char* ln = std::getenv("MPCX_LANES");
