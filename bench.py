@@ -638,7 +638,8 @@ def main():
     ap.add_argument("--extra-lines", type=int, default=1,
                     help="1: add the config-1 (Paillier batch) and config-3 (safe primes) objects at N=1")
     ap.add_argument("--cpu-sign-seconds", type=float, default=20.0)
-    ap.add_argument("--safe-primes", type=int, default=64, help="config 3: 1024-bit safe primes to find")
+    ap.add_argument("--safe-primes", type=int, default=256,
+                    help="config 3: 1024-bit safe primes to find (256: steady state, ~4 steps per GPU at N = 8)")
     ap.add_argument("--modbits", type=int, default=4096, choices=(2048, 4096),
                     help="4096: x^N mod N^2 (config 2, the bench line); 2048: x^N mod N (Paillier N / N~ class)")
     args = ap.parse_args()
