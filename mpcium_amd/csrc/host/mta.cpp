@@ -299,7 +299,7 @@ namespace {
 std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, const paillier::PublicKey& pk,
                                      const DLNParams& dln, const std::vector<const Nat*>& c1,
                                      const std::vector<const Nat*>& c2, const std::vector<const ProofBob*>& pfp,
-                                     const std::vector<const secp::Affine*>& X) {
+                                     const std::vector<const secp::Affine*>& X, const paillier::PrivateKey* own) {
   const size_t n = c1.size();
   const Nat N2 = pk.NSquare(), gamma = pk.Gamma();
   std::vector<uint8_t> ok(n, 0);
@@ -351,7 +351,32 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
     gt1[i] = gamma_pow(p.T1, pk.N);
     ok[i] = 1;
   });
-  ExpSet eN2(N2), eNt(dln.NTilde);
+  // Equation 7 holds mod N^2 iff it holds mod P^2 and mod Q^2 (CRT): the key
+  // holder (AliceEnd) checks it on the two half-width moduli, a quarter of the
+  // Montgomery work each; everyone else mod N^2.
+  const bool crt = own && !own->P.is_zero() && !own->Q.is_zero();
+  const Nat P2 = crt ? own->P * own->P : Nat(), Q2 = crt ? own->Q * own->Q : Nat();
+  struct Red {  // s, c1, c2, v, Gamma^t1 reduced mod P^2 and Q^2
+    Nat s, c1, c2, v, g;
+  };
+  std::vector<Red> rp(crt ? n : 0), rq(crt ? n : 0);
+  std::vector<Nat> q1q(crt ? n : 0), r3q(crt ? n : 0), l3q(crt ? n : 0);
+  if (crt) {
+    parallel_for(n, [&](size_t i) {
+      if (!ok[i]) return;
+      const auto& p = *pfp[i];
+      for (int h = 0; h < 2; ++h) {
+        const Nat& m = h ? Q2 : P2;
+        Red& r = h ? rq[i] : rp[i];
+        r.s = p.S % m;
+        r.c1 = *c1[i] % m;
+        r.c2 = *c2[i] % m;
+        r.v = p.V % m;
+        r.g = gt1[i] % m;
+      }
+    });
+  }
+  ExpSet eN2(crt ? P2 : N2), eQ2(crt ? Q2 : N2), eNt(dln.NTilde);
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
     const auto& p = *pfp[i];
@@ -359,18 +384,31 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
     eNt.add(dln.h1, p.T1, &p2[i]);          // 6. h1^t1
     eNt.add(p.Z, e[i], &r1[i], &p.ZPrm);    // 5. z^e z'
     eNt.add(p.T, e[i], &r2[i], &p.W);       // 6. t^e w
-    eN2.add(p.S, pk.N, &q1[i], &gt1[i]);    // 7. s^N Gamma^t1
-    eN2.add(*c2[i], e[i], &r3[i], &p.V);    // 7. c2^e v
+    if (crt) {
+      eN2.add(rp[i].s, pk.N, &q1[i], &rp[i].g);   // 7. s^N Gamma^t1 mod P^2
+      eN2.add(rp[i].c2, e[i], &r3[i], &rp[i].v);  // 7. c2^e v mod P^2
+      eQ2.add(rq[i].s, pk.N, &q1q[i], &rq[i].g);  //    and mod Q^2
+      eQ2.add(rq[i].c2, e[i], &r3q[i], &rq[i].v);
+    } else {
+      eN2.add(p.S, pk.N, &q1[i], &gt1[i]);    // 7. s^N Gamma^t1
+      eN2.add(*c2[i], e[i], &r3[i], &p.V);    // 7. c2^e v
+    }
   }
-  run_all({&eN2, &eNt});
+  run_all({&eN2, &eQ2, &eNt});
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
     eNt.add(dln.h2, pfp[i]->S2, &l1[i], &p1[i]);  // 5. h1^s1 h2^s2
     eNt.add(dln.h2, pfp[i]->T2, &l2[i], &p2[i]);  // 6. h1^t1 h2^t2
-    eN2.add(*c1[i], pfp[i]->S1, &l3[i], &q1[i]);  // 7. c1^s1 s^N Gamma^t1
+    if (crt) {
+      eN2.add(rp[i].c1, pfp[i]->S1, &l3[i], &q1[i]);   // 7. c1^s1 s^N Gamma^t1 mod P^2
+      eQ2.add(rq[i].c1, pfp[i]->S1, &l3q[i], &q1q[i]);  //    and mod Q^2
+    } else {
+      eN2.add(*c1[i], pfp[i]->S1, &l3[i], &q1[i]);  // 7. c1^s1 s^N Gamma^t1
+    }
   }
-  run_all({&eN2, &eNt});
-  for (size_t i = 0; i < n; ++i) ok[i] = ok[i] && l1[i] == r1[i] && l2[i] == r2[i] && l3[i] == r3[i];
+  run_all({&eN2, &eQ2, &eNt});
+  for (size_t i = 0; i < n; ++i)
+    ok[i] = ok[i] && l1[i] == r1[i] && l2[i] == r2[i] && l3[i] == r3[i] && (!crt || l3q[i] == r3q[i]);
   return ok;
 }
 }  // namespace
@@ -382,9 +420,7 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
   const size_t n = c1.size();
   if (session.size() != n || c2.size() != n || pf.size() != n || (X && X->size() != n))
     throw std::invalid_argument("ProofBob.Verify: sizes");
-  // own_sk (the verifier's own key) does not change any decision: gcd(x, N)
-  // == 1 is decided for the whole batch at once
-  (void)own_sk;
+  // own_sk: the verifier's own key (equation 7 checked mod P^2 and Q^2)
   std::vector<const Bytes*> sp(n);
   std::vector<const Nat*> c1p(n), c2p(n);
   std::vector<const ProofBob*> pfp(n);
@@ -396,7 +432,7 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
     pfp[i] = &pf[i];
     if (X) Xp[i] = &(*X)[i];
   }
-  return verify_bob_core(sp, pk, dln, c1p, c2p, pfp, Xp);
+  return verify_bob_core(sp, pk, dln, c1p, c2p, pfp, Xp, own_sk);
 }
 
 // ================================================================ protocol
@@ -674,7 +710,7 @@ void AliceEndPairBatch(const std::vector<Bytes>& session, const paillier::Privat
       a[i] = &(*res)[i];
       e[i] = &(*er)[i];
     }
-    const std::vector<uint8_t> ok = verify_bob_core(sp, skA.pub, dlnA, c1, c2, pp, Xp);
+    const std::vector<uint8_t> ok = verify_bob_core(sp, skA.pub, dlnA, c1, c2, pp, Xp, &skA);
     alice_decrypt(skA, c2, ok, a, e);
   };
   both([&] { half(pf, cB, nullptr, alpha, err); }, [&] { half(pfwc, cBwc, Bwc.data(), mu, errwc); });
