@@ -312,6 +312,17 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
   return unpack(out.p, n, md.words);
 }
 
+int Engine::set_lanes(int n) {
+  int prev = lanes_.exchange(n);
+  if (prev == 0) {
+    const char* e = std::getenv("MPCX_LANES");
+    prev = e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+  }
+  int rc = mpcx_set_option("lanes", n);
+  if (rc) throw_last(rc, "mpcx_set_option(lanes)");
+  return prev;
+}
+
 std::vector<Nat> Engine::mulmod(const Nat& m, const std::vector<Nat>& a, const std::vector<Nat>& b) {
   std::vector<Nat> one{Nat(1)};
   return exp(m, a, one, &b);

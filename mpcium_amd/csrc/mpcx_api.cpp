@@ -129,7 +129,7 @@ struct Lane {
 };
 constexpr int kMaxLanes = 8;
 // lanes in use per device: MPCX_LANES (1..8, read at init), default 4
-int g_lanes = 4;
+std::atomic<int> g_lanes{4};
 
 // One bound GPU.
 struct Device {
@@ -282,15 +282,16 @@ int selected(Device** out) {
 // A free lane of device d (round-robin start, first one not in use), else wait for one.
 Lane& acquire_lane(Device& d, std::unique_lock<std::mutex>& lk) {
   const unsigned start = d.lane_rr.fetch_add(1, std::memory_order_relaxed);
-  for (int i = 0; i < g_lanes; ++i) {
-    Lane& l = d.lanes[(start + i) % g_lanes];
+  const int nl = g_lanes.load(std::memory_order_relaxed);
+  for (int i = 0; i < nl; ++i) {
+    Lane& l = d.lanes[(start + i) % nl];
     std::unique_lock<std::mutex> t(l.mu, std::try_to_lock);
     if (t.owns_lock()) {
       lk = std::move(t);
       return l;
     }
   }
-  Lane& l = d.lanes[start % g_lanes];
+  Lane& l = d.lanes[start % nl];
   lk = std::unique_lock<std::mutex>(l.mu);
   return l;
 }
@@ -589,6 +590,10 @@ int mpcx_set_option(const char* key, int value) {
     // widest fixed window of per-operand exponents: 4 (Go's) or 5 (above 320 bits)
     if (value != 4 && value != 5) return fail(MPCX_EINVAL, "fixed_window %d not 4 or 5", value);
     g_fixed_win = value;
+  } else if (std::strcmp(key, "lanes") == 0) {
+    // execution lanes per device in use from now on (1..8; streams are created on first use)
+    if (value < 1 || value > kMaxLanes) return fail(MPCX_EINVAL, "lanes %d outside [1, %d]", value, kMaxLanes);
+    g_lanes = value;
   } else if (std::strcmp(key, "geom_policy") == 0) {
     // 1: the 4096-bit class picks main / mid / narrow by the launch-time model; 0: thresholds
     if (value < 0 || value > 1) return fail(MPCX_EINVAL, "geom_policy %d out of range", value);
@@ -1059,7 +1064,7 @@ int mpcx_modexp_submit(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, ui
   JobPool& p = job_pool();
   {
     std::lock_guard<std::mutex> lk(p.mu);
-    p.start((size_t)n * g_lanes);
+    p.start((size_t)n * kMaxLanes);
     p.q.push_back(j);
   }
   p.cv.notify_one();
