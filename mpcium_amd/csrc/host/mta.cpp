@@ -3,6 +3,7 @@
 #include "mta.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <exception>
 #include <functional>
 #include <map>
@@ -354,7 +355,11 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
   // Equation 7 holds mod N^2 iff it holds mod P^2 and mod Q^2 (CRT): the key
   // holder (AliceEnd) checks it on the two half-width moduli, a quarter of the
   // Montgomery work each; everyone else mod N^2.
-  const bool crt = own && !own->P.is_zero() && !own->Q.is_zero();
+  static const bool crt_on = [] {  // MPCX_VERIFY_CRT=0: mod N^2 also for the key holder (A/B runs)
+    const char* e = std::getenv("MPCX_VERIFY_CRT");
+    return !(e && e[0] == '0');
+  }();
+  const bool crt = crt_on && own && !own->P.is_zero() && !own->Q.is_zero();
   const Nat P2 = crt ? own->P * own->P : Nat(), Q2 = crt ? own->Q * own->Q : Nat();
   struct Red {  // s, c1, c2, v, Gamma^t1 reduced mod P^2 and Q^2
     Nat s, c1, c2, v, g;
