@@ -1,5 +1,8 @@
 // tsscommon.cpp -- see tsscommon.hpp.
 #include "tsscommon.hpp"
+#include <exception>
+#include <mutex>
+#include <condition_variable>
 
 #include "hostprof.hpp"
 
@@ -406,10 +409,119 @@ int host_threads() {
   return n;
 }
 
+namespace {
+// One process-wide pool of host_threads() - 1 workers shared by every
+// parallel_for: the signing and keygen drivers run several protocol tasks at
+// once, each issuing parallel loops, and a thread set per loop oversubscribed
+// the cores (tasks x 16 threads) and paid a spawn per loop. A loop is a task in
+// the pool's list; the caller works on its own loop too, so a loop started from
+// inside another one (or from any thread) always makes progress.
+struct Loop {
+  const std::function<void(size_t)>* fn;
+  size_t n;
+  std::atomic<size_t> next{0};
+  std::atomic<size_t> done{0};
+  std::atomic<bool> failed{false};
+  std::atomic<int> users{0};  // pool workers inside work()
+  std::exception_ptr err;
+  std::mutex err_mu;
+  // runs indices until none is left; returns after the last index it took
+  void work() {
+    for (;;) {
+      const size_t i = next.fetch_add(1);
+      if (i >= n) return;
+      if (!failed.load(std::memory_order_relaxed)) {
+        try {
+          (*fn)(i);
+        } catch (...) {
+          std::lock_guard<std::mutex> lk(err_mu);
+          if (!failed.exchange(true)) err = std::current_exception();
+        }
+      }
+      done.fetch_add(1);
+    }
+  }
+};
+
+class HostPool {
+ public:
+  static HostPool& get() {
+    static HostPool* p = new HostPool(host_threads() - 1);  // never destroyed: workers outlive static teardown
+    return *p;
+  }
+  void run(Loop& l) {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      loops_.push_back(&l);
+    }
+    cv_.notify_all();
+    l.work();
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto it = loops_.begin(); it != loops_.end(); ++it)
+        if (*it == &l) {
+          loops_.erase(it);
+          break;
+        }
+    }
+    // every index was taken and no worker can pick the loop up any more: wait
+    // for the indices still running elsewhere and for the workers to leave it
+    while (l.done.load() < l.n || l.users.load() > 0) std::this_thread::yield();
+  }
+
+ private:
+  explicit HostPool(int workers) {
+    for (int w = 0; w < workers; ++w)
+      std::thread([this] {
+        for (;;) {
+          Loop* l = nullptr;
+          {
+            std::unique_lock<std::mutex> lk(mu_);
+            cv_.wait(lk, [&] {
+              for (Loop* x : loops_)
+                if (x->next.load() < x->n) return true;
+              return false;
+            });
+            for (Loop* x : loops_)
+              if (x->next.load() < x->n) {
+                l = x;
+                l->users.fetch_add(1);  // l stays alive until users drops back to 0
+                break;
+              }
+          }
+          if (l) {
+            l->work();
+            l->users.fetch_sub(1);
+          }
+        }
+      }).detach();
+  }
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Loop*> loops_;
+};
+
+bool pool_enabled() {
+  static const bool on = [] {  // MPCX_HOST_POOL=0: a thread set per loop (A/B runs)
+    const char* e = std::getenv("MPCX_HOST_POOL");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+}  // namespace
+
 void parallel_for(size_t n, const std::function<void(size_t)>& fn) {
   const size_t nt = std::min<size_t>((size_t)host_threads(), n);
   if (nt <= 1) {
     for (size_t i = 0; i < n; ++i) fn(i);
+    return;
+  }
+  if (pool_enabled()) {
+    Loop l;
+    l.fn = &fn;
+    l.n = n;
+    HostPool::get().run(l);
+    if (l.err) std::rethrow_exception(l.err);
     return;
   }
   std::atomic<size_t> next{0};
