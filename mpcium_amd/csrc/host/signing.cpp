@@ -398,10 +398,13 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
     r4 += c4 - c3;
   };
 
-  // chunking: MPCX_SIGN_PIPELINE="chunks,workers" (default one chunk: on
-  // MI355X, 4 chunks on 2 workers measured 3310 vs 4467 sigs/s for one chunk
-  // -- the smaller launches cost more GPU time than the overlap saves)
-  size_t n_chunks = 1, n_workers = 1;
+  // chunking: MPCX_SIGN_PIPELINE="chunks,workers". Default: two concurrent
+  // half-wallet pipelines for 2 signers (2 ordered pairs leave the GPU idle
+  // while every chain is in a host phase; the halves' phases interleave), one
+  // for more signers (their 6+ chains already keep the GPU ~75% busy, and half
+  // launches cost more GPU time): measured on MI355X with the shared host pool,
+  // profiles/r02/pipe_ab/ (before the pool, halves measured slower)
+  size_t n_chunks = pairs.size() <= 2 ? 2 : 1, n_workers = n_chunks;
   if (const char* e = std::getenv("MPCX_SIGN_PIPELINE")) {
     unsigned a = 0, b = 0;
     if (std::sscanf(e, "%u,%u", &a, &b) == 2 && a > 0 && b > 0) {
@@ -416,8 +419,14 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
   {
     std::atomic<size_t> next{0};
     std::vector<std::function<void()>> workers;
+    // MPCX_SIGN_CHUNK_STAGGER_MS: worker t starts t times this late, so the
+    // pipelines' host phases fall into each other's launch phases
+    const char* cs = std::getenv("MPCX_SIGN_CHUNK_STAGGER_MS");
+    const double chunk_stagger_ms = cs ? std::atof(cs) : 0.0;
     for (size_t t = 0; t < n_workers; ++t)
-      workers.push_back([&] {
+      workers.push_back([&, t] {
+        if (chunk_stagger_ms > 0 && t)
+          std::this_thread::sleep_for(std::chrono::microseconds((long)(chunk_stagger_ms * 1000 * (double)t)));
         for (;;) {
           const size_t c = next.fetch_add(1);
           if (c >= n_chunks) return;
