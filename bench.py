@@ -557,7 +557,11 @@ def _job_roofline(alg_macs: float, seconds: float, world: int = 1) -> dict:
     achieved = alg_macs * world / seconds
     return {"bound": "valu", "achieved": achieved / 1e12, "peak": PEAK_INT32_NOMINAL * world / 1e12,
             "unit": "TOP/s", "frac": achieved / (PEAK_INT32_NOMINAL * world), "traffic": None,
-            "alg_ops_per_job": alg_macs, "scope": "end to end (wall time incl. host work)"}
+            "alg_ops_per_job": alg_macs, "scope": "end to end (wall time incl. host work)",
+            "note": "alg_ops are Go-equivalent (SURVEY.md 8(d) W per Exp, Go's 4-bit window); the GPU does less "
+                    "real work for the same Exps (fixed-base comb tables, CRT, sliding windows, algebraic "
+                    "shortcuts), so this job-level ratio can exceed 1: a rate of Go-equivalent work, not a "
+                    "utilization"}
 
 
 def signing_line(args, world, rank, signers: int):
