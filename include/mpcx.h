@@ -309,10 +309,10 @@ int mpcx_sync(void* stream);
  *                exponents (5 bits above 1024-bit exponents, else Go's 4).
  *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
  *                thread per candidate.
- *   "lanes"      1..8 (default 4, or MPCX_LANES): execution lanes (streams
+ *   "lanes"      1..8 (default 6, or MPCX_LANES): execution lanes (streams
  *                with their own workspaces) per device used from now on.
  * Environment, read at mpcx_init / mpcx_init_devices: MPCX_LANES (1..8,
- * default 4: execution lanes per device), MPCX_GEOM_POLICY, MPCX_MID_ROUNDS,
+ * default 6: execution lanes per device), MPCX_GEOM_POLICY, MPCX_MID_ROUNDS,
  * MPCX_SPLIT. */
 int mpcx_set_option(const char* key, int value);
 

@@ -316,7 +316,7 @@ int Engine::set_lanes(int n) {
   int prev = lanes_.exchange(n);
   if (prev == 0) {
     const char* e = std::getenv("MPCX_LANES");
-    prev = e ? std::max(1, std::min(8, std::atoi(e))) : 4;
+    prev = e ? std::max(1, std::min(8, std::atoi(e))) : 6;
   }
   int rc = mpcx_set_option("lanes", n);
   if (rc) throw_last(rc, "mpcx_set_option(lanes)");

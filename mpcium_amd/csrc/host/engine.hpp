@@ -76,7 +76,7 @@ class Engine {
   }
   // execution lanes per device libmpcx uses from now on (mpcx_set_option "lanes");
   // returns the previous count. Many small independent proof chains (config-5
-  // keygen load) gain from 8; signing's few latency-bound chains run best on 4.
+  // keygen load) gain from 8; signing's latency-bound chains run best on 6.
   int set_lanes(int n);
   std::vector<uint8_t> fermat2(const std::vector<Nat>& cands);
   // mpcx_safeprime_step: sieve + Pocklington over `count` stream candidates
@@ -122,7 +122,7 @@ class Engine {
   bool fixed_enabled_ = true;
   std::atomic<uint64_t> busy_ns_{0};
   std::atomic<uint64_t> alg_macs_{0};
-  std::atomic<int> lanes_{0};  // 0: libmpcx's default (MPCX_LANES or 4)
+  std::atomic<int> lanes_{0};  // 0: libmpcx's default (MPCX_LANES or 6)
   void count_work(const Nat& m, const std::vector<Nat>& exps, size_t count);
   std::map<std::vector<uint32_t>, Mod> mods_;
   std::map<std::pair<std::vector<uint32_t>, std::vector<uint32_t>>, Fixed> fixed_;
