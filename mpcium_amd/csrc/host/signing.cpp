@@ -398,13 +398,14 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
     r4 += c4 - c3;
   };
 
-  // chunking: MPCX_SIGN_PIPELINE="chunks,workers". Default: two concurrent
-  // half-wallet pipelines for 2 signers (2 ordered pairs leave the GPU idle
+  // chunking: MPCX_SIGN_PIPELINE="chunks,workers". Default: three concurrent
+  // third-wallet pipelines for 2 signers (2 ordered pairs leave the GPU idle
   // while every chain is in a host phase; the halves' phases interleave), one
   // for more signers (their 6+ chains already keep the GPU ~75% busy, and half
   // launches cost more GPU time): measured on MI355X with the shared host pool,
   // profiles/r02/pipe_ab/ (before the pool, halves measured slower)
-  size_t n_chunks = pairs.size() <= 2 ? 2 : 1, n_workers = n_chunks;
+  // (three pipelines measured mean 6,036 vs 5,770 for two, four alternating pairs, profiles/r02/pipe_ab/)
+  size_t n_chunks = pairs.size() <= 2 ? 3 : 1, n_workers = n_chunks;
   if (const char* e = std::getenv("MPCX_SIGN_PIPELINE")) {
     unsigned a = 0, b = 0;
     if (std::sscanf(e, "%u,%u", &a, &b) == 2 && a > 0 && b > 0) {
