@@ -60,6 +60,113 @@ def pmc_traffic(count: int, modbits: int, mod) -> dict:
     out["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) + " (FETCH_SIZE+WRITE_SIZE KB x 1024, uncorrected)"
     return out
 
+# GPU clock / power / temperature sampler: a separate process (started before
+# this one touches the GPU) that reads the amdsmi GPU metrics of one device every
+# `interval` seconds and appends one JSON line per sample (wall time "t") until
+# its stdin closes. bench.py keeps the samples inside its timed region.
+SMI_SAMPLER = r"""
+import json, select, sys, time
+bdf, interval, path = sys.argv[1], float(sys.argv[2]), sys.argv[3]
+import amdsmi
+amdsmi.amdsmi_init()
+hs = amdsmi.amdsmi_get_processor_handles()
+h = hs[0] if hs else None
+for x in hs:
+    try:
+        if bdf and amdsmi.amdsmi_get_gpu_device_bdf(x).lower().endswith(bdf.lower()):
+            h = x
+            break
+    except Exception:
+        pass
+KEEP = ("clk", "power", "temperature", "throttle", "activity", "energy")
+with open(path, "w") as f:
+    while h is not None:
+        rec = {"t": time.time()}
+        try:
+            m = amdsmi.amdsmi_get_gpu_metrics_info(h)
+            for k, v in m.items():
+                if not any(s in k for s in KEEP):
+                    continue
+                if isinstance(v, (int, float)):
+                    rec[k] = v
+                elif isinstance(v, list):
+                    nums = [y for y in v if isinstance(y, (int, float)) and y not in (65535, 0xFFFFFFFF)]
+                    if nums:
+                        rec[k] = nums
+        except Exception as e:
+            rec["error"] = repr(e)[:200]
+        f.write(json.dumps(rec) + "\n")
+        f.flush()
+        r, _, _ = select.select([sys.stdin], [], [], interval)
+        if r and not sys.stdin.read(1):
+            break
+amdsmi.amdsmi_shut_down()
+"""
+
+
+class SmiSampler:
+    """Runs SMI_SAMPLER beside the benchmark (a child process started before
+    the GPU is initialised in this process) and summarises the samples that
+    fall inside a wall-clock window."""
+
+    def __init__(self, gpu: int, interval: float = 0.1):
+        import subprocess
+        import tempfile
+        self.path = os.path.join(tempfile.gettempdir(), f"mpcx_smi_{os.getpid()}.jsonl")
+        bdf = ""
+        try:  # match the HIP ordinal to its amdsmi handle by PCI bus id (no GPU init needed)
+            ids = sorted(os.listdir("/sys/bus/pci/drivers/amdgpu"))
+            ids = [i for i in ids if i.count(":") == 2]
+            vis = os.environ.get("HIP_VISIBLE_DEVICES") or os.environ.get("ROCR_VISIBLE_DEVICES")
+            if vis:
+                ids = [ids[int(v)] for v in vis.split(",") if v.strip().isdigit() and int(v) < len(ids)]
+            bdf = ids[gpu] if gpu < len(ids) else ""
+        except OSError:
+            pass
+        self.bdf = bdf
+        try:
+            self.proc = subprocess.Popen([sys.executable, "-c", SMI_SAMPLER, bdf, str(interval), self.path],
+                                         stdin=subprocess.PIPE, stdout=subprocess.DEVNULL,
+                                         stderr=subprocess.DEVNULL)
+        except OSError:
+            self.proc = None
+
+    def stop(self):
+        if self.proc is None:
+            return
+        try:
+            self.proc.stdin.close()
+            self.proc.wait(timeout=10)
+        except Exception:
+            self.proc.kill()
+
+    def window(self, t0: float, t1: float) -> dict | None:
+        """Mean / min / max of every sampled metric with t in [t0, t1], plus
+        the first and last sample of the window (drift over the run)."""
+        try:
+            recs = [json.loads(x) for x in open(self.path) if x.strip()]
+        except (OSError, ValueError):
+            return None
+        win = [r for r in recs if t0 <= r["t"] <= t1]
+        if not win:
+            return {"samples": 0, "samples_total": len(recs), "bdf": self.bdf,
+                    "error": (recs[0].get("error") if recs else "no samples")}
+        out = {"samples": len(win), "bdf": self.bdf, "interval_s": (t1 - t0) / max(1, len(win))}
+        keys = sorted({k for r in win for k in r if k not in ("t", "error")})
+        for k in keys:
+            vals = []
+            for r in win:
+                v = r.get(k)
+                if isinstance(v, list):
+                    v = sum(v) / len(v)
+                if isinstance(v, (int, float)):
+                    vals.append(float(v))
+            if vals:
+                out[k] = {"mean": sum(vals) / len(vals), "min": min(vals), "max": max(vals),
+                          "first": vals[0], "last": vals[-1]}
+        return out
+
+
 def gpu_index() -> int:
     """This rank's GPU: LOCAL_RANK, wrapped onto the visible devices so a
     multi-rank rehearsal also runs on a one-GPU box (the driver's N-GPU runs
@@ -631,6 +738,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=20.0)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-smi", action="store_true", help="no amdsmi clock/power sampler beside the timed steps")
     ap.add_argument("--verify", type=int, default=16, help="results checked against CPython pow (untimed)")
     ap.add_argument("--opt", action="append", default=[], help="libmpcx tuning knob key=value (mpcx_set_option)")
     ap.add_argument("--wallets", type=int, default=10000,
@@ -654,6 +762,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = gpu_index()
+    # clock / power / temperature of this rank's GPU over the timed region
+    # (rank 0; a separate process, started before this one initialises the GPU)
+    smi = SmiSampler(local) if rank == 0 and not args.no_smi else None
     # The signing CPU baseline forks worker processes: run it before this
     # process touches the GPU.
     info = host_info()
@@ -715,20 +826,29 @@ def main():
         step()
     torch.cuda.synchronize()
 
+    # one HIP event pair per timed step, on the launch stream (the library's
+    # kernels run on `stream`, so the events bracket exactly one launch each)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    w0 = time.time()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for a, b in evs:
+        a.record(stream)
         step()
+        b.record(stream)
     ev1.record(stream)
     torch.cuda.synchronize()
+    w1 = time.time()
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     kernel_ms = ev0.elapsed_time(ev1) / args.steps  # one launch per step on `stream`
+    step_ms = [a.elapsed_time(b) for a, b in evs]
+    smi_window = smi.window(w0, w1) if smi else None
 
     # untimed correctness sample of the last step's outputs (after the timed
     # region so that --warmup 0 still checks real results)
@@ -836,6 +956,24 @@ def main():
         "cpu_baseline": None,
     }
     result["roofline"].update(pmc_traffic(count, args.modbits, mod))
+    if step_ms:
+        srt = sorted(step_ms)
+        q = max(1, len(step_ms) // 4)
+        result["step_kernel_ms"] = {
+            "min": srt[0], "median": srt[len(srt) // 2], "max": srt[-1],
+            "first_quarter_mean": sum(step_ms[:q]) / q, "last_quarter_mean": sum(step_ms[-q:]) / q,
+            "per_step": [round(x, 3) for x in step_ms],
+            "note": "HIP events around each timed step on the launch stream (k_expsched + k_modexp)"}
+    if smi is not None:
+        smi.stop()
+        result["gpu_telemetry"] = smi_window
+        if smi_window:
+            smi_window["scope"] = "amdsmi GPU metrics sampled every ~0.1 s by a separate process during the timed steps"
+            clk = (smi_window.get("current_gfxclk") or {}).get("mean")
+            if clk:  # the same work against the INT32 peak at the clock the GPU actually ran
+                peak_clk = 256 * 64 * clk * 1e6
+                result["roofline"]["gfxclk_mhz_measured"] = clk
+                result["roofline"]["frac_at_measured_clock"] = achieved / peak_clk
     if digest:
         result["batch_digest"] = digest
     if sub_lines:

@@ -170,9 +170,13 @@ int mpcxh_mta_alice_end_batch(uint32_t w, const uint8_t* sessions, uint32_t sess
 
 /* Signing round 2 runs BobMid and BobMidWC on every peer's round-1 message
  * (up:ecdsa/signing/round_2.go): both halves of each session in one call,
- * RangeProofAlice.Verify once for both, shared launches. b / readers / beta /
- * cB / betaPrm / pfB / err: the BobMid half; bwc, Bwc, readers_wc, *_wc: the
- * BobMidWC half. Every output equals the two separate calls'. */
+ * RangeProofAlice.Verify once for both. b / readers / beta / cB / betaPrm /
+ * pfB / err: the BobMid half; bwc, Bwc, readers_wc, *_wc: the BobMidWC half.
+ * With distinct readers the two halves run concurrently (readers[i] and
+ * readers_wc[i] may then be called at the same time); when readers[i] and
+ * readers_wc[i] are the same callback (same fn and ctx) for any session, the
+ * halves run one after the other, BobMid first. Every output equals the two
+ * separate calls' (BobMid, then BobMidWC). */
 int mpcxh_mta_bob_mid_pair_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len,
                                  const mpcxh_paillier_t* pkA, const mpcxh_dln_t* dlnA, const mpcxh_dln_t* dlnB,
                                  uint32_t count, const uint32_t* pfA, const uint32_t* cA, const uint32_t* b,
@@ -181,7 +185,8 @@ int mpcxh_mta_bob_mid_pair_batch(uint32_t w, const uint8_t* sessions, uint32_t s
                                  uint32_t* pfB, uint8_t* err, uint32_t* beta_wc, uint32_t* cB_wc,
                                  uint32_t* betaPrm_wc, uint32_t* pfB_wc, uint8_t* err_wc);
 /* Signing round 3's AliceEnd and AliceEndWC per peer (up:ecdsa/signing/round_3.go)
- * in one call: one verification batch and one Decrypt batch for both halves. */
+ * in one call: each half's ProofBob[WC] verification and Decrypt batch, the two
+ * halves as concurrent tasks (no reader is involved). */
 int mpcxh_mta_alice_end_pair_batch(uint32_t w, const uint8_t* sessions, uint32_t session_len,
                                    const mpcxh_paillier_t* skA, const mpcxh_dln_t* dlnA, uint32_t count,
                                    const uint32_t* cA, const uint32_t* pfB, const uint32_t* cB,
@@ -236,7 +241,8 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
  * wallets, sessions, errors, relation_failures, engine_busy_s (time inside
  * libmpcx calls), finalize_s, signatures, verified, alg_macs (Go-equivalent
  * algorithmic work of the exponentiations sent to the GPU).
- * trace_wallets > 0: trace_out receives, for the first trace_wallets wallets,
+ * trace_wallets > 0: trace_out receives, for the wallets floor(t * wallets /
+ * trace_wallets), t = 0 .. trace_wallets-1 (spread over every wallet pipeline),
  * per ordered pair (i-major) and wallet 40 words (alpha, beta, mu, nu as 8
  * words each, SHA512_256i over the session's cA, RangeProofAlice, cB,
  * ProofBob, cB', ProofBobWC fields), then per wallet 17 words (r, s, recid). */
@@ -281,9 +287,10 @@ int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int
 
 /* Go (*Int).ProbablyPrime(reps) for count odd or even n of `words` words
  * (go:src/math/big/prime.go: small-prime exits, Miller-Rabin with base 2 and
- * `reps` further bases, strong Lucas test for n < 2^1024; bases beyond 2 are
- * the build's deterministic stream, not Go's math/rand one -- decisions agree
- * except on a composite passing BPSW). ok[i] = 1: probably prime. */
+ * `reps` further bases drawn as Go draws them -- math/rand seeded with n's low
+ * word, nat.random below n - 3, plus 2 -- and the extra strong Lucas test with
+ * Baillie-OEIS parameter P, both on the GPU for n of up to 2048 bits). The same
+ * tests as Go; only their order differs (base 2 first). ok[i] = 1: probably prime. */
 int mpcxh_probably_prime_batch(uint32_t count, const uint32_t* n, uint32_t words, int reps, uint8_t* ok);
 /* ok[i] = gcd(x[i], m[i]) == 1 for odd m[i] (math/big GCD(nil, nil, x, m).Cmp(one)
  * == 0, the coprimality test behind common.GetRandomPositiveRelativelyPrimeInt
@@ -295,6 +302,11 @@ int mpcxh_coprime_batch(uint32_t count, const uint32_t* x, const uint32_t* m, ui
  * empty): "label: seconds (calls)" lines summed over threads, largest first,
  * written NUL-terminated into buf (truncated to cap); reset != 0 clears it. */
 int mpcxh_profile_report(char* buf, size_t cap, int reset);
+
+/* Host worker pool size: *threads = the threads parallel loops use now
+ * (MPCX_HOST_THREADS, else min(usable CPUs, 16 per bound GPU)); *usable = the
+ * CPUs this process may run on (affinity mask capped by the cgroup CPU quota). */
+int mpcxh_host_threads(int* threads, int* usable);
 
 /* tss-lib candidate q from raw stream bytes (masking + delta walk; test hook). */
 int mpcxh_candidate_from_bytes(const uint8_t* bytes, size_t n, int q_bit_len, uint32_t* q_out, uint32_t words);

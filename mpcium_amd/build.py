@@ -69,13 +69,26 @@ def build(force: bool = False, verbose: bool = True, jobs: int = 0) -> dict:
     out["libmpcx"] = lib
     host_srcs = [os.path.join(CSRC, s) for s in HOST_SRCS if os.path.exists(os.path.join(CSRC, s))]
     if host_srcs:
+        # one object per host source (compiled in parallel), then one link
         hlib = os.path.join(HERE, "libmpcx_host.so")
-        hdeps = host_srcs + [os.path.join(CSRC, "host", h) for h in os.listdir(os.path.join(CSRC, "host"))
-                             if h.endswith(".hpp")] + [os.path.join(ROOT, "include", "mpcx_host.h")]
-        if force or _newer(hlib, hdeps + [lib]):
-            _run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Wextra", "-pthread",
-                  "-I", os.path.join(ROOT, "include"), "-I", os.path.join(CSRC, "host"),
-                  "-o", hlib] + host_srcs + ["-L", HERE, "-lmpcx", "-lcrypto", "-Wl,-rpath,$ORIGIN"])
+        hdrs = [os.path.join(CSRC, "host", h) for h in os.listdir(os.path.join(CSRC, "host"))
+                if h.endswith(".hpp")] + [os.path.join(ROOT, "include", "mpcx_host.h"),
+                                          os.path.join(ROOT, "include", "mpcx.h")]
+        hdir = os.path.join(HERE, "build", "host")
+        os.makedirs(hdir, exist_ok=True)
+        hobjs = [(os.path.join(hdir, os.path.basename(src)[:-4] + ".o"), src) for src in host_srcs]
+        htodo = [(o, src) for o, src in hobjs if force or _newer(o, [src] + hdrs)]
+        if htodo:
+            def hone(item):
+                o, src = item
+                _run(["g++", "-O3", "-std=c++17", "-fPIC", "-Wall", "-Wextra", "-pthread",
+                      "-I", os.path.join(ROOT, "include"), "-I", os.path.join(CSRC, "host"), "-c", "-o", o, src])
+            n = jobs or min(len(htodo), max(1, (os.cpu_count() or 2)), 16)
+            with ThreadPoolExecutor(n) as ex:
+                list(ex.map(hone, htodo))
+        if force or htodo or _newer(hlib, [o for o, _ in hobjs] + [lib]):
+            _run(["g++", "-shared", "-pthread", "-o", hlib] + [o for o, _ in hobjs] +
+                 ["-L", HERE, "-lmpcx", "-lcrypto", "-Wl,-rpath,$ORIGIN"])
         out["libmpcx_host"] = hlib
     return out
 

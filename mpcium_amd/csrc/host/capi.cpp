@@ -336,6 +336,13 @@ int mpcxh_coprime_batch(uint32_t count, const uint32_t* x, const uint32_t* m, ui
   });
 }
 
+int mpcxh_host_threads(int* threads, int* usable) {
+  return guard([&] {
+    if (threads) *threads = host_threads();
+    if (usable) *usable = usable_cpus();
+  });
+}
+
 int mpcxh_profile_report(char* buf, size_t cap, int reset) {
   return guard([&] {
     if (!buf || !cap) throw std::invalid_argument("null buffer");
@@ -494,11 +501,16 @@ int mpcxh_mta_bob_mid_pair_batch(uint32_t w, const uint8_t* sessions, uint32_t s
     std::vector<CounterDRBG> d1, d2;
     const auto rd = readers(rdr, count, &d1);
     const auto rdwc = readers(rdr_wc, count, &d2);
+    // one callback reader object for both halves of a session: the halves run
+    // one after the other (the reader is never called concurrently for a session)
+    bool shared = false;
+    for (uint32_t i = 0; i < count && !shared; ++i)
+      shared = rdr[i].fn && rdr[i].fn == rdr_wc[i].fn && rdr[i].ctx == rdr_wc[i].ctx;
     std::vector<mta::BobMidResult> out, outwc;
     std::vector<uint8_t> e, ewc;
     mta::BobMidPairBatch(sessions_from(sessions, session_len, count), sk.pub, range_from(pfA, count, w),
                          nats(b, w, count), nats(bwc, w, count), nats(cA, w, count), dln_from(dlnA, w),
-                         dln_from(dlnB, w), points_from(Bwc, count), rd, rdwc, &out, &outwc, &e, &ewc);
+                         dln_from(dlnB, w), points_from(Bwc, count), rd, rdwc, &out, &outwc, &e, &ewc, shared);
     bob_results_out(out, w, beta, cB, betaPrm, pfB);
     bob_results_out(outwc, w, beta_wc, cB_wc, betaPrm_wc, pfB_wc);
     std::memcpy(err, e.data(), count);

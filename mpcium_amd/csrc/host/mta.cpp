@@ -546,7 +546,10 @@ void bob_mid_halves(const std::vector<Bytes>& session, const paillier::PublicKey
     std::vector<const RandFn*> rdj;
     for (size_t j = 0; j < k; ++j) {
       gbp[j] = gamma_pow(h[j].out->betaPrm, pkA.N);
-      if (!(*h[j].b < pkA.N)) {  // HomoMult(b, cA) fails before ProveBob draws anything
+      // HomoMult(b, cA): 0 <= b < N and 0 <= cA < N^2, else ErrMessageTooLong
+      // (RangeProofAlice.Verify accepts any invertible cA, so a verified cA may
+      // still be >= N^2); it fails after Encrypt's draws, before ProveBob's
+      if (!(*h[j].b < pkA.N) || !(cA[h[j].i] < N2)) {
         *h[j].err = ErrMessageTooLong;
         continue;
       }
@@ -598,8 +601,8 @@ void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& p
   err->assign(n, OK);
   // RangeProofAlice.Verify(ec, pkA, NTildeB, h1B, h2B, cA)
   const std::vector<uint8_t> ok = VerifyRangeAliceBatch(pkA, dlnB, cA, pf);
-  // HomoMult's range checks: cA < N^2 holds for every verified session; b < N
-  // is checked after betaPrm and the Encrypt randomness are drawn, as in Go.
+  // HomoMult's range checks (b < N, cA < N^2) follow the draws of betaPrm and
+  // the Encrypt randomness, as in Go (bob_mid_halves).
   std::vector<BobHalf> h;
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) (*err)[i] = ErrProofVerify;
@@ -613,7 +616,8 @@ void BobMidPairBatch(const std::vector<Bytes>& session, const paillier::PublicKe
                      const std::vector<Nat>& cA, const DLNParams& dlnA, const DLNParams& dlnB,
                      const std::vector<secp::Affine>& Bwc, const std::vector<RandFn>& rand,
                      const std::vector<RandFn>& randwc, std::vector<BobMidResult>* out,
-                     std::vector<BobMidResult>* outwc, std::vector<uint8_t>* err, std::vector<uint8_t>* errwc) {
+                     std::vector<BobMidResult>* outwc, std::vector<uint8_t>* err, std::vector<uint8_t>* errwc,
+                     bool serial_halves) {
   const size_t n = cA.size();
   if (session.size() != n || pf.size() != n || b.size() != n || bwc.size() != n || Bwc.size() != n ||
       rand.size() != n || randwc.size() != n)
@@ -637,6 +641,13 @@ void BobMidPairBatch(const std::vector<Bytes>& session, const paillier::PublicKe
   // the two halves as concurrent tasks: one half's host phases (draws, hashing,
   // gcd batches) overlap the other's launches (measured faster on MI355X than
   // one merged batch of both halves, whose host and GPU phases alternate)
+  // (serial_halves: the caller passed one reader object for both halves of a
+  // session -- BobMid's draws, then BobMidWC's, as two calls in that order)
+  if (serial_halves) {
+    bob_mid_halves(session, pkA, dlnA, cA, h);
+    bob_mid_halves(session, pkA, dlnA, cA, hwc);
+    return;
+  }
   both([&] { bob_mid_halves(session, pkA, dlnA, cA, h); }, [&] { bob_mid_halves(session, pkA, dlnA, cA, hwc); });
 }
 

@@ -105,13 +105,16 @@ void BobMidBatch(const std::vector<Bytes>& session, const paillier::PublicKey& p
 // as tss-lib's signing round 2 runs both per peer (up:ecdsa/signing/round_2.go):
 // RangeProofAlice.Verify once for both (the same pure decision twice in Go),
 // then the two halves as concurrent tasks; every output equals the two
-// separate calls'.
+// separate calls'. serial_halves: the halves share reader objects (one
+// io.Reader per session for both) -- BobMid runs to completion first, so the
+// draws are those of BobMid then BobMidWC called in that order.
 void BobMidPairBatch(const std::vector<Bytes>& session, const paillier::PublicKey& pkA,
                      const std::vector<RangeProofAlice>& pf, const std::vector<Nat>& b, const std::vector<Nat>& bwc,
                      const std::vector<Nat>& cA, const DLNParams& dlnA, const DLNParams& dlnB,
                      const std::vector<secp::Affine>& Bwc, const std::vector<RandFn>& rand,
                      const std::vector<RandFn>& randwc, std::vector<BobMidResult>* out,
-                     std::vector<BobMidResult>* outwc, std::vector<uint8_t>* err, std::vector<uint8_t>* errwc);
+                     std::vector<BobMidResult>* outwc, std::vector<uint8_t>* err, std::vector<uint8_t>* errwc,
+                     bool serial_halves = false);
 
 // AliceEnd (B == nullptr) / AliceEndWC -> alpha = Decrypt(cB) mod q
 void AliceEndBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,

@@ -449,7 +449,8 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
     trace->assign(pairs.size() * tw * kTracePairWords + tw * kTraceSigWords, 0);
     uint32_t* o = trace->data();
     for (const auto& p : pairs)
-      for (size_t wi = 0; wi < tw; ++wi, o += kTracePairWords) {
+      for (size_t t = 0; t < tw; ++t, o += kTracePairWords) {
+        const size_t wi = TraceWallet(t, tw, Wn);
         p.alpha[wi].to_words(o, 8);
         p.bob[wi].beta.to_words(o + 8, 8);
         p.mu[wi].to_words(o + 16, 8);
@@ -468,7 +469,8 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
         in.push_back(&uy);
         SHA512_256i(in).to_words(o + 32, 8);
       }
-    for (size_t wi = 0; wi < tw; ++wi, o += kTraceSigWords) {
+    for (size_t t = 0; t < tw; ++t, o += kTraceSigWords) {
+      const size_t wi = TraceWallet(t, tw, Wn);
       sig_r[wi].to_words(o, 8);
       sig_s[wi].to_words(o + 8, 8);
       o[16] = recid[wi];

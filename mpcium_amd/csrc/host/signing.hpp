@@ -56,13 +56,16 @@ struct MtaStats {
   uint64_t signatures = 0, verified = 0;          // signatures produced / passing ecdsa.Verify
 };
 
-// Per-session record of the first `trace_wallets` wallets (parity tests):
-// per ordered pair p (Alice i, Bob j, i-major order) and wallet w:
+// Per-session record of `trace_wallets` wallets (parity tests), spread evenly
+// over the batch so every concurrent wallet pipeline is sampled: traced wallet
+// t is TraceWallet(t, trace_wallets, wallets) = floor(t * wallets / trace_wallets).
+// Per ordered pair p (Alice i, Bob j, i-major order) and traced wallet:
 //   kTracePairWords words = alpha, beta, mu, nu (8 words each) and
 //   SHA512_256i(cA, pfA fields, cB, pfB fields, cB', pfB' fields, u.x, u.y);
 // then per wallet kTraceSigWords words = r, s (8 words each), recid.
 constexpr uint32_t kTracePairWords = 40;
 constexpr uint32_t kTraceSigWords = 17;
+inline size_t TraceWallet(size_t t, size_t traced, size_t wallets) { return t * wallets / traced; }
 
 // One GG18 signature per wallet for `signers` of the nodes (2 = 2-of-3 with a
 // minimal quorum, 3 = every ready peer, mpcium's default): the MtA / MtAwc

@@ -3,6 +3,11 @@
 #include <exception>
 #include <mutex>
 #include <condition_variable>
+#include <sched.h>
+#include <chrono>
+#include <cstdio>
+
+#include "mpcx.h"
 
 #include "hostprof.hpp"
 
@@ -399,14 +404,44 @@ void GetRandomPositiveRelativelyPrimeIntBatch(const std::vector<const RandFn*>& 
 }
 
 // ------------------------------------------------------------------ threads
-int host_threads() {
+// CPUs this process may use: its affinity mask, capped by the cgroup v2 CPU
+// quota (a GPU box gives a job a share of the machine: the affinity shows every
+// CPU, cpu.max how many may run at once).
+int usable_cpus() {
   static const int n = [] {
-    const char* e = std::getenv("MPCX_HOST_THREADS");
-    int v = e ? std::atoi(e) : 0;
-    if (v <= 0) v = std::min(16, (int)std::max(1u, std::thread::hardware_concurrency()));
-    return v;
+    int a = 0;
+    cpu_set_t set;
+    CPU_ZERO(&set);
+    if (sched_getaffinity(0, sizeof set, &set) == 0) a = CPU_COUNT(&set);
+    if (a <= 0) a = (int)std::max(1u, std::thread::hardware_concurrency());
+    if (FILE* f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+      char quota[32] = {0};
+      long period = 0;
+      if (std::fscanf(f, "%31s %ld", quota, &period) == 2 && std::strcmp(quota, "max") != 0 && period > 0) {
+        const long q = std::atol(quota);
+        if (q > 0) a = std::min(a, (int)std::max(1L, (q + period - 1) / period));
+      }
+      std::fclose(f);
+    }
+    return std::max(1, a);
   }();
   return n;
+}
+
+// Host threads for parallel loops: the usable CPUs, up to kThreadsPerDevice per
+// bound GPU (one node process drives all of its GPUs, and each GPU's protocol
+// batches need their own share of host work: /root/reference/pkg/mpc/node.go:69,109,170).
+// MPCX_HOST_THREADS overrides the total.
+int host_threads() {
+  static const int env = [] {
+    const char* e = std::getenv("MPCX_HOST_THREADS");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (env > 0) return env;
+  constexpr int kThreadsPerDevice = 16;
+  int dev = 0;
+  if (mpcx_bound_devices(&dev, nullptr, 0) != MPCX_OK || dev < 1) dev = 1;
+  return std::max(1, std::min(usable_cpus(), kThreadsPerDevice * dev));
 }
 
 namespace {
@@ -426,10 +461,12 @@ struct Loop {
   std::exception_ptr err;
   std::mutex err_mu;
   // runs indices until none is left; returns after the last index it took
-  void work() {
+  // (true: it finished the loop's last index)
+  bool work() {
+    bool last = false;
     for (;;) {
       const size_t i = next.fetch_add(1);
-      if (i >= n) return;
+      if (i >= n) return last;
       if (!failed.load(std::memory_order_relaxed)) {
         try {
           (*fn)(i);
@@ -438,7 +475,7 @@ struct Loop {
           if (!failed.exchange(true)) err = std::current_exception();
         }
       }
-      done.fetch_add(1);
+      last = done.fetch_add(1) + 1 == n;
     }
   }
 };
@@ -446,7 +483,8 @@ struct Loop {
 class HostPool {
  public:
   static HostPool& get() {
-    static HostPool* p = new HostPool(host_threads() - 1);  // never destroyed: workers outlive static teardown
+    static HostPool* p = new HostPool();  // never destroyed: workers outlive static teardown
+    p->grow(host_threads() - 1);
     return *p;
   }
   void run(Loop& l) {
@@ -464,41 +502,64 @@ class HostPool {
           break;
         }
     }
-    // every index was taken and no worker can pick the loop up any more: wait
-    // for the indices still running elsewhere and for the workers to leave it
-    while (l.done.load() < l.n || l.users.load() > 0) std::this_thread::yield();
+    // Every index was taken and no worker can pick the loop up any more. Until
+    // the indices still running elsewhere finish (and the workers leave it),
+    // help with other loops' pending indices, else sleep on the completion
+    // signal -- no spinning: many protocol tasks wait here at once.
+    for (;;) {
+      if (l.done.load() >= l.n && l.users.load() == 0) return;
+      Loop* o = take();
+      if (o) {
+        finish(o, o->work());
+        continue;
+      }
+      std::unique_lock<std::mutex> lk(done_mu_);
+      done_cv_.wait_for(lk, std::chrono::microseconds(500),
+                        [&] { return l.done.load() >= l.n && l.users.load() == 0; });
+    }
   }
 
  private:
-  explicit HostPool(int workers) {
-    for (int w = 0; w < workers; ++w)
+  HostPool() = default;
+  void grow(int workers) {
+    std::lock_guard<std::mutex> lk(grow_mu_);
+    for (; workers_ < workers; ++workers_)
       std::thread([this] {
         for (;;) {
           Loop* l = nullptr;
           {
             std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] {
-              for (Loop* x : loops_)
-                if (x->next.load() < x->n) return true;
-              return false;
-            });
-            for (Loop* x : loops_)
-              if (x->next.load() < x->n) {
-                l = x;
-                l->users.fetch_add(1);  // l stays alive until users drops back to 0
-                break;
-              }
+            cv_.wait(lk, [&] { return pending_locked() != nullptr; });
+            l = pending_locked();
+            l->users.fetch_add(1);  // l stays alive until users drops back to 0
           }
-          if (l) {
-            l->work();
-            l->users.fetch_sub(1);
-          }
+          finish(l, l->work());
         }
       }).detach();
   }
-  std::mutex mu_;
-  std::condition_variable cv_;
+  Loop* pending_locked() {
+    for (Loop* x : loops_)
+      if (x->next.load() < x->n) return x;
+    return nullptr;
+  }
+  Loop* take() {
+    std::lock_guard<std::mutex> lk(mu_);
+    Loop* l = pending_locked();
+    if (l) l->users.fetch_add(1);
+    return l;
+  }
+  // a worker leaves loop l (last: it completed l's final index)
+  void finish(Loop* l, bool last) {
+    const bool left_last = l->users.fetch_sub(1) == 1;
+    if (last || left_last) {
+      std::lock_guard<std::mutex> lk(done_mu_);
+      done_cv_.notify_all();
+    }
+  }
+  std::mutex mu_, grow_mu_, done_mu_;
+  std::condition_variable cv_, done_cv_;
   std::vector<Loop*> loops_;
+  int workers_ = 0;
 };
 
 bool pool_enabled() {

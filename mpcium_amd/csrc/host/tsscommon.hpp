@@ -72,9 +72,12 @@ Nat SHA512_256i_TAGGED(const std::vector<uint8_t>& tag, const std::vector<const 
 // common.RejectionSample(q, eHash) = eHash mod q
 Nat RejectionSample(const Nat& q, const Nat& eHash);
 
-// Parallel loop over [0, n) on the host worker pool (MPCX_HOST_THREADS,
-// default min(16, hardware threads)); fn must be thread-safe per index.
+// Parallel loop over [0, n) on the host worker pool (host_threads() threads
+// including the caller); fn must be thread-safe per index.
 void parallel_for(size_t n, const std::function<void(size_t)>& fn);
+// CPUs this process may run on: affinity mask capped by the cgroup CPU quota
+int usable_cpus();
+// pool size: MPCX_HOST_THREADS, else min(usable_cpus(), 16 per bound GPU)
 int host_threads();
 
 }  // namespace mpcx::host

@@ -67,6 +67,7 @@ SIGNATURES = [
     ("mpcxh_probably_prime_batch", _i, [_u32, _vp, _u32, _i, _vp]),
     ("mpcxh_coprime_batch", _i, [_u32, _vp, _vp, _u32, _vp]),
     ("mpcxh_profile_report", _i, [ctypes.c_char_p, ctypes.c_size_t, _i]),
+    ("mpcxh_host_threads", _i, [_vp, _vp]),
     ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
     ("mpcxh_go_rand_int63", _i, [ctypes.c_int64, _u32, _vp]),
     ("mpcxh_go_mr_bases", _i, [_vp, _u32, _u32, _vp]),
@@ -232,6 +233,13 @@ def generate_preparams(seed: int = 0, rand_fn=None):
     vals = dict(zip(PREPARAM_FIELDS, words_to_ints(out)))
     stats = dict(zip(STAT_KEYS, (int(x) for x in st)))
     return vals, stats
+
+
+def host_threads() -> tuple:
+    """(threads parallel loops use now, usable CPUs of this process)."""
+    t, u = ctypes.c_int(0), ctypes.c_int(0)
+    _check(lib().mpcxh_host_threads(ctypes.byref(t), ctypes.byref(u)))
+    return t.value, u.value
 
 
 def profile_report(reset: bool = False) -> str:

@@ -91,10 +91,16 @@ def lib() -> ctypes.CDLL:
     """Load libmpcx.so (raises if it has not been built)."""
     global _lib
     if _lib is None:
-        if not os.path.exists(_LIB_PATH):
-            raise MpcxError(MPCX_ENODEV, f"{_LIB_PATH} not built: run `python -m mpcium_amd.build`")
-        l = ctypes.CDLL(_LIB_PATH)
+        # MPCX_LIB_PATH: another build of libmpcx.so (an earlier round's, for
+        # interleaved A/B timing of the same bench command); symbols it lacks
+        # stay unbound
+        path = os.environ.get("MPCX_LIB_PATH") or _LIB_PATH
+        if not os.path.exists(path):
+            raise MpcxError(MPCX_ENODEV, f"{path} not built: run `python -m mpcium_amd.build`")
+        l = ctypes.CDLL(path)
         for name, res, args in SIGNATURES:
+            if path != _LIB_PATH and not hasattr(l, name):
+                continue
             f = getattr(l, name)
             f.restype = res
             f.argtypes = args

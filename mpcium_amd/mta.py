@@ -234,14 +234,17 @@ def bob_mid_pair(sessions: Sequence[bytes], pkA_N: int, pfA: Sequence[dict], b: 
                  dlnA: Dict[str, int], dlnB: Dict[str, int], seeds: Sequence, bwc: Sequence[int],
                  Bwc: Sequence[Tuple[int, int]], seeds_wc: Sequence):
     """BobMid (b, seeds) and BobMidWC (bwc, Bwc, seeds_wc) on the same Alice
-    messages in one call -> ((beta, cB, betaPrm, ProofBob, err), (the WC half))."""
+    messages in one call -> ((beta, cB, betaPrm, ProofBob, err), (the WC half)).
+    seeds_wc is seeds (the same list object): each session's one reader serves
+    both halves (the library then runs BobMid before BobMidWC)."""
     k = _Keep()
     pk, da, db = _paillier(k, pkA_N), _dln(k, dlnA), _dln(k, dlnB)
     n = len(b)
     ss, sl = _sessions(sessions)
     PA, Bw, Bwcw, CA = _proof_buf(pfA, RANGE_FIELDS, 6), _col(b), _col(bwc), _col(cA)
     Bp = _points(Bwc)
-    S, Swc = _host.Readers(seeds), _host.Readers(seeds_wc)
+    S = _host.Readers(seeds)
+    Swc = S if seeds_wc is seeds else _host.Readers(seeds_wc)
     outs = []
     for _ in range(2):
         outs.append([np.zeros((n, W), dtype="<u4") for _ in range(3)] + [np.zeros((n, 12 * W), dtype="<u4"),
@@ -334,8 +337,10 @@ def bench_signing(nodes: Sequence[Dict[str, int]], signers: int, wallets: int, s
     `wallets` wallets -- MtA / MtAwc on the GPU, then the signature and
     ecdsa.Verify. nodes: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i, p, q
     (node_preparams.json fields). Returns the stats dict, and with
-    trace_wallets > 0 also the trace: {"pairs": [[{alpha, beta, mu, nu,
-    digest} per wallet] per ordered pair], "sigs": [(r, s, recid)]}."""
+    trace_wallets > 0 also the trace of the wallets t * wallets // trace_wallets
+    (t < trace_wallets; spread over every concurrent wallet pipeline):
+    {"wallets": [index], "pairs": [[{alpha, beta, mu, nu, digest} per traced
+    wallet] per ordered pair], "sigs": [(r, s, recid)]}."""
     k = _Keep()
     sks = (PaillierKey * len(nodes))(*[_paillier(k, n["N"], n["LambdaN"], n["P"], n["Q"]) for n in nodes])
     dlns = (DLN * len(nodes))(*[_dln(k, {"NTilde": n["NTildei"], "h1": n["H1i"], "h2": n["H2i"],
@@ -363,7 +368,7 @@ def bench_signing(nodes: Sequence[Dict[str, int]], signers: int, wallets: int, s
         o = base + wi * 17
         r, s = words_to_ints(tr[o:o + 16].reshape(2, 8))
         sigs.append((r, s, int(tr[o + 16])))
-    return stats, {"pairs": pairs, "sigs": sigs}
+    return stats, {"wallets": [t * wallets // tw for t in range(tw)], "pairs": pairs, "sigs": sigs}
 
 
 def bench_signing_mta(nodes, signers: int, wallets: int, seed: int = 0x5167) -> dict:

@@ -162,30 +162,14 @@ def mod_prove(session: bytes, N: int, P: int, Qf: int, rd: T.Reader) -> ModProof
     return ModProof(W, X, A, B, Z)
 
 
-def _strong_probable_prime_base2(n: int) -> bool:
-    if n < 5 or n % 2 == 0:
-        return n in (2, 3)
-    d, s = n - 1, 0
-    while d % 2 == 0:
-        d //= 2
-        s += 1
-    x = _pw(2, d, n)
-    if x in (1, n - 1):
-        return True
-    for _ in range(s - 1):
-        x = x * x % n
-        if x == n - 1:
-            return True
-    return False
-
-
 def mod_verify(pf: ModProof, session: bytes, N: int) -> bool:
-    """(*ProofMod).Verify(Session, N). N's compositeness (Go: N.ProbablyPrime(30)
-    == false) is decided by a base-2 strong-probable-prime test: identical
-    except for base-2 strong pseudoprimes, negligible for a Blum modulus."""
+    """(*ProofMod).Verify(Session, N): a probable-prime N is rejected first
+    (Go: N.ProbablyPrime(30), restated in safeprime_ref.probably_prime with Go's
+    math/rand Miller-Rabin bases and the extra strong Lucas test)."""
+    from .safeprime_ref import probably_prime
     if pf is None or N <= 0 or N % 2 == 0:
         return False
-    if _strong_probable_prime_base2(N):
+    if probably_prime(N, 30):
         return False
     if jacobi(pf.W, N) != -1:
         return False
@@ -209,6 +193,31 @@ def mod_verify(pf: ModProof, session: bytes, N: int) -> bool:
         if _pw(pf.X[i], 4, N) != right:
             return False
     return True
+
+
+def mod_proof_for_prime(session: bytes, p: int, rd: T.Reader) -> ModProof:
+    """A ModProof for a PRIME p = 3 (mod 4) that satisfies every equation of
+    the verifier (Z_i^p = Y_i by Fermat, X_i^4 = (-1)^a W^b Y_i via the
+    ((p+1)/4)^2 power of a quadratic residue): only the N.ProbablyPrime(30)
+    check rejects it. Test helper for that check in isolation."""
+    assert p % 4 == 3
+    W = get_random_quadratic_non_residue(rd, p)
+    Y = _mod_challenges(session, W, p)
+    e4 = ((p + 1) // 4) ** 2 % (p - 1)
+    A = B = 1 << MOD_ITERATIONS
+    X, Z = [], []
+    for i, y in enumerate(Y):
+        for j in range(4):
+            a, b = j & 1, (j & 2) >> 1
+            yi = (-y) % p if a else y
+            yi = W * yi % p if b else yi
+            if jacobi(yi, p) == 1:
+                X.append(pow(yi, e4, p))
+                Z.append(y % p)
+                A |= a << i
+                B |= b << i
+                break
+    return ModProof(W, X, A, B, Z)
 
 
 # ----------------------------------------------------------------- Fac (no small factor)

@@ -253,3 +253,51 @@ def test_overlong_exponent_does_not_fail_the_batch(mta, nodes, vec, monkeypatch)
     pfs = [pf] * 79 + [bad]
     ok = mta.verify_range_alice(A["N"], dln(B), [c] * 80, pfs)
     assert ok == [True] * 79 + [False]
+
+
+def test_bob_mid_rejects_ciphertext_above_n2(mta, nodes, vec, monkeypatch):
+    """a range proof made for cA + N^2 verifies (Verify reduces c,
+    the hash binds it as given), but HomoMult(b, cA) requires cA < N^2: BobMid
+    must return ErrMessageTooLong, as Go and the oracle do; the honest session
+    beside it is unaffected."""
+    A, B = nodes[0], nodes[1]
+    v = vec[0]
+    N2 = A["N"] ** 2
+    rd = T.Reader(v["seed_a"])
+    cA, rA = M.encrypt_and_return_randomness(rd, A["N"], H(v["a"]))
+    assert cA == H(v["cA"])
+    big = cA + N2
+    pf_big = M.prove_range_alice(A["N"], big, B["NTildei"], B["H1i"], B["H2i"], H(v["a"]), rA, rd)
+    assert M.verify_range_alice(pf_big, A["N"], B["NTildei"], B["H1i"], B["H2i"], big)
+    with pytest.raises(M.ErrMessageTooLong):
+        M.bob_mid(bytes.fromhex(v["session"]), A["N"], pf_big, H(v["b"]), big, A["NTildei"], A["H1i"], A["H2i"],
+                  B["NTildei"], B["H1i"], B["H2i"], T.Reader(v["seed_b"]))
+    monkeypatch.setattr(mta, "W", 160)  # cA + N^2 has 4097 bits
+    pf_big = {f: getattr(pf_big, f) for f in M.RangeProofAlice.__dataclass_fields__}
+    ss = [bytes.fromhex(v["session"])] * 2
+    beta, cB, bp, pfB, err = mta.bob_mid(ss, A["N"], [hx(v["pfA"]), pf_big], [H(v["b"])] * 2, [cA, big], dln(A),
+                                         dln(B), [v["seed_b"]] * 2)
+    assert err == [0, mta.ERR_MESSAGE_TOO_LONG]
+    assert cB[0] == H(v["bob"]["cB"])
+
+
+def test_bob_mid_pair_with_one_reader_per_session(mta, nodes, vec):
+    """one callback reader object passed for both halves of each
+    session (as a tss-lib integration passing the party's reader to BobMid and
+    BobMidWC) is never called concurrently: the pair entry then equals BobMid
+    followed by BobMidWC on the same readers."""
+    vec = by_pair(vec)[(0, 1)]
+    A, B = nodes[0], nodes[1]
+    n = len(vec)
+    ss = [bytes.fromhex(v["session"]) for v in vec]
+    Bpts = [(H(v["Bx"]), H(v["By"])) for v in vec]
+    pfA, cA = [hx(v["pfA"]) for v in vec], [H(v["cA"]) for v in vec]
+    bs, ws = [H(v["b"]) for v in vec], [H(v["wB"]) for v in vec]
+    shared = [T.Reader(0x5EED + i) for i in range(n)]
+    plain, wc = mta.bob_mid_pair(ss, A["N"], pfA, bs, cA, dln(A), dln(B, own=True), shared, ws, Bpts, shared)
+    sep = [T.Reader(0x5EED + i) for i in range(n)]
+    want_plain = mta.bob_mid(ss, A["N"], pfA, bs, cA, dln(A), dln(B, own=True), sep)
+    want_wc = mta.bob_mid(ss, A["N"], pfA, ws, cA, dln(A), dln(B, own=True), sep, B=Bpts)
+    assert plain == want_plain
+    assert wc == want_wc
+    assert plain[4] == [0] * n and wc[4] == [0] * n

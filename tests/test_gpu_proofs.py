@@ -72,6 +72,28 @@ def test_mod_golden_and_rejections(pr, nodes, vec):
     assert pr.mod_verify([ss], P, [got[0]]) == [False]
 
 
+def test_mod_verify_rejects_prime_modulus_alone(pr, nodes, vec, monkeypatch):
+    """ModProof.Verify's N.ProbablyPrime(30) check in isolation: a proof for a
+    prime P (a 1024-bit safe prime, P = 3 mod 4) that satisfies every equation
+    -- the oracle accepts it once its primality check is disabled -- is rejected
+    by the GPU verifier and the oracle. A composite N with its honest proof in
+    the same batch verifies."""
+    from oracle import safeprime_ref as SP
+    from oracle import tss_ref as T
+    n0 = nodes[0]
+    ss = bytes.fromhex(vec["session"])
+    P = n0["P"]
+    crafted = PR.mod_proof_for_prime(ss, P, T.Reader(0x9F1E))
+    assert PR.mod_verify(crafted, ss, P) is False
+    monkeypatch.setattr(SP, "probably_prime", lambda n, reps=20: False)
+    assert PR.mod_verify(crafted, ss, P) is True  # every other check passes
+    monkeypatch.undo()
+    honest = pr.mod_prove([ss], n0["N"], n0["P"], n0["Q"], [vec["mod"]["seed"]])[0]
+    pf = {"W": crafted.W, "X": list(crafted.X), "A": crafted.A, "B": crafted.B, "Z": list(crafted.Z)}
+    assert pr.mod_verify([ss], P, [pf]) == [False]
+    assert pr.mod_verify([ss], n0["N"], [honest]) == [True]
+
+
 def test_fac_golden_and_rejections(pr, nodes, vec):
     n0, n1 = nodes[0], nodes[1]
     ss = bytes.fromhex(vec["session"])

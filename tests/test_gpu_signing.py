@@ -47,20 +47,26 @@ def fast_exp():
     M._pw = old
 
 
-@pytest.mark.parametrize("signers,trace", [(2, 2), (3, 1)])
-def test_signing_1000_wallets_matches_oracle(drv, nodes, fast_exp, signers, trace):
+@pytest.mark.parametrize("signers,wallets,trace", [(2, 10000, 6), (3, 1000, 3)])
+def test_signing_wallets_match_oracle(drv, nodes, fast_exp, signers, wallets, trace):
+    """Config 4 at its stated size for 2 signers (10,000 wallets, three
+    concurrent wallet pipelines by default): traced wallets are spread over the
+    batch, so every pipeline's sessions are compared with the oracle."""
     seed = 0x516E + signers
-    st, tr = drv.bench_signing(nodes, signers, 1000, seed=seed, trace_wallets=trace)
+    st, tr = drv.bench_signing(nodes, signers, wallets, seed=seed, trace_wallets=trace)
     assert st["errors"] == 0 and st["relation_failures"] == 0
-    assert st["signatures"] == 1000 and st["verified"] == 1000
-    assert st["sessions"] == 1000 * signers * (signers - 1)
+    assert st["signatures"] == wallets and st["verified"] == wallets
+    assert st["sessions"] == wallets * signers * (signers - 1)
     order = S.pair_order(signers)
-    for wi in range(trace):
+    assert tr["wallets"] == [t * wallets // trace for t in range(trace)]
+    if signers == 2:  # one traced wallet in each third (the default pipelines' chunks)
+        assert {wi * 3 // wallets for wi in tr["wallets"]} == {0, 1, 2}
+    for t, wi in enumerate(tr["wallets"]):
         pairs, sig, ok = S.sign_wallet(nodes, signers, seed, wi)
         assert ok
-        assert tr["sigs"][wi] == sig, wi
+        assert tr["sigs"][t] == sig, wi
         for p, ij in enumerate(order):
-            assert tr["pairs"][p][wi] == pairs[ij], (wi, ij)
+            assert tr["pairs"][p][t] == pairs[ij], (wi, ij)
 
 
 def test_keygen_reshare_5_parties(gpu, nodes):

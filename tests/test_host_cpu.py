@@ -55,3 +55,21 @@ def test_host_fails_loudly_without_gpu(hostlib):
         hostlib.init(0)
     with pytest.raises(mpcx.MpcxError):
         hostlib.modint_exp(65537, [3], 5)
+
+
+def test_host_pool_sized_from_affinity_and_quota(hostlib):
+    """Verdict r2 item 5: the host pool follows the CPUs the process may use
+    (affinity mask capped by the cgroup v2 CPU quota), 16 per bound GPU, not
+    min(16, hardware_concurrency)."""
+    if os.environ.get("MPCX_HOST_THREADS"):
+        pytest.skip("MPCX_HOST_THREADS overrides the pool size")
+    threads, usable = hostlib.host_threads()
+    want = len(os.sched_getaffinity(0))
+    try:
+        a, b = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if a != "max":
+            want = min(want, max(1, -(-int(a) // int(b))))
+    except (OSError, ValueError):
+        pass
+    assert usable == want
+    assert threads == min(usable, 16)  # no GPU bound here: one device's share
