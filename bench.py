@@ -702,7 +702,7 @@ def signing_line(args, world, rank, signers: int):
     if world > 1:
         dist.barrier()
     el = time.perf_counter() - t0
-    if st["errors"] or st["relation_failures"] or st["verified"] != args.wallets:
+    if st["errors"] or st["relation_failures"] or st["verified"] != args.wallets or st["aborted"]:
         raise SystemExit(f"rank {rank}: signing failed: {st}")
     el, r1, r2, r3, fin = max_over_ranks([el, st["round1_s"], st["round2_s"], st["round3_s"], st["finalize_s"]],
                                          world)
@@ -713,15 +713,18 @@ def signing_line(args, world, rank, signers: int):
             "signatures_verified": int(st["verified"]) * world,
             "rounds_s": {"round1_alice_init": r1, "round2_bob_mid": r2, "round3_alice_end": r3,
                          "rounds4_9_finalize_verify": fin},
+            "host_cpu_s_per_signature": host_cpu_s / args.wallets,
             "engine_busy_s": st["engine_busy_s"], "host_share": 1.0 - st["engine_busy_s"] / max(el, 1e-9),
             "host_cpu_s": host_cpu_s,
             "sessions_per_gpu": int(st["sessions"]),
-            "checked": "alpha+beta == k*gamma, mu+nu == k*w (mod q) on every session; ecdsa.Verify on every "
-                       "signature",
+            "checked": "alpha+beta == k*gamma, mu+nu == k*w (mod q) on every session; every round-1/4-9 "
+                       "commitment, Schnorr and ZKV proof of every signer; ecdsa.Verify of every signature by "
+                       "every signer (tss-lib finalize and mpcium's session)",
             "roofline": _job_roofline(st["alg_macs"], el, world),
             "alg_ops_per_signature": st["alg_macs"] / args.wallets,
-            "scope": "MtA/MtAwc + range proofs (rounds 1-3) on the GPU; signature algebra + ecdsa.Verify on the "
-                     "host; phase-5 commitments/Schnorr proofs (no Paillier work, no effect on (r, s)) not replayed",
+            "scope": "all of tss-lib's GG18 signing rounds: MtA/MtAwc + range proofs (rounds 1-3) on the GPU; "
+                     "round-1/5/7 commitments, round-4/6 Schnorr and ZKV proofs and their verification, "
+                     "finalize and ecdsa.Verify on the host",
             "cpu_baseline": None}
     prof = mhost.profile_report()
     if prof:  # MPCX_HOST_PROFILE=1: host seconds per label, summed over threads

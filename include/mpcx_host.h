@@ -231,32 +231,46 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
 
 /* Config-4 driver: one GG18 signature for each of `wallets` wallets, signed by
  * the first `signers` of `n_nodes` nodes (keys: Paillier private keys + own
- * DLN params with factors, width w). Plays every signer: rounds 1-3 MtA /
- * MtAwc of up:ecdsa/signing on the GPU (csrc/host/signing.hpp), checking
- * alpha + beta = k gamma and mu + nu = k w (mod q) for every session; then
- * delta, sigma, R = delta^-1 Gamma, r, s (low-s) and ecdsa.Verify of every
- * signature against the wallet key, as mpcium does when the party ends
- * (/root/reference/pkg/mpc/ecdsa_signing_session.go:162).
+ * DLN params with factors, width w). Plays every signer through all of tss-lib
+ * v2's signing rounds (csrc/host/signing.hpp): rounds 1-3 MtA / MtAwc of
+ * up:ecdsa/signing on the GPU, checking alpha + beta = k gamma and mu + nu = k w
+ * (mod q) for every session; the round-1 commitments, round-4 Schnorr proofs,
+ * round 5-9 commitments, Schnorr / ZKV proofs and their checks; then s
+ * (low-s) and ecdsa.Verify of every signature by every signer, twice (tss-lib's
+ * finalize and mpcium's session: /root/reference/pkg/mpc/ecdsa_signing_session.go:162).
  * stats_out[MPCXH_SIGNING_STATS]: round1_s, round2_s, round3_s, total_s,
  * wallets, sessions, errors, relation_failures, engine_busy_s (time inside
- * libmpcx calls), finalize_s, signatures, verified, alg_macs (Go-equivalent
- * algorithmic work of the exponentiations sent to the GPU).
+ * libmpcx calls), finalize_s (rounds 4-9 + finalize), signatures, verified,
+ * alg_macs (Go-equivalent algorithmic work of the exponentiations sent to the
+ * GPU), aborted (wallets whose transcript failed a check).
  * trace_wallets > 0: trace_out receives, for the wallets floor(t * wallets /
  * trace_wallets), t = 0 .. trace_wallets-1 (spread over every wallet pipeline),
  * per ordered pair (i-major) and wallet 40 words (alpha, beta, mu, nu as 8
  * words each, SHA512_256i over the session's cA, RangeProofAlice, cB,
- * ProofBob, cB', ProofBobWC fields), then per wallet 17 words (r, s, recid). */
-#define MPCXH_SIGNING_STATS 13
+ * ProofBob, cB', ProofBobWC fields), then per wallet 25 words (r, s, recid,
+ * SHA512_256i of the GG18 round 1/4-9 transcript). tamper_wallet >= 0 (test
+ * hook): corrupt signer 0's round-4 Schnorr proof (tamper_kind 1), round-6
+ * ZKV proof (2) or round-7 decommitment (3) in that wallet, which must abort. */
+#define MPCXH_SIGNING_STATS 14
 int mpcxh_bench_signing(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
                         uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out, uint32_t trace_wallets,
-                        uint32_t* trace_out);
+                        uint32_t* trace_out, int64_t tamper_wallet, int tamper_kind);
 
 /* Config-5 driver: the proof work of `sessions` keygen / reshare sessions of
  * n_parties nodes (csrc/host/keygenload.hpp): every party proves DLN x2,
  * Paillier-Blum Mod, and a Fac proof to each peer; every party verifies
- * every peer's proofs. Integers are w words wide (w >= 64).
- * stats_out[10]: prove_s, verify_s, total_s, sessions, parties, proofs,
- * verifications, failures, engine_busy_s, alg_macs. */
+ * every peer's proofs. Integers are w words wide (w >= 64). Sessions stream in
+ * waves of wave_sessions (0: 1024), two waves in flight: host memory is bounded
+ * by the waves, not by `sessions`.
+ * stats_out[MPCXH_KEYGEN_STATS]: prove_s, verify_s, total_s, sessions, parties,
+ * proofs, verifications, failures, engine_busy_s, alg_macs, waves,
+ * wave_sessions, max_wave_s.
+ * trace_out (NULL: none): per wave, one traced session of
+ * 1 + n(n+2)*8 + 1 words: its index, per party the 8-word SHA512_256i digests of
+ * its DLN (h1, h2, alpha), DLN (h2, h1, beta), Mod proof and its Fac proof to
+ * each peer (ascending), then the count of its verifications that passed
+ * (keygenload.hpp TraceSessionWords). */
+#define MPCXH_KEYGEN_STATS 13
 typedef struct {
   mpcxh_paillier_t paillier;  /* the party's own Paillier private key */
   const uint32_t* NTilde;
@@ -268,7 +282,7 @@ typedef struct {
   const uint32_t* q;
 } mpcxh_party_t;
 int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
-                              uint64_t seed, double* stats_out);
+                              uint64_t seed, uint32_t wave_sessions, double* stats_out, uint32_t* trace_out);
 
 /* Host-side helpers of the MtA path, exported as test hooks (no GPU needed):
  * common.SHA512_256i / SHA512_256i_TAGGED (tag == NULL: untagged) over count
@@ -307,6 +321,10 @@ int mpcxh_profile_report(char* buf, size_t cap, int reset);
  * (MPCX_HOST_THREADS, else min(usable CPUs, 16 per bound GPU)); *usable = the
  * CPUs this process may run on (affinity mask capped by the cgroup CPU quota). */
 int mpcxh_host_threads(int* threads, int* usable);
+/* Pool self-test (no GPU): `tasks` threads each run a parallel loop of `outer`
+ * indices, each index a nested parallel loop of `inner` indices adding
+ * (task+1)(o+1)(i+1); *sum = the total. */
+int mpcxh_pool_selftest(uint32_t tasks, uint32_t outer, uint32_t inner, uint64_t* sum);
 
 /* tss-lib candidate q from raw stream bytes (masking + delta walk; test hook). */
 int mpcxh_candidate_from_bytes(const uint8_t* bytes, size_t n, int q_bit_len, uint32_t* q_out, uint32_t words);

@@ -5,7 +5,9 @@
 #include "mpcx_host.h"
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
+#include <thread>
 #include <functional>
 #include <string>
 #include <vector>
@@ -343,6 +345,27 @@ int mpcxh_host_threads(int* threads, int* usable) {
   });
 }
 
+int mpcxh_pool_selftest(uint32_t tasks, uint32_t outer, uint32_t inner, uint64_t* sum) {
+  return guard([&] {
+    if (!sum) throw std::invalid_argument("null sum");
+    // `tasks` threads each run a parallel loop of `outer` indices whose every
+    // index runs a nested loop of `inner` indices (the drivers' shape: protocol
+    // tasks issuing parallel loops from inside parallel loops)
+    std::atomic<uint64_t> acc{0};
+    std::vector<std::thread> th;
+    for (uint32_t t = 0; t < tasks; ++t)
+      th.emplace_back([&, t] {
+        parallel_for(outer, [&](size_t o) {
+          std::atomic<uint64_t> part{0};
+          parallel_for(inner, [&](size_t i) { part += (uint64_t)(t + 1) * (o + 1) * (i + 1); });
+          acc += part.load();
+        });
+      });
+    for (auto& x : th) x.join();
+    *sum = acc.load();
+  });
+}
+
 int mpcxh_profile_report(char* buf, size_t cap, int reset) {
   return guard([&] {
     if (!buf || !cap) throw std::invalid_argument("null buffer");
@@ -593,7 +616,7 @@ int mpcxh_random_draws(uint64_t seed, const uint32_t* less_than, uint32_t w, int
 
 int mpcxh_bench_signing(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln_t* dlns, uint32_t n_nodes,
                         uint32_t signers, uint32_t wallets, uint64_t seed, double* stats_out, uint32_t trace_wallets,
-                        uint32_t* trace_out) {
+                        uint32_t* trace_out, int64_t tamper_wallet, int tamper_kind) {
   return guard([&] {
     check_width(w);
     if (!stats_out) throw std::invalid_argument("null stats_out");
@@ -604,11 +627,12 @@ int mpcxh_bench_signing(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln
       nodes[i].dln = dln_from(&dlns[i], w);
     }
     std::vector<uint32_t> tr;
-    const auto st = signing::RunSigning(nodes, (int)signers, wallets, seed, trace_wallets, &tr);
+    const auto st =
+        signing::RunSigning(nodes, (int)signers, wallets, seed, trace_wallets, &tr, tamper_wallet, tamper_kind);
     const double v[MPCXH_SIGNING_STATS] = {st.round1_s, st.round2_s, st.round3_s, st.total_s, (double)st.wallets,
                                            (double)st.sessions, (double)st.errors, (double)st.relation_failures,
                                            st.engine_busy_s, st.finalize_s, (double)st.signatures,
-                                           (double)st.verified, st.alg_macs};
+                                           (double)st.verified, st.alg_macs, (double)st.aborted};
     std::memcpy(stats_out, v, sizeof v);
     if (trace_wallets) std::memcpy(trace_out, tr.data(), tr.size() * sizeof(uint32_t));
   });
@@ -735,7 +759,7 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
 }  // extern "C"
 
 int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
-                              uint64_t seed, double* stats_out) {
+                              uint64_t seed, uint32_t wave_sessions, double* stats_out, uint32_t* trace_out) {
   return guard([&] {
     if (w < 64) throw std::invalid_argument("party integer width must be >= 64 words");
     if (!parties || !stats_out) throw std::invalid_argument("null argument");
@@ -753,10 +777,13 @@ int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t
       ps[i].p = Nat::from_words(a.p, w);
       ps[i].q = Nat::from_words(a.q, w);
     }
-    const auto st = keygenload::RunKeygenProofs(ps, sessions, seed);
-    const double v[10] = {st.prove_s, st.verify_s, st.total_s, (double)st.sessions, (double)st.parties,
-                          (double)st.proofs, (double)st.verifications, (double)st.failures, st.engine_busy_s,
-                          st.alg_macs};
+    std::vector<uint32_t> tr;
+    const auto st = keygenload::RunKeygenProofs(ps, sessions, seed, wave_sessions, trace_out ? &tr : nullptr);
+    const double v[MPCXH_KEYGEN_STATS] = {st.prove_s, st.verify_s, st.total_s, (double)st.sessions,
+                                          (double)st.parties, (double)st.proofs, (double)st.verifications,
+                                          (double)st.failures, st.engine_busy_s, st.alg_macs, (double)st.waves,
+                                          (double)st.wave_sessions, st.max_wave_s};
     std::memcpy(stats_out, v, sizeof v);
+    if (trace_out) std::memcpy(trace_out, tr.data(), tr.size() * sizeof(uint32_t));
   });
 }

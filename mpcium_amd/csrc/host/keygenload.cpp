@@ -50,73 +50,55 @@ void run_bounded(const std::vector<std::function<void()>>& tasks, size_t width) 
     if (e) std::rethrow_exception(e);
 }
 
-// one random stream per (session, party, proof kind, peer)
+// one random stream per (session, party, proof kind, peer) for sessions [lo, hi)
 struct Streams {
   std::vector<CounterDRBG> drbg;
   std::vector<RandFn> fn;
-  Streams(uint64_t seed, size_t sessions, uint64_t party, uint64_t kind) {
-    drbg.reserve(sessions);
-    for (size_t s = 0; s < sessions; ++s) drbg.emplace_back(mix(seed, s, party, kind));
+  Streams(uint64_t seed, size_t lo, size_t hi, uint64_t party, uint64_t kind) {
+    drbg.reserve(hi - lo);
+    for (size_t s = lo; s < hi; ++s) drbg.emplace_back(mix(seed, s, party, kind));
     for (auto& d : drbg) fn.push_back(d.fn());
   }
 };
 
+Nat digest(const std::vector<const Nat*>& v) { return SHA512_256i(v); }
+Nat dln_digest(const proofs::DLNProof& p) {
+  std::vector<const Nat*> v;
+  for (const auto& x : p.Alpha) v.push_back(&x);
+  for (const auto& x : p.T) v.push_back(&x);
+  return digest(v);
+}
+Nat mod_digest(const proofs::ModProof& p) {
+  std::vector<const Nat*> v{&p.W, &p.A, &p.B};
+  for (const auto& x : p.X) v.push_back(&x);
+  for (const auto& x : p.Z) v.push_back(&x);
+  return digest(v);
+}
+Nat fac_digest(const proofs::FacProof& p) {
+  const Nat vabs = p.V.mag, vneg(p.V.neg ? 1u : 0u);
+  return digest({&p.P, &p.Q, &p.A, &p.B, &p.T, &p.Sigma, &p.Z1, &p.Z2, &p.W1, &p.W2, &vabs, &vneg});
+}
+
 }  // namespace
 
-ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t sessions, uint64_t seed) {
+ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t sessions, uint64_t seed,
+                           size_t wave_sessions, std::vector<uint32_t>* trace) {
   const size_t n = parties.size();
   if (n < 2) throw std::invalid_argument("need at least two parties");
+  const size_t W = wave_sessions ? wave_sessions : kDefaultWave;
+  const size_t n_waves = sessions ? (sessions + W - 1) / W : 0;
   ProofStats st;
   st.sessions = sessions;
   st.parties = n;
-  // session ids (SSID bytes) shared by the parties of a session
-  std::vector<proofs::Bytes> sess(sessions);
-  {
-    CounterDRBG d(mix(seed, 0xFFFF, 0, 0));
-    for (auto& b : sess) {
-      b.resize(32);
-      d.read(b.data(), 32);
-    }
-  }
-  std::vector<std::vector<proofs::DLNProof>> dln1(n), dln2(n);
-  std::vector<std::vector<proofs::ModProof>> mod(n);
-  std::vector<std::vector<std::vector<proofs::FacProof>>> fac(n, std::vector<std::vector<proofs::FacProof>>(n));
-  std::vector<std::unique_ptr<Streams>> streams;
-  auto stream = [&](uint64_t party, uint64_t kind) -> const std::vector<RandFn>& {
-    streams.push_back(std::make_unique<Streams>(seed, sessions, party, kind));
-    return streams.back()->fn;
-  };
-  // streams are created up front (the task bodies only read them)
-  std::vector<const std::vector<RandFn>*> r_dln1(n), r_dln2(n), r_mod(n);
-  std::vector<std::vector<const std::vector<RandFn>*>> r_fac(n, std::vector<const std::vector<RandFn>*>(n));
-  for (size_t i = 0; i < n; ++i) {
-    r_dln1[i] = &stream(i, 1);
-    r_dln2[i] = &stream(i, 2);
-    r_mod[i] = &stream(i, 3);
-    for (size_t j = 0; j < n; ++j)
-      if (j != i) r_fac[i][j] = &stream(i, 16 + j);
-  }
-  const size_t width = 8;
-  const char* ce = std::getenv("MPCX_KEYGEN_CHAINS");
-  const bool chains = !(ce && ce[0] == '0');
-  std::atomic<uint64_t> fails{0};
-  auto count = [&](const std::vector<uint8_t>& ok) {
-    uint64_t f = 0;
-    for (auto v : ok) f += v == 0;
-    fails += f;
-  };
+  st.waves = n_waves;
+  st.wave_sessions = W;
   st.proofs = (uint64_t)sessions * n * (3 + (n - 1));
   st.verifications = (uint64_t)sessions * n * (n - 1) * 4;
-  // One chain per proof batch: prove, then every peer's verification of it.
-  // A verification depends only on its proof, so the chains run with no
-  // barrier between proving and verifying: one chain's host steps overlap
-  // another's GPU batches.
+  const size_t tw = TraceSessionWords(n);
+  if (trace) trace->assign(n_waves * tw, 0);
+  std::atomic<uint64_t> fails{0};
   std::mutex tm;
-  double last_prove = 0;
-  auto proved = [&] {
-    std::lock_guard<std::mutex> lk(tm);
-    last_prove = std::max(last_prove, now());
-  };
+  double last_prove = 0, max_wave = 0;
   // lane budget of this workload (MPCX_KEYGEN_LANES, default 8: its many small
   // independent chains overlap better; measured +10-15% over 4), restored after
   const char* kl = std::getenv("MPCX_KEYGEN_LANES");
@@ -133,9 +115,52 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
       }
     }
   } budget(lanes);
-  Engine::get().reset_busy();
-  const double t0 = now();
-  {
+
+  // One wave [lo, hi): one chain per proof batch -- prove, then every peer's
+  // verification of it (no barrier between proving and verifying: one chain's
+  // host steps overlap another's GPU batches); the wave's proofs are dropped
+  // when it returns.
+  auto run_wave = [&](size_t w) {
+    const size_t lo = w * W, hi = std::min(sessions, lo + W), m = hi - lo;
+    const double w0 = now();
+    std::vector<proofs::Bytes> sess(m);  // SSID bytes shared by the parties of a session
+    {
+      CounterDRBG d(mix(seed, 0xFFFF, 0, 0));
+      d.seek((uint64_t)lo * 32);
+      for (auto& b : sess) {
+        b.resize(32);
+        d.read(b.data(), 32);
+      }
+    }
+    std::vector<std::unique_ptr<Streams>> streams;
+    auto stream = [&](uint64_t party, uint64_t kind) -> const std::vector<RandFn>& {
+      streams.push_back(std::make_unique<Streams>(seed, lo, hi, party, kind));
+      return streams.back()->fn;
+    };
+    std::vector<const std::vector<RandFn>*> r_dln1(n), r_dln2(n), r_mod(n);
+    std::vector<std::vector<const std::vector<RandFn>*>> r_fac(n, std::vector<const std::vector<RandFn>*>(n));
+    for (size_t i = 0; i < n; ++i) {
+      r_dln1[i] = &stream(i, 1);
+      r_dln2[i] = &stream(i, 2);
+      r_mod[i] = &stream(i, 3);
+      for (size_t j = 0; j < n; ++j)
+        if (j != i) r_fac[i][j] = &stream(i, 16 + j);
+    }
+    std::vector<std::vector<proofs::DLNProof>> dln1(n), dln2(n);
+    std::vector<std::vector<proofs::ModProof>> mod(n);
+    std::vector<std::vector<std::vector<proofs::FacProof>>> fac(n, std::vector<std::vector<proofs::FacProof>>(n));
+    const size_t ts = TracedSession(w, lo, hi) - lo;  // traced session within the wave
+    std::atomic<uint32_t> traced_ok{0};
+    auto count = [&](const std::vector<uint8_t>& ok) {
+      uint64_t f = 0;
+      for (auto v : ok) f += v == 0;
+      fails += f;
+      traced_ok += ok[ts] != 0;
+    };
+    auto proved = [&] {
+      std::lock_guard<std::mutex> lk(tm);
+      last_prove = std::max(last_prove, now());
+    };
     std::vector<std::function<void()>> tasks;
     for (size_t i = 0; i < n; ++i) {
       const PartyKeys& P = parties[i];
@@ -167,36 +192,48 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
         });
       }
     }
-    if (chains) {
-      run_bounded(tasks, width);
-    } else {  // every proof first, then every verification (MPCX_KEYGEN_CHAINS=0)
-      std::vector<std::function<void()>> prove, verify;
+    run_bounded(tasks, 8);
+    if (trace) {
+      uint32_t* o = trace->data() + w * tw;
+      o[0] = (uint32_t)(lo + ts);
+      uint32_t* d = o + 1;
       for (size_t i = 0; i < n; ++i) {
-        const PartyKeys& P = parties[i];
-        prove.push_back([&, i] { dln1[i] = proofs::DLNProveBatch(P.h1, P.h2, P.alpha, P.p, P.q, P.NTilde, *r_dln1[i]); });
-        prove.push_back([&, i] { dln2[i] = proofs::DLNProveBatch(P.h2, P.h1, P.beta, P.p, P.q, P.NTilde, *r_dln2[i]); });
-        prove.push_back([&, i] { mod[i] = proofs::ModProveBatch(sess, P.sk.pub.N, P.sk.P, P.sk.Q, *r_mod[i]); });
-        for (size_t j = 0; j < n; ++j) {
-          if (j == i) continue;
-          const PartyKeys& V = parties[j];
-          prove.push_back([&, i, j] {
-            fac[i][j] = proofs::FacProveBatch(sess, P.sk.pub.N, V.NTilde, V.h1, V.h2, P.sk.P, P.sk.Q, *r_fac[i][j]);
-          });
-          verify.push_back([&, i] { count(proofs::DLNVerifyBatch(P.h1, P.h2, P.NTilde, dln1[i])); });
-          verify.push_back([&, i] { count(proofs::DLNVerifyBatch(P.h2, P.h1, P.NTilde, dln2[i])); });
-          verify.push_back([&, i] { count(proofs::ModVerifyBatch(sess, P.sk.pub.N, mod[i])); });
-          verify.push_back([&, i, j] { count(proofs::FacVerifyBatch(sess, P.sk.pub.N, V.NTilde, V.h1, V.h2, fac[i][j])); });
-        }
+        dln_digest(dln1[i][ts]).to_words(d, 8);
+        dln_digest(dln2[i][ts]).to_words(d + 8, 8);
+        mod_digest(mod[i][ts]).to_words(d + 16, 8);
+        d += 24;
+        for (size_t j = 0; j < n; ++j)
+          if (j != i) {
+            fac_digest(fac[i][j][ts]).to_words(d, 8);
+            d += 8;
+          }
       }
-      run_bounded(prove, width);
-      proved();
-      run_bounded(verify, width);
+      *d = traced_ok.load();
     }
+    std::lock_guard<std::mutex> lk(tm);
+    max_wave = std::max(max_wave, now() - w0);
+  };
+
+  Engine::get().reset_busy();
+  const double t0 = now();
+  {  // kWavesInFlight workers take the waves in order
+    std::atomic<size_t> next{0};
+    std::vector<std::function<void()>> workers;
+    for (size_t k = 0; k < std::min(kWavesInFlight, n_waves); ++k)
+      workers.push_back([&] {
+        for (;;) {
+          const size_t w = next.fetch_add(1);
+          if (w >= n_waves) return;
+          run_wave(w);
+        }
+      });
+    run_bounded(workers, workers.size());
   }
   const double t2 = now();
-  st.prove_s = last_prove - t0;  // until the last proof batch was done
-  st.verify_s = t2 - last_prove;  // verification tail after it
+  st.prove_s = std::max(0.0, last_prove - t0);  // until the last proof batch was done
+  st.verify_s = t2 - std::max(t0, last_prove);  // verification tail after it
   st.total_s = t2 - t0;
+  st.max_wave_s = max_wave;
   st.failures = fails.load();
   st.engine_busy_s = Engine::get().busy_seconds();
   st.alg_macs = Engine::get().alg_macs();

@@ -41,8 +41,32 @@ struct ProofStats {
   double alg_macs = 0;  // Go-equivalent algorithmic work sent to the GPU (Engine::alg_macs)
   uint64_t sessions = 0, parties = 0, proofs = 0, verifications = 0;
   uint64_t failures = 0;  // verifications that did not pass (honest proofs: must be 0)
+  uint64_t waves = 0, wave_sessions = 0;
+  double max_wave_s = 0;  // slowest wave, prove + verify
 };
 
-ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t sessions, uint64_t seed);
+// Sessions stream through in waves of `wave_sessions` (<= 0: kDefaultWave),
+// kWavesInFlight at a time: a wave's proofs are built, verified by every peer
+// and dropped before a later wave starts, so host memory is bounded by the
+// waves in flight (~0.9 MB of proofs per 5-party session), not by `sessions`
+// -- mpcium's keygen / reshare consumers run sessions as they arrive
+// (/root/reference/pkg/eventconsumer/event_consumer.go:103-204,375-518).
+// Every session's streams and session id are functions of (seed, session
+// index), so the wave size changes no proof.
+constexpr size_t kDefaultWave = 1024;
+constexpr size_t kWavesInFlight = 2;
+
+// Trace of one session per wave (parity tests): session
+// TracedSession(w, lo, hi) of wave w = [lo, hi), then per party i: 8-word
+// digests SHA512_256i of its DLN proof (h1, h2, alpha) (Alpha[], T[]), its DLN
+// proof (h2, h1, beta), its ModProof (W, A, B, X[], Z[]), and per peer j != i
+// (ascending) of its FacProof to j (P, Q, A, B, T, Sigma, Z1, Z2, W1, W2, |V|,
+// V < 0); a final word = the number of that session's verifications that
+// passed.
+inline size_t TraceSessionWords(size_t n) { return 1 + n * (3 + (n - 1)) * 8 + 1; }
+inline size_t TracedSession(size_t wave, size_t lo, size_t hi) { return lo + (wave * 7919u) % (hi - lo); }
+
+ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t sessions, uint64_t seed,
+                           size_t wave_sessions = 0, std::vector<uint32_t>* trace = nullptr);
 
 }  // namespace mpcx::host::keygenload

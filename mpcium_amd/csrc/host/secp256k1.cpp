@@ -2,6 +2,7 @@
 #include "secp256k1.hpp"
 
 #include "hostprof.hpp"
+#include "tsscommon.hpp"
 
 #include <algorithm>
 #include <vector>
@@ -492,6 +493,31 @@ Affine ScalarMult(const Affine& p, const Nat& k) {
 Affine LinComb(const Nat& u1, const Affine& X, const Nat& u2) {
   MPCX_PROF("ec.lincomb");
   return to_affine(add_base_mult(var_mult(X, scalar_limbs(u2)), scalar_limbs(u1)));
+}
+
+const Affine& Generator() { return generator(); }
+
+const Nat& FieldP() {
+  static const Nat p = Nat::from_hex("FFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEFFFFFC2F");
+  return p;
+}
+
+Affine Combine(const Nat& a, const Affine& P, const Nat& b, const Affine& Q, const Nat& c) {
+  MPCX_PROF("ec.combine");
+  Jac acc;
+  if (!b.is_zero() && !P.inf) acc = var_mult(P, scalar_limbs(b));
+  if (!c.is_zero() && !Q.inf) acc = jac_add(acc, var_mult(Q, scalar_limbs(c)));
+  if (!a.is_zero()) acc = add_base_mult(acc, scalar_limbs(a));
+  return to_affine(acc);
+}
+
+std::vector<Affine> CombineBatch(const std::vector<Comb>& items) {
+  std::vector<Affine> out(items.size());
+  parallel_for(items.size(), [&](size_t i) {
+    const Comb& t = items[i];
+    out[i] = Combine(t.a, t.P, t.b, t.Q, t.c);
+  });
+  return out;
 }
 
 }  // namespace mpcx::host::secp

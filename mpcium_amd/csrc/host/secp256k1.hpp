@@ -12,6 +12,7 @@
 
 #include <array>
 #include <cstdint>
+#include <vector>
 
 #include "bignum.hpp"
 
@@ -25,6 +26,8 @@ struct Affine {
 };
 
 extern const Nat& CurveN();  // group order n (= q in tss-lib)
+const Affine& Generator();   // G
+const Nat& FieldP();         // p = 2^256 - 2^32 - 977
 
 // k*G, k reduced mod n
 Affine ScalarBaseMult(const Nat& k);
@@ -33,6 +36,16 @@ Affine ScalarMult(const Affine& P, const Nat& k);
 Affine Add(const Affine& P, const Affine& Q);
 // u1*G + u2*X (both scalars reduced mod n) with one affine conversion
 Affine LinComb(const Nat& u1, const Affine& X, const Nat& u2);
+// a*G + b*P + c*Q (scalars reduced mod n; a zero scalar or an infinite point
+// drops its term): every point equation of GG18's rounds 5-9 and of the
+// Schnorr proofs is one of these
+Affine Combine(const Nat& a, const Affine& P, const Nat& b, const Affine& Q, const Nat& c);
+struct Comb {
+  Nat a, b, c;
+  Affine P, Q;
+};
+// Combine over a batch of independent items (parallel over the host pool)
+std::vector<Affine> CombineBatch(const std::vector<Comb>& items);
 bool IsOnCurve(const Affine& P);
 bool Equal(const Affine& P, const Affine& Q);
 

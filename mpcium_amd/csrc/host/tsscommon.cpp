@@ -502,21 +502,15 @@ class HostPool {
           break;
         }
     }
-    // Every index was taken and no worker can pick the loop up any more. Until
-    // the indices still running elsewhere finish (and the workers leave it),
-    // help with other loops' pending indices, else sleep on the completion
-    // signal -- no spinning: many protocol tasks wait here at once.
-    for (;;) {
-      if (l.done.load() >= l.n && l.users.load() == 0) return;
-      Loop* o = take();
-      if (o) {
-        finish(o, o->work());
-        continue;
-      }
-      std::unique_lock<std::mutex> lk(done_mu_);
-      done_cv_.wait_for(lk, std::chrono::microseconds(500),
-                        [&] { return l.done.load() >= l.n && l.users.load() == 0; });
-    }
+    // Every index was taken and no worker can pick the loop up any more: sleep
+    // on the completion signal until the indices still running elsewhere finish
+    // and the workers leave the loop (no spinning: many protocol tasks wait here
+    // at once). The waiter does not run other loops' indices meanwhile: with
+    // nested loops that recursion would be unbounded (a worker inside an outer
+    // index helping the outer loop again, one stack frame set per index).
+    std::unique_lock<std::mutex> lk(done_mu_);
+    while (!(l.done.load() >= l.n && l.users.load() == 0))
+      done_cv_.wait_for(lk, std::chrono::milliseconds(2));
   }
 
  private:
@@ -541,12 +535,6 @@ class HostPool {
     for (Loop* x : loops_)
       if (x->next.load() < x->n) return x;
     return nullptr;
-  }
-  Loop* take() {
-    std::lock_guard<std::mutex> lk(mu_);
-    Loop* l = pending_locked();
-    if (l) l->users.fetch_add(1);
-    return l;
   }
   // a worker leaves loop l (last: it completed l's final index)
   void finish(Loop* l, bool last) {

@@ -597,8 +597,9 @@ int mpcx_set_option(const char* key, int value) {
     if (value < 1 || value > kMaxLanes) return fail(MPCX_EINVAL, "lanes %d outside [1, %d]", value, kMaxLanes);
     g_lanes = value;
   } else if (std::strcmp(key, "geom_policy") == 0) {
-    // 1: the 4096-bit class picks main / mid / narrow by the launch-time model; 0: thresholds
-    if (value < 0 || value > 1) return fail(MPCX_EINVAL, "geom_policy %d out of range", value);
+    // 1: the 4096-bit class picks main / mid / narrow by the launch-time model; 0: thresholds;
+    // 2: the main geometry for every batch
+    if (value < 0 || value > 2) return fail(MPCX_EINVAL, "geom_policy %d out of range", value);
     g_geom_policy = value;
   } else if (std::strcmp(key, "main_geom") == 0) {
     // main (throughput) geometry of the geometry's class
@@ -637,7 +638,7 @@ static void read_env_options() {
   const char* pc = std::getenv("MPCX_PRIME_COOP");
   if (pc) g_prime_coop = pc[0] != '0';
   const char* gp = std::getenv("MPCX_GEOM_POLICY");
-  if (gp) g_geom_policy = gp[0] == '0' ? 0 : 1;
+  if (gp) g_geom_policy = std::max(0, std::min(2, std::atoi(gp)));
   const char* ln = std::getenv("MPCX_LANES");
   if (ln && g_ndev.load() == 0) g_lanes = std::max(1, std::min(kMaxLanes, std::atoi(ln)));
 }
@@ -846,7 +847,11 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     // spread over the narrow geometry's 3x more wavefronts; from ~0.3 rounds up
     // the main geometry wins, and a narrow tail launch did not pay.
     const int gmid = MPCX_MID_GEOM(mod->cls);
-    if (g_geom_policy == 1 && gmid >= 0 && gn >= 0) {
+    if (g_geom_policy == 2) {
+      // throughput: the main geometry at every size (concurrent launches from
+      // other lanes fill the SIMDs a small batch leaves idle)
+      parts[nparts++] = {gm, 0, count};
+    } else if (g_geom_policy == 1 && gmid >= 0 && gn >= 0) {
       parts[nparts++] = {fastest_geom(mod->cls, count, dev.num_cus * 4), 0, count};
     } else if (gn >= 0 && rounds < g_narrow_rounds) {
       parts[nparts++] = {gn, 0, count};

@@ -68,6 +68,7 @@ SIGNATURES = [
     ("mpcxh_coprime_batch", _i, [_u32, _vp, _vp, _u32, _vp]),
     ("mpcxh_profile_report", _i, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("mpcxh_host_threads", _i, [_vp, _vp]),
+    ("mpcxh_pool_selftest", _i, [_u32, _u32, _u32, _vp]),
     ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
     ("mpcxh_go_rand_int63", _i, [ctypes.c_int64, _u32, _vp]),
     ("mpcxh_go_mr_bases", _i, [_vp, _u32, _u32, _vp]),
@@ -240,6 +241,12 @@ def host_threads() -> tuple:
     t, u = ctypes.c_int(0), ctypes.c_int(0)
     _check(lib().mpcxh_host_threads(ctypes.byref(t), ctypes.byref(u)))
     return t.value, u.value
+
+
+def pool_selftest(tasks: int, outer: int, inner: int) -> int:
+    s = ctypes.c_uint64(0)
+    _check(lib().mpcxh_pool_selftest(tasks, outer, inner, ctypes.byref(s)))
+    return s.value
 
 
 def profile_report(reset: bool = False) -> str:

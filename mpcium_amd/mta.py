@@ -48,7 +48,7 @@ SIGNATURES = [
     ("mpcxh_secp_scalar_mult", _i, [_vp, _vp, _u32, _vp]),
     ("mpcxh_secp_lincomb", _i, [_vp, _vp, _vp, _u32, _vp]),
     ("mpcxh_random_draws", _i, [_u64, _vp, _u32, _i, _u32, _vp]),
-    ("mpcxh_bench_signing", _i, [_u32, _vp, _vp, _u32, _u32, _u32, _u64, _vp, _u32, _vp]),
+    ("mpcxh_bench_signing", _i, [_u32, _vp, _vp, _u32, _u32, _u32, _u64, _vp, _u32, _vp, ctypes.c_int64, _i]),
 ]
 
 _bound = False
@@ -328,19 +328,22 @@ def random_draws(seed: int, less_than: int, count: int, relprime: bool = False) 
 
 
 SIGNING_STATS = ["round1_s", "round2_s", "round3_s", "total_s", "wallets", "sessions", "errors",
-                 "relation_failures", "engine_busy_s", "finalize_s", "signatures", "verified", "alg_macs"]
+                 "relation_failures", "engine_busy_s", "finalize_s", "signatures", "verified", "alg_macs", "aborted"]
+TAMPER_R4_SCHNORR, TAMPER_R6_ZKV, TAMPER_R7_DECOMMIT = 1, 2, 3  # signing.hpp kTamper*
 
 
 def bench_signing(nodes: Sequence[Dict[str, int]], signers: int, wallets: int, seed: int = 0x5167,
-                  trace_wallets: int = 0):
+                  trace_wallets: int = 0, tamper: Optional[Tuple[int, int]] = None):
     """Config-4 driver (csrc/host/signing.hpp): one GG18 signature for each of
-    `wallets` wallets -- MtA / MtAwc on the GPU, then the signature and
-    ecdsa.Verify. nodes: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i, p, q
-    (node_preparams.json fields). Returns the stats dict, and with
+    `wallets` wallets -- MtA / MtAwc on the GPU, rounds 1/4-9 (commitments,
+    Schnorr and ZKV proofs, their checks), the signature and ecdsa.Verify.
+    nodes: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i, p, q
+    (node_preparams.json fields). tamper = (wallet, kind): corrupt that
+    wallet's transcript (TAMPER_*; test hook). Returns the stats dict, and with
     trace_wallets > 0 also the trace of the wallets t * wallets // trace_wallets
     (t < trace_wallets; spread over every concurrent wallet pipeline):
     {"wallets": [index], "pairs": [[{alpha, beta, mu, nu, digest} per traced
-    wallet] per ordered pair], "sigs": [(r, s, recid)]}."""
+    wallet] per ordered pair], "sigs": [(r, s, recid)], "gg18": [digest]}."""
     k = _Keep()
     sks = (PaillierKey * len(nodes))(*[_paillier(k, n["N"], n["LambdaN"], n["P"], n["Q"]) for n in nodes])
     dlns = (DLN * len(nodes))(*[_dln(k, {"NTilde": n["NTildei"], "h1": n["H1i"], "h2": n["H2i"],
@@ -348,9 +351,10 @@ def bench_signing(nodes: Sequence[Dict[str, int]], signers: int, wallets: int, s
     st = np.zeros(len(SIGNING_STATS), dtype=np.float64)
     npairs = signers * (signers - 1)
     tw = min(trace_wallets, wallets)
-    tr = np.zeros(max(1, npairs * tw * 40 + tw * 17), dtype="<u4")
+    tr = np.zeros(max(1, npairs * tw * 40 + tw * 25), dtype="<u4")
+    tw_idx, tk = tamper if tamper else (-1, 0)
     _check(lib().mpcxh_bench_signing(W, sks, dlns, len(nodes), signers, wallets, seed, st.ctypes.data, tw,
-                                     tr.ctypes.data if tw else None))
+                                     tr.ctypes.data if tw else None, tw_idx, tk))
     stats = dict(zip(SIGNING_STATS, [float(x) for x in st]))
     if not tw:
         return stats
@@ -363,12 +367,13 @@ def bench_signing(nodes: Sequence[Dict[str, int]], signers: int, wallets: int, s
             rows.append({"alpha": a, "beta": b, "mu": m, "nu": n_, "digest": d})
         pairs.append(rows)
     base = npairs * tw * 40
-    sigs = []
+    sigs, gg = [], []
     for wi in range(tw):
-        o = base + wi * 17
+        o = base + wi * 25
         r, s = words_to_ints(tr[o:o + 16].reshape(2, 8))
-        sigs.append((r, s, int(tr[o + 16])))
-    return stats, {"wallets": [t * wallets // tw for t in range(tw)], "pairs": pairs, "sigs": sigs}
+        sigs.append((r, s, int(tr[o + 16])) if r else None)
+        gg.append(words_to_ints(tr[o + 17:o + 25].reshape(1, 8))[0] if r else None)
+    return stats, {"wallets": [t * wallets // tw for t in range(tw)], "pairs": pairs, "sigs": sigs, "gg18": gg}
 
 
 def bench_signing_mta(nodes, signers: int, wallets: int, seed: int = 0x5167) -> dict:

@@ -27,7 +27,7 @@ SIGNATURES = [
     ("mpcxh_mod_verify_batch", _i, [_u32, _vp, _u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("mpcxh_fac_prove_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("mpcxh_fac_verify_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
-    ("mpcxh_bench_keygen_proofs", _i, [_u32, _vp, _u32, _u32, _u64, _vp]),
+    ("mpcxh_bench_keygen_proofs", _i, [_u32, _vp, _u32, _u32, _u64, _u32, _vp, _vp]),
 ]
 _bound = False
 
@@ -150,10 +150,19 @@ class _Party(ctypes.Structure):
                 ("alpha", _vp), ("beta", _vp), ("p", _vp), ("q", _vp)]
 
 
-def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B67) -> dict:
+KEYGEN_STATS = ["prove_s", "verify_s", "total_s", "sessions", "parties", "proofs", "verifications", "failures",
+                "engine_busy_s", "alg_macs", "waves", "wave_sessions", "max_wave_s"]
+
+
+def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B67, wave: int = 0,
+                        trace: bool = False):
     """Config-5 driver (csrc/host/keygenload.hpp): the DLN / Mod / Fac proof
-    work of `sessions` keygen or reshare sessions of len(parties) nodes.
-    parties: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i, Alpha, Beta, p, q."""
+    work of `sessions` keygen or reshare sessions of len(parties) nodes,
+    streamed in waves of `wave` sessions (0: the driver's default, 1024), two
+    waves in flight. parties: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i,
+    Alpha, Beta, p, q. trace: also return one traced session per wave --
+    [{"session": s, "digests": {(i, "dln1"|"dln2"|"mod"): d, (i, "fac", j): d},
+    "verified": count}]."""
     keep = []
 
     def ptr(v):
@@ -165,9 +174,29 @@ def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B
     for k, n in enumerate(parties):
         arr[k] = _Party(ptr(n["N"]), ptr(n["LambdaN"]), ptr(n["P"]), ptr(n["Q"]), ptr(n["NTildei"]), ptr(n["H1i"]),
                         ptr(n["H2i"]), ptr(n["Alpha"]), ptr(n["Beta"]), ptr(n["p"]), ptr(n["q"]))
-    st = np.zeros(10, dtype=np.float64)
-    rc = lib().mpcxh_bench_keygen_proofs(W, arr, len(parties), sessions, seed, st.ctypes.data)
+    st = np.zeros(len(KEYGEN_STATS), dtype=np.float64)
+    n = len(parties)
+    wv = wave or 1024
+    n_waves = (sessions + wv - 1) // wv
+    tw = 1 + n * (3 + (n - 1)) * 8 + 1
+    tr = np.zeros(max(1, n_waves * tw), dtype="<u4")
+    rc = lib().mpcxh_bench_keygen_proofs(W, arr, n, sessions, seed, wave, st.ctypes.data,
+                                         tr.ctypes.data if trace else None)
     _host._check(rc)
-    keys = ["prove_s", "verify_s", "total_s", "sessions", "parties", "proofs", "verifications", "failures",
-            "engine_busy_s", "alg_macs"]
-    return dict(zip(keys, [float(x) for x in st]))
+    stats = dict(zip(KEYGEN_STATS, [float(x) for x in st]))
+    if not trace:
+        return stats
+    out = []
+    for w in range(n_waves):
+        o = tr[w * tw:(w + 1) * tw]
+        d, k = {}, 1
+        for i in range(n):
+            for kind in ("dln1", "dln2", "mod"):
+                d[(i, kind)] = words_to_ints(o[k:k + 8].reshape(1, 8))[0]
+                k += 8
+            for j in range(n):
+                if j != i:
+                    d[(i, "fac", j)] = words_to_ints(o[k:k + 8].reshape(1, 8))[0]
+                    k += 8
+        out.append({"session": int(o[0]), "digests": d, "verified": int(o[k])})
+    return stats, out

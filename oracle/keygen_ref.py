@@ -1,0 +1,62 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import
+this module.  The product path (mpcium_amd/) never imports it.
+
+One session of the config-5 keygen / reshare proof driver
+(mpcium_amd/csrc/host/keygenload.hpp): every party i proves DLN (h1, h2, alpha),
+DLN (h2, h1, beta), the Paillier-Blum Mod proof of N_i and a Fac proof of N_i to
+every peer j over (N~_j, h1_j, h2_j) -- oracle/proofs_ref.py restates each
+(tss-lib up:crypto/dlnproof, up:crypto/modproof, up:crypto/facproof) -- drawn
+from the driver's per-(session, party, kind) streams, with the session id the
+driver assigns; plus the per-proof SHA512_256i digests its trace records.
+"""
+from __future__ import annotations
+
+from typing import Dict, Sequence
+
+from . import proofs_ref as PR
+from . import tss_ref as T
+from .gomath import CounterDRBG
+from .signing_ref import mix
+
+
+def session_id(seed: int, s: int) -> bytes:
+    """keygenload.cpp: 32 bytes per session from CounterDRBG(mix(seed, 0xFFFF, 0, 0))."""
+    return CounterDRBG(mix(seed, 0xFFFF, 0, 0)).read(32 * (s + 1))[32 * s:]
+
+
+def _dln_digest(p: PR.DLNProof) -> int:
+    return T.sha512_256i(*p.Alpha, *p.T)
+
+
+def _mod_digest(p: PR.ModProof) -> int:
+    return T.sha512_256i(p.W, p.A, p.B, *p.X, *p.Z)
+
+
+def _fac_digest(p: PR.FacProof) -> int:
+    return T.sha512_256i(p.P, p.Q, p.A, p.B, p.T, p.Sigma, p.Z1, p.Z2, p.W1, p.W2, abs(p.V), 1 if p.V < 0 else 0)
+
+
+def session_digests(parties: Sequence[Dict[str, int]], seed: int, s: int, verify: bool = True):
+    """-> ({(i, "dln1"|"dln2"|"mod"): digest, (i, "fac", j): digest}, verifications passed)."""
+    n = len(parties)
+    ss = session_id(seed, s)
+    out, passed = {}, 0
+    for i, P in enumerate(parties):
+        d1 = PR.dln_prove(P["H1i"], P["H2i"], P["Alpha"], P["p"], P["q"], P["NTildei"], T.Reader(mix(seed, s, i, 1)))
+        d2 = PR.dln_prove(P["H2i"], P["H1i"], P["Beta"], P["p"], P["q"], P["NTildei"], T.Reader(mix(seed, s, i, 2)))
+        md = PR.mod_prove(ss, P["N"], P["P"], P["Q"], T.Reader(mix(seed, s, i, 3)))
+        out[(i, "dln1")], out[(i, "dln2")], out[(i, "mod")] = _dln_digest(d1), _dln_digest(d2), _mod_digest(md)
+        if verify:  # every peer runs the same verification of i's broadcast proofs
+            ok = (PR.dln_verify(d1, P["H1i"], P["H2i"], P["NTildei"]) + PR.dln_verify(d2, P["H2i"], P["H1i"], P["NTildei"])
+                  + PR.mod_verify(md, ss, P["N"]))
+            passed += (n - 1) * ok
+        for j, V in enumerate(parties):
+            if j == i:
+                continue
+            fp = PR.fac_prove(ss, P["N"], V["NTildei"], V["H1i"], V["H2i"], P["P"], P["Q"], T.Reader(mix(seed, s, i, 16 + j)))
+            out[(i, "fac", j)] = _fac_digest(fp)
+            if verify:
+                passed += PR.fac_verify(fp, ss, P["N"], V["NTildei"], V["H1i"], V["H2i"])
+    return out, passed

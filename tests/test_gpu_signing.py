@@ -6,10 +6,13 @@ Config 4 (csrc/host/signing.hpp, mpcxh_bench_signing): 1,000 wallets signed by
 and mu + nu = k w on every session and ecdsa.Verify on every signature; sampled
 wallets are recomputed by the oracle (oracle/signing_ref.py) and compared field
 by field: every pair's alpha, beta, mu, nu, a digest of the whole session
-transcript (cA, both proofs, cB, cB'), and the signature (r, s, recid).
+transcript (cA, both proofs, cB, cB'), a digest of the GG18 round 1/4-9
+transcript (commitments, Schnorr and ZKV proofs, s_i) and the signature
+(r, s, recid). A tampered proof or decommitment aborts its wallet only.
 
 Config 5 (csrc/host/keygenload.hpp): 5-party keygen / reshare proof work
-(3-of-5), every proof verified."""
+(3-of-5), streamed in waves, every proof verified, one session per wave
+compared with the oracle (oracle/keygen_ref.py)."""
 import json
 import os
 
@@ -61,29 +64,75 @@ def test_signing_wallets_match_oracle(drv, nodes, fast_exp, signers, wallets, tr
     assert tr["wallets"] == [t * wallets // trace for t in range(trace)]
     if signers == 2:  # one traced wallet in each third (the default pipelines' chunks)
         assert {wi * 3 // wallets for wi in tr["wallets"]} == {0, 1, 2}
+    assert st["aborted"] == 0
     for t, wi in enumerate(tr["wallets"]):
-        pairs, sig, ok = S.sign_wallet(nodes, signers, seed, wi)
+        pairs, sig, ok, gg18 = S.sign_wallet(nodes, signers, seed, wi)
         assert ok
         assert tr["sigs"][t] == sig, wi
+        assert tr["gg18"][t] == gg18, wi  # rounds 1, 4-9: commitments, Schnorr / ZKV proofs, s_i
         for p, ij in enumerate(order):
             assert tr["pairs"][p][t] == pairs[ij], (wi, ij)
 
 
-def test_keygen_reshare_5_parties(gpu, nodes):
-    """Config 5's shape: 3-of-5 keygen / reshare proof work. The 3 fixture nodes
-    plus 2 nodes whose preparams come from the GPU GeneratePreParams; every
-    party proves DLN x2, Mod and a Fac proof per peer, and verifies every
-    peer's proofs."""
+@pytest.mark.parametrize("kind", [1, 2, 3])
+def test_tampered_transcript_aborts_only_its_wallet(drv, nodes, fast_exp, kind):
+    """A corrupted round-4 Schnorr proof, round-6 ZKV proof or round-7
+    decommitment of one signer in one wallet aborts that wallet only (the
+    oracle aborts it too); every other wallet is signed and verified, and a
+    traced honest wallet still matches the oracle."""
+    seed, wallets, bad = 0x7A3F, 96, 37
+    st, tr = drv.bench_signing(nodes, 2, wallets, seed=seed, trace_wallets=2, tamper=(bad, kind))
+    assert st["errors"] == 0 and st["relation_failures"] == 0
+    assert st["aborted"] == 1 and st["signatures"] == wallets - 1 and st["verified"] == wallets - 1
+    _, sig, ok, _ = S.sign_wallet(nodes, 2, seed, bad, tamper=kind)
+    assert sig is None and not ok
+    pairs, sig, ok, gg18 = S.sign_wallet(nodes, 2, seed, tr["wallets"][1])
+    assert ok and tr["sigs"][1] == sig and tr["gg18"][1] == gg18
+
+
+@pytest.fixture(scope="module")
+def five_parties(drv, nodes):
+    """The 3 fixture nodes plus 2 nodes whose preparams come from the GPU
+    GeneratePreParams (config 5 is 3-of-5)."""
     from mpcium_amd import host as mhost
-    from mpcium_amd import proofs as mproofs
-    mhost.init(0)
     parties = list(nodes)
     for seed in (0x6D706335, 0x6D706336):
         pp, _ = mhost.generate_preparams(seed=seed)
         assert pp["N"] == pp["P"] * pp["Q"] and pp["NTildei"] == (2 * pp["p"] + 1) * (2 * pp["q"] + 1)
         parties.append(pp)
-    n, sessions = 5, 16
-    st = mproofs.bench_keygen_proofs(parties, sessions, seed=0x6B69)
+    return parties
+
+
+def test_keygen_reshare_waves_match_oracle(five_parties):
+    """Config 5's driver streaming sessions in bounded-memory waves (3 waves of
+    32 sessions here): every party proves DLN x2, Mod and a Fac proof per peer
+    and verifies every peer's proofs; one traced session per wave is recomputed
+    by the oracle (oracle/keygen_ref.py) and every proof's digest compared, and
+    the wave split changes no proof (same traced session, other wave size)."""
+    from mpcium_amd import proofs as mproofs
+    from oracle import keygen_ref as KR
+    from oracle import proofs_ref as PR
+    lib = cc.load_c_oracle(64)
+    if lib is None:
+        pytest.skip("oracle/libgomodexp64.so not built")
+    n, sessions, wave, seed = 5, 96, 32, 0x6B69
+    st, tr = mproofs.bench_keygen_proofs(five_parties, sessions, seed=seed, wave=wave, trace=True)
     assert st["failures"] == 0
+    assert st["waves"] == 3 and st["wave_sessions"] == wave
     assert st["proofs"] == sessions * n * (2 + 1 + (n - 1))
     assert st["verifications"] == sessions * n * (n - 1) * 4
+    assert [t["session"] for t in tr] == [w * wave + (w * 7919) % wave for w in range(3)]
+    old = PR._pw
+    PR._pw = lambda x, y, m: cc.c_expnn(lib, x % m, y, m)
+    try:
+        for t in tr:
+            want, passed = KR.session_digests(five_parties, seed, t["session"])
+            assert t["digests"] == want, t["session"]
+            assert t["verified"] == passed == n * (n - 1) * 4
+    finally:
+        PR._pw = old
+    # the same sessions in one wave of 96: the traced session 0's proofs are unchanged
+    st1, tr1 = mproofs.bench_keygen_proofs(five_parties, sessions, seed=seed, wave=sessions, trace=True)
+    assert st1["failures"] == 0 and st1["waves"] == 1
+    assert tr1[0]["session"] == tr[0]["session"] == 0
+    assert tr1[0]["digests"] == tr[0]["digests"]

@@ -73,3 +73,12 @@ def test_host_pool_sized_from_affinity_and_quota(hostlib):
         pass
     assert usable == want
     assert threads == min(usable, 16)  # no GPU bound here: one device's share
+
+
+def test_host_pool_nested_loops_from_many_tasks(hostlib):
+    """Nested parallel loops issued concurrently by several tasks (the signing
+    and keygen drivers' shape) complete with every index run once."""
+    tasks, outer, inner = 6, 3000, 40
+    want = sum(t + 1 for t in range(tasks)) * (outer * (outer + 1) // 2) * (inner * (inner + 1) // 2)
+    for _ in range(3):
+        assert hostlib.pool_selftest(tasks, outer, inner) == want

@@ -39,7 +39,7 @@ def test_mix_matches_driver_constants():
 
 
 def test_two_signer_wallet_signature_verifies(nodes, fast_exp):
-    pairs, (r, s, recid), ok = S.sign_wallet(nodes, 2, 0x5163, 0)
+    pairs, (r, s, recid), ok, digest = S.sign_wallet(nodes, 2, 0x5163, 0)
     assert ok and 0 < r < S.Q and 0 < s <= S.Q // 2 and recid in (0, 1, 2, 3)
     _, shares, m = S.wallet_setup(0x5163, 0, 2)
     for (i, j), p in pairs.items():
@@ -52,3 +52,35 @@ def test_two_signer_wallet_signature_verifies(nodes, fast_exp):
     assert S.ecdsa_verify(X, m, r, S.Q - s)          # ECDSA accepts both s forms
     assert not S.ecdsa_verify(X, m + 1, r, s)
     assert not S.ecdsa_verify(X, m, r, (s + 1) % S.Q)
+
+
+def test_schnorr_proofs_and_commitments():
+    """tss-lib's round 1/4-9 building blocks (oracle/signing_ref.py): honest
+    ZK / ZKV proofs verify, a proof for another point, another session or a
+    shifted response does not; a hash commitment opens only to its own D."""
+    rd = T.Reader(77)
+    x, s_, l_ = 12345678901234567890, 987654321, 555
+    X = T.scalar_base_mult(x)
+    ss = b"session-0123456789abcdef-0123456"
+    pf = S.zk_prove(ss, x, X, rd)
+    assert S.zk_verify(ss, pf, X)
+    assert not S.zk_verify(ss, pf, T.scalar_base_mult(x + 1))
+    assert not S.zk_verify(ss[:-1] + b"7", pf, X)
+    assert not S.zk_verify(ss, (pf[0], (pf[1] + 1) % S.Q), X)
+    R = T.scalar_base_mult(99)
+    V = T.ec_add(T.ec_mul(s_, R), T.scalar_base_mult(l_))
+    pv = S.zkv_prove(ss, V, R, s_, l_, rd)
+    assert S.zkv_verify(ss, pv, V, R)
+    assert not S.zkv_verify(ss, (pv[0], pv[1], (pv[2] + 1) % S.Q), V, R)
+    assert not S.zkv_verify(ss, pv, V, T.scalar_base_mult(98))
+    C, D = S.hash_commit(rd, X[0], X[1])
+    assert S.hash_decommit(C, D) == [X[0], X[1]]
+    assert S.hash_decommit(C, [D[0], D[1] + 1, D[2]]) is None
+
+
+@pytest.mark.parametrize("tamper", [S.TAMPER_R4_SCHNORR, S.TAMPER_R6_ZKV, S.TAMPER_R7_DECOMMIT])
+def test_tampered_gg18_transcript_aborts_wallet(nodes, fast_exp, tamper):
+    """A corrupted round-4 Schnorr proof, round-6 ZKV proof or round-7
+    decommitment of one signer aborts the wallet: no signature."""
+    pairs, sig, ok, digest = S.sign_wallet(nodes, 2, 0x5163, 1, tamper=tamper)
+    assert sig is None and not ok
