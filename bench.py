@@ -493,32 +493,39 @@ def load_nodes():
 
 
 def _signing_worker(args):
-    """One process of the signing CPU baseline: 2-signer MtA/MtAwc work
-    (oracle/mta_ref.py with the C restatement of Go's expNN), ordered signer
-    pair by pair, until the deadline; returns completed pairs (2 per signature)."""
-    deadline, seed = args
+    """One process of the signing CPU baseline: whole GG18 signatures of
+    `signers` of the fixture nodes, wallet after wallet, until the deadline
+    (oracle/signing_ref.py sign_wallet: every ordered pair's MtA / MtAwc with
+    all proofs verified, then rounds 1/4-9 and ecdsa.Verify), with Go's expNN
+    restated in C (oracle/gomodexp.c, 64-bit Words) and secp256k1 through
+    OpenSSL (oracle/ossl_ec.py). Returns (signatures, seconds inside the C
+    arithmetic, seconds)."""
+    deadline, seed, signers = args
+    from oracle import crosscheck as cc
     from oracle import mta_ref as M
-    from oracle import tss_ref as T
-    M.use_go_modexp(64)
+    from oracle import ossl_ec
+    from oracle import signing_ref as S
+    lib = cc.load_c_oracle(64)
+    ec = ossl_ec.install()
+    c_mod = [0.0]
+
+    def pw(x, y, m):
+        t = time.perf_counter()
+        r = cc.c_expnn(lib, x % m, y, m)
+        c_mod[0] += time.perf_counter() - t
+        return r
+    M._pw = pw
     nodes = load_nodes()
-    rd = T.Reader(seed)
-    pairs = 0
+    t0 = time.perf_counter()
+    sigs, wi = 0, 0
     while time.time() < deadline:
-        k, g, w = (T.get_random_positive_int(rd, M.Q) for _ in range(3))
-        ss = rd.read(32)
-        i, j = pairs % 2, 1 - pairs % 2
-        A, B = nodes[i], nodes[j]
-        cA, pf = M.alice_init(A["N"], k, B["NTildei"], B["H1i"], B["H2i"], rd)
-        Wj = T.scalar_base_mult(w)
-        _, cB, _, piB = M.bob_mid(ss, A["N"], pf, g, cA, A["NTildei"], A["H1i"], A["H2i"], B["NTildei"],
-                                  B["H1i"], B["H2i"], rd)
-        _, cBw, _, piBw = M.bob_mid(ss, A["N"], pf, w, cA, A["NTildei"], A["H1i"], A["H2i"], B["NTildei"],
-                                    B["H1i"], B["H2i"], rd, B=Wj, wc=True)
-        M.alice_end(ss, A["N"], piB, A["H1i"], A["H2i"], cA, cB, A["NTildei"], A["LambdaN"])
-        M.alice_end(ss, A["N"], piBw, A["H1i"], A["H2i"], cA, cBw, A["NTildei"], A["LambdaN"], B=Wj, wc=True)
+        _, sig, ok, _ = S.sign_wallet(nodes, signers, seed, wi)
+        if not ok:
+            raise SystemExit("signing CPU baseline: a signature did not verify")
+        wi += 1
         if time.time() <= deadline:
-            pairs += 1
-    return pairs
+            sigs += 1
+    return sigs, c_mod[0] + ec.c_seconds, time.perf_counter() - t0
 
 
 def _keygen_worker(args):
@@ -528,9 +535,18 @@ def _keygen_worker(args):
     deadline, seed = args
     from oracle import crosscheck as cc
     from oracle import proofs_ref as PR
+    from oracle import safeprime_ref as SP
     from oracle import tss_ref as T
     lib = cc.load_c_oracle(64)
-    PR._pw = lambda x, y, m: cc.c_expnn(lib, x % m, y, m)
+    c_s = [0.0]
+
+    def pw(x, y, m):
+        t = time.perf_counter()
+        r = cc.c_expnn(lib, x % m, y, m)
+        c_s[0] += time.perf_counter() - t
+        return r
+    PR._pw = SP._pw = pw
+    t_start = time.perf_counter()
     nodes = load_nodes()
     A, B = nodes[0], nodes[1]
     rd = T.Reader(seed)
@@ -562,6 +578,8 @@ def _keygen_worker(args):
         assert PR.fac_verify(fac, ss, A["N"], B["NTildei"], B["H1i"], B["H2i"])
         acc["fac_verify"][0] += 1
         acc["fac_verify"][1] += time.perf_counter() - t
+    acc["_c_seconds"] = [0, c_s[0]]
+    acc["_seconds"] = [0, time.perf_counter() - t_start]
     return acc
 
 
@@ -579,7 +597,8 @@ def cpu_baseline_keygen(seconds: float, info: dict, parties: int):
     deadline = time.time() + seconds
     with ProcessPoolExecutor(procs, mp_context=mp.get_context("fork")) as ex:
         res = list(ex.map(_keygen_worker, [(deadline, 0x6B0 + i) for i in range(procs)]))
-    tot = {k: [sum(r[k][0] for r in res), sum(r[k][1] for r in res)] for k in res[0]}
+    c_share = sum(r["_c_seconds"][1] for r in res) / max(1e-9, sum(r["_seconds"][1] for r in res))
+    tot = {k: [sum(r[k][0] for r in res), sum(r[k][1] for r in res)] for k in res[0] if not k.startswith("_")}
     if any(c == 0 for c, _ in tot.values()):
         return None
     per = {k: s / c for k, (c, s) in tot.items()}
@@ -589,11 +608,12 @@ def cpu_baseline_keygen(seconds: float, info: dict, parties: int):
     cpu_s = sum(mix[k] * per[k] for k in mix)
     return {"value": procs / cpu_s, "unit": "sessions/s", "cores": procs, "kind": "port",
             "one_core": 1.0 / cpu_s, "all_cores_extrapolated": info["nproc"] / cpu_s,
-            "per_primitive_s": per, **info,
+            "per_primitive_s": per, "python_share": 1.0 - c_share, **info,
             "sample": f"{sum(c for c, _ in tot.values())} proof primitives (DLN/Mod/Fac prove + verify) in "
                       f"{seconds:.0f} s on {procs} processes, composed into one {n}-party session's mix "
                       f"({cpu_s:.1f} CPU-s per session); oracle/proofs_ref.py with Go expNN restated in C "
-                      f"(64-bit Words); one_core = 1 / CPU-s per session"}
+                      f"(64-bit Words); python_share = time outside those C calls (the Lucas test and "
+                      f"Jacobi symbols run in Python); one_core = 1 / CPU-s per session"}
 
 
 def keygen_line(args):
@@ -610,31 +630,40 @@ def keygen_line(args):
         pp, _ = mhost.generate_preparams(seed=seed)
         parties.append(pp)
     parties = parties[:args.parties]
-    # warm-up at the timed size: the node-lifetime fixed-base comb tables (h1, h2
-    # of every party's N~ and their inverses) are built on first use, as a node
+    # warm-up of one wave: the node-lifetime fixed-base comb tables (h1, h2 of
+    # every party's N~ and their inverses) are built on first use, as a node
     # builds them once for its peers' preparams, not per session
-    warm = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B66)
+    wave = args.keygen_wave or 1024
+    warm = mproofs.bench_keygen_proofs(parties, min(wave, args.keygen_sessions), seed=0x6B66, wave=wave)
     if warm["failures"]:
         raise SystemExit(f"keygen proofs warmup: {warm}")
-    st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67)
+    import resource
+    rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67, wave=wave)
+    rss1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
     if st["failures"]:
         raise SystemExit(f"keygen proofs: {st}")
     line = {"metric": f"{len(parties)}-party keygen/reshare sessions/s (config 5: DLN x2 + Mod + Fac proofs per party, "
-                      f"every peer verified)",
+                      f"every peer verified, {args.keygen_sessions} sessions)",
             "value": st["sessions"] / st["total_s"], "unit": "sessions/s", "n_gpus": 1,
             "sessions": int(st["sessions"]), "parties": len(parties), "proofs": int(st["proofs"]),
             "verifications": int(st["verifications"]), "seconds": st["total_s"], "prove_s": st["prove_s"],
             "verify_s": st["verify_s"], "engine_busy_s": st["engine_busy_s"],
+            "waves": int(st["waves"]), "wave_sessions": int(st["wave_sessions"]), "max_wave_s": st["max_wave_s"],
+            "host_max_rss_mb": rss1 / 1024.0, "host_max_rss_mb_before": rss0 / 1024.0,
             "verifications_per_s": st["verifications"] / st["total_s"], "checked": "every verification passes",
             "roofline": _job_roofline(st["alg_macs"], st["total_s"]),
             "cpu_baseline": None}
     return line
 
 
-def cpu_baseline_signing(seconds: float, info: dict):
-    """2-of-3 signing's MtA work on host cores: the oracle restatement of
-    tss-lib's MtA (oracle/mta_ref.py) with exponentiations by the C
-    restatement of Go's nat.expNN, one process per core."""
+def cpu_baseline_signing(seconds: float, info: dict, signers: int):
+    """GG18 signing on host cores: the oracle restatement of tss-lib's signing
+    (MtA / MtAwc with range proofs, rounds 1/4-9, ecdsa.Verify) with its
+    arithmetic in C -- Go's expNN restated (oracle/gomodexp.c) and OpenSSL
+    secp256k1 -- one process per usable core. python_share: the part of the
+    processes' time outside those C calls (Python orchestration, hashing,
+    draws), which a Go build would spend in Go."""
     from concurrent.futures import ProcessPoolExecutor
     from oracle import crosscheck as cc
     if cc.load_c_oracle(64) is None:
@@ -644,15 +673,18 @@ def cpu_baseline_signing(seconds: float, info: dict):
     deadline = t0 + seconds
     import multiprocessing as mp
     with ProcessPoolExecutor(procs, mp_context=mp.get_context("fork")) as ex:
-        n = sum(ex.map(_signing_worker, [(deadline, 0x51C0 + i) for i in range(procs)]))
+        res = list(ex.map(_signing_worker, [(deadline, 0x51C0 + 97 * i, signers) for i in range(procs)]))
     el = max(time.time() - t0, seconds)
-    return {"value": n / 2 / el, "unit": "sigs/s", "cores": procs, "kind": "port",
-            "one_core": n / 2 / el / procs, "all_cores_extrapolated": n / 2 / el / procs * info["nproc"], **info,
-            "sample": f"{n} ordered signer pairs = {n / 2:g} 2-signer signatures' MtA/MtAwc (per pair: AliceInit, "
-                      f"BobMid, BobMidWC, AliceEnd, AliceEndWC, all proofs verified) in {el:.1f} s on {procs} "
-                      f"processes; "
-                      f"oracle/mta_ref.py with Go expNN restated in C (oracle/gomodexp.c, 64-bit Words); "
-                      f"one_core = per process while all ran"}
+    n = sum(r[0] for r in res)
+    c_s, tot_s = sum(r[1] for r in res), sum(r[2] for r in res)
+    return {"value": n / el, "unit": "sigs/s", "cores": procs, "kind": "port", "signers": signers,
+            "one_core": n / el / procs, "all_cores_extrapolated": n / el / procs * info["nproc"],
+            "python_share": 1.0 - c_s / max(tot_s, 1e-9), **info,
+            "sample": f"{n} whole {signers}-signer GG18 signatures (every ordered pair's MtA/MtAwc with all "
+                      f"proofs verified, rounds 1/4-9 commitments and Schnorr/ZKV proofs, ecdsa.Verify) in "
+                      f"{el:.1f} s on {procs} processes; oracle/signing_ref.py with Go expNN restated in C "
+                      f"(oracle/gomodexp.c, 64-bit Words) and OpenSSL secp256k1 (oracle/ossl_ec.py); "
+                      f"python_share = time outside those C calls; one_core = per process while all ran"}
 
 
 def _job_roofline(alg_macs: float, seconds: float, world: int = 1) -> dict:
@@ -747,12 +779,14 @@ def main():
     ap.add_argument("--wallets", type=int, default=10000,
                     help="config 4: wallets per GPU for the 2-of-3 signing MtA line (0: skip)")
     ap.add_argument("--signers", type=int, default=2)
-    ap.add_argument("--keygen-sessions", type=int, default=256,
+    ap.add_argument("--keygen-sessions", type=int, default=50000,
                     help="config 5: keygen/reshare sessions for the proof-work line (0: skip)")
+    ap.add_argument("--keygen-wave", type=int, default=0,
+                    help="config 5: sessions per bounded-memory wave (0: the driver's 1024)")
     ap.add_argument("--parties", type=int, default=5)
     ap.add_argument("--extra-lines", type=int, default=1,
                     help="1: add the config-1 (Paillier batch) and config-3 (safe primes) objects at N=1")
-    ap.add_argument("--cpu-sign-seconds", type=float, default=20.0)
+    ap.add_argument("--cpu-sign-seconds", type=float, default=15.0)
     ap.add_argument("--safe-primes", type=int, default=256,
                     help="config 3: 1024-bit safe primes to find (256: steady state, ~4 steps per GPU at N = 8)")
     ap.add_argument("--modbits", type=int, default=4096, choices=(2048, 4096),
@@ -773,9 +807,11 @@ def main():
     info = host_info()
     if args.cpu_threads:
         info["usable_threads"] = args.cpu_threads
-    sign_cpu = None
+    sign_cpu = sign3_cpu = None
     if args.wallets > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sign_cpu = cpu_baseline_signing(args.cpu_sign_seconds, info)
+        sign_cpu = cpu_baseline_signing(args.cpu_sign_seconds, info, args.signers)
+        if args.signers != 3:
+            sign3_cpu = cpu_baseline_signing(args.cpu_sign_seconds, info, 3)
     keygen_cpu = None
     if args.keygen_sessions > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
         keygen_cpu = cpu_baseline_keygen(16.0, info, args.parties)
@@ -988,6 +1024,7 @@ def main():
         result["signing"]["cpu_baseline"] = sign_cpu
         if args.signers != 3:  # mpcium signs with every ready peer (/root/reference/pkg/mpc/node.go:148)
             result["signing_3_signers"] = signing_line(args, world, rank, 3)
+            result["signing_3_signers"]["cpu_baseline"] = sign3_cpu
     if args.extra_lines:
         cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
         if world == 1:

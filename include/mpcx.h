@@ -96,6 +96,11 @@ int mpcx_partition(uint32_t count, int n_devices, uint32_t min_slice, uint32_t* 
 /* Number of bound devices and (optionally) their HIP ordinals, bind order. */
 int mpcx_bound_devices(int* out_count, int* ordinals, int max_ordinals);
 
+/* Kernel launches issued so far by the batch entry points on bound device
+ * `index` (modexp, fixed-base, secp256k1 batches): which devices a workload
+ * actually used. */
+int mpcx_device_launches(int index, uint64_t* out);
+
 /* Device (index into the bound set, default 0) used by THIS thread's
  * device-buffer calls, modulus registration, comb-table builds, mpcx_dev_alloc
  * and mpcx_stream_create. Moduli and comb tables are usable on every bound
@@ -193,6 +198,19 @@ int mpcx_mulmod_batch(mpcx_mod_t mod, uint32_t count,
  * mod p_i == 1) for count odd candidates p_i of p_words words each
  * (5 <= p_i < 2^1024, p_words <= 32). Each candidate is its own modulus. */
 int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint8_t* ok);
+
+/* secp256k1 (btcec/v2 S256, /root/reference/go.mod:29): out_i = a_i G + b_i P_i
+ * + c_i Q_i for count independent items, one GPU thread each -- every point
+ * equation of tss-lib's GG18 signing outside the MtA (up:ecdsa/signing
+ * round_1.go .. finalize.go: Gamma_i = gamma_i G, Schnorr / ZKV proofs and their
+ * checks, R = theta^-1 sum Gamma, V_i = s_i R + l_i G, U_i = rho_i V, and
+ * ecdsa.Verify's u1 G + u2 X; up:crypto/schnorr).
+ * scalars: count x 24 words (a, b, c: 8 little-endian words each, any 256-bit
+ * value, i.e. taken mod the group order); points: count x 32 words (P.x, P.y,
+ * Q.x, Q.y, 8 little-endian words each; an all-zero point is the point at
+ * infinity; others must be on the curve -- the caller checks, as
+ * crypto.NewECPoint does); out: count x 16 words (x, y; all zero = infinity). */
+int mpcx_ec_combine_batch(uint32_t count, const uint32_t* scalars, const uint32_t* points, uint32_t* out);
 
 /* Miller-Rabin: ok[i] = n_i is a strong probable prime to base bases[i]
  * (5 <= n_i < 2^1024 odd, bases[i] < 2^(32*n_words); a base that is 0 mod
@@ -302,7 +320,11 @@ int mpcx_sync(void* stream);
  *   "geom_policy" 1 (default): 4096-bit batches pick the main, mid (8 x 19)
  *                or narrow geometry by a measured launch-time model of
  *                wavefronts per SIMD; 0: the "narrow_rounds" / "mid_rounds"
- *                thresholds only.
+ *                thresholds only; 2: every batch in its class's main geometry.
+ *   "duplicate_device" 0 (default) / 1 (test hook): mpcx_init of an already
+ *                bound ordinal binds it again as another logical device (own
+ *                lanes, constants, workspaces), so the multi-device split and
+ *                gather run concurrently on a one-GPU box.
  *   "mid_rounds" 0..400 (default 0): with geom_policy 0, 4096-bit batches
  *                under mid_rounds/100 of a main round run in the mid geometry.
  *   "fixed_window" 4 or 5 (default 5): widest fixed window for per-operand

@@ -44,6 +44,7 @@ def _objects():
     objs = [(os.path.join(objdir, f"mpcx_geom{g}.o"), "mpcx_geom.hip", [f"-DMPCX_GEOM_ID={g}"])
             for g in range(NUM_GEOMS)]
     objs.append((os.path.join(objdir, "mpcx_prime.o"), "mpcx_prime.hip", []))
+    objs.append((os.path.join(objdir, "mpcx_ec.o"), "mpcx_ec.hip", []))
     objs.append((os.path.join(objdir, "mpcx_api.o"), "mpcx_api.cpp", []))
     return objs
 

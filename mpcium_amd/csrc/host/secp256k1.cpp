@@ -3,6 +3,10 @@
 
 #include "hostprof.hpp"
 #include "tsscommon.hpp"
+#include "mpcx.h"
+
+#include <stdexcept>
+#include <string>
 
 #include <algorithm>
 #include <vector>
@@ -512,10 +516,43 @@ Affine Combine(const Nat& a, const Affine& P, const Nat& b, const Affine& Q, con
 }
 
 std::vector<Affine> CombineBatch(const std::vector<Comb>& items) {
-  std::vector<Affine> out(items.size());
-  parallel_for(items.size(), [&](size_t i) {
-    const Comb& t = items[i];
-    out[i] = Combine(t.a, t.P, t.b, t.Q, t.c);
+  MPCX_PROF("ec.combine_batch");
+  const size_t n = items.size();
+  std::vector<Affine> out(n);
+  if (!n) return out;
+  // one GPU thread per item (mpcx_ec_combine_batch, libmpcx's k_ec_combine)
+  std::vector<uint32_t> sc(n * 24, 0), pt(n * 32, 0), res(n * 16, 0);
+  auto put_scalar = [&](const Nat& k, uint32_t* w) {
+    if (k.bit_len() > 256) (k % CurveN()).to_words(w, 8);
+    else k.to_words(w, 8);
+  };
+  auto put_point = [&](const Affine& p, uint32_t* w) {
+    if (p.inf) return;  // all zero = infinity
+    FeToNat(p.x).to_words(w, 8);
+    FeToNat(p.y).to_words(w + 8, 8);
+  };
+  parallel_for((n + 255) / 256, [&](size_t blk) {
+    for (size_t i = blk * 256; i < std::min(n, blk * 256 + 256); ++i) {
+      const Comb& t = items[i];
+      put_scalar(t.a, &sc[i * 24]);
+      put_scalar(t.b, &sc[i * 24 + 8]);
+      put_scalar(t.c, &sc[i * 24 + 16]);
+      put_point(t.P, &pt[i * 32]);
+      put_point(t.Q, &pt[i * 32 + 16]);
+    }
+  });
+  const int rc = mpcx_ec_combine_batch((uint32_t)n, sc.data(), pt.data(), res.data());
+  if (rc != MPCX_OK) throw std::runtime_error(std::string("mpcx_ec_combine_batch: ") + mpcx_last_error());
+  parallel_for((n + 255) / 256, [&](size_t blk) {
+    for (size_t i = blk * 256; i < std::min(n, blk * 256 + 256); ++i) {
+      const uint32_t* w = &res[i * 16];
+      uint32_t o = 0;
+      for (int k = 0; k < 16; ++k) o |= w[k];
+      if (!o) continue;  // infinity
+      out[i].x = NatToFe(Nat::from_words(w, 8));
+      out[i].y = NatToFe(Nat::from_words(w + 8, 8));
+      out[i].inf = false;
+    }
   });
   return out;
 }

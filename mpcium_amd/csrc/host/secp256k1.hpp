@@ -44,7 +44,8 @@ struct Comb {
   Nat a, b, c;
   Affine P, Q;
 };
-// Combine over a batch of independent items (parallel over the host pool)
+// Combine over a batch of independent items, on the GPU (one thread per item:
+// mpcx_ec_combine_batch); throws without a bound device
 std::vector<Affine> CombineBatch(const std::vector<Comb>& items);
 bool IsOnCurve(const Affine& P);
 bool Equal(const Affine& P, const Affine& Q);

@@ -57,6 +57,8 @@ hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t waves
 hipError_t mpcx_launch_fixedbase_g1(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_sieve(const mpcx::SieveArgs* a, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
+hipError_t mpcx_launch_ec_combine(const uint32_t* sc, const uint32_t* pts, uint32_t* out, const uint32_t* gtab,
+                                  uint32_t* ws, uint32_t count, hipStream_t st);
 }
 
 namespace {
@@ -101,6 +103,7 @@ int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w):
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
 bool g_prime_coop = true;                // mpcx_set_option("prime_coop", 0): thread-per-candidate prime kernels
+bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 1): test hook, see below
 struct Staging {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -146,6 +149,9 @@ struct Device {
   std::mutex dev_mu;
   std::map<hipStream_t, std::unique_ptr<Lane>> dev_lanes;
   Lane build_lane;  // fixed-base table builds
+  std::atomic<uint64_t> launches{0};  // kernel launches of the batch entry points on this device
+  std::mutex ec_mu;            // guards the lazy secp256k1 base-point comb build
+  uint32_t* ec_gtab = nullptr;  // d 256^w G, w < 32, 1 <= d <= 255 (affine x, y)
 };
 Device g_devs[kMaxDevices];
 std::atomic<int> g_ndev{0};
@@ -440,7 +446,10 @@ int run_selftest() {
 // Bind HIP ordinal `ordinal` as the next device (g_mu held).
 int bind_new_device(int ordinal) {
   const int n = g_ndev.load();
-  for (int i = 0; i < n; ++i)
+  // duplicate_device (test hook): bind the ordinal again as one more logical
+  // device with its own lanes, constants and workspaces, so the multi-device
+  // split / gather paths run concurrently on a one-GPU box
+  for (int i = 0; i < n && !g_dup_device; ++i)
     if (g_devs[i].ordinal == ordinal) return MPCX_OK;
   if (n >= kMaxDevices) return fail(MPCX_EINVAL, "more than %d devices", kMaxDevices);
   int vis = 0;
@@ -608,6 +617,9 @@ int mpcx_set_option(const char* key, int value) {
   } else if (std::strcmp(key, "prime_coop") == 0) {
     // 1: cooperative base-2 / Miller-Rabin kernels (k_prime2c, k_mrc); 0: thread per candidate
     g_prime_coop = value != 0;
+  } else if (std::strcmp(key, "duplicate_device") == 0) {
+    // test hook: mpcx_init(ordinal) binds an already bound ordinal again as another logical device
+    g_dup_device = value != 0;
   } else if (std::strcmp(key, "device_split_min") == 0) {
     // smallest per-device slice of a host-buffer batch split across the bound GPUs (0: never split)
     if (value < 0) return fail(MPCX_EINVAL, "device_split_min %d < 0", value);
@@ -678,6 +690,14 @@ int mpcx_partition(uint32_t count, int n_devices, uint32_t min_slice, uint32_t* 
   return MPCX_OK;
 }
 
+int mpcx_device_launches(int index, uint64_t* out) {
+  const int n = g_ndev.load(std::memory_order_acquire);
+  if (!out) return fail(MPCX_EINVAL, "null out");
+  if (index < 0 || index >= n) return fail(MPCX_EINVAL, "device index %d not bound (%d bound)", index, n);
+  *out = g_devs[index].launches.load();
+  return MPCX_OK;
+}
+
 int mpcx_select_device(int index) {
   const int n = g_ndev.load(std::memory_order_acquire);
   if (index < 0 || index >= n) return fail(MPCX_EINVAL, "device index %d not bound (%d bound)", index, n);
@@ -694,6 +714,8 @@ int mpcx_shutdown(void) {
     t_hip = d.ordinal;
     for (auto& l : d.lanes) drop_lane(l);
     drop_lane(d.build_lane);
+    if (d.ec_gtab) (void)hipFree(d.ec_gtab);
+    d.ec_gtab = nullptr;
     {
       std::lock_guard<std::mutex> dl(d.dev_mu);
       for (auto& kv : d.dev_lanes) drop_lane(*kv.second);
@@ -915,6 +937,7 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     a.sched = use_sched ? lane.ws + sched_off : nullptr;
     hipError_t e = mpcx_launch_modexp(pt.geom, &a, waves, st);
     if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
+    g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
     ws_off += (size_t)waves * MPCX_TABLE_ENTRIES * K * 64u;
   }
   return MPCX_OK;
@@ -1104,6 +1127,86 @@ int mpcx_mulmod_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* a, uint32_
   if (!a || !b) return fail(MPCX_EINVAL, "null operands");
   const uint32_t one = 1;
   return modexp_host(mod, count, a, a_words, &one, 1, 1, b, b_words, out, out_words);
+}
+
+// ------------------------------------------------------------ secp256k1
+namespace {
+constexpr uint32_t kEcG[16] = {0x16F81798u, 0x59F2815Bu, 0x2DCE28D9u, 0x029BFCDBu, 0xCE870B07u, 0x55A06295u,
+                               0xF9DCBBACu, 0x79BE667Eu, 0xFB10D4B8u, 0x9C47D08Fu, 0xA6855419u, 0xFD17B448u,
+                               0x0E1108A8u, 0x5DA4FBFCu, 0x26A3C465u, 0x483ADA77u};
+constexpr uint32_t kEcTabEntries = 32u * 255u;
+constexpr size_t ec_ws_words(uint32_t count) { return (size_t)((count + 63u) / 64u) * 30u * 24u * 64u; }
+
+// The base-point comb of device d (built on first use by k_ec_combine itself:
+// entry (w, v) = (v 2^(8w)) G as a plain scalar multiple of G). Lane l locked.
+int ec_gtab(Device& d, Lane& l, const uint32_t** out) {
+  std::lock_guard<std::mutex> lk(d.ec_mu);
+  if (!d.ec_gtab) {
+    std::vector<uint32_t> sc((size_t)kEcTabEntries * 24u, 0u), pts((size_t)kEcTabEntries * 32u, 0u);
+    for (uint32_t w = 0; w < 32; ++w)
+      for (uint32_t v = 1; v <= 255; ++v) {
+        const size_t e = (size_t)w * 255u + (v - 1u);
+        const uint32_t bit = 8u * w;  // b = v << bit (spans at most two words)
+        const uint64_t x = (uint64_t)v << (bit % 32u);
+        sc[e * 24u + 8u + bit / 32u] = (uint32_t)x;
+        if (bit / 32u + 1u < 8u) sc[e * 24u + 8u + bit / 32u + 1u] = (uint32_t)(x >> 32);
+        std::memcpy(&pts[e * 32u], kEcG, sizeof kEcG);
+      }
+    int rc;
+    const size_t sb = sc.size() * 4, pb = pts.size() * 4;
+    if ((rc = ensure_buffer(l.stage[0], sb)) || (rc = ensure_buffer(l.stage[1], pb)) ||
+        (rc = ensure_workspace(l, ec_ws_words(kEcTabEntries) * 4)))
+      return rc;
+    uint32_t* tab = nullptr;
+    hipError_t e = hipMalloc((void**)&tab, (size_t)kEcTabEntries * 16u * 4u);
+    if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(secp256k1 comb): %s", hipGetErrorString(e));
+    if ((rc = h2d(l.stage[0].ptr, sc.data(), sb, l.st)) || (rc = h2d(l.stage[1].ptr, pts.data(), pb, l.st))) {
+      (void)hipFree(tab);
+      return rc;
+    }
+    e = mpcx_launch_ec_combine((const uint32_t*)l.stage[0].ptr, (const uint32_t*)l.stage[1].ptr, tab, nullptr, l.ws,
+                               kEcTabEntries, l.st);
+    if (e != hipSuccess) {
+      (void)hipFree(tab);
+      return hip_fail(e, "launch k_ec_combine (comb build)");
+    }
+    if ((rc = lane_wait(l))) {
+      (void)hipFree(tab);
+      return rc;
+    }
+    d.ec_gtab = tab;
+  }
+  *out = d.ec_gtab;
+  return MPCX_OK;
+}
+
+int ec_range(int di, uint32_t count, const uint32_t* scalars, const uint32_t* points, uint32_t* out) {
+  Device& d = g_devs[di];
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(d, lk);
+  int rc;
+  if ((rc = lane_stream(l))) return rc;
+  const uint32_t* gtab = nullptr;
+  if ((rc = ec_gtab(d, l, &gtab))) return rc;
+  const size_t sb = (size_t)count * 24u * 4u, pb = (size_t)count * 32u * 4u, ob = (size_t)count * 16u * 4u;
+  if ((rc = ensure_buffer(l.stage[0], sb)) || (rc = ensure_buffer(l.stage[1], pb)) ||
+      (rc = ensure_buffer(l.stage[2], ob)) || (rc = ensure_workspace(l, ec_ws_words(count) * 4)))
+    return rc;
+  if ((rc = h2d(l.stage[0].ptr, scalars, sb, l.st)) || (rc = h2d(l.stage[1].ptr, points, pb, l.st))) return rc;
+  hipError_t e = mpcx_launch_ec_combine((const uint32_t*)l.stage[0].ptr, (const uint32_t*)l.stage[1].ptr,
+                                        (uint32_t*)l.stage[2].ptr, gtab, l.ws, count, l.st);
+  if (e != hipSuccess) return hip_fail(e, "launch k_ec_combine");
+  d.launches.fetch_add(1, std::memory_order_relaxed);
+  return d2h_sync(out, l.stage[2].ptr, ob, l);
+}
+}  // namespace
+
+int mpcx_ec_combine_batch(uint32_t count, const uint32_t* scalars, const uint32_t* points, uint32_t* out) {
+  if (count == 0) return MPCX_OK;
+  if (!scalars || !points || !out) return fail(MPCX_EINVAL, "null buffer");
+  return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t n) {
+    return ec_range(di, n, scalars + (size_t)first * 24u, points + (size_t)first * 32u, out + (size_t)first * 16u);
+  });
 }
 
 int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint8_t* ok) {
@@ -1515,6 +1618,7 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     hipError_t e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
                                              : mpcx_launch_fixedbase_g1(&a, waves, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
+    g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
     return d2h_sync(out + (size_t)first * out_words, sg[2].ptr, ob, l);
   });
 }

@@ -30,6 +30,7 @@ SIGNATURES = [
     ("mpcx_init_devices", ctypes.c_int, [ctypes.c_int]),
     ("mpcx_bound_devices", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("mpcx_select_device", ctypes.c_int, [ctypes.c_int]),
+    ("mpcx_device_launches", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
     ("mpcx_partition", ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, _u32p, _u32p, _u32p]),
     ("mpcx_shutdown", ctypes.c_int, []),
     ("mpcx_modulus_register", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(_vp)]),
@@ -53,6 +54,7 @@ SIGNATURES = [
     ("mpcx_mulmod_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp,
                                          ctypes.c_uint32]),
     ("mpcx_fermat2_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
+    ("mpcx_ec_combine_batch", ctypes.c_int, [ctypes.c_uint32, _vp, _vp, _vp]),
     ("mpcx_mr_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
     ("mpcx_fixedbase_register", ctypes.c_int, [_vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_vp)]),
     ("mpcx_fixedbase_release", ctypes.c_int, [_vp]),
@@ -142,6 +144,12 @@ def partition(count: int, n_devices: int, min_slice: int = 4096):
     k = ctypes.c_uint32(0)
     _check(lib().mpcx_partition(count, n_devices, min_slice, f, n, ctypes.byref(k)))
     return [(f[i], n[i]) for i in range(k.value)]
+
+
+def device_launches(index: int) -> int:
+    v = ctypes.c_uint64(0)
+    _check(lib().mpcx_device_launches(index, ctypes.byref(v)))
+    return v.value
 
 
 def select_device(index: int):
@@ -367,6 +375,28 @@ def exp_batch(m: int, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> 
         return mod.exp(bases, exps)
     finally:
         mod.release()
+
+
+def ec_combine_batch(items) -> list:
+    """secp256k1 a G + b P + c Q per item (a, b, c, P, Q), points as (x, y)
+    tuples or None (infinity) -> list of (x, y) or None."""
+    n = len(items)
+    if n == 0:
+        return []
+    sc = np.zeros((n, 24), dtype="<u4")
+    pt = np.zeros((n, 32), dtype="<u4")
+    mask = (1 << 256) - 1
+    for i, (a, b, c, P, Q) in enumerate(items):
+        sc[i] = int_to_words((a & mask) | ((b & mask) << 256) | ((c & mask) << 512), 24)
+        px = (P[0] | (P[1] << 256)) if P is not None else 0
+        qx = (Q[0] | (Q[1] << 256)) if Q is not None else 0
+        pt[i] = int_to_words(px | (qx << 512), 32)
+    out = np.zeros((n, 16), dtype="<u4")
+    _check(lib().mpcx_ec_combine_batch(n, sc.ctypes.data, pt.ctypes.data, out.ctypes.data))
+    res = []
+    for v in words_to_ints(out):
+        res.append(None if v == 0 else (v & mask, v >> 256))
+    return res
 
 
 def fermat2_batch(cands: Sequence[int]) -> List[bool]:

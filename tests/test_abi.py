@@ -83,3 +83,12 @@ def test_device_partition_plan(libs):
                     assert max(n for _, n in plan) - min(n for _, n in plan) <= len(plan)
     with pytest.raises(mpcx.MpcxError):
         mpcx.partition(10, 0, 1)
+
+
+def test_no_undefined_library_symbols():
+    """Every mpcx_* symbol libmpcx.so references is defined in it (a launcher
+    declared extern "C" but defined with C++ linkage fails only at load time)."""
+    import subprocess
+    so = os.path.join(ROOT, "mpcium_amd", "libmpcx.so")
+    out = subprocess.run(["nm", "-D", "--undefined-only", so], capture_output=True, text=True, check=True).stdout
+    assert [l for l in out.splitlines() if " mpcx" in l] == []

@@ -120,3 +120,55 @@ def test_device_buffers_on_two_streams(mx):
             assert r1[i] == pow(xs[i], e1, N) and r2[i] == pow(xs[i], e2, N), i
     finally:
         mod.release()
+
+
+_LOGICAL = r"""
+import json, random, sys
+sys.path.insert(0, sys.argv[1]); sys.path.insert(0, sys.argv[1] + "/tests")
+from conftest import load_golden
+from mpcium_amd import host, mpcx, mta, proofs
+mpcx.set_option("duplicate_device", 1)
+host.init(0)
+host.init(0)
+out = {"devices": mpcx.bound_devices()}
+N = int(load_golden("paillier_key_2048.json")["N"], 16)
+N2 = N * N
+rng = random.Random(11)
+mod = mpcx.Modulus(N2)
+xs = [rng.randrange(N2) for _ in range(300)]
+mpcx.set_option("device_split_min", 64)
+l0 = [mpcx.device_launches(i) for i in range(2)]
+out["split_ok"] = mod.exp(xs, N) == [pow(x, N, N2) for x in xs]
+out["split_launches"] = [mpcx.device_launches(i) - l0[i] for i in range(2)]
+mod.release()
+mpcx.set_option("device_split_min", 4096)
+d = load_golden("node_preparams.json")
+nodes = [{k: int(v, 16) for k, v in n.items() if isinstance(v, str) and k != "paillier_source"} for n in d["nodes"]]
+l1 = [mpcx.device_launches(i) for i in range(2)]
+out["signing"] = mta.bench_signing(nodes, 2, 300, seed=0x10D)
+out["keygen"] = proofs.bench_keygen_proofs(nodes, 24, seed=0x10E, wave=12)
+out["work_launches"] = [mpcx.device_launches(i) - l1[i] for i in range(2)]
+print(json.dumps(out))
+"""
+
+
+def test_two_logical_devices(gpu):
+    """One HIP ordinal bound twice (mpcx_set_option "duplicate_device", a test
+    hook) in a child process: a split batch runs one slice per logical device
+    concurrently and gathers in order, and the signing and keygen drivers
+    spread their batches over both devices' lanes -- the one-process-many-GPUs
+    node shape (/root/reference/pkg/mpc/node.go:69,109) exercised on one GPU."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", _LOGICAL, root], capture_output=True, text=True, timeout=280)
+    assert r.returncode == 0, r.stderr[-3000:]
+    out = json.loads(r.stdout.strip().splitlines()[-1])
+    assert out["devices"] == [0, 0]
+    assert out["split_ok"] and all(n >= 1 for n in out["split_launches"])
+    s = out["signing"]
+    assert s["errors"] == 0 and s["relation_failures"] == 0 and s["verified"] == 300 and s["aborted"] == 0
+    assert out["keygen"]["failures"] == 0 and out["keygen"]["waves"] == 2
+    assert all(n > 0 for n in out["work_launches"]), out["work_launches"]

@@ -84,3 +84,18 @@ def test_tampered_gg18_transcript_aborts_wallet(nodes, fast_exp, tamper):
     decommitment of one signer aborts the wallet: no signature."""
     pairs, sig, ok, digest = S.sign_wallet(nodes, 2, 0x5163, 1, tamper=tamper)
     assert sig is None and not ok
+
+
+def test_openssl_ec_matches_restatement():
+    """The OpenSSL-backed secp256k1 of the CPU baseline (oracle/ossl_ec.py)
+    returns the same points as the pure-Python restatement."""
+    from oracle import ossl_ec
+    ec = ossl_ec._Ec()
+    rd = T.Reader(5)
+    for _ in range(8):
+        k1, k2 = (T.get_random_positive_int(rd, S.Q) for _ in range(2))
+        P = T.scalar_base_mult(k1)
+        assert ec.base(k1) == P
+        assert ec.mul(k2, P) == T.ec_mul(k2, P)
+        assert ec.add(P, ec.base(k2)) == T.ec_add(P, T.scalar_base_mult(k2))
+    assert ec.mul(S.Q, T.SECP_G) is None and ec.add(P, (P[0], T.SECP_P - P[1])) is None
