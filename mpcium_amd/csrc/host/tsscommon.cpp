@@ -508,9 +508,10 @@ class HostPool {
     // at once). The waiter does not run other loops' indices meanwhile: with
     // nested loops that recursion would be unbounded (a worker inside an outer
     // index helping the outer loop again, one stack frame set per index).
+    // (finish() notifies under done_mu_ after every transition that can make
+    // this true: the last index done, the last worker gone)
     std::unique_lock<std::mutex> lk(done_mu_);
-    while (!(l.done.load() >= l.n && l.users.load() == 0))
-      done_cv_.wait_for(lk, std::chrono::milliseconds(2));
+    done_cv_.wait(lk, [&] { return l.done.load() >= l.n && l.users.load() == 0; });
   }
 
  private:
@@ -522,10 +523,11 @@ class HostPool {
         for (;;) {
           Loop* l = nullptr;
           {
+            // the loop is taken by the predicate itself: other threads advance
+            // `next` without the lock, so a second look could find none left
             std::unique_lock<std::mutex> lk(mu_);
-            cv_.wait(lk, [&] { return pending_locked() != nullptr; });
-            l = pending_locked();
-            l->users.fetch_add(1);  // l stays alive until users drops back to 0
+            cv_.wait(lk, [&] { return (l = pending_locked()) != nullptr; });
+            l->users.fetch_add(1);  // l stays alive (listed or waited for) until users drops back to 0
           }
           finish(l, l->work());
         }

@@ -173,6 +173,30 @@ int hip_fail(hipError_t e, const char* what) {
   return fail(MPCX_EHIP, "%s: %s", what, hipGetErrorString(e));
 }
 
+// Launch log (environment MPCX_LAUNCH_LOG=<path>): one CSV line per kernel
+// launch of the batch entry points -- kind, geometry, operands, modulus bits,
+// longest exponent bits, Go-equivalent algorithmic MACs (SURVEY.md 8(d):
+// (E + ceil(E/4)) 2 L^2 per exponentiation, summed over the operands' own
+// exponent lengths where the host has them) -- so a kernel trace's per-kernel
+// time can be set against the work it did (tools/kernel_frac.py).
+double go_macs(uint32_t mod_bits, uint32_t e_bits) {
+  const double L = (double)((mod_bits + 31) / 32);
+  return ((double)e_bits + (double)((e_bits + 3) / 4)) * 2.0 * L * L;
+}
+void launch_log(const char* kind, int geom, uint32_t count, uint32_t mod_bits, uint32_t exp_bits, double alg) {
+  static std::mutex mu;
+  static FILE* f = [] {
+    const char* p = std::getenv("MPCX_LAUNCH_LOG");
+    FILE* h = p && *p ? std::fopen(p, "w") : nullptr;
+    if (h) std::fprintf(h, "kind,geom,operands,modulus_bits,exp_bits,alg_macs\n");
+    return h;
+  }();
+  if (!f) return;
+  std::lock_guard<std::mutex> lk(mu);
+  std::fprintf(f, "%s,%d,%u,%u,%u,%.0f\n", kind, geom, count, mod_bits, exp_bits, alg);
+  std::fflush(f);
+}
+
 int class_for_bits(uint32_t bits) {
   for (int c = 0; c < MPCX_NUM_CLASSES; ++c)
     if ((int)bits <= MPCX_CLASS_MAXBITS(c)) return c;
@@ -835,7 +859,7 @@ static int fastest_geom(int cls, uint32_t count, int nsimd) {
 static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases,
                           uint32_t base_words, const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
                           uint32_t exp_bits, const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out,
-                          uint32_t out_words) {
+                          uint32_t out_words, double alg_macs = -1.0) {
   const Device& dev = g_devs[di];
   hipStream_t st = lane.st;
   const uint32_t class_words = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
@@ -938,6 +962,8 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     hipError_t e = mpcx_launch_modexp(pt.geom, &a, waves, st);
     if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
+    launch_log("modexp", pt.geom, pt.count, mod->bits, a.exp_bits,
+               alg_macs >= 0 ? alg_macs * pt.count / count : go_macs(mod->bits, a.exp_bits) * pt.count);
     ws_off += (size_t)waves * MPCX_TABLE_ENTRIES * K * 64u;
   }
   return MPCX_OK;
@@ -970,9 +996,15 @@ static int modexp_host_range(int di, mpcx_mod_t mod, uint32_t count, const uint3
   if ((rc = h2d(sg[0].ptr, bases, bb, l.st)) || (rc = h2d(sg[1].ptr, exps, n_exp_words * 4, l.st)) ||
       (muls && (rc = h2d(sg[3].ptr, muls, mb, l.st))))
     return rc;
+  double alg = -1.0;
+  if (!exp_shared && exp_words) {  // the operands' own exponent lengths (launch log)
+    alg = 0.0;
+    for (uint32_t i = 0; i < count; ++i)
+      alg += go_macs(mod->bits, bit_length_words(exps + (size_t)i * exp_words, exp_words));
+  }
   rc = modexp_enqueue(di, l, mod, count, (const uint32_t*)sg[0].ptr, base_words, (const uint32_t*)sg[1].ptr,
                       exp_words, exp_shared, exp_bits, muls ? (const uint32_t*)sg[3].ptr : nullptr, mul_words,
-                      (uint32_t*)sg[2].ptr, out_words);
+                      (uint32_t*)sg[2].ptr, out_words, alg);
   if (rc) return rc;
   return d2h_sync(out, sg[2].ptr, ob, l);
 }
@@ -1197,6 +1229,7 @@ int ec_range(int di, uint32_t count, const uint32_t* scalars, const uint32_t* po
                                         (uint32_t*)l.stage[2].ptr, gtab, l.ws, count, l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_ec_combine");
   d.launches.fetch_add(1, std::memory_order_relaxed);
+  launch_log("ec_combine", -1, count, 256, 256, 0.0);
   return d2h_sync(out, l.stage[2].ptr, ob, l);
 }
 }  // namespace
@@ -1619,6 +1652,17 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
                                              : mpcx_launch_fixedbase_g1(&a, waves, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
+    {
+      double alg = 0.0;  // Go-equivalent: one Exp per base per operand
+      uint32_t eb_max = 0;
+      for (uint32_t t = 0; t < nbases; ++t)
+        for (uint32_t i = 0; i < n && exp_words[t]; ++i) {
+          const uint32_t b = bit_length_words(exps[t] + (size_t)(first + i) * exp_words[t], exp_words[t]);
+          alg += go_macs(mod->bits, b);
+          eb_max = std::max(eb_max, b);
+        }
+      launch_log("fixedbase", geom, n, mod->bits, eb_max, alg);
+    }
     return d2h_sync(out + (size_t)first * out_words, sg[2].ptr, ob, l);
   });
 }
