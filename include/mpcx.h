@@ -199,6 +199,28 @@ int mpcx_mulmod_batch(mpcx_mod_t mod, uint32_t count,
  * (5 <= p_i < 2^1024, p_words <= 32). Each candidate is its own modulus. */
 int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint8_t* ok);
 
+/* Several batches in ONE kernel launch: each group has its own registered
+ * modulus (all of one size class), bases, shared or per-operand exponents,
+ * optional multipliers and output, exactly as one mpcx_modexp_batch /
+ * mpcx_modexp_mul_batch call (same semantics per group). The groups become
+ * segments of one launch, so the concurrent small batches of many sessions
+ * and moduli (an MtA step of every signer pair of every wallet pipeline) run
+ * in the main, widest geometry instead of as many small launches. */
+typedef struct {
+  mpcx_mod_t mod;
+  uint32_t count;
+  const uint32_t* bases;
+  uint32_t base_words;
+  const uint32_t* exps;
+  uint32_t exp_words;
+  int exp_shared;
+  const uint32_t* muls; /* NULL: no multiplier */
+  uint32_t mul_words;
+  uint32_t* out;
+  uint32_t out_words;
+} mpcx_modexp_group_t;
+int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* groups);
+
 /* secp256k1 (btcec/v2 S256, /root/reference/go.mod:29): out_i = a_i G + b_i P_i
  * + c_i Q_i for count independent items, one GPU thread each -- every point
  * equation of tss-lib's GG18 signing outside the MtA (up:ecdsa/signing

@@ -1,6 +1,10 @@
 // engine.cpp -- see engine.hpp.
 #include "engine.hpp"
 
+#include <condition_variable>
+#include <deque>
+#include <string>
+
 #include "hostprof.hpp"
 #include "tsscommon.hpp"
 
@@ -167,6 +171,89 @@ struct HostBuf {
 };
 }  // namespace
 
+namespace {
+// Launch coalescing across concurrent callers (ExpSets of different signer
+// pairs, wallet pipelines and moduli): each exp() call is a group; a caller
+// that finds fewer than max_inflight dispatches running becomes the leader
+// and issues every pending group of its modulus class as ONE
+// mpcx_modexp_multi_batch launch; the others wait for their results. Under
+// load the GPU thus receives few large launches (the main geometry's
+// throughput) instead of many narrow ones; alone, a call dispatches at once.
+class Coalescer {
+ public:
+  struct Req {
+    mpcx_modexp_group_t g{};
+    bool taken = false, done = false;
+    int rc = MPCX_OK;
+    std::string err;
+  };
+  int run(Req& r, int max_inflight, uint64_t max_ops) {
+    std::unique_lock<std::mutex> lk(mu_);
+    q_.push_back(&r);
+    while (!r.done) {
+      if (!r.taken && inflight_ < max_inflight) {
+        std::vector<Req*> batch{&r};  // the leader's own group first, then arrival order
+        r.taken = true;
+        uint64_t ops = r.g.count;
+        for (auto it = q_.begin(); it != q_.end();) {
+          if (*it == &r) {
+            it = q_.erase(it);
+          } else if (!(*it)->taken && ops + (*it)->g.count <= max_ops) {
+            ops += (*it)->g.count;
+            (*it)->taken = true;
+            batch.push_back(*it);
+            it = q_.erase(it);
+          } else {
+            ++it;
+          }
+        }
+        ++inflight_;
+        lk.unlock();
+        std::vector<mpcx_modexp_group_t> gs;
+        for (Req* b : batch) gs.push_back(b->g);
+        const int rc = mpcx_modexp_multi_batch((uint32_t)gs.size(), gs.data());
+        const std::string err = rc ? mpcx_last_error() : std::string();
+        lk.lock();
+        --inflight_;
+        for (Req* b : batch) {
+          b->rc = rc;
+          b->err = err;
+          b->done = true;
+        }
+        cv_.notify_all();
+      } else {
+        cv_.wait(lk);
+      }
+    }
+    return r.rc;
+  }
+
+ private:
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::deque<Req*> q_;
+  int inflight_ = 0;
+};
+
+Coalescer& coalescer(uint32_t class_words) {
+  static Coalescer c[3];
+  return c[class_words <= 32 ? 0 : class_words <= 65 ? 1 : 2];
+}
+
+// MPCX_COALESCE = max coalesced dispatches in flight per bound device (0: off,
+// each exp() call is its own launch); default kCoalesceInflight
+int coalesce_inflight() {
+  static const int v = [] {
+    const char* e = std::getenv("MPCX_COALESCE");
+    return e ? std::atoi(e) : kCoalesceInflight;
+  }();
+  if (v <= 0) return 0;
+  int dev = 1;
+  if (mpcx_bound_devices(&dev, nullptr, 0) != MPCX_OK || dev < 1) dev = 1;
+  return v * dev;
+}
+}  // namespace
+
 static void pack_into(const std::vector<Nat>& v, uint32_t w, uint32_t* out) {
   par_chunks(v.size(), [&](size_t lo, size_t hi) {
     for (size_t i = lo; i < hi; ++i) v[i].to_words(out + i * w, w);
@@ -229,7 +316,26 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
   {
     MPCX_PROF("engine.exp.gpu");
     enter_call();
-    if (muls) {
+    const int inflight = coalesce_inflight();
+    if (inflight > 0) {
+      Coalescer::Req r;
+      r.g.mod = md.h;
+      r.g.count = (uint32_t)n;
+      r.g.bases = B.p;
+      r.g.base_words = md.class_words;
+      r.g.exps = E.p;
+      r.g.exp_words = ew;
+      r.g.exp_shared = shared ? 1 : 0;
+      r.g.muls = muls ? M.p : nullptr;
+      r.g.mul_words = muls ? md.class_words : 0;
+      r.g.out = out.p;
+      r.g.out_words = md.words;
+      rc = coalescer(md.class_words).run(r, inflight, kCoalesceMaxOps);
+      if (rc) {
+        leave_call();
+        throw EngineError(rc, "mpcx_modexp_multi_batch: " + r.err);
+      }
+    } else if (muls) {
       rc = mpcx_modexp_mul_batch(md.h, (uint32_t)n, B.p, md.class_words, E.p, ew, shared ? 1 : 0, M.p,
                                  md.class_words, out.p, md.words);
     } else {

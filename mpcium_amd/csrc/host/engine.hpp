@@ -19,6 +19,12 @@
 
 namespace mpcx::host {
 
+// Launch coalescing (engine.cpp Coalescer): at most kCoalesceInflight merged
+// dispatches per bound GPU in flight (environment MPCX_COALESCE overrides;
+// 0 turns coalescing off), each at most kCoalesceMaxOps operands.
+constexpr int kCoalesceInflight = 3;
+constexpr uint64_t kCoalesceMaxOps = 131072;
+
 class EngineError : public std::runtime_error {
  public:
   EngineError(int code, const std::string& msg) : std::runtime_error(msg), code(code) {}

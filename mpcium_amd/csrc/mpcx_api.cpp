@@ -37,8 +37,10 @@
 #include "mpcx_internal.h"
 
 // per-geometry kernels (mpcx_geom.hip, one translation unit per geometry id)
-#define MPCX_GEOM_DECL(g)                                                                          \
-  hipError_t mpcx_launch_modexp_g##g(const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st); \
+#define MPCX_GEOM_DECL(g)                                                                              \
+  hipError_t mpcx_launch_modexp_g##g(const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st);     \
+  hipError_t mpcx_launch_modexp_multi_g##g(const mpcx::ModexpArgs* segs, const uint32_t* first,      \
+                                           uint32_t nsegs, uint32_t waves, hipStream_t st);          \
   hipError_t mpcx_modexp_occupancy_g##g(int* blocks_per_cu);
 #define MPCX_FOR_EACH_GEOM(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6)
 static_assert(MPCX_NUM_GEOMS == 7, "update MPCX_FOR_EACH_GEOM and build.py GEOMS");
@@ -266,6 +268,19 @@ hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t wave
 #define MPCX_CASE(g) \
   case g:            \
     return mpcx_launch_modexp_g##g(a, waves, st);
+    MPCX_FOR_EACH_GEOM(MPCX_CASE)
+#undef MPCX_CASE
+    default:
+      return hipErrorInvalidValue;
+  }
+}
+
+hipError_t mpcx_launch_modexp_multi(int geom, const mpcx::ModexpArgs* segs, const uint32_t* first, uint32_t nsegs,
+                                    uint32_t waves, hipStream_t st) {
+  switch (geom) {
+#define MPCX_CASE(g) \
+  case g:            \
+    return mpcx_launch_modexp_multi_g##g(segs, first, nsegs, waves, st);
     MPCX_FOR_EACH_GEOM(MPCX_CASE)
 #undef MPCX_CASE
     default:
@@ -856,6 +871,22 @@ static int fastest_geom(int cls, uint32_t count, int nsimd) {
   return best;
 }
 
+// Single-geometry choice for a launch of `count` operands of class cls (the
+// forced geometry, or policy 2's main, or policy 1's launch-time model, or
+// the thresholds) -- the multi-batch launch takes one geometry for all its
+// segments.
+static int choose_geom(const Device& dev, int cls, uint32_t count) {
+  const int gm = g_main_geom[cls], gn = MPCX_NARROW_GEOM(cls), gmid = MPCX_MID_GEOM(cls);
+  if (g_force_geom >= 0 && MPCX_GEOM_CLASS(g_force_geom) == cls) return g_force_geom;
+  if (g_geom_policy == 2) return gm;
+  if (g_geom_policy == 1 && gmid >= 0 && gn >= 0) return fastest_geom(cls, count, dev.num_cus * 4);
+  const uint32_t G = (uint32_t)MPCX_GEOM_G(gm);
+  const double rounds = (double)((count + G - 1) / G) / (double)std::max(1, dev.geom_slots[gm]);
+  if (gn >= 0 && rounds < g_narrow_rounds) return gn;
+  if (gmid >= 0 && rounds < g_mid_rounds) return gmid;
+  return gm;
+}
+
 static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases,
                           uint32_t base_words, const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
                           uint32_t exp_bits, const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out,
@@ -1159,6 +1190,154 @@ int mpcx_mulmod_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* a, uint32_
   if (!a || !b) return fail(MPCX_EINVAL, "null operands");
   const uint32_t one = 1;
   return modexp_host(mod, count, a, a_words, &one, 1, 1, b, b_words, out, out_words);
+}
+
+// ------------------------------------------------------------ multi-batch
+// Several batches (moduli of one class) in one k_modexp_multi launch on one
+// device: inputs packed into one staging buffer, per-group schedules, one
+// segment table, one output copy scattered back to the groups.
+int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
+  if (n_groups == 0) return MPCX_OK;
+  if (!gs) return fail(MPCX_EINVAL, "null groups");
+  const int n = ndev_or_fail();
+  if (n < 0) return -n;
+  int cls = -1;
+  uint64_t total = 0;
+  for (uint32_t i = 0; i < n_groups; ++i) {
+    const mpcx_modexp_group_t& g = gs[i];
+    if (!g.mod) return fail(MPCX_EINVAL, "group %u: null modulus", i);
+    if (cls < 0) cls = g.mod->cls;
+    if (g.mod->cls != cls) return fail(MPCX_EINVAL, "group %u: modulus class differs from group 0's", i);
+    const uint32_t cw = (uint32_t)MPCX_CLASS_WORDS(cls);
+    if (g.count == 0) continue;
+    if (!g.bases || !g.out || (g.exp_words && !g.exps)) return fail(MPCX_EINVAL, "group %u: null buffer", i);
+    if (g.base_words == 0 || g.base_words > cw) return fail(MPCX_EINVAL, "group %u: base_words %u", i, g.base_words);
+    if (g.muls && (g.mul_words == 0 || g.mul_words > cw)) return fail(MPCX_EINVAL, "group %u: mul_words", i);
+    if (g.out_words < g.mod->words) return fail(MPCX_EINVAL, "group %u: out_words < modulus words", i);
+    total += g.count;
+  }
+  if (total == 0) return MPCX_OK;
+  if (total > 0xFFFFFFFFull) return fail(MPCX_EINVAL, "too many operands");
+  const int di = (int)(g_dev_rr.fetch_add(1, std::memory_order_relaxed) % (unsigned)n);
+  Device& dev = g_devs[di];
+  int rc = bind(dev);
+  if (rc) return rc;
+  const int geom = choose_geom(dev, cls, (uint32_t)total);
+  const uint32_t G = (uint32_t)MPCX_GEOM_G(geom), K = (uint32_t)MPCX_GEOM_K(geom), L = (uint32_t)MPCX_GEOM_L(geom);
+  // host-side layout of the packed inputs and outputs (words)
+  struct Seg {
+    uint32_t gi, waves, exp_bits;
+    size_t in_b, in_e, in_m, out_o, ws, sched;
+    bool use_sched;
+    double alg;
+  };
+  std::vector<Seg> segs;
+  size_t in_words = 0, out_words = 0, ws_words = 0;
+  for (uint32_t i = 0; i < n_groups; ++i) {
+    const mpcx_modexp_group_t& g = gs[i];
+    if (g.count == 0) continue;
+    Seg sg{};
+    sg.gi = i;
+    sg.waves = (g.count + G - 1) / G;
+    sg.exp_bits = max_exp_bits(g.exps, g.exp_words, g.exp_shared, g.count);
+    sg.in_b = in_words;
+    in_words += (size_t)g.count * g.base_words;
+    sg.in_e = in_words;
+    in_words += g.exp_shared ? g.exp_words : (size_t)g.count * g.exp_words;
+    sg.in_m = in_words;
+    if (g.muls) in_words += (size_t)g.count * g.mul_words;
+    sg.out_o = out_words;
+    out_words += (size_t)g.count * g.out_words;
+    sg.ws = ws_words;
+    ws_words += (size_t)sg.waves * MPCX_TABLE_ENTRIES * K * 64u;
+    sg.use_sched = g.exp_shared && sg.exp_bits > 0 && g_sched_width > 0;
+    if (g.exp_shared || !g.exp_words) {
+      sg.alg = go_macs(g.mod->bits, sg.exp_bits) * g.count;
+    } else {
+      sg.alg = 0.0;
+      for (uint32_t k = 0; k < g.count; ++k)
+        sg.alg += go_macs(g.mod->bits, bit_length_words(g.exps + (size_t)k * g.exp_words, g.exp_words));
+    }
+    segs.push_back(sg);
+  }
+  for (auto& sg : segs)
+    if (sg.use_sched) {
+      sg.sched = ws_words;
+      ws_words += MPCX_SCHED_WORDS(32u * gs[sg.gi].exp_words);
+    }
+  const size_t nseg = segs.size();
+  const size_t seg_bytes = nseg * sizeof(mpcx::ModexpArgs), first_bytes = (nseg + 1) * sizeof(uint32_t);
+  std::vector<uint32_t> host_in(in_words);
+  for (const auto& sg : segs) {
+    const mpcx_modexp_group_t& g = gs[sg.gi];
+    std::memcpy(&host_in[sg.in_b], g.bases, (size_t)g.count * g.base_words * 4);
+    const size_t ne = g.exp_shared ? g.exp_words : (size_t)g.count * g.exp_words;
+    if (ne) std::memcpy(&host_in[sg.in_e], g.exps, ne * 4);
+    if (g.muls) std::memcpy(&host_in[sg.in_m], g.muls, (size_t)g.count * g.mul_words * 4);
+  }
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(dev, lk);
+  if ((rc = lane_stream(l))) return rc;
+  if ((rc = ensure_buffer(l.stage[0], std::max<size_t>(in_words * 4, 4))) ||
+      (rc = ensure_buffer(l.stage[2], out_words * 4)) || (rc = ensure_buffer(l.stage[3], seg_bytes + first_bytes)) ||
+      (rc = ensure_workspace(l, ws_words * 4)))
+    return rc;
+  const uint32_t* d_in = (const uint32_t*)l.stage[0].ptr;
+  uint32_t* d_out = (uint32_t*)l.stage[2].ptr;
+  if ((rc = h2d(l.stage[0].ptr, host_in.data(), in_words * 4, l.st))) return rc;
+  std::vector<mpcx::ModexpArgs> args(nseg);
+  std::vector<uint32_t> first(nseg + 1, 0);
+  std::vector<const uint32_t*> dconst(nseg);
+  for (size_t k = 0; k < nseg; ++k) {
+    const Seg& sg = segs[k];
+    const mpcx_modexp_group_t& g = gs[sg.gi];
+    if ((rc = mod_const(g.mod, di, &dconst[k]))) return rc;
+    if (sg.use_sched) {
+      mpcx::ExpSchedArgs sa{};
+      sa.exp = d_in + sg.in_e;
+      sa.exp_words = g.exp_words;
+      sa.max_width = (uint32_t)g_sched_width;
+      sa.sched = l.ws + sg.sched;
+      hipError_t e = mpcx_launch_expsched(&sa, l.st);
+      if (e != hipSuccess) return hip_fail(e, "launch k_expsched");
+    }
+    mpcx::ModexpArgs& a = args[k];
+    a.nd = dconst[k] + g.mod->const_off[geom];
+    a.r1d = a.nd + L;
+    a.r2d = a.nd + 2 * L;
+    a.base = d_in + sg.in_b;
+    a.exps = g.exp_words ? d_in + sg.in_e : nullptr;
+    a.mul = g.muls ? d_in + sg.in_m : nullptr;
+    a.out = d_out + sg.out_o;
+    a.table = l.ws + sg.ws;
+    a.count = g.count;
+    a.base_words = g.base_words;
+    a.exp_words = g.exp_words;
+    a.mul_words = g.muls ? g.mul_words : 0;
+    a.exp_bits = g.exp_words ? sg.exp_bits : 0;
+    a.win_bits = (!g.exp_shared && a.exp_bits > 1024u && g_fixed_win >= 5) ? 5u : 4u;
+    a.out_words = g.out_words;
+    a.n0inv = g.mod->n0inv;
+    a.exp_shared = g.exp_shared ? 1 : 0;
+    a.sched = sg.use_sched ? l.ws + sg.sched : nullptr;
+    first[k + 1] = first[k] + sg.waves;
+  }
+  if ((rc = h2d(l.stage[3].ptr, args.data(), seg_bytes, l.st)) ||
+      (rc = h2d((char*)l.stage[3].ptr + seg_bytes, first.data(), first_bytes, l.st)))
+    return rc;
+  hipError_t e = mpcx_launch_modexp_multi(geom, (const mpcx::ModexpArgs*)l.stage[3].ptr,
+                                          (const uint32_t*)((const char*)l.stage[3].ptr + seg_bytes),
+                                          (uint32_t)nseg, first[nseg], l.st);
+  if (e != hipSuccess) return hip_fail(e, "launch k_modexp_multi");
+  dev.launches.fetch_add(1, std::memory_order_relaxed);
+  for (const auto& sg : segs) launch_log("modexp_multi", geom, gs[sg.gi].count, gs[sg.gi].mod->bits, sg.exp_bits, sg.alg);
+  std::vector<uint32_t> host_out(out_words);
+  if ((rc = d2h_sync(host_out.data(), d_out, out_words * 4, l))) return rc;
+  for (const auto& sg : segs) {
+    const mpcx_modexp_group_t& g = gs[sg.gi];
+    std::memcpy(g.out, &host_out[sg.out_o], (size_t)g.count * g.out_words * 4);
+  }
+  return MPCX_OK;
 }
 
 // ------------------------------------------------------------ secp256k1

@@ -323,9 +323,11 @@ __device__ __forceinline__ void store_result(uint32_t (&A)[K], const uint32_t (&
   }
 }
 
-// Batched x_i^e_i mod m for one registered odd modulus m.
-template <int P, int K, int G, int WPE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp(const ModexpArgs a) {
+// Batched x_i^e_i mod m for one registered odd modulus m: wavefront `blk` of
+// the batch described by a (k_modexp: one batch per launch; k_modexp_multi:
+// several batches, each its own segment of the launch's wavefronts).
+template <int P, int K, int G>
+__device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t blk) {
   constexpr int L = P * K;
   __shared__ uint32_t lds[(G + 1) * L + 2];  // +2: the b prefetch reads up to two past a row
   const int lane = threadIdx.x;
@@ -333,7 +335,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const bool idle = g_raw >= G;  // lanes beyond G*P carry zeros
   const int g = idle ? G : g_raw;
   const int p = lane - g_raw * P;
-  const uint32_t op = blockIdx.x * G + (idle ? 0 : g_raw);
+  const uint32_t op = blk * G + (idle ? 0 : g_raw);
   const bool active = !idle && op < a.count;
   uint32_t* bl = lds + g * L;
   const int m_src_addr = (idle ? lane : g_raw * P) * 4;
@@ -373,7 +375,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   // Per-wavefront table of MPCX_TABLE_ENTRIES entries x K digit-slots x 64 lanes, accessed
   // through a buffer descriptor: lane offset in one VGPR, entry/slot offset
   // in an SGPR (no per-slot address registers live across the montmuls).
-  uint32_t* tbl = a.table + (size_t)blockIdx.x * MPCX_TABLE_ENTRIES * K * 64u;
+  uint32_t* tbl = a.table + (size_t)blk * MPCX_TABLE_ENTRIES * K * 64u;
   const auto tbl_rsrc =
       __builtin_amdgcn_make_buffer_rsrc(tbl, (short)0, (int)(MPCX_TABLE_ENTRIES * K * 64u * 4u), 0x00020000);
   const int tbl_lane_off = lane * 4;
@@ -559,6 +561,25 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   }
 
   store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
+}
+
+template <int P, int K, int G, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp(const ModexpArgs a) {
+  modexp_wave<P, K, G>(a, blockIdx.x);
+}
+
+// Several batches of one modulus class in one launch (mpcx_modexp_multi_batch:
+// different moduli, shared or per-operand exponents, multipliers): segment s
+// owns wavefronts [first[s], first[s+1]) and its own ModexpArgs (constants,
+// schedule, window-table region), read wave-uniformly.
+template <int P, int K, int G, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp_multi(
+    const ModexpArgs* __restrict__ segs, const uint32_t* __restrict__ first, uint32_t nsegs) {
+  const uint32_t b = blockIdx.x;
+  uint32_t s = 0;
+  while (s + 1u < nsegs && __builtin_amdgcn_readfirstlane(first[s + 1u]) <= b) ++s;
+  s = __builtin_amdgcn_readfirstlane(s);
+  modexp_wave<P, K, G>(segs[s], b - __builtin_amdgcn_readfirstlane(first[s]));
 }
 
 // Fixed-base multi-exponentiation: out_i = mul_i * prod_t b_t^(e_t,i) mod m

@@ -36,6 +36,15 @@ __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_g, 
   return hipGetLastError();
 }
 
+// several batches in one launch: segs / first are device arrays of nsegs entries
+__attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_multi_g, MPCX_GEOM_ID)(
+    const mpcx::ModexpArgs* segs, const uint32_t* first, uint32_t nsegs, uint32_t waves, hipStream_t st) {
+  hipLaunchKernelGGL((mpcx::k_modexp_multi<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
+                                           MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>),
+                     dim3(waves), dim3(64), 0, st, segs, first, nsegs);
+  return hipGetLastError();
+}
+
 #if MPCX_GEOM_ID == MPCX_MAIN_GEOM(0) || MPCX_GEOM_ID == MPCX_MAIN_GEOM(1)
 // fixed-base comb kernel: main geometry of the <= 2080-bit classes (N~, N; tables are laid out for it)
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_fixedbase_g, MPCX_GEOM_ID)(

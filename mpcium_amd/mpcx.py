@@ -55,6 +55,7 @@ SIGNATURES = [
                                          ctypes.c_uint32]),
     ("mpcx_fermat2_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp]),
     ("mpcx_ec_combine_batch", ctypes.c_int, [ctypes.c_uint32, _vp, _vp, _vp]),
+    ("mpcx_modexp_multi_batch", ctypes.c_int, [ctypes.c_uint32, _vp]),
     ("mpcx_mr_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
     ("mpcx_fixedbase_register", ctypes.c_int, [_vp, _vp, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(_vp)]),
     ("mpcx_fixedbase_release", ctypes.c_int, [_vp]),
@@ -294,6 +295,34 @@ class Modulus:
         B = self._operands(bases, "bases")
         E, shared = self._exps(exps, len(bases))
         return words_to_ints(self.exp_words(B, E, shared))
+
+
+class ModexpGroup(ctypes.Structure):
+    """mpcx_modexp_group_t"""
+    _fields_ = [("mod", _vp), ("count", ctypes.c_uint32), ("bases", _vp), ("base_words", ctypes.c_uint32),
+                ("exps", _vp), ("exp_words", ctypes.c_uint32), ("exp_shared", ctypes.c_int), ("muls", _vp),
+                ("mul_words", ctypes.c_uint32), ("out", _vp), ("out_words", ctypes.c_uint32)]
+
+
+def modexp_multi(groups) -> List[List[int]]:
+    """Several batches in one launch (mpcx_modexp_multi_batch): groups of
+    (Modulus, bases, exps: one shared int or one per base, muls or None) ->
+    [[mul_i * b_i^e_i mod m] per group]."""
+    keep, outs = [], []
+    arr = (ModexpGroup * max(1, len(groups)))()
+    for i, (mod, bases, exps, muls) in enumerate(groups):
+        B = mod._operands(bases, "bases")
+        E, shared = Modulus._exps(exps, len(bases))
+        Mu = mod._operands(muls, "muls") if muls is not None else None
+        out = np.zeros((len(bases), mod.words), dtype="<u4")
+        keep += [B, E, Mu]
+        outs.append(out)
+        arr[i] = ModexpGroup(mod.handle, len(bases), B.ctypes.data if len(bases) else None, mod.class_words,
+                             E.ctypes.data if E.size else None, E.shape[-1] if E.size else 0, 1 if shared else 0,
+                             Mu.ctypes.data if Mu is not None else None, mod.class_words if Mu is not None else 0,
+                             out.ctypes.data if len(bases) else None, mod.words)
+    _check(lib().mpcx_modexp_multi_batch(len(groups), arr))
+    return [words_to_ints(o) if o.shape[0] else [] for o in outs]
 
 
 class Job:

@@ -268,3 +268,41 @@ def test_fixed_base_tables(gpu, paillier_key):
     f2.release()
     f1.release()
     mod.release()
+
+
+def test_multi_batch_groups_of_different_moduli(gpu):
+    """mpcx_modexp_multi_batch: groups of three different 4096-bit moduli (the
+    nodes' N^2), shared and per-operand exponents, with and without
+    multipliers, an empty group and a one-operand group, in ONE launch; every
+    result equals pow(). Groups of two classes are refused."""
+    import json
+    import os
+    import random
+    from conftest import GOLDEN
+    from mpcium_amd import mpcx
+    mpcx.init(0)
+    d = json.load(open(os.path.join(GOLDEN, "node_preparams.json")))
+    Ns = [int(n["N"], 16) for n in d["nodes"]]
+    rng = random.Random(0x3A17)
+    mods = [mpcx.Modulus(N * N) for N in Ns]
+    try:
+        groups, want = [], []
+        for k, (N, mod) in enumerate(zip(Ns, mods)):
+            N2 = N * N
+            xs = [rng.randrange(N2) for _ in range(37 + 50 * k)]
+            es = [rng.getrandbits(rng.choice([256, 768, 2048])) for _ in xs]
+            ms = [rng.randrange(N2) for _ in xs]
+            groups += [(mod, xs, N, None), (mod, xs, es, ms), (mod, xs[:1], es[:1], None), (mod, [], N, None)]
+            want += [[pow(x, N, N2) for x in xs], [m * pow(x, e, N2) % N2 for x, e, m in zip(xs, es, ms)],
+                     [pow(xs[0], es[0], N2)], []]
+        got = mpcx.modexp_multi(groups)
+        assert got == want
+        modn = mpcx.Modulus(Ns[0])
+        try:
+            with pytest.raises(mpcx.MpcxError):
+                mpcx.modexp_multi([(mods[0], [3], 5, None), (modn, [3], 5, None)])
+        finally:
+            modn.release()
+    finally:
+        for m in mods:
+            m.release()
