@@ -51,6 +51,9 @@
 #ifndef MPCX_PREFETCH_B
 #define MPCX_PREFETCH_B 1
 #endif
+#ifndef MPCX_PRIME2C_DBL_FOLD
+#define MPCX_PRIME2C_DBL_FOLD 1  // k_prime2c: the square-and-double step as one product with B = 2^bit x
+#endif
 #ifndef MPCX_WAVES_PER_EU_FERMAT
 #define MPCX_WAVES_PER_EU_FERMAT 1
 #endif
@@ -1326,6 +1329,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0) ? 1u : 0u;
       lds_store_digits<K>(sv, p, A);
       lds_store_digits<K>(bl, p, one);
+    } else if (MPCX_PRIME2C_DBL_FOLD && st == SQ) {
+      // x <- 2^bit x^2 as ONE squaring product: B = 2^bit x in LDS, x in
+      // registers -- the half-product schedule then sums x_i (2 x_j) pairs
+      // (digits of B < 2^29 + 2^11, b2 < 2^31: the schedule's bounds hold, and
+      // x (2x) < 8n^2 < nR keeps the result < 2n); no separate doubling pass
+      const int jb = i + sh;  // bit jb of n - 1: bit jb of n except bit 0 (n odd)
+      const uint32_t dsh = (jb > 0 && jb < nbits && word_bit(nw, jb)) ? 1u : 0u;
+      uint32_t B2[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) B2[k] = A[k] << dsh;
+      lds_store_digits<K>(bl, p, B2);
     } else {
       lds_store_digits<K>(bl, p, A);
     }
@@ -1336,8 +1350,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       montmul<P, K, true>(A, bl, Nd, n0inv, 0, p);
     }
     if (st == SQ) {
-      const int jb = i + sh;  // bit jb of n - 1: bit jb of n except bit 0 (n odd)
-      double_digits<P, K>(A, jb > 0 && jb < nbits && word_bit(nw, jb));
+      if (!MPCX_PRIME2C_DBL_FOLD) {
+        const int jb = i + sh;  // bit jb of n - 1: bit jb of n except bit 0 (n odd)
+        double_digits<P, K>(A, jb > 0 && jb < nbits && word_bit(nw, jb));
+      }
       if (--i < 0) st = EX;
     } else if (st == SS) {
       st = EX;

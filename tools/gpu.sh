@@ -7,6 +7,7 @@
 #   bash tools/gpu.sh trace  OUT [bench args]    rocprofv3 --kernel-trace --stats of bench.py + segments
 #   bash tools/gpu.sh pmc    OUT COUNTERS [bench args]   one rocprofv3 --pmc pass (COUNTERS comma-free, space-joined in quotes)
 #   bash tools/gpu.sh ab     OUT N LIB_A LIB_B [bench args]  N interleaved config-2 runs per libmpcx build
+#   bash tools/gpu.sh abswap OUT N LIB_A LIB_B [bench args]  N interleaved full-bench runs, LIB swapped in place
 #   bash tools/gpu.sh envab  OUT N "ENV_A" "ENV_B" [bench args]  N interleaved runs under two environments
 #   bash tools/gpu.sh py     OUT script.py [args]            any python tool (tools/*.py) under a 600 s limit
 set -o pipefail
@@ -65,6 +66,23 @@ ab)
       echo -n "$lib run $i: "; summ $O/ab_$tag.json short
     done
   done ;;
+abswap)
+  # whole-library A/B: the variant replaces mpcium_amd/libmpcx.so for its runs
+  # (libmpcx_host.so loads that file), the original is restored after each
+  n=$1; la=$2; lb=$3; shift 3
+  cp mpcium_amd/libmpcx.so $O/orig_libmpcx.so
+  for i in $(seq 1 $n); do
+    for lib in $la $lb; do
+      [ $lib = $la ] && tag=A_$i || tag=B_$i
+      cp $lib mpcium_amd/libmpcx.so.tmp && mv mpcium_amd/libmpcx.so.tmp mpcium_amd/libmpcx.so
+      timeout -k 10 600 python3 bench.py "$@" > $O/ab_$tag.json 2> $O/ab_$tag.err
+      rc=$?
+      cp $O/orig_libmpcx.so mpcium_amd/libmpcx.so
+      [ $rc -eq 0 ] || { tail $O/ab_$tag.err; exit 1; }
+      echo "== $lib run $i"; summ $O/ab_$tag.json
+    done
+  done
+  rm -f $O/orig_libmpcx.so ;;
 envab)
   n=$1; ea=$2; eb=$3; shift 3
   for i in $(seq 1 $n); do
