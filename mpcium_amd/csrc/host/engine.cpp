@@ -317,7 +317,10 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
     MPCX_PROF("engine.exp.gpu");
     enter_call();
     const int inflight = coalesce_inflight();
-    if (inflight > 0) {
+    // a batch already wide enough to fill the GPU gains nothing from merging
+    // (config-5's 128-iteration DLN batches): it launches alone, outside the
+    // coalescer's in-flight budget
+    if (inflight > 0 && n < kCoalesceAloneOps) {
       Coalescer::Req r;
       r.g.mod = md.h;
       r.g.count = (uint32_t)n;

@@ -21,9 +21,11 @@ namespace mpcx::host {
 
 // Launch coalescing (engine.cpp Coalescer): at most kCoalesceInflight merged
 // dispatches per bound GPU in flight (environment MPCX_COALESCE overrides;
-// 0 turns coalescing off), each at most kCoalesceMaxOps operands.
+// 0 turns coalescing off), each at most kCoalesceMaxOps operands; a call of
+// kCoalesceAloneOps operands or more launches on its own.
 constexpr int kCoalesceInflight = 3;
 constexpr uint64_t kCoalesceMaxOps = 131072;
+constexpr size_t kCoalesceAloneOps = 16384;  // wider calls launch on their own
 
 class EngineError : public std::runtime_error {
  public:

@@ -36,6 +36,7 @@ inline void run_concurrently(const std::vector<std::function<void()>>& fs) {
   std::vector<std::thread> th;
   for (size_t i = 0; i + 1 < fs.size(); ++i)
     th.emplace_back([&, i] {
+      MPCX_PROF_CPU("cpu.launch_threads");
       try {
         fs[i]();
       } catch (...) {

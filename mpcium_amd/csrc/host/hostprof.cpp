@@ -5,6 +5,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <mutex>
 #include <vector>
 
@@ -33,6 +34,12 @@ int slot_of(const char* label) {
   if (g_n >= kSlots) return kSlots - 1;
   g_label[g_n] = label;
   return g_n++;
+}
+
+uint64_t thread_cpu_ns() {
+  timespec ts{};
+  clock_gettime(CLOCK_THREAD_CPUTIME_ID, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
 void add(int slot, uint64_t ns) {

@@ -33,6 +33,25 @@ class Scope {
   std::chrono::steady_clock::time_point t0_;
 };
 
+// CPU seconds of the calling thread (CLOCK_THREAD_CPUTIME_ID)
+uint64_t thread_cpu_ns();
+
+// CPU time (not wall time) of this thread from construction to destruction,
+// summed under `slot`: wraps a thread's entry function so the report splits
+// the process's CPU by thread role (pool workers, protocol tasks, launch
+// threads); whatever the roles do not cover is the HIP runtime's and Python's.
+class ThreadCpu {
+ public:
+  explicit ThreadCpu(int slot) : slot_(enabled() ? slot : -1), t0_(slot_ >= 0 ? thread_cpu_ns() : 0) {}
+  ~ThreadCpu() {
+    if (slot_ >= 0) add(slot_, thread_cpu_ns() - t0_);
+  }
+
+ private:
+  int slot_;
+  uint64_t t0_;
+};
+
 }  // namespace mpcx::host::prof
 
 #define MPCX_PROF_CAT2(a, b) a##b
@@ -41,3 +60,7 @@ class Scope {
 #define MPCX_PROF(label)                                                       \
   static const int MPCX_PROF_CAT(mpcx_prof_slot_, __LINE__) = ::mpcx::host::prof::slot_of(label); \
   ::mpcx::host::prof::Scope MPCX_PROF_CAT(mpcx_prof_scope_, __LINE__)(MPCX_PROF_CAT(mpcx_prof_slot_, __LINE__))
+// MPCX_PROF_CPU("label"): this thread's CPU time over the rest of the scope
+#define MPCX_PROF_CPU(label)                                                   \
+  static const int MPCX_PROF_CAT(mpcx_profc_slot_, __LINE__) = ::mpcx::host::prof::slot_of(label); \
+  ::mpcx::host::prof::ThreadCpu MPCX_PROF_CAT(mpcx_profc_scope_, __LINE__)(MPCX_PROF_CAT(mpcx_profc_slot_, __LINE__))

@@ -11,6 +11,7 @@
 #include <thread>
 
 #include "engine.hpp"
+#include "hostprof.hpp"
 #include "proofs.hpp"
 
 namespace mpcx::host::keygenload {
@@ -33,6 +34,7 @@ void run_bounded(const std::vector<std::function<void()>>& tasks, size_t width) 
   std::atomic<size_t> next{0};
   std::vector<std::exception_ptr> errs(tasks.size());
   auto worker = [&] {
+    MPCX_PROF_CPU("cpu.keygen_tasks");
     for (;;) {
       const size_t t = next.fetch_add(1);
       if (t >= tasks.size()) return;

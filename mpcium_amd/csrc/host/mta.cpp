@@ -210,11 +210,18 @@ void bob_draw(std::vector<BobProveState>& st, const std::vector<size_t>& js, con
   std::vector<Nat*> beta(n);
   for (size_t k = 0; k < n; ++k) beta[k] = &st[js[k]].beta;
   GetRandomPositiveRelativelyPrimeIntBatch(rd, pk.N, beta);
-  parallel_for(n, [&](size_t k) {
-    BobProveState& s = st[js[k]];
-    s.gamma = GetRandomPositiveInt(*rd[k], q7());
-    if (s.wc) s.u = secp::ScalarBaseMult(s.alpha);  // 5. u = alpha*G
-  });
+  parallel_for(n, [&](size_t k) { st[js[k]].gamma = GetRandomPositiveInt(*rd[k], q7()); });
+  // 5. u = alpha*G of every WC session, one GPU batch (k_ec_combine)
+  std::vector<secp::Comb> cu;
+  std::vector<size_t> wc;
+  for (size_t k = 0; k < n; ++k)
+    if (st[js[k]].wc) {
+      wc.push_back(js[k]);
+      cu.emplace_back();
+      cu.back().a = st[js[k]].alpha;
+    }
+  const std::vector<secp::Affine> u = secp::CombineBatch(cu);
+  for (size_t k = 0; k < wc.size(); ++k) st[wc[k]].u = u[k];
 }
 
 // stage A of ProveBob: N^2 -> bg = Gamma^gamma beta^N ; N~ -> h1^x, h1^alpha, h1^y, h1^gamma
@@ -331,27 +338,43 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
     for (size_t j = 0; j < sel.size(); ++j)
       ok[sel[j]] = ct[4 * j] && ct[4 * j + 1] && ct[4 * j + 2] && ct[4 * j + 3] && cn[2 * j] && cn[2 * j + 1];
   }
+  // 4. (WC) s1*G == e*X + u, rejected when e*X + u is the point at infinity
+  // (Go: xEU nil). Evaluated as one combination T = s1*G + (q - e)*X compared
+  // with u: T == u  <=>  s1*G == e*X + u as group elements, and when that
+  // holds, e*X + u = infinity  <=>  s1*G = infinity  <=>  s1 == 0 (mod q).
+  // Every session's combination in one GPU batch (k_ec_combine).
+  std::vector<secp::Comb> cw(n);
+  std::vector<uint8_t> is_wc(n, 0);
   parallel_for(n, [&](size_t i) {
     if (!ok[i]) return;
-    ok[i] = 0;
     const auto& p = *pfp[i];
     e[i] = bob_challenge(*session[i], pk, gamma, X[i], *c1[i], *c2[i], p);
     if (X[i]) {
-      // 4. s1*G == e*X + u, rejected when e*X + u is the point at infinity
-      // (Go: xEU nil). Evaluated as one combination T = s1*G + (q - e)*X
-      // compared with u: T == u  <=>  s1*G == e*X + u as group elements, and
-      // when that holds, e*X + u = infinity  <=>  s1*G = infinity  <=>
-      // s1 == 0 (mod q). Same decision as two scalar multiplications, an
-      // addition and three affine conversions, for one chain and one.
       const Nat s1q = p.S1 % Q();
-      if (s1q.is_zero()) return;
+      if (s1q.is_zero()) {
+        ok[i] = 0;
+        return;
+      }
       const Nat eq = e[i] % Q();
-      const secp::Affine T = secp::LinComb(s1q, *X[i], eq.is_zero() ? eq : Q() - eq);
-      if (!secp::Equal(T, p.U)) return;
+      cw[i].a = s1q;
+      cw[i].P = *X[i];
+      cw[i].b = eq.is_zero() ? eq : Q() - eq;
+      is_wc[i] = 1;
     }
     gt1[i] = gamma_pow(p.T1, pk.N);
-    ok[i] = 1;
   });
+  {
+    std::vector<secp::Comb> items;
+    std::vector<size_t> idx;
+    for (size_t i = 0; i < n; ++i)
+      if (ok[i] && is_wc[i]) {
+        idx.push_back(i);
+        items.push_back(std::move(cw[i]));
+      }
+    const std::vector<secp::Affine> T = secp::CombineBatch(items);
+    for (size_t k = 0; k < idx.size(); ++k)
+      if (!secp::Equal(T[k], pfp[idx[k]]->U)) ok[idx[k]] = 0;
+  }
   // Equation 7 holds mod N^2 iff it holds mod P^2 and mod Q^2 (CRT): the key
   // holder (AliceEnd) checks it on the two half-width moduli, a quarter of the
   // Montgomery work each; everyone else mod N^2.
@@ -494,6 +517,7 @@ namespace {
 void both(const std::function<void()>& f, const std::function<void()>& g) {
   std::exception_ptr ef, eg;
   std::thread t([&] {
+    MPCX_PROF_CPU("cpu.mta_halves");
     try {
       g();
     } catch (...) {

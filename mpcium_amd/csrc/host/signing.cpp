@@ -25,6 +25,7 @@ void run_tasks(const std::vector<std::function<void()>>& tasks) {
   std::vector<std::thread> th;
   for (size_t t = 0; t < tasks.size(); ++t)
     th.emplace_back([&, t] {
+      MPCX_PROF_CPU("cpu.sign_tasks");
       try {
         tasks[t]();
       } catch (...) {
@@ -157,6 +158,7 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
   std::vector<secp::Affine> XW(Wn);
   std::exception_ptr ec_err;
   std::thread ec_task([&] {
+    MPCX_PROF_CPU("cpu.sign_ec_task");
     try {
       MPCX_PROF("sign.rounds1_4_ec");
       std::vector<secp::Comb> c(2 * Wn * S);

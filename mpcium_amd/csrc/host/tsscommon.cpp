@@ -529,6 +529,7 @@ class HostPool {
             cv_.wait(lk, [&] { return (l = pending_locked()) != nullptr; });
             l->users.fetch_add(1);  // l stays alive (listed or waited for) until users drops back to 0
           }
+          MPCX_PROF_CPU("cpu.pool_workers");
           finish(l, l->work());
         }
       }).detach();
