@@ -1,11 +1,18 @@
 // hostprof.cpp -- see hostprof.hpp.
 #include "hostprof.hpp"
 
+#include <dlfcn.h>
+#include <execinfo.h>
+#include <signal.h>
+#include <sys/time.h>
+
 #include <algorithm>
+#include <cerrno>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <ctime>
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -47,7 +54,110 @@ void add(int slot, uint64_t ns) {
   g_calls[slot].fetch_add(1, std::memory_order_relaxed);
 }
 
+
+// ---------------------------------------------------------------- sampler
+// MPCX_HOST_SAMPLE=<hz> with MPCX_HOST_SAMPLE_OUT=<file>: SIGPROF (process
+// CPU time, so samples land on whichever thread burns CPU) records a call
+// stack per tick; reset() (re)arms it, report() stops it and writes
+// <file>.<k> (k counts the reports), one line per distinct stack, "count module+0xoff@dynsym;..." innermost first,
+// for tools/host_samples.py to symbolize (addr2line on the same build).
+namespace {
+constexpr int kDepth = 24;
+constexpr size_t kMaxSamples = 1 << 18;
+struct Sample {
+  int n;
+  void* pc[kDepth];
+};
+Sample* g_samples = nullptr;
+std::atomic<size_t> g_nsamp{0};
+std::atomic<bool> g_armed{false};
+
+int sample_hz() {
+  static const int hz = [] {
+    const char* e = std::getenv("MPCX_HOST_SAMPLE");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  return hz;
+}
+
+void on_prof(int, siginfo_t*, void*) {
+  if (!g_armed.load(std::memory_order_relaxed)) return;
+  const int saved = errno;
+  const size_t i = g_nsamp.fetch_add(1, std::memory_order_relaxed);
+  if (i < kMaxSamples) g_samples[i].n = backtrace(g_samples[i].pc, kDepth);
+  errno = saved;
+}
+
+void set_timer(int hz) {
+  itimerval it{};
+  if (hz > 0) {
+    it.it_interval.tv_usec = 1000000 / hz;
+    it.it_value = it.it_interval;
+  }
+  setitimer(ITIMER_PROF, &it, nullptr);
+}
+
+void sampler_arm() {
+  const int hz = sample_hz();
+  if (hz <= 0) return;
+  if (!g_samples) {
+    g_samples = new Sample[kMaxSamples];
+    void* warm[4];
+    (void)backtrace(warm, 4);  // loads the unwinder outside the handler
+    struct sigaction sa {};
+    sa.sa_sigaction = on_prof;
+    sa.sa_flags = SA_SIGINFO | SA_RESTART;
+    sigemptyset(&sa.sa_mask);
+    sigaction(SIGPROF, &sa, nullptr);
+  }
+  g_nsamp = 0;
+  g_armed = true;
+  set_timer(hz);
+}
+
+void sampler_dump() {
+  const char* path = std::getenv("MPCX_HOST_SAMPLE_OUT");
+  if (sample_hz() <= 0 || !g_samples || !g_armed.exchange(false)) return;
+  set_timer(0);
+  const size_t n = std::min(g_nsamp.load(), kMaxSamples);
+  std::map<std::vector<void*>, uint64_t> stacks;
+  for (size_t i = 0; i < n; ++i) {
+    const Sample& s = g_samples[i];
+    // frames 0-1: this handler and the signal trampoline
+    if (s.n > 2) ++stacks[std::vector<void*>(s.pc + 2, s.pc + s.n)];
+  }
+  static int seq = 0;
+  const std::string file = path ? std::string(path) + "." + std::to_string(seq++) : std::string();
+  std::FILE* f = path ? std::fopen(file.c_str(), "w") : nullptr;
+  if (!f) return;
+  std::map<void*, std::string> names;
+  for (const auto& kv : stacks) {
+    std::fprintf(f, "%llu ", (unsigned long long)kv.second);
+    for (size_t j = 0; j < kv.first.size(); ++j) {
+      void* pc = kv.first[j];
+      auto it = names.find(pc);
+      if (it == names.end()) {
+        Dl_info di{};
+        char buf[512];
+        // return addresses point after the call: -1 lands inside it
+        if (dladdr(pc, &di) && di.dli_fname)
+          std::snprintf(buf, sizeof buf, "%s+0x%llx@%s", di.dli_fname,
+                        (unsigned long long)((char*)pc - (char*)di.dli_fbase - (j ? 1 : 0)),
+                        di.dli_sname ? di.dli_sname : "");
+        else
+          std::snprintf(buf, sizeof buf, "?+0x%llx", (unsigned long long)(uintptr_t)pc);
+        it = names.emplace(pc, buf).first;
+      }
+      std::fprintf(f, "%s%s", j ? ";" : "", it->second.c_str());
+    }
+    std::fputc('\n', f);
+  }
+  std::fclose(f);
+}
+}  // namespace
+
 void reset() {
+  sampler_arm();
   for (int i = 0; i < kSlots; ++i) {
     g_ns[i] = 0;
     g_calls[i] = 0;
@@ -55,6 +165,7 @@ void reset() {
 }
 
 std::string report() {
+  sampler_dump();
   std::vector<int> idx;
   {
     std::lock_guard<std::mutex> lk(g_mu);

@@ -1267,14 +1267,6 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
     }
   const size_t nseg = segs.size();
   const size_t seg_bytes = nseg * sizeof(mpcx::ModexpArgs), first_bytes = (nseg + 1) * sizeof(uint32_t);
-  std::vector<uint32_t> host_in(in_words);
-  for (const auto& sg : segs) {
-    const mpcx_modexp_group_t& g = gs[sg.gi];
-    std::memcpy(&host_in[sg.in_b], g.bases, (size_t)g.count * g.base_words * 4);
-    const size_t ne = g.exp_shared ? g.exp_words : (size_t)g.count * g.exp_words;
-    if (ne) std::memcpy(&host_in[sg.in_e], g.exps, ne * 4);
-    if (g.muls) std::memcpy(&host_in[sg.in_m], g.muls, (size_t)g.count * g.mul_words * 4);
-  }
   std::unique_lock<std::mutex> lk;
   Lane& l = acquire_lane(dev, lk);
   if ((rc = lane_stream(l))) return rc;
@@ -1284,7 +1276,16 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
     return rc;
   const uint32_t* d_in = (const uint32_t*)l.stage[0].ptr;
   uint32_t* d_out = (uint32_t*)l.stage[2].ptr;
-  if ((rc = h2d(l.stage[0].ptr, host_in.data(), in_words * 4, l.st))) return rc;
+  // each group's arrays straight from the caller's buffers into their offsets
+  // (DMA from page-locked buffers such as libmpcx_host's; no host-side packing)
+  for (const auto& sg : segs) {
+    const mpcx_modexp_group_t& g = gs[sg.gi];
+    const size_t ne = g.exp_shared ? g.exp_words : (size_t)g.count * g.exp_words;
+    if ((rc = h2d((uint32_t*)l.stage[0].ptr + sg.in_b, g.bases, (size_t)g.count * g.base_words * 4, l.st)) ||
+        (rc = h2d((uint32_t*)l.stage[0].ptr + sg.in_e, g.exps, ne * 4, l.st)) ||
+        (g.muls && (rc = h2d((uint32_t*)l.stage[0].ptr + sg.in_m, g.muls, (size_t)g.count * g.mul_words * 4, l.st))))
+      return rc;
+  }
   std::vector<mpcx::ModexpArgs> args(nseg);
   std::vector<uint32_t> first(nseg + 1, 0);
   std::vector<const uint32_t*> dconst(nseg);
@@ -1331,13 +1332,12 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
   if (e != hipSuccess) return hip_fail(e, "launch k_modexp_multi");
   dev.launches.fetch_add(1, std::memory_order_relaxed);
   for (const auto& sg : segs) launch_log("modexp_multi", geom, gs[sg.gi].count, gs[sg.gi].mod->bits, sg.exp_bits, sg.alg);
-  std::vector<uint32_t> host_out(out_words);
-  if ((rc = d2h_sync(host_out.data(), d_out, out_words * 4, l))) return rc;
-  for (const auto& sg : segs) {
+  for (const auto& sg : segs) {  // results straight into each group's buffer
     const mpcx_modexp_group_t& g = gs[sg.gi];
-    std::memcpy(g.out, &host_out[sg.out_o], (size_t)g.count * g.out_words * 4);
+    e = hipMemcpyAsync(g.out, d_out + sg.out_o, (size_t)g.count * g.out_words * 4, hipMemcpyDeviceToHost, l.st);
+    if (e != hipSuccess) return hip_fail(e, "copy results");
   }
-  return MPCX_OK;
+  return lane_wait(l);
 }
 
 // ------------------------------------------------------------ secp256k1
