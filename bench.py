@@ -383,6 +383,7 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict):
     for i in range(0, batch, max(1, batch // 8)):  # untimed spot check vs the oracle formulas
         if cs[i] != gm.paillier_encrypt(N, ms[i], rs[i]) or out[i] != gm.paillier_homo_mult(N, bs[i], cs[i]):
             raise SystemExit(f"paillier line: mismatch at {i}")
+    _kernel_stats_reset()
     t0 = time.perf_counter()
     for _ in range(reps):
         cs, _ = pk.encrypt(ms, rs)
@@ -398,8 +399,9 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict):
     # (E = bit length of b < q); a 1,024-op batch is a small latency-bound launch pair, not a throughput shape
     L2 = 2 * 128 * 128
     alg = sum((2048 + 512) * L2 + (b.bit_length() + (b.bit_length() + 3) // 4) * L2 for b in bs) * reps
-    line["roofline"] = _job_roofline(alg, el)
-    line["roofline"]["scope"] = "end to end (host buffers, Python conversions); batch of 1,024 = latency-bound"
+    line["roofline"] = _kernel_roofline()
+    line["job_roofline"] = _job_roofline(alg, el)
+    line["job_roofline"]["scope"] = "end to end (host buffers, Python conversions); batch of 1,024 = latency-bound"
     line["alg_ops_per_op"] = alg / (batch * reps)
     if cpu:
         line["cpu_baseline"] = cpu_baseline_paillier(N, 12.0, info)
@@ -639,6 +641,7 @@ def keygen_line(args):
         raise SystemExit(f"keygen proofs warmup: {warm}")
     import resource
     rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
+    _kernel_stats_reset()
     st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67, wave=wave)
     rss1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
     if st["failures"]:
@@ -652,7 +655,8 @@ def keygen_line(args):
             "waves": int(st["waves"]), "wave_sessions": int(st["wave_sessions"]), "max_wave_s": st["max_wave_s"],
             "host_max_rss_mb": rss1 / 1024.0, "host_max_rss_mb_before": rss0 / 1024.0,
             "verifications_per_s": st["verifications"] / st["total_s"], "checked": "every verification passes",
-            "roofline": _job_roofline(st["alg_macs"], st["total_s"]),
+            "roofline": _kernel_roofline(),
+            "job_roofline": _job_roofline(st["alg_macs"], st["total_s"]),
             "cpu_baseline": None}
     return line
 
@@ -703,6 +707,43 @@ def _job_roofline(alg_macs: float, seconds: float, world: int = 1) -> dict:
                     "utilization"}
 
 
+def _kernel_stats_reset():
+    """Start per-kernel GPU timing (mpcx_kernel_stats) for a protocol line's
+    timed region: an event pair around every launch, read at the lane's
+    host wait (a few us per launch of several ms)."""
+    from mpcium_amd import mpcx
+    mpcx.set_option("kernel_stats", 1)
+    mpcx.kernel_stats(reset=True)
+
+
+def _kernel_roofline(world: int = 1) -> dict:
+    """Kernel-level roofline of a protocol line (VALU-bound big-int kernels):
+    the kernels' work MACs over the GPU busy time -- the union of every
+    launch's [start, end) on the device, so overlapping lanes count once --
+    against the nominal INT32 MAD peak. Work MACs: Go-equivalent W for the
+    exponentiation kernels (within ~5% of executed: same squarings, 5-bit /
+    sliding windows), executed products x 2 L^2 for the fixed-base comb.
+    Per kernel: its MACs over its summed launch durations (concurrent lanes
+    share the CUs, so these understate each kernel in isolation)."""
+    from mpcium_amd import mpcx
+    ks = mpcx.kernel_stats()
+    mpcx.set_option("kernel_stats", 0)
+    busy_s = ks["busy_ms"] / 1e3
+    tot_ms = sum(k["kernel_ms"] for k in ks["kernels"]) or 1e-9
+    per = []
+    for k in sorted(ks["kernels"], key=lambda k: -k["kernel_ms"]):
+        t = k["kernel_ms"] / 1e3
+        per.append({"kind": k["kind"], "geom": k["geom"], "launches": k["launches"], "operands": k["operands"],
+                    "kernel_ms": k["kernel_ms"], "share_of_kernel_time": k["kernel_ms"] / tot_ms,
+                    "alg_ops": k["alg_macs"],
+                    "frac": (k["alg_macs"] / t / PEAK_INT32_NOMINAL) if t > 0 and k["alg_macs"] else None})
+    ach = ks["alg_macs"] / busy_s if busy_s > 0 else 0.0
+    return {"bound": "valu", "achieved": ach / 1e12, "peak": PEAK_INT32_NOMINAL / 1e12, "unit": "TOP/s",
+            "frac": ach / PEAK_INT32_NOMINAL, "traffic": None, "gpu_busy_s": busy_s, "world": world,
+            "scope": "GPU busy time of rank 0's device (union of launch intervals), all kernels' work MACs",
+            "kernels": per}
+
+
 def signing_line(args, world, rank, signers: int):
     """Config 4 (BASELINE.json): GG18 ECDSA signing of `wallets` wallets per
     GPU by `signers` of the 3 nodes (csrc/host/signing.hpp): MtA / MtAwc with
@@ -717,13 +758,17 @@ def signing_line(args, world, rank, signers: int):
     from mpcium_amd.shard import max_over_ranks
     mhost.init(gpu_index())
     nodes = load_nodes()
-    warm = mta.bench_signing(nodes, signers, 256, seed=0x5167 + 7919 * rank)
-    if warm["errors"] or warm["relation_failures"] or warm["verified"] != 256:
+    # warm-up at the timed size: lane staging buffers and workspaces reach
+    # their steady-state sizes (a node's steady state), so the timed run does
+    # no hipMalloc / hipFree
+    warm = mta.bench_signing(nodes, signers, args.wallets, seed=0x5167 + 7919 * rank)
+    if warm["errors"] or warm["relation_failures"] or warm["verified"] != args.wallets:
         raise SystemExit(f"rank {rank}: signing warmup failed: {warm}")
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     mhost.profile_report(reset=True)
+    _kernel_stats_reset()
     import resource
     ru0 = resource.getrusage(resource.RUSAGE_SELF)
     t0 = time.perf_counter()
@@ -752,7 +797,8 @@ def signing_line(args, world, rank, signers: int):
             "checked": "alpha+beta == k*gamma, mu+nu == k*w (mod q) on every session; every round-1/4-9 "
                        "commitment, Schnorr and ZKV proof of every signer; ecdsa.Verify of every signature by "
                        "every signer (tss-lib finalize and mpcium's session)",
-            "roofline": _job_roofline(st["alg_macs"], el, world),
+            "roofline": _kernel_roofline(world),
+            "job_roofline": _job_roofline(st["alg_macs"], el, world),
             "alg_ops_per_signature": st["alg_macs"] / args.wallets,
             "scope": "all of tss-lib's GG18 signing rounds: MtA/MtAwc + range proofs (rounds 1-3) on the GPU; "
                      "round-1/5/7 commitments, round-4/6 Schnorr and ZKV proofs and their verification, "

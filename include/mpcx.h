@@ -101,6 +101,23 @@ int mpcx_bound_devices(int* out_count, int* ordinals, int max_ordinals);
  * actually used. */
 int mpcx_device_launches(int index, uint64_t* out);
 
+/* Kernel statistics of the batch entry points (modexp, multi-batch,
+ * fixed-base, secp256k1), collected while option "kernel_stats" is 1: an
+ * event pair around every launch, resolved at the lane's host wait. Writes a
+ * JSON object to buf (NUL-terminated; MPCX_EINVAL if cap is too small):
+ *   {"enabled":0|1,"busy_ms":B,"alg_macs":A,"kernels":[{"kind":..,"geom":g,
+ *    "launches":n,"operands":n,"alg_macs":a,"kernel_ms":t},...]}
+ * alg_macs: Go-equivalent work (SURVEY.md 8(d) W per exponentiation) for
+ * the exponentiation kernels -- within ~5% of what they execute (same
+ * squarings; 5-bit or sliding windows instead of 4-bit) -- and the executed
+ * products x 2 L^2 for the fixed-base comb (one per 8-bit window, far below
+ * Go's work for the same Exp); 0 for secp256k1;
+ * kernel_ms: summed launch durations (lanes overlap, so the kinds' sum can
+ * exceed busy_ms, the union of all launches' intervals per device, summed
+ * over devices). reset != 0: clear after reading and start a new time
+ * origin on every bound device (call while no launch is in flight). */
+int mpcx_kernel_stats(char* buf, size_t cap, int reset);
+
 /* Device (index into the bound set, default 0) used by THIS thread's
  * device-buffer calls, modulus registration, comb-table builds, mpcx_dev_alloc
  * and mpcx_stream_create. Moduli and comb tables are usable on every bound
@@ -347,6 +364,8 @@ int mpcx_sync(void* stream);
  *                bound ordinal binds it again as another logical device (own
  *                lanes, constants, workspaces), so the multi-device split and
  *                gather run concurrently on a one-GPU box.
+ *   "kernel_stats" 0 (default) / 1: time every batch-entry-point launch
+ *                with an event pair for mpcx_kernel_stats.
  *   "mid_rounds" 0..400 (default 0): with geom_policy 0, 4096-bit batches
  *                under mid_rounds/100 of a main round run in the mid geometry.
  *   "fixed_window" 4 or 5 (default 5): widest fixed window for per-operand

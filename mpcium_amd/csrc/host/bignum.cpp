@@ -24,6 +24,11 @@ Nat Nat::from_words(const uint32_t* w, size_t n) {
   return r;
 }
 
+void Nat::set_words(const uint32_t* w, size_t n) {
+  while (n && !w[n - 1]) --n;
+  w_.assign(w, w + n);
+}
+
 Nat Nat::from_bytes_be(const uint8_t* b, size_t n) {
   Nat r;
   r.w_.assign((n + 3) / 4, 0);

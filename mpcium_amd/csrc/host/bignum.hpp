@@ -16,6 +16,7 @@ class Nat {
   Nat() = default;
   explicit Nat(uint64_t v);
   static Nat from_words(const uint32_t* w, size_t n);
+  void set_words(const uint32_t* w, size_t n);  // = from_words(w, n), one exact-size allocation
   static Nat from_bytes_be(const uint8_t* b, size_t n);  // Go big.Int.SetBytes
   static Nat from_hex(const std::string& s);
 

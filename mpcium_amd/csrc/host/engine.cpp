@@ -3,6 +3,7 @@
 
 #include <condition_variable>
 #include <deque>
+#include <malloc.h>
 #include <string>
 
 #include "hostprof.hpp"
@@ -26,7 +27,23 @@ Engine& Engine::get() {
   return *e;
 }
 
+// The protocol mirrors allocate and free millions of small bignums per second
+// from many threads. glibc's per-thread arenas then grow (mprotect) and trim
+// their heaps back on nearly every batch: an eighth of a signing run's CPU
+// (profiles/r03/sample1). A high trim threshold and top pad keep the arenas'
+// heaps mapped instead (MPCX_MALLOC_TUNE=0: glibc defaults, for A/B runs).
+static void tune_malloc() {
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const char* e = std::getenv("MPCX_MALLOC_TUNE");
+    if (e && e[0] == '0') return;
+    mallopt(M_TRIM_THRESHOLD, 512 << 20);
+    mallopt(M_TOP_PAD, 8 << 20);
+  });
+}
+
 void Engine::init(int device) {
+  tune_malloc();
   std::lock_guard<std::mutex> lk(mu_);
   int rc = mpcx_init(device);
   if (rc) throw_last(rc, "mpcx_init");
@@ -36,6 +53,7 @@ void Engine::init(int device) {
 }
 
 void Engine::init_devices(int n_gpus) {
+  tune_malloc();
   std::lock_guard<std::mutex> lk(mu_);
   int rc = mpcx_init_devices(n_gpus);
   if (rc) throw_last(rc, "mpcx_init_devices");
@@ -65,17 +83,17 @@ double Engine::busy_seconds_now() {
   return (double)ns * 1e-9;
 }
 
-void Engine::count_work(const Nat& m, const std::vector<Nat>& exps, size_t count) {
+void Engine::count_work(const Nat& m, const Nat* const* exps, size_t n_exps, size_t count) {
   const uint64_t L = m.words(), l2 = 2 * L * L;
   uint64_t w = 0;
   auto one = [&](const Nat& e) {
     const uint64_t E = e.bit_len();
     return (E + (E + 3) / 4) * l2;
   };
-  if (exps.size() == 1 && count != 1) {
-    w = one(exps[0]) * count;
+  if (n_exps == 1 && count != 1) {
+    w = one(*exps[0]) * count;
   } else {
-    for (const auto& e : exps) w += one(e);
+    for (size_t i = 0; i < n_exps; ++i) w += one(*exps[i]);
   }
   alg_macs_ += w;
 }
@@ -260,26 +278,54 @@ static void pack_into(const std::vector<Nat>& v, uint32_t w, uint32_t* out) {
   });
 }
 
+static void pack_ptrs(const Nat* const* v, size_t n, uint32_t w, uint32_t* out) {
+  par_chunks(n, [&](size_t lo, size_t hi) {
+    for (size_t i = lo; i < hi; ++i) v[i]->to_words(out + i * w, w);
+  });
+}
+
 static std::vector<uint32_t> pack(const std::vector<Nat>& v, uint32_t w) {
   std::vector<uint32_t> out((size_t)v.size() * w);
   pack_into(v, w, out.data());
   return out;
 }
 
-static std::vector<Nat> unpack(const uint32_t* buf, size_t count, uint32_t w) {
+static void unpack_into(const uint32_t* buf, size_t count, uint32_t w, Nat* const* outs) {
   MPCX_PROF("engine.unpack");
-  std::vector<Nat> out(count);
   par_chunks(count, [&](size_t lo, size_t hi) {
-    for (size_t i = lo; i < hi; ++i) out[i] = Nat::from_words(buf + i * w, w);
+    for (size_t i = lo; i < hi; ++i) outs[i]->set_words(buf + i * w, w);
   });
-  return out;
+}
+
+template <class T>
+static std::vector<const T*> ptrs(const std::vector<T>& v) {
+  std::vector<const T*> p(v.size());
+  for (size_t i = 0; i < v.size(); ++i) p[i] = &v[i];
+  return p;
+}
+
+static std::vector<Nat*> out_ptrs(std::vector<Nat>& v) {
+  std::vector<Nat*> p(v.size());
+  for (size_t i = 0; i < v.size(); ++i) p[i] = &v[i];
+  return p;
 }
 
 std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const std::vector<Nat>& exps,
                              const std::vector<Nat>* muls) {
   if (exps.size() != 1 && exps.size() != bases.size()) throw std::invalid_argument("exps: 1 or one per base");
   if (muls && muls->size() != bases.size()) throw std::invalid_argument("muls: one per base");
-  if (bases.empty()) return {};
+  std::vector<Nat> out(bases.size());
+  const auto bp = ptrs(bases), ep = ptrs(exps);
+  std::vector<const Nat*> mp;
+  if (muls) mp = ptrs(*muls);
+  exp_into(m, bases.size(), bp.data(), ep.data(), ep.size(), muls ? mp.data() : nullptr, out_ptrs(out).data());
+  return out;
+}
+
+void Engine::exp_into(const Nat& m, size_t n, const Nat* const* bases, const Nat* const* exps, size_t n_exps,
+                      const Nat* const* muls, Nat* const* outs) {
+  if (n_exps != 1 && n_exps != n) throw std::invalid_argument("exps: 1 or one per base");
+  if (!n) return;
   Mod md;
   {
     std::lock_guard<std::mutex> lk(mu_);
@@ -288,30 +334,33 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
   // Host-side packing runs outside the lock, so another thread's batch can
   // use the GPU meanwhile. math/big reduces x mod m first when
   // len(x) > len(m) (nat.expNNMontgomery); here: only when x does not fit
-  // the kernel class width.
-  auto packed = [&](const std::vector<Nat>& v, uint32_t* out) {
-    par_chunks(v.size(), [&](size_t lo, size_t hi) {
+  // the kernel class width. A null multiplier is 1.
+  auto packed = [&](const Nat* const* v, uint32_t* out) {
+    par_chunks(n, [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
-        if (v[i].words() > md.class_words) {
-          (v[i] % m).to_words(out + i * md.class_words, md.class_words);
+        uint32_t* o = out + i * md.class_words;
+        if (!v[i]) {
+          std::fill(o, o + md.class_words, 0u);
+          o[0] = 1;
+        } else if (v[i]->words() > md.class_words) {
+          (*v[i] % m).to_words(o, md.class_words);
         } else {
-          v[i].to_words(out + i * md.class_words, md.class_words);
+          v[i]->to_words(o, md.class_words);
         }
       }
     });
   };
-  const bool shared = exps.size() == 1;
+  const bool shared = n_exps == 1;
   uint32_t ew = 1;
-  for (const auto& e : exps) ew = std::max<uint32_t>(ew, (uint32_t)e.words());
-  const size_t n = bases.size();
-  HostBuf B(n * md.class_words), E(exps.size() * ew), M(muls ? n * md.class_words : 1), out(n * md.words);
+  for (size_t i = 0; i < n_exps; ++i) ew = std::max<uint32_t>(ew, (uint32_t)exps[i]->words());
+  HostBuf B(n * md.class_words), E(n_exps * ew), M(muls ? n * md.class_words : 1), out(n * md.words);
   {
     MPCX_PROF("engine.exp.pack");
     packed(bases, B.p);
-    pack_into(exps, ew, E.p);
-    if (muls) packed(*muls, M.p);
+    pack_ptrs(exps, n_exps, ew, E.p);
+    if (muls) packed(muls, M.p);
   }
-  count_work(m, exps, n);
+  count_work(m, exps, n_exps, n);
   int rc;
   {
     MPCX_PROF("engine.exp.gpu");
@@ -347,7 +396,7 @@ std::vector<Nat> Engine::exp(const Nat& m, const std::vector<Nat>& bases, const 
     leave_call();
   }
   if (rc) throw_last(rc, "mpcx_modexp_batch");
-  return unpack(out.p, n, md.words);
+  unpack_into(out.p, n, md.words, outs);
 }
 
 bool Engine::fixed_base_ok(const Nat& m) const {
@@ -377,26 +426,41 @@ Engine::Fixed Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
 std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vector<Nat>& exps,
                                    const std::vector<Nat>* muls) {
   if (muls && muls->size() != exps.size()) throw std::invalid_argument("muls: one per exponent");
-  if (exps.empty()) return {};
+  std::vector<Nat> out(exps.size());
+  const auto ep = ptrs(exps);
+  std::vector<const Nat*> mp;
+  if (muls) mp = ptrs(*muls);
+  fixed_exp_into(m, base, exps.size(), ep.data(), muls ? mp.data() : nullptr, out_ptrs(out).data());
+  return out;
+}
+
+void Engine::fixed_exp_into(const Nat& m, const Nat& base, size_t n, const Nat* const* exps, const Nat* const* muls,
+                            Nat* const* outs) {
+  if (!n) return;
   Mod md;
   {
     std::lock_guard<std::mutex> lk(mu_);
     md = modulus(m);
   }
   uint32_t ew = 1, need = 1;
-  for (const auto& e : exps) {
-    ew = std::max<uint32_t>(ew, (uint32_t)e.words());
-    need = std::max<uint32_t>(need, e.bit_len());
+  for (size_t i = 0; i < n; ++i) {
+    ew = std::max<uint32_t>(ew, (uint32_t)exps[i]->words());
+    need = std::max<uint32_t>(need, exps[i]->bit_len());
   }
   const Nat b = base.words() > md.class_words || base >= m ? base % m : base;
-  const size_t n = exps.size();
   HostBuf E(n * ew), Mw(muls ? n * md.class_words : 1), out(n * md.words);
-  pack_into(exps, ew, E.p);
+  pack_ptrs(exps, n, ew, E.p);
   if (muls) {
     par_chunks(n, [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
-        const Nat& x = (*muls)[i];
-        (x.words() > md.class_words ? x % m : x).to_words(Mw.p + i * md.class_words, md.class_words);
+        uint32_t* o = Mw.p + i * md.class_words;
+        const Nat* x = muls[i];
+        if (!x) {
+          std::fill(o, o + md.class_words, 0u);
+          o[0] = 1;
+        } else {
+          (x->words() > md.class_words ? *x % m : *x).to_words(o, md.class_words);
+        }
       }
     });
   }
@@ -408,7 +472,7 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
     f = fixed(m, b, need);
   }
   const uint32_t* ep = E.p;
-  count_work(m, exps, n);
+  count_work(m, exps, n, n);
   int rc;
   {
     MPCX_PROF("engine.fixed.gpu");
@@ -418,7 +482,7 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
     leave_call();
   }
   if (rc) throw_last(rc, "mpcx_fixedbase_exp_batch");
-  return unpack(out.p, n, md.words);
+  unpack_into(out.p, n, md.words, outs);
 }
 
 int Engine::set_lanes(int n) {

@@ -55,12 +55,19 @@ class Engine {
   // (reduced mod m on the host first when wider than the kernel class).
   std::vector<Nat> exp(const Nat& m, const std::vector<Nat>& bases, const std::vector<Nat>& exps,
                        const std::vector<Nat>* muls = nullptr);
+  // The same over pointer arrays, results written through outs (no copies of
+  // the operands): n bases, n_exps == 1 (shared) or n exponents, muls null or
+  // n entries (a null entry: 1), n outputs.
+  void exp_into(const Nat& m, size_t n, const Nat* const* bases, const Nat* const* exps, size_t n_exps,
+                const Nat* const* muls, Nat* const* outs);
   std::vector<Nat> mulmod(const Nat& m, const std::vector<Nat>& a, const std::vector<Nat>& b);
   // out[i] = (muls ? muls[i] : 1) * base^exps[i] mod m through a comb table of
   // `base` (mpcx_fixedbase_*), built on first use and cached: the bases that
   // recur across every session (h1, h2 of a node's N~) pay for it once.
   std::vector<Nat> fixed_exp(const Nat& m, const Nat& base, const std::vector<Nat>& exps,
                              const std::vector<Nat>* muls = nullptr);
+  void fixed_exp_into(const Nat& m, const Nat& base, size_t n, const Nat* const* exps, const Nat* const* muls,
+                      Nat* const* outs);
   // fixed-base path usable for m (odd, <= 2080 bits) and enabled
   // (environment MPCX_FIXED_BASE=0 turns it off, for A/B runs)
   bool fixed_base_ok(const Nat& m) const;
@@ -131,7 +138,7 @@ class Engine {
   std::atomic<uint64_t> busy_ns_{0};
   std::atomic<uint64_t> alg_macs_{0};
   std::atomic<int> lanes_{0};  // 0: libmpcx's default (MPCX_LANES or 6)
-  void count_work(const Nat& m, const std::vector<Nat>& exps, size_t count);
+  void count_work(const Nat& m, const Nat* const* exps, size_t n_exps, size_t count);
   std::map<std::vector<uint32_t>, Mod> mods_;
   std::map<std::pair<std::vector<uint32_t>, std::vector<uint32_t>>, Fixed> fixed_;
 };

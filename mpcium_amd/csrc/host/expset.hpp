@@ -131,33 +131,40 @@ class ExpSet {
     Nat* out;
   };
   static constexpr size_t kFixedMin = 64;  // requests on one base before a comb table pays
+  // the requests' own operands and outputs, through pointers: no copies
   void launch_fixed(const std::vector<size_t>& idx) {
     MPCX_PROF("expset.launch_fixed");
-    std::vector<Nat> exps, muls;
-    exps.reserve(idx.size());
+    std::vector<const Nat*> exps(idx.size()), muls;
+    std::vector<Nat*> outs(idx.size());
     bool any_mul = false;
     for (size_t i : idx) any_mul |= reqs_[i].mul != nullptr;
-    for (size_t i : idx) {
-      exps.push_back(*reqs_[i].e);
-      if (any_mul) muls.push_back(reqs_[i].mul ? *reqs_[i].mul : Nat(1));
+    if (any_mul) muls.resize(idx.size());
+    for (size_t j = 0; j < idx.size(); ++j) {
+      const Req& r = reqs_[idx[j]];
+      exps[j] = r.e;
+      outs[j] = r.out;
+      if (any_mul) muls[j] = r.mul;
     }
-    std::vector<Nat> r = Engine::get().fixed_exp(m_, *reqs_[idx[0]].b, exps, any_mul ? &muls : nullptr);
-    for (size_t j = 0; j < idx.size(); ++j) *reqs_[idx[j]].out = std::move(r[j]);
+    Engine::get().fixed_exp_into(m_, *reqs_[idx[0]].b, idx.size(), exps.data(), any_mul ? muls.data() : nullptr,
+                                 outs.data());
   }
   void launch(const std::vector<size_t>& idx, bool shared) {
     MPCX_PROF("expset.launch");
-    std::vector<Nat> bases, exps, muls;
-    bases.reserve(idx.size());
+    std::vector<const Nat*> bases(idx.size()), exps(shared ? 1 : idx.size()), muls;
+    std::vector<Nat*> outs(idx.size());
     bool any_mul = false;
     for (size_t i : idx) any_mul |= reqs_[i].mul != nullptr;
-    for (size_t i : idx) {
-      bases.push_back(*reqs_[i].b);
-      if (!shared) exps.push_back(*reqs_[i].e);
-      if (any_mul) muls.push_back(reqs_[i].mul ? *reqs_[i].mul : Nat(1));
+    if (any_mul) muls.resize(idx.size());
+    for (size_t j = 0; j < idx.size(); ++j) {
+      const Req& r = reqs_[idx[j]];
+      bases[j] = r.b;
+      if (!shared) exps[j] = r.e;
+      outs[j] = r.out;
+      if (any_mul) muls[j] = r.mul;
     }
-    if (shared) exps.push_back(*reqs_[idx[0]].e);
-    std::vector<Nat> r = Engine::get().exp(m_, bases, exps, any_mul ? &muls : nullptr);
-    for (size_t j = 0; j < idx.size(); ++j) *reqs_[idx[j]].out = std::move(r[j]);
+    if (shared) exps[0] = reqs_[idx[0]].e;
+    Engine::get().exp_into(m_, idx.size(), bases.data(), exps.data(), exps.size(), any_mul ? muls.data() : nullptr,
+                           outs.data());
   }
   const Nat m_;  // by value: callers pass temporaries (pk.NSquare())
   std::vector<Req> reqs_;

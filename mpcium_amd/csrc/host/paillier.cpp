@@ -86,13 +86,15 @@ void PrivateKey::DecryptBatch(const std::vector<Int>& c, std::vector<Nat>* m, st
   err->assign(c.size(), OK);
   std::vector<Nat> cs;
   std::vector<size_t> idx;
+  const bool crt = !P.is_zero() && !Q.is_zero() && P * Q == N;
   for (size_t i = 0; i < c.size(); ++i) {
     if (!in_range(c[i], N2)) {
       (*err)[i] = ErrMessageTooLong;
       continue;
     }
-    // gcd(c, N^2) > 1  <=>  P | c or Q | c
-    if ((c[i].mag % P).is_zero() || (c[i].mag % Q).is_zero()) {
+    // gcd(c, N^2) > 1  <=>  P | c or Q | c: checked here on a key without
+    // factors, from the CRT exponentiations below otherwise
+    if (!crt && !coprime_odd(c[i].mag, N)) {
       (*err)[i] = ErrMessageMalFormed;
       continue;
     }
@@ -100,7 +102,7 @@ void PrivateKey::DecryptBatch(const std::vector<Int>& c, std::vector<Nat>* m, st
     cs.push_back(c[i].mag);
   }
   if (idx.empty()) return;
-  if (P.is_zero() || Q.is_zero() || !(P * Q == N)) {
+  if (!crt) {
     // no factors on this key: tss-lib's formula as written
     // 1. L(c^lambda mod N^2) -- GPU, shared exponent lambda
     std::vector<Nat> u = Engine::get().exp(N2, cs, {LambdaN});
@@ -134,7 +136,13 @@ void PrivateKey::DecryptBatch(const std::vector<Int>& c, std::vector<Nat>* m, st
   if (!mod_inverse(Int(Q % P), P, &qinv)) throw EngineError(MPCX_EINVAL, "Paillier key: P, Q not coprime");
   std::vector<Nat> up = Engine::get().exp(P * P, cs, {Pm1});
   std::vector<Nat> uq = Engine::get().exp(Q * Q, cs, {Qm1});
+  // p | c  <=>  c^(p-1) mod p^2 == 0 (p^2 | c^(p-1), p - 1 >= 2); otherwise it
+  // is 1 mod p. tss-lib rejects such c (gcd(c, N^2) != 1) with ErrMessageMalFormed.
   parallel_for(idx.size(), [&](size_t j) {
+    if (up[j].is_zero() || uq[j].is_zero()) {
+      (*err)[idx[j]] = ErrMessageMalFormed;
+      return;
+    }
     const Nat mp = mulmod(L(up[j], P), hP, P), mq = mulmod(L(uq[j], Q), hQ, Q);
     const Nat mqp = mq % P;
     const Nat d = mp < mqp ? mp + P - mqp : mp - mqp;

@@ -18,6 +18,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <cstdarg>
@@ -131,6 +132,22 @@ struct Lane {
   // tables + counters, Fermat passes' p words, their indices, ride-along q +
   // verdicts, per-item constants of the cooperative kernels (R mod n, meta)
   Staging sieve[8];
+  // kernel timing (mpcx_kernel_stats): event pairs around this lane's
+  // launches, resolved at the lane's next host wait; guarded by mu like the rest
+  struct KEv {
+    hipEvent_t a = nullptr, b = nullptr;
+  };
+  struct KPend {
+    KEv ev;
+    hipEvent_t ref;
+    int dev;
+    const char* kind;
+    int geom;
+    uint32_t ops;
+    double alg;
+  };
+  std::vector<KEv> kev_free;
+  std::vector<KPend> kpend;
 };
 constexpr int kMaxLanes = 8;
 // lanes in use per device: MPCX_LANES (1..8, read at init) or the "lanes" option;
@@ -141,6 +158,7 @@ std::atomic<int> g_lanes{6};
 // One bound GPU.
 struct Device {
   int ordinal = -1;
+  hipEvent_t kref = nullptr;  // kernel-stats time origin (recorded at each stats reset)
   int num_cus = 0;
   int geom_slots[MPCX_NUM_GEOMS] = {0};  // resident wavefronts per geometry
   Lane lanes[kMaxLanes];
@@ -197,6 +215,73 @@ void launch_log(const char* kind, int geom, uint32_t count, uint32_t mod_bits, u
   std::lock_guard<std::mutex> lk(mu);
   std::fprintf(f, "%s,%d,%u,%u,%u,%.0f\n", kind, geom, count, mod_bits, exp_bits, alg);
   std::fflush(f);
+}
+
+// Kernel statistics (mpcx_kernel_stats; off until the "kernel_stats" option
+// is set): per kernel kind and geometry, launches, operands, Go-equivalent
+// algorithmic MACs and GPU time from an event pair around each launch, plus
+// the union of all kernels' intervals per device (lanes overlap on the GPU,
+// so per-kernel times add up to more than the busy time). A protocol line's
+// kernel roofline is alg_macs over that busy time.
+std::atomic<bool> g_kstats{false};
+struct KAgg {
+  uint64_t launches = 0, ops = 0;
+  double alg = 0.0, ms = 0.0;
+};
+std::mutex g_kmu;
+std::map<std::pair<std::string, int>, KAgg> g_kagg;
+std::vector<std::pair<double, double>> g_kiv[8];  // per device: [start, end) ms from its kref
+
+int kstat_begin(Lane& l) {
+  if (!g_kstats.load(std::memory_order_relaxed) || l.kpend.size() >= 512) return -1;
+  Lane::KEv ev;
+  if (!l.kev_free.empty()) {
+    ev = l.kev_free.back();
+    l.kev_free.pop_back();
+  } else if (hipEventCreate(&ev.a) != hipSuccess || hipEventCreate(&ev.b) != hipSuccess) {
+    return -1;
+  }
+  if (hipEventRecord(ev.a, l.st) != hipSuccess) {
+    l.kev_free.push_back(ev);
+    return -1;
+  }
+  l.kpend.push_back({ev, nullptr, -1, nullptr, 0, 0, 0.0});
+  return (int)l.kpend.size() - 1;
+}
+
+void kstat_end(Lane& l, int slot, const Device& d, int dev, const char* kind, int geom, uint32_t ops, double alg) {
+  if (slot < 0) return;
+  Lane::KPend& p = l.kpend[(size_t)slot];
+  if (!d.kref || hipEventRecord(p.ev.b, l.st) != hipSuccess) {
+    l.kev_free.push_back(p.ev);
+    l.kpend.erase(l.kpend.begin() + slot);
+    return;
+  }
+  p.ref = d.kref;
+  p.dev = dev;
+  p.kind = kind;
+  p.geom = geom;
+  p.ops = ops;
+  p.alg = alg;
+}
+
+// after the lane's stream drained: every pending pair has completed
+void kstat_resolve(Lane& l) {
+  std::lock_guard<std::mutex> lk(g_kmu);
+  for (auto& p : l.kpend) {
+    float ms = 0.f, t0 = 0.f;
+    if (p.kind && hipEventElapsedTime(&ms, p.ev.a, p.ev.b) == hipSuccess &&
+        hipEventElapsedTime(&t0, p.ref, p.ev.a) == hipSuccess) {
+      KAgg& a = g_kagg[{p.kind, p.geom}];
+      a.launches += 1;
+      a.ops += p.ops;
+      a.alg += p.alg;
+      a.ms += ms;
+      if (p.dev >= 0 && p.dev < 8) g_kiv[p.dev].push_back({(double)t0, (double)t0 + ms});
+    }
+    l.kev_free.push_back(p.ev);
+  }
+  l.kpend.clear();
 }
 
 int class_for_bits(uint32_t bits) {
@@ -361,21 +446,36 @@ int lane_stream(Lane& l) {
   return MPCX_OK;
 }
 
-// wait (sleeping) until the lane's stream has drained; MPCX_SPIN_WAIT=1:
-// hipStreamSynchronize (the runtime's default spin) for A/B runs
+// Wait until the lane's stream has drained. Default: poll the lane's event
+// with a sleep that backs off from 20 to 100 us -- hipEventSynchronize, even
+// on a hipEventBlockingSync event, spins inside the HSA runtime before it
+// sleeps, and a signing run keeps 4-12 host threads waiting on launches of a
+// few ms each: those spins were a third of the process's CPU time
+// (profiles/r03/sample1). The added latency is <= 100 us per launch.
+// MPCX_LANE_WAIT=event: hipEventSynchronize; =stream: hipStreamSynchronize.
 int lane_wait(Lane& l) {
-  static const bool spin = [] {
-    const char* e = std::getenv("MPCX_SPIN_WAIT");
-    return e && e[0] == '1';
+  static const int mode = [] {
+    const char* e = std::getenv("MPCX_LANE_WAIT");
+    return !e ? 0 : std::strcmp(e, "event") == 0 ? 1 : std::strcmp(e, "stream") == 0 ? 2 : 0;
   }();
   hipError_t e;
-  if (spin) {
+  if (mode == 2) {
     e = hipStreamSynchronize(l.st);
   } else {
     e = hipEventRecord(l.ev, l.st);
-    if (e == hipSuccess) e = hipEventSynchronize(l.ev);
+    if (e == hipSuccess && mode == 1) {
+      e = hipEventSynchronize(l.ev);
+    } else if (e == hipSuccess) {
+      for (int us = 20;; us = std::min(100, us + us / 2)) {
+        e = hipEventQuery(l.ev);
+        if (e != hipErrorNotReady) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(us));
+      }
+    }
   }
-  return e == hipSuccess ? MPCX_OK : hip_fail(e, "lane wait");
+  if (e != hipSuccess) return hip_fail(e, "lane wait");
+  if (!l.kpend.empty()) kstat_resolve(l);
+  return MPCX_OK;
 }
 
 int h2d(void* d, const void* h, size_t bytes, hipStream_t st) {
@@ -435,6 +535,13 @@ void drop_lane(Lane& l) {
   l.st = nullptr;
   if (l.ev) (void)hipEventDestroy(l.ev);
   l.ev = nullptr;
+  for (auto& p : l.kpend) l.kev_free.push_back(p.ev);
+  l.kpend.clear();
+  for (auto& ev : l.kev_free) {
+    (void)hipEventDestroy(ev.a);
+    (void)hipEventDestroy(ev.b);
+  }
+  l.kev_free.clear();
   if (l.ws) (void)hipFree(l.ws);
   l.ws = nullptr;
   l.ws_bytes = 0;
@@ -659,6 +766,9 @@ int mpcx_set_option(const char* key, int value) {
   } else if (std::strcmp(key, "duplicate_device") == 0) {
     // test hook: mpcx_init(ordinal) binds an already bound ordinal again as another logical device
     g_dup_device = value != 0;
+  } else if (std::strcmp(key, "kernel_stats") == 0) {
+    // time every batch-entry-point kernel with an event pair (mpcx_kernel_stats)
+    g_kstats = value != 0;
   } else if (std::strcmp(key, "device_split_min") == 0) {
     // smallest per-device slice of a host-buffer batch split across the bound GPUs (0: never split)
     if (value < 0) return fail(MPCX_EINVAL, "device_split_min %d < 0", value);
@@ -734,6 +844,64 @@ int mpcx_device_launches(int index, uint64_t* out) {
   if (!out) return fail(MPCX_EINVAL, "null out");
   if (index < 0 || index >= n) return fail(MPCX_EINVAL, "device index %d not bound (%d bound)", index, n);
   *out = g_devs[index].launches.load();
+  return MPCX_OK;
+}
+
+int mpcx_kernel_stats(char* buf, size_t cap, int reset) {
+  const int n = g_ndev.load(std::memory_order_acquire);
+  std::string out;
+  {
+    std::lock_guard<std::mutex> lk(g_kmu);
+    double busy = 0.0, alg = 0.0;
+    for (int i = 0; i < n && i < 8; ++i) {  // union of the device's kernel intervals
+      auto iv = g_kiv[i];
+      std::sort(iv.begin(), iv.end());
+      double s0 = 0.0, e0 = -1.0;
+      for (const auto& x : iv) {
+        if (x.first > e0) {
+          if (e0 > s0) busy += e0 - s0;
+          s0 = x.first;
+          e0 = x.second;
+        } else {
+          e0 = std::max(e0, x.second);
+        }
+      }
+      if (e0 > s0) busy += e0 - s0;
+    }
+    char line[320];
+    std::string ks;
+    for (const auto& kv : g_kagg) {
+      alg += kv.second.alg;
+      std::snprintf(line, sizeof line,
+                    "%s{\"kind\":\"%s\",\"geom\":%d,\"launches\":%llu,\"operands\":%llu,\"alg_macs\":%.6e,"
+                    "\"kernel_ms\":%.4f}",
+                    ks.empty() ? "" : ",", kv.first.first.c_str(), kv.first.second,
+                    (unsigned long long)kv.second.launches, (unsigned long long)kv.second.ops, kv.second.alg,
+                    kv.second.ms);
+      ks += line;
+    }
+    std::snprintf(line, sizeof line, "{\"enabled\":%d,\"busy_ms\":%.4f,\"alg_macs\":%.6e,\"kernels\":[",
+                  g_kstats.load() ? 1 : 0, busy, alg);
+    out = line + ks + "]}";
+    if (reset) {
+      g_kagg.clear();
+      for (auto& v : g_kiv) v.clear();
+    }
+  }
+  if (reset) {  // new time origin on every bound device
+    for (int i = 0; i < n; ++i) {
+      Device& d = g_devs[i];
+      if (int rc = bind(d)) return rc;
+      hipError_t e = d.kref ? hipSuccess : hipEventCreate(&d.kref);
+      if (e == hipSuccess) e = hipEventRecord(d.kref, nullptr);
+      if (e == hipSuccess) e = hipEventSynchronize(d.kref);
+      if (e != hipSuccess) return hip_fail(e, "kernel stats time origin");
+    }
+  }
+  if (buf && cap) {
+    if (out.size() + 1 > cap) return fail(MPCX_EINVAL, "kernel stats need %zu bytes", out.size() + 1);
+    std::memcpy(buf, out.c_str(), out.size() + 1);
+  }
   return MPCX_OK;
 }
 
@@ -990,11 +1158,13 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     a.n0inv = mod->n0inv;
     a.exp_shared = exp_shared ? 1 : 0;
     a.sched = use_sched ? lane.ws + sched_off : nullptr;
+    const int ks = kstat_begin(lane);
     hipError_t e = mpcx_launch_modexp(pt.geom, &a, waves, st);
     if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
-    launch_log("modexp", pt.geom, pt.count, mod->bits, a.exp_bits,
-               alg_macs >= 0 ? alg_macs * pt.count / count : go_macs(mod->bits, a.exp_bits) * pt.count);
+    const double alg = alg_macs >= 0 ? alg_macs * pt.count / count : go_macs(mod->bits, a.exp_bits) * pt.count;
+    kstat_end(lane, ks, g_devs[di], di, "modexp", pt.geom, pt.count, alg);
+    launch_log("modexp", pt.geom, pt.count, mod->bits, a.exp_bits, alg);
     ws_off += (size_t)waves * MPCX_TABLE_ENTRIES * K * 64u;
   }
   return MPCX_OK;
@@ -1326,11 +1496,21 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
   if ((rc = h2d(l.stage[3].ptr, args.data(), seg_bytes, l.st)) ||
       (rc = h2d((char*)l.stage[3].ptr + seg_bytes, first.data(), first_bytes, l.st)))
     return rc;
+  const int ks = kstat_begin(l);
   hipError_t e = mpcx_launch_modexp_multi(geom, (const mpcx::ModexpArgs*)l.stage[3].ptr,
                                           (const uint32_t*)((const char*)l.stage[3].ptr + seg_bytes),
                                           (uint32_t)nseg, first[nseg], l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_modexp_multi");
   dev.launches.fetch_add(1, std::memory_order_relaxed);
+  {
+    double alg = 0.0;
+    uint32_t ops = 0;
+    for (const auto& sg : segs) {
+      alg += sg.alg;
+      ops += gs[sg.gi].count;
+    }
+    kstat_end(l, ks, dev, di, "modexp_multi", geom, ops, alg);
+  }
   for (const auto& sg : segs) launch_log("modexp_multi", geom, gs[sg.gi].count, gs[sg.gi].mod->bits, sg.exp_bits, sg.alg);
   for (const auto& sg : segs) {  // results straight into each group's buffer
     const mpcx_modexp_group_t& g = gs[sg.gi];
@@ -1404,9 +1584,11 @@ int ec_range(int di, uint32_t count, const uint32_t* scalars, const uint32_t* po
       (rc = ensure_buffer(l.stage[2], ob)) || (rc = ensure_workspace(l, ec_ws_words(count) * 4)))
     return rc;
   if ((rc = h2d(l.stage[0].ptr, scalars, sb, l.st)) || (rc = h2d(l.stage[1].ptr, points, pb, l.st))) return rc;
+  const int ks = kstat_begin(l);
   hipError_t e = mpcx_launch_ec_combine((const uint32_t*)l.stage[0].ptr, (const uint32_t*)l.stage[1].ptr,
                                         (uint32_t*)l.stage[2].ptr, gtab, l.ws, count, l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_ec_combine");
+  kstat_end(l, ks, d, di, "ec_combine", -1, count, 0.0);
   d.launches.fetch_add(1, std::memory_order_relaxed);
   launch_log("ec_combine", -1, count, 256, 256, 0.0);
   return d2h_sync(out, l.stage[2].ptr, ob, l);
@@ -1827,19 +2009,27 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     a.count = n;
     a.n0inv = mod->n0inv;
     const uint32_t waves = (n + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
+    const int ks = kstat_begin(l);
     hipError_t e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
                                              : mpcx_launch_fixedbase_g1(&a, waves, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
     {
-      double alg = 0.0;  // Go-equivalent: one Exp per base per operand
+      // Go-equivalent (launch log): one Exp per base per operand; executed
+      // (kernel stats): one product per 8-bit window of each exponent, plus
+      // the multiplier's, 2 L^2 MACs each
+      double alg = 0.0, exec = 0.0;
+      const double l2 = 2.0 * (double)((mod->bits + 31) / 32) * (double)((mod->bits + 31) / 32);
       uint32_t eb_max = 0;
       for (uint32_t t = 0; t < nbases; ++t)
         for (uint32_t i = 0; i < n && exp_words[t]; ++i) {
           const uint32_t b = bit_length_words(exps[t] + (size_t)(first + i) * exp_words[t], exp_words[t]);
           alg += go_macs(mod->bits, b);
+          exec += (double)((b + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS) * l2;
           eb_max = std::max(eb_max, b);
         }
+      if (muls) exec += (double)n * l2;
+      kstat_end(l, ks, g_devs[di], di, "fixedbase", geom, n, exec);
       launch_log("fixedbase", geom, n, mod->bits, eb_max, alg);
     }
     return d2h_sync(out + (size_t)first * out_words, sg[2].ptr, ob, l);

@@ -31,6 +31,7 @@ SIGNATURES = [
     ("mpcx_bound_devices", ctypes.c_int, [ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_int), ctypes.c_int]),
     ("mpcx_select_device", ctypes.c_int, [ctypes.c_int]),
     ("mpcx_device_launches", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_uint64)]),
+    ("mpcx_kernel_stats", ctypes.c_int, [ctypes.c_char_p, ctypes.c_size_t, ctypes.c_int]),
     ("mpcx_partition", ctypes.c_int, [ctypes.c_uint32, ctypes.c_int, ctypes.c_uint32, _u32p, _u32p, _u32p]),
     ("mpcx_shutdown", ctypes.c_int, []),
     ("mpcx_modulus_register", ctypes.c_int, [_vp, ctypes.c_uint32, ctypes.POINTER(_vp)]),
@@ -151,6 +152,15 @@ def device_launches(index: int) -> int:
     v = ctypes.c_uint64(0)
     _check(lib().mpcx_device_launches(index, ctypes.byref(v)))
     return v.value
+
+
+def kernel_stats(reset: bool = False) -> dict:
+    """mpcx_kernel_stats: per-kernel launches, operands, Go-equivalent MACs and
+    GPU ms since the last reset (collected while set_option("kernel_stats", 1))."""
+    import json
+    buf = ctypes.create_string_buffer(1 << 16)
+    _check(lib().mpcx_kernel_stats(buf, len(buf), 1 if reset else 0))
+    return json.loads(buf.value.decode())
 
 
 def select_device(index: int):

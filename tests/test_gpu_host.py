@@ -74,6 +74,10 @@ def test_paillier_errors(host, paillier_key):
     assert err == [1, 1]
     _, err = sk.decrypt([N2, -3, P * 5, Q, 0, 12345])
     assert err == [1, 1, 2, 2, 2, 0]
+    # a key without its factors: tss-lib's lambda formula, gcd checked up front
+    m, err = host.PrivateKey(N, lam, 0, 0).decrypt([N2, P * 5, Q * 7, 0, 12345])
+    assert err == [1, 2, 2, 2, 0]
+    assert m[4] == gm.paillier_decrypt(N, lam, 12345)
 
 
 def test_paillier_random_roundtrip(host, paillier_key):

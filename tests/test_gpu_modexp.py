@@ -306,3 +306,32 @@ def test_multi_batch_groups_of_different_moduli(gpu):
     finally:
         for m in mods:
             m.release()
+
+
+def test_kernel_stats_count_launches_and_work(gpu, paillier_key):
+    """mpcx_kernel_stats: the launches of a shared-exponent batch are timed and
+    carry the Go-equivalent work (E + ceil(E/4)) 2 L^2 per operand."""
+    from mpcium_amd import mpcx
+    N = paillier_key["N"]
+    N2 = N * N
+    mod = gpu.Modulus(N2)
+    rng = random.Random(11)
+    xs = [rng.randrange(N2) for _ in range(3000)]
+    mpcx.set_option("kernel_stats", 1)
+    try:
+        mpcx.kernel_stats(reset=True)
+        got = mod.exp(xs, N)
+        ks = mpcx.kernel_stats(reset=True)
+    finally:
+        mpcx.set_option("kernel_stats", 0)
+    assert got[:4] == [pow(x, N, N2) for x in xs[:4]]
+    assert ks["enabled"] == 1
+    mods = [k for k in ks["kernels"] if k["kind"].startswith("modexp")]
+    assert sum(k["operands"] for k in mods) == len(xs)
+    E, L = N.bit_length(), 128
+    assert sum(k["alg_macs"] for k in mods) == pytest.approx(len(xs) * (E + (E + 3) // 4) * 2 * L * L, rel=1e-6)
+    assert all(k["kernel_ms"] > 0 for k in mods)
+    assert 0 < ks["busy_ms"] <= sum(k["kernel_ms"] for k in ks["kernels"]) + 1e-3
+    # disabled: nothing is collected
+    mod.exp(xs[:64], N)
+    assert mpcx.kernel_stats()["kernels"] == []

@@ -53,7 +53,9 @@ def symbolize(frames):
 
 def main():
     path = sys.argv[1]
-    top = int(sys.argv[2]) if len(sys.argv) > 2 else 40
+    top = int(sys.argv[2]) if len(sys.argv) > 2 and sys.argv[2].isdigit() else 40
+    # --callers SUBSTR: the own-code frames above every sample whose stack holds SUBSTR
+    callers = sys.argv[sys.argv.index("--callers") + 1] if "--callers" in sys.argv else None
     stacks = []
     for ln in open(path):
         c, _, st = ln.strip().partition(" ")
@@ -63,6 +65,19 @@ def main():
     names = {f: names[f.partition("@")[0]] for _, fr in stacks for f in fr}
     total = sum(c for c, _ in stacks)
     self_c, own, incl = collections.Counter(), collections.Counter(), collections.Counter()
+    if callers:
+        chains = collections.Counter()
+        for c, fr in stacks:
+            syms = [names[f] for f in fr]
+            hit = [i for i, s in enumerate(syms) if callers in s]
+            if hit:
+                up = [s.split("(")[0][-60:] for s in syms[hit[0]:] if not s.startswith("[")][:5]
+                chains[" <- ".join(up)] += c
+        n = sum(chains.values())
+        print(f"{n} of {total} samples hold {callers!r}")
+        for s, c in chains.most_common(top):
+            print(f"{100.0 * c / total:6.2f}%  {s}")
+        return
     for c, fr in stacks:
         syms = [names[f] for f in fr]
         self_c[syms[0]] += c
