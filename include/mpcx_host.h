@@ -326,6 +326,12 @@ int mpcxh_host_threads(int* threads, int* usable);
  * (task+1)(o+1)(i+1); *sum = the total. */
 int mpcxh_pool_selftest(uint32_t tasks, uint32_t outer, uint32_t inner, uint64_t* sum);
 
+/* Host bignum arithmetic (test hook, no GPU): op 0: a * b, 1: a / b, 2: a mod b,
+ * 3: a^-1 mod b (Go ModInverse; MPCX_EINVAL when none), 4: gcd(a, b). Little-endian
+ * words; *out_words = the result's normalized length (<= nout). */
+int mpcxh_nat_arith(int op, const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* out,
+                    uint32_t nout, uint32_t* out_words);
+
 /* tss-lib candidate q from raw stream bytes (masking + delta walk; test hook). */
 int mpcxh_candidate_from_bytes(const uint8_t* bytes, size_t n, int q_bit_len, uint32_t* q_out, uint32_t words);
 

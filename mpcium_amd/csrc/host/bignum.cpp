@@ -4,6 +4,7 @@
 #include "hostprof.hpp"
 
 #include <algorithm>
+#include <cstring>
 #include <stdexcept>
 
 namespace mpcx::host {
@@ -130,21 +131,62 @@ Nat operator-(const Nat& a, const Nat& b) {
   return r;
 }
 
+namespace {
+using u128 = unsigned __int128;
+
+// 64-bit limb view of a normalized word vector: ceil(n / 2) limbs (x86-64 is
+// little-endian, so word pairs are the limbs; an odd top word is zero-padded)
+inline size_t limbs64(size_t n32) { return (n32 + 1) / 2; }
+inline void load64(const std::vector<uint32_t>& w, uint64_t* out) {
+  const size_t n = w.size();
+  if (!n) return;
+  out[(n - 1) / 2] = 0;
+  std::memcpy(out, w.data(), n * 4);
+}
+// words [0, n32) of a limb array into a normalized word vector
+inline void store64(const uint64_t* l, size_t n32, std::vector<uint32_t>* w) {
+  const uint32_t* p = reinterpret_cast<const uint32_t*>(l);
+  while (n32 && !p[n32 - 1]) --n32;
+  w->assign(p, p + n32);
+}
+
+// Per-thread scratch limbs: the protocol mirrors run millions of products and
+// reductions from the host pool, so no allocation per operation.
+uint64_t* scratch(size_t n) {
+  thread_local std::vector<uint64_t> buf;
+  if (buf.size() < n) buf.resize(std::max<size_t>(n, 2 * buf.size()));
+  return buf.data();
+}
+
+// r[0, na + nb) = a * b (schoolbook on 64-bit limbs, mulx chains)
+void mul_limbs(const uint64_t* a, size_t na, const uint64_t* b, size_t nb, uint64_t* r) {
+  std::fill(r, r + na + nb, 0ull);
+  for (size_t i = 0; i < nb; ++i) {
+    const uint64_t bi = b[i];
+    if (!bi) continue;
+    uint64_t c = 0;
+    uint64_t* ri = r + i;
+    for (size_t j = 0; j < na; ++j) {
+      const u128 t = (u128)a[j] * bi + ri[j] + c;
+      ri[j] = (uint64_t)t;
+      c = (uint64_t)(t >> 64);
+    }
+    ri[na] = c;
+  }
+}
+}  // namespace
+
 Nat operator*(const Nat& a, const Nat& b) {
   Nat r;
   if (a.is_zero() || b.is_zero()) return r;
-  r.w_.assign(a.w_.size() + b.w_.size(), 0);
-  for (size_t i = 0; i < b.w_.size(); ++i) {
-    uint64_t c = 0;
-    const uint64_t bi = b.w_[i];
-    for (size_t j = 0; j < a.w_.size(); ++j) {
-      c += (uint64_t)a.w_[j] * bi + r.w_[i + j];
-      r.w_[i + j] = (uint32_t)c;
-      c >>= 32;
-    }
-    r.w_[i + a.w_.size()] = (uint32_t)c;
-  }
-  r.norm();
+  const size_t na = limbs64(a.w_.size()), nb = limbs64(b.w_.size());
+  uint64_t* s = scratch(2 * (na + nb));
+  uint64_t *x = s, *y = s + na, *z = s + na + nb;
+  load64(a.w_, x);
+  load64(b.w_, y);
+  if (na >= nb) mul_limbs(x, na, y, nb, z);
+  else mul_limbs(y, nb, x, na, z);
+  store64(z, a.w_.size() + b.w_.size(), &r.w_);
   return r;
 }
 
@@ -180,7 +222,8 @@ uint32_t Nat::mod_u32(uint32_t m) const {
   return (uint32_t)r;
 }
 
-// Knuth, TAOCP vol. 2, 4.3.1, Algorithm D.
+// Knuth, TAOCP vol. 2, 4.3.1, Algorithm D, on 64-bit limbs (128-bit trial
+// quotients).
 void Nat::divmod(const Nat& u, const Nat& v, Nat* q, Nat* r) {
   if (v.is_zero()) throw std::domain_error("division by zero");
   if (cmp(u, v) < 0) {
@@ -188,69 +231,77 @@ void Nat::divmod(const Nat& u, const Nat& v, Nat* q, Nat* r) {
     if (r) *r = u;
     return;
   }
-  const size_t n = v.w_.size(), m = u.w_.size() - n;
+  const size_t nu = limbs64(u.w_.size()), n = limbs64(v.w_.size()), m = nu - n;
+  uint64_t* s = scratch(nu + 1 + n + (m + 1) + nu);
+  uint64_t *un = s, *vn = s + nu + 1, *qq = vn + n, *tmp = qq + m + 1;
   if (n == 1) {
-    Nat qq;
-    qq.w_.assign(u.w_.size(), 0);
-    uint64_t rem = 0;
-    for (int i = (int)u.w_.size() - 1; i >= 0; --i) {
-      const uint64_t cur = (rem << 32) | u.w_[i];
-      qq.w_[i] = (uint32_t)(cur / v.w_[0]);
-      rem = cur % v.w_[0];
+    load64(u.w_, tmp);
+    load64(v.w_, vn);
+    const uint64_t d = vn[0];
+    u128 rem = 0;
+    for (size_t i = nu; i-- > 0;) {
+      const u128 cur = (rem << 64) | tmp[i];
+      qq[i] = (uint64_t)(cur / d);
+      rem = cur % d;
     }
-    qq.norm();
-    if (q) *q = qq;
-    if (r) *r = Nat(rem);
+    if (q) store64(qq, 2 * nu, &q->w_);
+    if (r) *r = Nat((uint64_t)rem);
     return;
   }
-  const int s = __builtin_clz(v.w_.back());
-  std::vector<uint32_t> vn(n), un(u.w_.size() + 1);
-  for (size_t i = n - 1; i > 0; --i) vn[i] = s ? (v.w_[i] << s) | (v.w_[i - 1] >> (32 - s)) : v.w_[i];
-  vn[0] = v.w_[0] << s;
-  un[u.w_.size()] = s ? u.w_.back() >> (32 - s) : 0;
-  for (size_t i = u.w_.size() - 1; i > 0; --i) un[i] = s ? (u.w_[i] << s) | (u.w_[i - 1] >> (32 - s)) : u.w_[i];
-  un[0] = u.w_[0] << s;
-  Nat qq;
-  qq.w_.assign(m + 1, 0);
-  for (int j = (int)m; j >= 0; --j) {
-    const uint64_t num = ((uint64_t)un[j + n] << 32) | un[j + n - 1];
-    uint64_t qhat = num / vn[n - 1], rhat = num % vn[n - 1];
-    while (qhat >= (1ull << 32) || qhat * vn[n - 2] > ((rhat << 32) | un[j + n - 2])) {
+  load64(v.w_, vn);
+  load64(u.w_, tmp);
+  const int sh = __builtin_clzll(vn[n - 1]);
+  if (sh) {
+    for (size_t i = n - 1; i > 0; --i) vn[i] = (vn[i] << sh) | (vn[i - 1] >> (64 - sh));
+    vn[0] <<= sh;
+    un[nu] = tmp[nu - 1] >> (64 - sh);
+    for (size_t i = nu - 1; i > 0; --i) un[i] = (tmp[i] << sh) | (tmp[i - 1] >> (64 - sh));
+    un[0] = tmp[0] << sh;
+  } else {
+    std::memcpy(un, tmp, nu * 8);
+    un[nu] = 0;
+  }
+  const uint64_t vt = vn[n - 1], vs = vn[n - 2];
+  for (size_t j = m + 1; j-- > 0;) {
+    // trial quotient from the top two limbs, corrected by the third (at most
+    // two decrements; then at most one add-back below)
+    const u128 num = ((u128)un[j + n] << 64) | un[j + n - 1];
+    u128 qhat = num / vt, rhat = num % vt;
+    while ((qhat >> 64) || (u128)(uint64_t)qhat * vs > ((rhat << 64) | un[j + n - 2])) {
       --qhat;
-      rhat += vn[n - 1];
-      if (rhat >= (1ull << 32)) break;
+      rhat += vt;
+      if (rhat >> 64) break;
     }
-    int64_t borrow = 0;
-    uint64_t carry = 0;
+    const uint64_t qh = (uint64_t)qhat;
+    uint64_t mc = 0, br = 0;
     for (size_t i = 0; i < n; ++i) {
-      const uint64_t p = qhat * vn[i] + carry;
-      carry = p >> 32;
-      const int64_t t = (int64_t)un[i + j] - (int64_t)(uint32_t)p + borrow;
-      un[i + j] = (uint32_t)t;
-      borrow = t >> 32;
+      const u128 p = (u128)qh * vn[i] + mc;
+      mc = (uint64_t)(p >> 64);
+      const uint64_t pl = (uint64_t)p, ui = un[i + j];
+      const uint64_t d = ui - pl - br;
+      br = (ui < pl || (ui - pl) < br) ? 1u : 0u;
+      un[i + j] = d;
     }
-    const int64_t t = (int64_t)un[j + n] - (int64_t)carry + borrow;
-    un[j + n] = (uint32_t)t;
-    if (t < 0) {
-      --qhat;
+    const uint64_t top = un[j + n];
+    const uint64_t d = top - mc - br;
+    const bool neg = top < mc || (top - mc) < br;
+    un[j + n] = d;
+    qq[j] = qh;
+    if (neg) {  // qhat was one too large: add v back
+      --qq[j];
       uint64_t c = 0;
       for (size_t i = 0; i < n; ++i) {
-        const uint64_t sum = (uint64_t)un[i + j] + vn[i] + c;
-        un[i + j] = (uint32_t)sum;
-        c = sum >> 32;
+        const u128 t = (u128)un[i + j] + vn[i] + c;
+        un[i + j] = (uint64_t)t;
+        c = (uint64_t)(t >> 64);
       }
-      un[j + n] += (uint32_t)c;
+      un[j + n] += c;
     }
-    qq.w_[j] = (uint32_t)qhat;
   }
-  qq.norm();
-  if (q) *q = qq;
+  if (q) store64(qq, 2 * (m + 1), &q->w_);
   if (r) {
-    Nat rr;
-    rr.w_.assign(n, 0);
-    for (size_t i = 0; i < n; ++i) rr.w_[i] = s ? (un[i] >> s) | (un[i + 1] << (32 - s)) : un[i];
-    rr.norm();
-    *r = rr;
+    for (size_t i = 0; i < n; ++i) tmp[i] = sh ? (un[i] >> sh) | (un[i + 1] << (64 - sh)) : un[i];
+    store64(tmp, 2 * n, &r->w_);
   }
 }
 

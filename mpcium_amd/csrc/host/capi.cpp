@@ -249,7 +249,8 @@ int mpcxh_paillier_decrypt_batch(const uint32_t* N, uint32_t nw, const uint32_t*
     sk.LambdaN = Nat::from_words(lambda, lw);
     sk.P = Nat::from_words(P, pw);
     sk.Q = Nat::from_words(Q, qw);
-    sk.PhiN = (sk.P - Nat(1)) * (sk.Q - Nat(1));
+    // a key without its factors (P = Q = 0) decrypts by tss-lib's lambda formula
+    if (!sk.P.is_zero() && !sk.Q.is_zero()) sk.PhiN = (sk.P - Nat(1)) * (sk.Q - Nat(1));
     std::vector<Nat> o;
     std::vector<uint8_t> e;
     sk.DecryptBatch(ints(c, cw, c_neg, count), &o, &e);
@@ -342,6 +343,28 @@ int mpcxh_host_threads(int* threads, int* usable) {
   return guard([&] {
     if (threads) *threads = host_threads();
     if (usable) *usable = usable_cpus();
+  });
+}
+
+int mpcxh_nat_arith(int op, const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* out,
+                    uint32_t nout, uint32_t* out_words) {
+  return guard([&] {
+    if (!out || !out_words || (na && !a) || (nb && !b)) throw std::invalid_argument("null buffer");
+    const Nat x = Nat::from_words(a, na), y = Nat::from_words(b, nb);
+    Nat r;
+    switch (op) {
+      case 0: r = x * y; break;
+      case 1: r = x / y; break;
+      case 2: r = x % y; break;
+      case 3:
+        if (!mod_inverse(Int(x), y, &r)) throw EngineError(MPCX_EINVAL, "not invertible");
+        break;
+      case 4: r = gcd(x, y); break;
+      default: throw std::invalid_argument("nat_arith: unknown op");
+    }
+    if (r.words() > nout) throw std::length_error("nat_arith: output buffer too small");
+    r.to_words(out, nout);
+    *out_words = (uint32_t)r.words();
   });
 }
 

@@ -51,6 +51,9 @@
 #ifndef MPCX_PREFETCH_B
 #define MPCX_PREFETCH_B 1
 #endif
+#ifndef MPCX_MID_CARRY
+#define MPCX_MID_CARRY 1  // montmul: a carry pass half-way through the L iterations (A/B: 0 drops it)
+#endif
 #ifndef MPCX_PRIME2C_DBL_FOLD
 #define MPCX_PRIME2C_DBL_FOLD 1  // k_prime2c: the square-and-double step as one product with B = 2^bit x
 #endif
@@ -252,7 +255,7 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
     });
     // Keep every accumulator below 2^64: at most ~P/2*K + K more iterations of
     // two < 2^56.01 products follow this pass (<= 127 for every class).
-    if (o == P / 2 - 1) carry_pass64<P, K>(acc);
+    if (MPCX_MID_CARRY && o == P / 2 - 1) carry_pass64<P, K>(acc);
   }
   carry_pass64<P, K>(acc);
   // digits are now < 2^28 + 2^37: one more pass brings them to <= 2^28 + 2^10

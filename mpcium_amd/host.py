@@ -69,6 +69,7 @@ SIGNATURES = [
     ("mpcxh_profile_report", _i, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("mpcxh_host_threads", _i, [_vp, _vp]),
     ("mpcxh_pool_selftest", _i, [_u32, _u32, _u32, _vp]),
+    ("mpcxh_nat_arith", _i, [_i, _vp, _u32, _vp, _u32, _vp, _u32, _vp]),
     ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
     ("mpcxh_go_rand_int63", _i, [ctypes.c_int64, _u32, _vp]),
     ("mpcxh_go_mr_bases", _i, [_vp, _u32, _u32, _vp]),
@@ -247,6 +248,19 @@ def pool_selftest(tasks: int, outer: int, inner: int) -> int:
     s = ctypes.c_uint64(0)
     _check(lib().mpcxh_pool_selftest(tasks, outer, inner, ctypes.byref(s)))
     return s.value
+
+
+def nat_arith(op: int, a: int, b: int) -> int:
+    """Host bignum op (test hook): 0 a*b, 1 a//b, 2 a%b, 3 a^-1 mod b, 4 gcd."""
+    def words(x):
+        n = max(1, (x.bit_length() + 31) // 32)
+        return (ctypes.c_uint32 * n)(*[(x >> (32 * i)) & 0xFFFFFFFF for i in range(n)]), (n if x else 0)
+    wa, na = words(a)
+    wb, nb = words(b)
+    nout = na + nb + 2
+    out, ow = (ctypes.c_uint32 * nout)(), ctypes.c_uint32(0)
+    _check(lib().mpcxh_nat_arith(op, wa, na, wb, nb, out, nout, ctypes.byref(ow)))
+    return sum(int(out[i]) << (32 * i) for i in range(ow.value))
 
 
 def profile_report(reset: bool = False) -> str:
