@@ -838,6 +838,13 @@ def main():
     ap.add_argument("--modbits", type=int, default=4096, choices=(2048, 4096),
                     help="4096: x^N mod N^2 (config 2, the bench line); 2048: x^N mod N (Paillier N / N~ class)")
     args = ap.parse_args()
+    # progress lines on stderr (stdout carries the one JSON line): phases
+    # here, keygen waves from the C++ driver
+    os.environ.setdefault("MPCX_PROGRESS", "1")
+    t_start = time.time()
+
+    def progress(msg):
+        print(f"[bench {time.time() - t_start:7.1f} s] {msg}", file=sys.stderr, flush=True)
 
     import torch
     import torch.distributed as dist
@@ -855,11 +862,13 @@ def main():
         info["usable_threads"] = args.cpu_threads
     sign_cpu = sign3_cpu = None
     if args.wallets > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("CPU baseline: signing")
         sign_cpu = cpu_baseline_signing(args.cpu_sign_seconds, info, args.signers)
         if args.signers != 3:
             sign3_cpu = cpu_baseline_signing(args.cpu_sign_seconds, info, 3)
     keygen_cpu = None
     if args.keygen_sessions > 0 and rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("CPU baseline: keygen proofs")
         keygen_cpu = cpu_baseline_keygen(16.0, info, args.parties)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
@@ -907,9 +916,11 @@ def main():
         if rc != 0:
             raise mpcx.MpcxError(rc, L.mpcx_last_error().decode())
 
+    progress("config 2: warm-up")
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
+    progress("config 2: timed steps")
 
     # one HIP event pair per timed step, on the launch stream (the library's
     # kernels run on `stream`, so the events bracket exactly one launch each)
@@ -1003,6 +1014,7 @@ def main():
 
     sub_lines = None
     if rank == 0 and args.extra_lines and args.modbits == 4096:
+        progress("config 2: per-operand exponents")
         sub_lines = [per_operand(2048), per_operand(4096)]
 
     from mpcium_amd.shard import max_over_ranks
@@ -1064,21 +1076,27 @@ def main():
     if sub_lines:
         result["config2_per_operand_exponents"] = sub_lines
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        progress("CPU baseline: config 2")
         result["cpu_baseline"] = cpu_baseline(N, args.cpu_seconds, info)
     if args.wallets > 0:
+        progress(f"config 4: signing, {args.signers} signers")
         result["signing"] = signing_line(args, world, rank, args.signers)
         result["signing"]["cpu_baseline"] = sign_cpu
         if args.signers != 3:  # mpcium signs with every ready peer (/root/reference/pkg/mpc/node.go:148)
+            progress("config 4: signing, 3 signers")
             result["signing_3_signers"] = signing_line(args, world, rank, 3)
             result["signing_3_signers"]["cpu_baseline"] = sign3_cpu
     if args.extra_lines:
         cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
+        progress("config 1 and 3: Paillier batch, safe primes")
         if world == 1:
             result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, info)
         result["safe_prime"] = safeprime_line(args.safe_primes, 0x5AFE, cpu, info, world, rank)
     if args.keygen_sessions > 0 and world == 1:
+        progress(f"config 5: keygen/reshare proofs, {args.keygen_sessions} sessions")
         result["keygen"] = keygen_line(args)
         result["keygen"]["cpu_baseline"] = keygen_cpu
+    progress("done")
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

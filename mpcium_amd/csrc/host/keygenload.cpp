@@ -1,6 +1,9 @@
 // keygenload.cpp -- see keygenload.hpp.
 #include "keygenload.hpp"
 
+#include <cstdio>
+#include <cstdlib>
+
 #include <atomic>
 #include <mutex>
 #include <chrono>
@@ -214,6 +217,13 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
     }
     std::lock_guard<std::mutex> lk(tm);
     max_wave = std::max(max_wave, now() - w0);
+    // MPCX_PROGRESS=1: one line per finished wave on stderr (long runs are
+    // otherwise silent for minutes)
+    static const bool progress = [] {
+      const char* e = std::getenv("MPCX_PROGRESS");
+      return e && e[0] == '1';
+    }();
+    if (progress) std::fprintf(stderr, "[keygenload] wave %zu/%zu done (%.1f s)\n", w + 1, n_waves, now() - w0);
   };
 
   Engine::get().reset_busy();

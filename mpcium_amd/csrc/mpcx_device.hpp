@@ -51,6 +51,9 @@
 #ifndef MPCX_PREFETCH_B
 #define MPCX_PREFETCH_B 1
 #endif
+#ifndef MPCX_SQR_B2
+#define MPCX_SQR_B2 0  // k_modexp / k_prime2c squarings read 2*b from LDS (no per-iteration doubling)
+#endif
 #ifndef MPCX_MID_CARRY
 #define MPCX_MID_CARRY 1  // montmul: a carry pass half-way through the L iterations (A/B: 0 drops it)
 #endif
@@ -179,9 +182,12 @@ __device__ __forceinline__ void carry_pass32(uint32_t (&d)[K]) {
 // unrolled index. Each pair lands in its column before that column is
 // reduced (both orientations use an iteration <= i + j). K must be odd.
 // Saves (K-1)/2 of the K a*b mads of every squaring iteration.
-template <int P, int K, bool SQR>
+// B2IN (squarings only): the LDS row holds 2*b (digits < 2^30.01), stored so
+// by the caller, which saves the per-iteration doubling.
+template <int P, int K, bool SQR, bool B2IN = false>
 __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, const uint32_t (&Nd)[K],
                                         uint32_t n0inv, int m_src_addr, int p) {
+  static_assert(SQR || !B2IN, "doubled multiplier rows are for squarings");
   static_assert(!SQR || (K % 2) == 1, "squaring schedule needs an odd digit count per lane");
   uint64_t acc[K];
 #pragma unroll
@@ -207,7 +213,7 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
         bnext = bnext2;
         bnext2 = bo[u + 2];
       }
-      const uint32_t b2 = bi << 1;
+      const uint32_t b2 = B2IN ? bi : bi << 1;
       const uint32_t bd = b2 >> dsh;
       auto ab = [&](auto kc) __attribute__((always_inline)) {
         constexpr int k = decltype(kc)::value;
@@ -282,6 +288,13 @@ template <int K>
 __device__ __forceinline__ void lds_store_digits(uint32_t* bl, int p, const uint32_t (&A)[K]) {
 #pragma unroll
   for (int k = 0; k < K; ++k) bl[p * K + k] = A[k];
+}
+
+// the squaring's multiplier row: 2*A when montmul reads it as B2IN, else A
+template <int K>
+__device__ __forceinline__ void lds_store_sqr(uint32_t* bl, int p, const uint32_t (&A)[K]) {
+#pragma unroll
+  for (int k = 0; k < K; ++k) bl[p * K + k] = MPCX_SQR_B2 ? A[k] << 1 : A[k];
 }
 
 // bits [wb*j, wb*j + wb) of the ew-word exponent e (wb <= 8; bits past the
@@ -475,7 +488,7 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
     for (;;) {
       if (sq_left) {
         --sq_left;
-        lds_store_digits<K>(bl, p, A);
+        lds_store_sqr<K>(bl, p, A);
         sqr = true;
         return;
       }
@@ -509,7 +522,7 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
 
   for (;;) {
     if (MPCX_SQR_OPT && sqr) {
-      montmul<P, K, true>(A, bl, Nd, a.n0inv, m_src_addr, p);
+      montmul<P, K, true, (bool)MPCX_SQR_B2>(A, bl, Nd, a.n0inv, m_src_addr, p);
     } else {
       montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
     }
@@ -524,7 +537,7 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
     } else if (st == ST_TAB) {
       tbl_store(sched ? 0u : idx, A);
       if (sched && T > 0u) {
-        lds_store_digits<K>(bl, p, A);
+        lds_store_sqr<K>(bl, p, A);
         sqr = true;
         st = ST_TSQ;
       } else if (!sched && idx == 1) {
@@ -1341,16 +1354,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
       const uint32_t dsh = (jb > 0 && jb < nbits && word_bit(nw, jb)) ? 1u : 0u;
       uint32_t B2[K];
 #pragma unroll
-      for (int k = 0; k < K; ++k) B2[k] = A[k] << dsh;
+      for (int k = 0; k < K; ++k) B2[k] = A[k] << (dsh + (MPCX_SQR_B2 ? 1u : 0u));  // montmul reads 2B
       lds_store_digits<K>(bl, p, B2);
     } else {
-      lds_store_digits<K>(bl, p, A);
+      lds_store_sqr<K>(bl, p, A);  // SS (or SQ without the fold): a plain squaring
     }
     wave_lds_fence();
     if (st == EX) {
       montmul<P, K, false>(A, bl, Nd, n0inv, 0, p);
     } else {
-      montmul<P, K, true>(A, bl, Nd, n0inv, 0, p);
+      montmul<P, K, true, (bool)MPCX_SQR_B2>(A, bl, Nd, n0inv, 0, p);
     }
     if (st == SQ) {
       if (!MPCX_PRIME2C_DBL_FOLD) {

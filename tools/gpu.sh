@@ -83,6 +83,23 @@ abswap)
     done
   done
   rm -f $O/orig_libmpcx.so ;;
+abn)
+  # like abswap for any number of builds (comma-separated); tag = position in the list
+  n=$1; libs=$2; shift 2
+  cp mpcium_amd/libmpcx.so $O/orig_libmpcx.so
+  for i in $(seq 1 $n); do
+    k=0
+    for lib in ${libs//,/ }; do
+      k=$((k+1)); tag=L${k}_$i
+      cp $lib mpcium_amd/libmpcx.so.tmp && mv mpcium_amd/libmpcx.so.tmp mpcium_amd/libmpcx.so
+      timeout -k 10 600 python3 bench.py "$@" > $O/ab_$tag.json 2> $O/ab_$tag.err
+      rc=$?
+      cp $O/orig_libmpcx.so mpcium_amd/libmpcx.so
+      [ $rc -eq 0 ] || { tail $O/ab_$tag.err; exit 1; }
+      echo "== $tag $lib"; summ $O/ab_$tag.json
+    done
+  done
+  rm -f $O/orig_libmpcx.so ;;
 envab)
   n=$1; ea=$2; eb=$3; shift 3
   for i in $(seq 1 $n); do
