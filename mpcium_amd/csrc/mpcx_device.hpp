@@ -52,10 +52,10 @@
 #define MPCX_PREFETCH_B 1
 #endif
 #ifndef MPCX_SQR_B2
-#define MPCX_SQR_B2 0  // k_modexp / k_prime2c squarings read 2*b from LDS (no per-iteration doubling)
+#define MPCX_SQR_B2 1  // k_modexp / k_prime2c squarings read 2*b from LDS (no per-iteration doubling)
 #endif
 #ifndef MPCX_MID_CARRY
-#define MPCX_MID_CARRY 1  // montmul: a carry pass half-way through the L iterations (A/B: 0 drops it)
+#define MPCX_MID_CARRY 0  // montmul: an extra carry pass half-way through the L iterations (not needed, see montmul)
 #endif
 #ifndef MPCX_PRIME2C_DBL_FOLD
 #define MPCX_PRIME2C_DBL_FOLD 1  // k_prime2c: the square-and-double step as one product with B = 2^bit x
@@ -168,10 +168,10 @@ __device__ __forceinline__ void carry_pass32(uint32_t (&d)[K]) {
 
 // A <- A * B * R^-1 (almost Montgomery, result < 2N given A, B < 2N), with
 // B's L digits in LDS at bl[0..L) (p = this lane's index in its group).
-// Result digits are <= 2^28 + 2^10 (two carry passes), which keeps every
-// product below 2^56.01 (2^57.01 for the doubled squaring products: a
-// position then takes <= L/2+1 of those plus one m*N per iteration, < 2^63.8
-// over the longest 84-iteration segment between carry passes).
+// Result digits are <= 2^28 + 2^8 (two carry passes at the end), which keeps
+// every product below 2^56.01 (2^57.02 for the doubled squaring products);
+// each accumulator register restarts every K iterations (see the end of the
+// block loop), so it stays below 2^63 with no carry pass inside the product.
 //
 // SQR (B == A, squaring): each unordered digit pair {i, j} needs ONE product
 // 2*a_i*a_j (plus a_i^2 on the diagonal). In iteration t the product of
@@ -259,8 +259,12 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
       __builtin_amdgcn_sched_barrier(0);
 #endif
     });
-    // Keep every accumulator below 2^64: at most ~P/2*K + K more iterations of
-    // two < 2^56.01 products follow this pass (<= 127 for every class).
+    // No mid-way carry pass is needed: a register is reset (slot 0 retires to
+    // a 28-bit value) once every K iterations, so it sums at most K iterations
+    // of one a*b and one m*N product (< 2^58.02 + 2^56 for the doubled
+    // squaring row of k_prime2c, whose digits reach 2^30.01) plus a < 2^35
+    // fold: < 2^62.8 for K <= 37. profiles/r03/kernel_ab: dropping the pass
+    // took the config-2 kernel from 176.3 to 171.7 ms.
     if (MPCX_MID_CARRY && o == P / 2 - 1) carry_pass64<P, K>(acc);
   }
   carry_pass64<P, K>(acc);

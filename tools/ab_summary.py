@@ -2,7 +2,7 @@
 one summary.json under profiles/: per-run headline values plus per-side means.
 
     python tools/ab_summary.py gpurun_out/r03/prime_ab profiles/r03/prime_ab/summary.json \
-        "bash tools/gpu.sh abswap ..." ["A label" "B label"]
+        "bash tools/gpu.sh abswap ..." ["A label" "B label" ...]   (abn: one label per build)
 """
 import glob
 import json
@@ -19,6 +19,9 @@ FIELDS = (
     ("signing_3_host_cpu_s", lambda d: d["signing_3_signers"].get("host_cpu_s")),
     ("keygen", lambda d: d["keygen"]["value"]),
     ("safe_prime", lambda d: d["safe_prime"]["value"]),
+    ("config2_kernel_ms", lambda d: round(d["roofline"]["kernel_ms"], 2)),
+    ("per_operand_2048_kernel_ms", lambda d: round(d["config2_per_operand_exponents"][0]["kernel_ms"], 2)),
+    ("paillier_batch", lambda d: d["paillier_batch"]["value"]),
 )
 
 
@@ -37,21 +40,25 @@ def row(path):
 
 def main():
     src, dst, cmd = sys.argv[1:4]
-    labels = sys.argv[4:6] if len(sys.argv) >= 6 else ["A", "B"]
-    runs, sides = [], {"A": [], "B": []}
-    for p in sorted(glob.glob(os.path.join(src, "ab_*.json")), key=lambda p: (p[-6:-5], p)):
-        m = re.search(r"ab_([AB])_(\d+)\.json$", p)
+    labels = sys.argv[4:]
+    runs, sides = [], {}
+    for p in sorted(glob.glob(os.path.join(src, "ab_*.json"))):
+        # ab_A_1 / ab_B_1 (ab, abswap, envab) or ab_L3_1 (abn: position in the build list)
+        m = re.search(r"ab_([AB]|L\d+)_(\d+)\.json$", p)
         if not m:
             continue
-        r = {"run": f"{m.group(1)}_{m.group(2)}", "side": labels["AB".index(m.group(1))]}
+        tag = m.group(1)
+        k = "AB".index(tag) if tag in "AB" else int(tag[1:]) - 1
+        side = labels[k] if k < len(labels) else tag
+        r = {"run": f"{tag}_{m.group(2)}", "side": side}
         r.update(row(p))
         runs.append(r)
-        sides[m.group(1)].append(r)
+        sides.setdefault(side, []).append(r)
+    runs.sort(key=lambda r: (int(r["run"].rsplit("_", 1)[1]), r["run"]))
     means = {}
     for s, rs in sides.items():
         keys = sorted({k for r in rs for k in r if k not in ("run", "side")})
-        means[labels["AB".index(s)]] = {k: round(sum(r[k] for r in rs if k in r) / sum(1 for r in rs if k in r), 4)
-                                        for k in keys}
+        means[s] = {k: round(sum(r[k] for r in rs if k in r) / sum(1 for r in rs if k in r), 4) for k in keys}
     os.makedirs(os.path.dirname(dst), exist_ok=True)
     json.dump({"command": cmd, "runs": runs, "means": means}, open(dst, "w"), indent=1)
     print(json.dumps(means, indent=1))
