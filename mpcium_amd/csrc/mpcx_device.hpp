@@ -54,6 +54,9 @@
 #ifndef MPCX_SQR_B2
 #define MPCX_SQR_B2 1  // k_modexp / k_prime2c squarings read 2*b from LDS (no per-iteration doubling)
 #endif
+#ifndef MPCX_BLOCK_FENCE
+#define MPCX_BLOCK_FENCE 0  // scheduling fence between montmul's P blocks (the prime kernels' TU sets 1)
+#endif
 #ifndef MPCX_MID_CARRY
 #define MPCX_MID_CARRY 0  // montmul: an extra carry pass half-way through the L iterations (not needed, see montmul)
 #endif
@@ -199,6 +202,9 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
   constexpr bool PF2 = K < MPCX_PREFETCH2_KMAX;
   uint32_t bnext = bl[0];
   uint32_t bnext2 = PF2 ? bl[1] : 0u;
+  // one copy of the K-iteration block (unrolling the P blocks would multiply
+  // the code and the live ranges: k_prime2c spilled with P = 2 unrolled)
+#pragma nounroll
   for (int o = 0; o < P; ++o) {
     const uint32_t* bo = bl + o * K;
     // diagonal-register factor of this lane for the whole block (2 above the
@@ -266,6 +272,12 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
     // fold: < 2^62.8 for K <= 37. profiles/r03/kernel_ab: dropping the pass
     // took the config-2 kernel from 176.3 to 171.7 ms.
     if (MPCX_MID_CARRY && o == P / 2 - 1) carry_pass64<P, K>(acc);
+#if MPCX_BLOCK_FENCE
+    // block boundary as a scheduling fence (mpcx_prime.hip: without it
+    // k_prime2c's live ranges grew past its 3-wave budget and spilled; the
+    // k_modexp geometries fit better without it)
+    __builtin_amdgcn_sched_barrier(0);
+#endif
   }
   carry_pass64<P, K>(acc);
   // digits are now < 2^28 + 2^37: one more pass brings them to <= 2^28 + 2^10

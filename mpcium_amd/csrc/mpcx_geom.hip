@@ -23,6 +23,14 @@
 #endif
 #endif
 
+// the multi-batch kernel's own budget (A/B: -DMPCX_WPE_MULTI_G<id>=n)
+#if MPCX_GEOM_ID == 1 && defined(MPCX_WPE_MULTI_G1)
+#define MPCX_WPE_MULTI MPCX_WPE_MULTI_G1
+#endif
+#ifndef MPCX_WPE_MULTI
+#define MPCX_WPE_MULTI MPCX_WPE
+#endif
+
 #define MPCX_CAT2(a, b) a##b
 #define MPCX_CAT(a, b) MPCX_CAT2(a, b)
 #define MPCX_THIS_KERNEL \
@@ -40,7 +48,7 @@ __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_g, 
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_multi_g, MPCX_GEOM_ID)(
     const mpcx::ModexpArgs* segs, const uint32_t* first, uint32_t nsegs, uint32_t waves, hipStream_t st) {
   hipLaunchKernelGGL((mpcx::k_modexp_multi<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
-                                           MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>),
+                                           MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE_MULTI>),
                      dim3(waves), dim3(64), 0, st, segs, first, nsegs);
   return hipGetLastError();
 }
