@@ -110,7 +110,7 @@ int mpcx_device_launches(int index, uint64_t* out);
  * alg_macs: Go-equivalent work (SURVEY.md 8(d) W per exponentiation) for
  * the exponentiation kernels -- within ~5% of what they execute (same
  * squarings; 5-bit or sliding windows instead of 4-bit) -- and the executed
- * products x 2 L^2 for the fixed-base comb (one per 8-bit window, far below
+ * products x 2 L^2 for the fixed-base comb (one per w-bit window, far below
  * Go's work for the same Exp); 0 for secp256k1;
  * kernel_ms: summed launch durations (lanes overlap, so the kinds' sum can
  * exceed busy_ms, the union of all launches' intervals per device, summed
@@ -302,10 +302,12 @@ int mpcx_safeprime_sieve_fermat(const uint8_t* raw, uint32_t nbytes, uint32_t co
  * h1, h2 of a node's N~ that every MtA range proof and DLN proof
  * exponentiates: up:crypto/mta/range_proof.go, up:crypto/mta/proofs.go,
  * up:crypto/dlnproof/proof.go; SURVEY.md 8(b) "_fixed_base"). Registration
- * precomputes b^(v 2^(8j)) R mod m for every 8-bit window j below
- * max_exp_bits on the GPU (256 entries per window, ~27 MB for 2816-bit
- * exponents of a 2048-bit modulus); the table lives until
- * mpcx_fixedbase_release (release it before its modulus). */
+ * precomputes b^(v 2^(wj)) R mod m for every w-bit window j below
+ * max_exp_bits on the GPU (2^w entries per window; w = 12 by default, option
+ * "fb_window", narrowed while the table would exceed 512 MB: ~320 MB for
+ * 3072-bit exponents of a 2048-bit modulus, a small share of 288 GB of HBM);
+ * the table lives until mpcx_fixedbase_release (release it before its
+ * modulus). */
 typedef struct mpcx_fixedbase_s* mpcx_fb_t;
 #define MPCX_FB_MAX_EXP_BITS 65536
 int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_words,
@@ -316,7 +318,7 @@ int mpcx_fixedbase_info(mpcx_fb_t fb, uint32_t* max_exp_bits, size_t* table_byte
 
 /* out[i] = (muls ? muls[i] : 1) * prod_{t < nbases} b_t^(e_t,i) mod m, with
  * 1 <= nbases <= 2 tables of the SAME modulus (e.g. z = h1^m h2^rho mod N~
- * as one product: one Montgomery product per 8-bit window, no squarings).
+ * as one product: one Montgomery product per w-bit window, no squarings).
  * exps[t]: count x exp_words[t] words (exp_words[t] may be 0: e = 0); every
  * exponent must fit its table (EINVAL otherwise). Synchronous. */
 int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t count,

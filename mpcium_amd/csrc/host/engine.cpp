@@ -408,7 +408,12 @@ Engine::Fixed Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
   auto it = fixed_.find(key);
   if (it != fixed_.end() && it->second->max_bits >= need_bits) return it->second;
   if (it != fixed_.end()) fixed_.erase(it);  // grow: rebuild for the longer exponent
-  if (fixed_.size() >= 256) fixed_.clear();  // bound the device footprint (~30 MB per table)
+  // bound the device footprint (~320 MB per 12-bit table): drop every cached
+  // table past kFixedMaxBytes (handles in use keep theirs alive)
+  if (fixed_bytes_ >= kFixedMaxBytes || fixed_.size() >= 256) {
+    fixed_.clear();
+    fixed_bytes_ = 0;
+  }
   if (need_bits > kFixedMaxBits) throw std::invalid_argument("fixed-base exponent above kFixedMaxBits");
   Mod& md = modulus(m);
   // MtA exponents on h1, h2 reach ~2818 bits (s2, t2 < q^3 N~ + e q N~); one size serves them all
@@ -419,6 +424,8 @@ Engine::Fixed Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
   int rc = mpcx_fixedbase_register(md.h, bw.data(), md.class_words, bits, &f->h);
   if (rc) throw_last(rc, "mpcx_fixedbase_register");
   f->max_bits = bits;
+  size_t tb = 0;
+  if (mpcx_fixedbase_info(f->h, nullptr, &tb) == MPCX_OK) fixed_bytes_ += tb;
   fixed_.emplace(key, f);
   return f;
 }

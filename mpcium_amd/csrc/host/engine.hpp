@@ -141,6 +141,8 @@ class Engine {
   void count_work(const Nat& m, const Nat* const* exps, size_t n_exps, size_t count);
   std::map<std::vector<uint32_t>, Mod> mods_;
   std::map<std::pair<std::vector<uint32_t>, std::vector<uint32_t>>, Fixed> fixed_;
+  size_t fixed_bytes_ = 0;                                  // device bytes of the cached tables
+  static constexpr size_t kFixedMaxBytes = size_t(24) << 30;  // of the 288 GB per GPU
 };
 
 [[noreturn]] void throw_last(int rc, const char* what);

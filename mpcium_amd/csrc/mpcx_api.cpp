@@ -83,8 +83,9 @@ struct mpcx_modulus_s {
 struct mpcx_fixedbase_s {
   mpcx_mod_t mod;
   int geom;                          // main geometry of the modulus class (table layout)
-  uint32_t nwin;                     // 8-bit windows: exponents of up to 8*nwin bits
-  std::vector<uint32_t> host_table;  // nwin x 256 entries x L digits ([k][p] interleaved)
+  uint32_t nwin;                     // windows: exponents of up to wbits*nwin bits
+  uint32_t wbits;                    // window width (entries per window: 2^wbits)
+  std::vector<uint32_t> host_table;  // nwin x 2^wbits entries x L digits ([k][p] interleaved)
   std::mutex mu;
   uint32_t* d_table[kMaxDevices] = {};
 };
@@ -104,6 +105,7 @@ int g_geom_policy = 1;                   // 1: 4096-bit class by the launch-time
 int g_fixed_win = 5;                     // widest fixed window for per-operand exponents (4 or 5)
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
+int g_fb_window = MPCX_FB_WINDOW_BITS;  // mpcx_set_option("fb_window", w): fixed-base comb width of new tables
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
 bool g_prime_coop = true;                // mpcx_set_option("prime_coop", 0): thread-per-candidate prime kernels
 bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 1): test hook, see below
@@ -743,6 +745,11 @@ int mpcx_set_option(const char* key, int value) {
     // the class's mid geometry (twice the wavefronts per operand count)
     if (value < 0 || value > 400) return fail(MPCX_EINVAL, "mid_rounds %d out of range", value);
     g_mid_rounds = value / 100.0;
+  } else if (std::strcmp(key, "fb_window") == 0) {
+    // window width of fixed-base tables registered from now on (4..12; one
+    // product per window, 2^w entries per window)
+    if (value < 4 || value > MPCX_FB_MAX_WINDOW_BITS) return fail(MPCX_EINVAL, "fb_window %d out of range", value);
+    g_fb_window = value;
   } else if (std::strcmp(key, "fixed_window") == 0) {
     // widest fixed window of per-operand exponents: 4 (Go's) or 5 (above 320 bits)
     if (value != 4 && value != 5) return fail(MPCX_EINVAL, "fixed_window %d not 4 or 5", value);
@@ -802,6 +809,8 @@ static void read_env_options() {
   if (gp) g_geom_policy = std::max(0, std::min(2, std::atoi(gp)));
   const char* ln = std::getenv("MPCX_LANES");
   if (ln && g_ndev.load() == 0) g_lanes = std::max(1, std::min(kMaxLanes, std::atoi(ln)));
+  const char* fw = std::getenv("MPCX_FB_WINDOW");  // fixed-base comb width of new tables
+  if (fw) g_fb_window = std::max(4, std::min(MPCX_FB_MAX_WINDOW_BITS, std::atoi(fw)));
 }
 
 int mpcx_init(int device) {
@@ -1822,6 +1831,8 @@ int mpcx_sync(void* stream) { return mpcx_stream_sync(stream); }
 // exponents), then T(j, v) = (R mod m) * b_j^v (fused multiplier), then
 // reordered into the kernel geometry's digit layout on the host; the host copy
 // is kept so other bound devices receive the table on first use.
+constexpr size_t kFbBuildSlice = 65536;  // table entries per build launch
+
 int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_words, uint32_t max_exp_bits,
                             mpcx_fb_t* out) {
   if (!mod || !base || !out) return fail(MPCX_EINVAL, "null argument");
@@ -1839,16 +1850,24 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   if ((rc = lane_stream(bl))) return rc;
   const int geom = MPCX_MAIN_GEOM(mod->cls);
   const uint32_t L = (uint32_t)MPCX_GEOM_L(geom), P = (uint32_t)MPCX_GEOM_P(geom), K = (uint32_t)MPCX_GEOM_K(geom);
-  const uint32_t nwin = (max_exp_bits + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS;
-  const uint32_t nv = MPCX_FB_ENTRIES - 1;  // v = 1..255 computed; v = 0 is R mod m
+  // window width: the configured one, narrowed until the table fits
+  // MPCX_FB_MAX_TABLE_BYTES (one product per window; 2^w entries per window)
+  uint32_t wb = (uint32_t)g_fb_window;
+  auto tbytes = [&](uint32_t w) {
+    return (unsigned long long)((max_exp_bits + w - 1) / w) * (1ull << w) * L * 4ull;
+  };
+  while (wb > 4 && tbytes(wb) > MPCX_FB_MAX_TABLE_BYTES) --wb;
+  const uint32_t nwin = (max_exp_bits + wb - 1) / wb;
+  const uint32_t entries = 1u << wb;
+  const uint32_t nv = entries - 1;  // v = 1..2^w-1 computed; v = 0 is R mod m
   const size_t n2 = (size_t)nwin * nv;
   if (n2 > 0xFFFFFFFFull) return fail(MPCX_EINVAL, "table too large");
-  const uint32_t ew1 = (MPCX_FB_WINDOW_BITS * (nwin - 1)) / 32 + 1;  // 2^(8j) needs bit 8j
+  const uint32_t ew1 = (wb * (nwin - 1)) / 32 + 1;  // 2^(w j) needs bit w j
   // host inputs
   std::vector<uint32_t> hb((size_t)nwin * cw, 0), he1((size_t)nwin * ew1, 0);
   for (uint32_t j = 0; j < nwin; ++j) {
     std::memcpy(&hb[(size_t)j * cw], base, base_words * 4);
-    const uint32_t bit = MPCX_FB_WINDOW_BITS * j;
+    const uint32_t bit = wb * j;
     he1[(size_t)j * ew1 + bit / 32] = 1u << (bit % 32);
   }
   const std::vector<uint32_t> r1w = pow2_mod(kDigitBits * L, mod->m);  // R mod m, mod->words words
@@ -1878,9 +1897,8 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     cleanup();
     return hip_fail(e, "upload fixed-base inputs");
   }
-  rc = modexp_enqueue(di, bl, mod, nwin, d_b, cw, d_e1, ew1, 0, MPCX_FB_WINDOW_BITS * (nwin - 1) + 1, nullptr, 0,
-                      d_bj, cw);
-  // T(j, v) = R * b_j^v: operand i = j*255 + (v-1) takes base b_j -> replicate b_j rows
+  rc = modexp_enqueue(di, bl, mod, nwin, d_b, cw, d_e1, ew1, 0, wb * (nwin - 1) + 1, nullptr, 0, d_bj, cw);
+  // T(j, v) = R * b_j^v: operand i = j*nv + (v-1) takes base b_j -> replicate b_j rows
   std::vector<uint32_t> hbj((size_t)nwin * cw), hb2;
   if (!rc) rc = d2h_sync(hbj.data(), d_bj, hbj.size() * 4, bl);
   if (!rc) {
@@ -1892,8 +1910,13 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   }
   if (!rc) rc = h2d(d_b, hb2.data(), hb2.size() * 4, bl.st);
   if (!rc)
-    rc = modexp_enqueue(di, bl, mod, (uint32_t)n2, d_b, cw, d_e2, 1, 0, MPCX_FB_WINDOW_BITS, d_m, mod->words, d_t,
-                        cw);
+    // in slices: the build lane's window-table workspace grows with the
+    // operands of one launch (a 12-bit table has ~1M entries)
+    for (size_t off = 0; off < n2 && !rc; off += kFbBuildSlice) {
+      const uint32_t cnt = (uint32_t)std::min<size_t>(kFbBuildSlice, n2 - off);
+      rc = modexp_enqueue(di, bl, mod, cnt, d_b + off * cw, cw, d_e2 + off, 1, 0, wb, d_m + off * mod->words,
+                          mod->words, d_t + off * cw, cw);
+    }
   std::vector<uint32_t> ht(n2 * cw);
   if (!rc) rc = d2h_sync(ht.data(), d_t, ht.size() * 4, bl);
   cleanup();
@@ -1902,24 +1925,33 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   fb->mod = mod;
   fb->geom = geom;
   fb->nwin = nwin;
+  fb->wbits = wb;
   // digits, [k][p] interleaved per entry
   const size_t ent_words = L;
   auto& tab = fb->host_table;
-  tab.assign((size_t)nwin * MPCX_FB_ENTRIES * ent_words, 0);
+  tab.assign((size_t)nwin * entries * ent_words, 0);
   auto put = [&](size_t ent, const std::vector<uint32_t>& words) {
     const std::vector<uint32_t> d = to_digits(words, L);
     uint32_t* dst = &tab[ent * ent_words];
     for (uint32_t pp = 0; pp < P; ++pp)
       for (uint32_t k = 0; k < K; ++k) dst[k * P + pp] = d[pp * K + k];
   };
-  std::vector<uint32_t> w(cw);
-  for (uint32_t j = 0; j < nwin; ++j) {
-    put((size_t)j * MPCX_FB_ENTRIES, r1w);
-    for (uint32_t v = 1; v < MPCX_FB_ENTRIES; ++v) {
-      std::memcpy(w.data(), &ht[((size_t)j * nv + (v - 1)) * cw], cw * 4);
-      put((size_t)j * MPCX_FB_ENTRIES + v, w);
-    }
-  }
+  // 2^w entries per window: the conversion to interleaved digits runs on the
+  // host threads (a 12-bit table is ~1M entries)
+  const uint32_t nthr = std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> conv;
+  for (uint32_t t = 0; t < nthr; ++t)
+    conv.emplace_back([&, t] {
+      std::vector<uint32_t> w(cw);
+      for (uint32_t j = t; j < nwin; j += nthr) {
+        put((size_t)j * entries, r1w);
+        for (uint32_t v = 1; v < entries; ++v) {
+          std::memcpy(w.data(), &ht[((size_t)j * nv + (v - 1)) * cw], cw * 4);
+          put((size_t)j * entries + v, w);
+        }
+      }
+    });
+  for (auto& th : conv) th.join();
   const uint32_t* dt = nullptr;
   if ((rc = fb_table(fb, di, &dt))) {
     delete fb;
@@ -1940,8 +1972,8 @@ int mpcx_fixedbase_release(mpcx_fb_t fb) {
 
 int mpcx_fixedbase_info(mpcx_fb_t fb, uint32_t* max_exp_bits, size_t* table_bytes) {
   if (!fb) return fail(MPCX_EINVAL, "null fixed base");
-  if (max_exp_bits) *max_exp_bits = fb->nwin * MPCX_FB_WINDOW_BITS;
-  if (table_bytes) *table_bytes = (size_t)fb->nwin * MPCX_FB_ENTRIES * MPCX_GEOM_L(fb->geom) * 4;
+  if (max_exp_bits) *max_exp_bits = fb->nwin * fb->wbits;
+  if (table_bytes) *table_bytes = ((size_t)fb->nwin << fb->wbits) * MPCX_GEOM_L(fb->geom) * 4;
   return MPCX_OK;
 }
 
@@ -1966,9 +1998,10 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     uint32_t bits = 0;
     for (uint32_t i = 0; i < count && exp_words[t]; ++i)
       bits = std::max(bits, bit_length_words(exps[t] + (size_t)i * exp_words[t], exp_words[t]));
-    if (bits > fbs[t]->nwin * MPCX_FB_WINDOW_BITS)
-      return fail(MPCX_EINVAL, "exponent of %u bits > fixed-base table's %u", bits, fbs[t]->nwin * MPCX_FB_WINDOW_BITS);
-    nwin[t] = (bits + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS;
+    const uint32_t wb = fbs[t]->wbits;
+    if (bits > fbs[t]->nwin * wb)
+      return fail(MPCX_EINVAL, "exponent of %u bits > fixed-base table's %u", bits, fbs[t]->nwin * wb);
+    nwin[t] = (bits + wb - 1) / wb;
   }
   return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t n) {
     const uint32_t* dconst = nullptr;
@@ -2000,6 +2033,7 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
       a.exps[t] = (const uint32_t*)sg[t].ptr;
       a.exp_words[t] = exp_words[t];
       a.nwin[t] = nwin[t];
+      a.wbits[t] = fbs[t]->wbits;
     }
     a.nbases = nbases;
     a.mul = muls ? (const uint32_t*)sg[3].ptr : nullptr;
@@ -2016,7 +2050,7 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
     {
       // Go-equivalent (launch log): one Exp per base per operand; executed
-      // (kernel stats): one product per 8-bit window of each exponent, plus
+      // (kernel stats): one product per window of each exponent, plus
       // the multiplier's, 2 L^2 MACs each
       double alg = 0.0, exec = 0.0;
       const double l2 = 2.0 * (double)((mod->bits + 31) / 32) * (double)((mod->bits + 31) / 32);
@@ -2025,7 +2059,7 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
         for (uint32_t i = 0; i < n && exp_words[t]; ++i) {
           const uint32_t b = bit_length_words(exps[t] + (size_t)(first + i) * exp_words[t], exp_words[t]);
           alg += go_macs(mod->bits, b);
-          exec += (double)((b + MPCX_FB_WINDOW_BITS - 1) / MPCX_FB_WINDOW_BITS) * l2;
+          exec += (double)((b + fbs[t]->wbits - 1) / fbs[t]->wbits) * l2;
           eb_max = std::max(eb_max, b);
         }
       if (muls) exec += (double)n * l2;

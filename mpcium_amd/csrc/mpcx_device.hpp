@@ -313,7 +313,7 @@ __device__ __forceinline__ void lds_store_sqr(uint32_t* bl, int p, const uint32_
   for (int k = 0; k < K; ++k) bl[p * K + k] = MPCX_SQR_B2 ? A[k] << 1 : A[k];
 }
 
-// bits [wb*j, wb*j + wb) of the ew-word exponent e (wb <= 8; bits past the
+// bits [wb*j, wb*j + wb) of the ew-word exponent e (wb <= 32; bits past the
 // top word read as 0)
 __device__ __forceinline__ uint32_t window_of(const uint32_t* e, uint32_t j, uint32_t wb, uint32_t ew) {
   const uint32_t bit = wb * j, w = bit >> 5, sh = bit & 31u;
@@ -620,7 +620,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 // Fixed-base multi-exponentiation: out_i = mul_i * prod_t b_t^(e_t,i) mod m
 // for up to MPCX_FB_MAX_BASES registered bases (h1, h2 of a node's N~;
 // up:crypto/mta/range_proof.go z = h1^m h2^rho, up:crypto/dlnproof/proof.go
-// alpha_i = h1^a_i). With the comb table b^(v 2^(8j)) per 8-bit window there
+// alpha_i = h1^a_i). With the comb table b^(v 2^(wj)) per w-bit window there
 // are no squarings at all: one Montgomery product per window of each
 // exponent, z <- mont(z, T[j][v]), against Go's E squarings + E/4 multiplies
 // for the same Exp. Every operand multiplies in every window (v = 0 reads
@@ -657,13 +657,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   bool fin = false;
   auto next = [&] __attribute__((always_inline))() -> bool {
     for (; t < a.nbases; ++t, j = 0) {
-      const uint32_t ew = a.exp_words[t];
+      const uint32_t ew = a.exp_words[t], wb = a.wbits[t];
       const uint32_t* ex = a.exps[t] + (size_t)(active ? op : 0) * ew;
       for (; j < a.nwin[t]; ++j) {
-        const uint32_t wi = j >> 2;
-        const uint32_t v = (active && wi < ew) ? (ex[wi] >> ((j & 3u) * 8u)) & 0xFFu : 0u;
+        const uint32_t v = (active && ew) ? window_of(ex, j, wb, ew) : 0u;
         if (__ballot(v != 0u) == 0ull) continue;  // no operand of the wave has bits here
-        const uint32_t* e = a.tables[t] + ((size_t)j * MPCX_FB_ENTRIES + v) * L;
+        const uint32_t* e = a.tables[t] + (((size_t)j << wb) + v) * L;
         uint32_t tv[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) tv[k] = idle ? 0u : e[k * P + p];

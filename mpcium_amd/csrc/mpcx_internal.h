@@ -89,12 +89,14 @@ struct ModexpArgs {
   const uint32_t* sched; // shared exponent: its window schedule (nullptr: fixed window)
 };
 
-// Fixed-base tables (mpcx_fixedbase_register): for window j < nwin and byte
-// value v < 256, entry (j, v) = b^(v * 2^(8j)) R mod m as L radix-2^28 digits
-// of the class's main geometry, interleaved [digit slot k][lane p] so a
-// group's P lanes read P consecutive words per slot. Entry (j, 0) = R mod m.
-#define MPCX_FB_WINDOW_BITS 8
-#define MPCX_FB_ENTRIES 256
+// Fixed-base tables (mpcx_fixedbase_register): w-bit windows (w chosen per
+// table, <= MPCX_FB_MAX_WINDOW_BITS); for window j < nwin and value v < 2^w,
+// entry (j, v) = b^(v * 2^(w j)) R mod m as L radix-2^28 digits of the class's
+// main geometry, interleaved [digit slot k][lane p] so a group's P lanes read
+// P consecutive words per slot. Entry (j, 0) = R mod m.
+#define MPCX_FB_WINDOW_BITS 12      // default width (option "fb_window")
+#define MPCX_FB_MAX_WINDOW_BITS 12
+#define MPCX_FB_MAX_TABLE_BYTES (512ull << 20)  // narrower windows above this per table
 #define MPCX_FB_MAX_BASES 2
 
 struct FixedBaseArgs {
@@ -104,7 +106,8 @@ struct FixedBaseArgs {
   const uint32_t* tables[MPCX_FB_MAX_BASES];
   const uint32_t* exps[MPCX_FB_MAX_BASES];  // count x exp_words[t]
   uint32_t exp_words[MPCX_FB_MAX_BASES];
-  uint32_t nwin[MPCX_FB_MAX_BASES];         // 8-bit windows processed per base
+  uint32_t nwin[MPCX_FB_MAX_BASES];         // windows processed per base
+  uint32_t wbits[MPCX_FB_MAX_BASES];        // window width of each base's table
   uint32_t nbases;
   const uint32_t* mul;  // optional count x mul_words multipliers
   uint32_t mul_words;

@@ -235,16 +235,23 @@ def test_shared_exponent_window_schedules(gpu, paillier_key, width):
         gpu.set_option("sched_width", 6)
 
 
-def test_fixed_base_tables(gpu, paillier_key):
-    """Fixed-base comb (h1^a h2^b mod N~ shape): one and two bases, with and
-    without a multiplier, zero/one/boundary exponents, ragged batches, and
-    exponents past the table rejected."""
+@pytest.mark.parametrize("wbits", [12, 11, 8])
+def test_fixed_base_tables(gpu, paillier_key, wbits):
+    """Fixed-base comb (h1^a h2^b mod N~ shape) with w-bit windows (12: the
+    default; 11: windows straddling 32-bit words at varying offsets; 8: round
+    2's): one and two bases, with and without a multiplier, zero/one/boundary
+    exponents, ragged batches, and exponents past the table rejected."""
     N = paillier_key["N"]
-    rng = random.Random(77)
+    rng = random.Random(77 + wbits)
     mod = gpu.Modulus(N)
     h1, h2 = rng.randrange(N), rng.randrange(N)
-    f1, f2 = gpu.FixedBase(mod, h1, 2816), gpu.FixedBase(mod, h2, 300)
-    assert f1.max_exp_bits == 2816 and f2.max_exp_bits == 304
+    gpu.set_option("fb_window", wbits)
+    try:
+        f1, f2 = gpu.FixedBase(mod, h1, 2816), gpu.FixedBase(mod, h2, 300)
+    finally:
+        gpu.set_option("fb_window", 12)
+    cap = lambda b: -(-b // wbits) * wbits  # noqa: E731
+    assert f1.max_exp_bits == cap(2816) and f2.max_exp_bits == cap(300)
     for count in (1, mod.G - 1, mod.G + 1, 3 * mod.G + 5):
         a = [rng.getrandbits(rng.choice([0, 1, 8, 9, 256, 2048, 2816])) for _ in range(count)]
         b = [rng.getrandbits(rng.choice([0, 7, 64, 300])) for _ in range(count)]
@@ -253,10 +260,10 @@ def test_fixed_base_tables(gpu, paillier_key):
         assert gpu.fixedbase_exp([f1, f2], [a, b]) == want, count
         cs = [rng.randrange(N) for _ in range(count)]
         assert gpu.fixedbase_exp([f1, f2], [a, b], cs) == [c * w % N for c, w in zip(cs, want)], count
-    edge = [0, 1, 255, 256, (1 << 2816) - 1, 1 << 2815]
+    edge = [0, 1, 255, 256, 4095, 4096, (1 << 2816) - 1, 1 << 2815, (1 << cap(2816)) - 1]
     assert gpu.fixedbase_exp([f1], [edge]) == [pow(h1, x, N) for x in edge]
     with pytest.raises(gpu.MpcxError):
-        gpu.fixedbase_exp([f2], [[1 << 304]])
+        gpu.fixedbase_exp([f2], [[1 << cap(300)]])
     # N~-shape modulus from the node fixtures and the 1024-bit class
     for m in (paillier_key["P"], rng.getrandbits(1500) | 1 | (1 << 1499)):
         md = gpu.Modulus(m)
