@@ -20,6 +20,7 @@ expNNMontgomery timed on this host's cores, rank 0, N=1 only).
 from __future__ import annotations
 
 import argparse
+import collections
 import json
 import math
 import os
@@ -225,9 +226,22 @@ def host_info() -> dict:
     return info
 
 
+_C_SECONDS = collections.defaultdict(float)  # thread ident -> seconds inside the C restatement's calls
+
+
+def _c_call(fn, *a):
+    """Call the C restatement, adding its duration to this thread's C time
+    (python_share of the CPU legs = the rest of the threads' time)."""
+    t0 = time.perf_counter()
+    r = fn(*a)
+    _C_SECONDS[threading.get_ident()] += time.perf_counter() - t0
+    return r
+
+
 def _time_threads(make_work, seconds: float, threads: int):
     """Run make_work(t)() repeatedly on `threads` Python threads (the work is
     a ctypes call that releases the GIL) for `seconds`; -> (ops, elapsed)."""
+    _C_SECONDS.clear()
     done = [0] * threads
     stop = time.perf_counter() + seconds
 
@@ -246,11 +260,17 @@ def _time_threads(make_work, seconds: float, threads: int):
     return sum(done), time.perf_counter() - t0
 
 
+_LAST_PYTHON_SHARE = [None]
+
+
 def _one_and_all(make_work, seconds: float, info: dict):
-    """1-thread and all-usable-thread rates of the same work (seconds split 1:2)."""
+    """1-thread and all-usable-thread rates of the same work (seconds split 1:2).
+    _LAST_PYTHON_SHARE[0]: the all-thread run's share of thread time outside
+    the C calls (Python orchestration and conversions, GIL waits)."""
     n1, e1 = _time_threads(make_work, seconds / 3, 1)
     thr = info["usable_threads"]
     nn, en = _time_threads(make_work, 2 * seconds / 3, thr) if thr > 1 else (n1, e1)
+    _LAST_PYTHON_SHARE[0] = max(0.0, 1.0 - sum(_C_SECONDS.values()) / (thr * en)) if _C_SECONDS else None
     return n1 / e1, nn / en, thr, (n1, e1, nn, en)
 
 
@@ -277,11 +297,12 @@ def cpu_baseline(N: int, seconds: float, info: dict):
             xs = rng.integers(0, 1 << 32, size=nw, dtype=np.uint64).astype(np.uint32)
             xs[-1] = xs[-1] % max((N2 >> (32 * (nw - 1))), 1)
             xw = (ctypes.c_uint32 * nw)(*[int(v) for v in xs])
-            return lambda: lib.gomodexp_montgomery(out, xw, nw, yw, ew, mw, nw)
+            return lambda: _c_call(lib.gomodexp_montgomery, out, xw, nw, yw, ew, mw, nw)
         return make
 
     r1, rn, thr, raw = _one_and_all(c_work(lib64), seconds * 0.5, info)
     out = {"value": rn, "unit": "modexp/s", "cores": thr, "kind": "port", "one_core": r1,
+           "python_share": _LAST_PYTHON_SHARE[0],
            "all_cores_extrapolated": r1 * info["nproc"],
            "sample": f"{raw[2]} x (x^N mod N^2, 4096-bit modulus, 2048-bit exponent) in {raw[3]:.1f} s on {thr} "
                      f"threads (+ {raw[0]} on 1 thread in {raw[1]:.1f} s); C restatement of Go expNNMontgomery with "
@@ -318,7 +339,8 @@ def _c_exp_words(lib, nw):
     def f(x, y, m):
         out = (ctypes.c_uint32 * nw)()
         ew = max(1, (y.bit_length() + 31) // 32)
-        lib.gomodexp_montgomery(out, cc._words(x, nw), nw, cc._words(y, ew), ew, cc._words(m, nw), nw)
+        xw, yw, mw = cc._words(x, nw), cc._words(y, ew), cc._words(m, nw)
+        _c_call(lib.gomodexp_montgomery, out, xw, nw, yw, ew, mw, nw)
         return int.from_bytes(bytes(out), "little")
     return f
 
@@ -351,8 +373,10 @@ def cpu_baseline_paillier(N: int, seconds: float, info: dict):
         return mk
 
     r1, rn, thr, raw = _one_and_all(make(False), seconds * 0.6, info)
+    py_share = _LAST_PYTHON_SHARE[0]
     s1, sn, _, sraw = _one_and_all(make(True), seconds * 0.4, info)
     return {"value": rn, "unit": "Encrypt+HomoMult ops/s", "cores": thr, "kind": "port", "one_core": r1,
+            "python_share": py_share,
             "all_cores_extrapolated": r1 * info["nproc"],
             "same_work_as_gpu": {"value": sn, "one_core": s1, "cores": thr,
                                  "all_cores_extrapolated": s1 * info["nproc"]},
@@ -429,6 +453,7 @@ def cpu_baseline_fermat(seconds: float, info: dict):
 
     r1, rn, thr, raw = _one_and_all(make, seconds, info)
     return {"value": rn, "unit": "1024-bit Fermat tests/s", "cores": thr, "kind": "port", "one_core": r1,
+            "python_share": _LAST_PYTHON_SHARE[0],
             "all_cores_extrapolated": r1 * info["nproc"],
             "sample": f"{raw[2]} x 2^(p-1) mod p (1024-bit p) in {raw[3]:.1f} s on {thr} threads; "
                       f"oracle/gomodexp.c (64-bit Words)", **info}

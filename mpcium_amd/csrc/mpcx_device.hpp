@@ -54,6 +54,9 @@
 #ifndef MPCX_SQR_B2
 #define MPCX_SQR_B2 1  // k_modexp / k_prime2c squarings read 2*b from LDS (no per-iteration doubling)
 #endif
+#ifndef MPCX_FB_PREFETCH
+#define MPCX_FB_PREFETCH 1  // k_fixedbase loads the next table entry during the current product
+#endif
 #ifndef MPCX_BLOCK_FENCE
 #define MPCX_BLOCK_FENCE 0  // scheduling fence between montmul's P blocks (the prime kernels' TU sets 1)
 #endif
@@ -650,12 +653,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     lds_store_digits<K>(bl, p, t);
   };
   // ONE montmul call site (three would triple the unrolled product and its
-  // register allocation): each pass of the loop below prepares the next B.
+  // register allocation). The next product's multiplier (a table entry: one
+  // scattered 304-B read per operand, mostly from HBM for a 12-bit table) is
+  // loaded into registers while the current product runs, so the load latency
+  // hides behind the Montgomery work instead of stalling every product.
   uint32_t t = 0, j = 0;  // next window: base t, window j
-  // B for the next product: the next window with bits in some operand of
-  // the wave, else the exit multiplier 1; false once the exit product is done
+  uint32_t nx[K];         // the next product's B digits, in flight
+  // nx <- the next window with bits in some operand of the wave, else the exit
+  // multiplier 1; false once the exit product has been handed out
   bool fin = false;
-  auto next = [&] __attribute__((always_inline))() -> bool {
+  auto fetch = [&] __attribute__((always_inline))() -> bool {
     for (; t < a.nbases; ++t, j = 0) {
       const uint32_t ew = a.exp_words[t], wb = a.wbits[t];
       const uint32_t* ex = a.exps[t] + (size_t)(active ? op : 0) * ew;
@@ -663,25 +670,23 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
         const uint32_t v = (active && ew) ? window_of(ex, j, wb, ew) : 0u;
         if (__ballot(v != 0u) == 0ull) continue;  // no operand of the wave has bits here
         const uint32_t* e = a.tables[t] + (((size_t)j << wb) + v) * L;
-        uint32_t tv[K];
 #pragma unroll
-        for (int k = 0; k < K; ++k) tv[k] = idle ? 0u : e[k * P + p];
-        lds_store_digits<K>(bl, p, tv);
+        for (int k = 0; k < K; ++k) nx[k] = idle ? 0u : e[k * P + p];
         ++j;
         return true;
       }
     }
     if (fin) return false;
     fin = true;  // leave the Montgomery domain: z = mont(z R, 1) <= m
-    uint32_t one[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
-    lds_store_digits<K>(bl, p, one);
+    for (int k = 0; k < K; ++k) nx[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
     return true;
   };
 
+  // B of the first product: R^2 already in LDS (z = mul R = mont(mul, R^2)),
+  // or the first fetched entry
+  bool more = true, b_in_lds = a.mul != nullptr;
   if (a.mul) {
-    // z = mul R = mont(mul, R^2)
     lds_digits(a.r2d);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -699,13 +704,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   } else {
 #pragma unroll
     for (int k = 0; k < K; ++k) A[k] = idle ? 0u : a.r1d[p * K + k];  // z = R mod m
-    next();
+    more = fetch();
   }
-  do {
+  while (more) {
+    if (!b_in_lds) lds_store_digits<K>(bl, p, nx);
+    b_in_lds = false;
     wave_lds_fence();
+    if (MPCX_FB_PREFETCH) more = fetch();  // the following B's loads overlap this product
     montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
     wave_lds_fence();
-  } while (next());
+    if (!MPCX_FB_PREFETCH) more = fetch();
+  }
   store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
 }
 

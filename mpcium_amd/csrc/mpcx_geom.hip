@@ -23,8 +23,14 @@
 #endif
 #endif
 
-// the multi-batch kernel's own budget (A/B: -DMPCX_WPE_MULTI_G<id>=n)
-#if MPCX_GEOM_ID == 1 && defined(MPCX_WPE_MULTI_G1)
+// the multi-batch kernel's own budget (A/B: -DMPCX_WPE_MULTI_G<id>=n): the
+// 2048-bit main geometry's multi kernel fits 128 VGPRs without scratch and
+// runs 4 waves per SIMD (profiles/r03/wpe4: keygen 385 vs 368 sessions/s,
+// signing +2-4%, two interleaved rounds)
+#if MPCX_GEOM_ID == 1
+#ifndef MPCX_WPE_MULTI_G1
+#define MPCX_WPE_MULTI_G1 4
+#endif
 #define MPCX_WPE_MULTI MPCX_WPE_MULTI_G1
 #endif
 #ifndef MPCX_WPE_MULTI
