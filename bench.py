@@ -40,13 +40,13 @@ PEAK_MAD_MEASURED = 33.8e12            # tools/microbench/valu_rates.hip, 8 wave
 
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r02", "pmc2", "summary.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03", "pmc", "config2_traffic.json")
 
 
 def pmc_traffic(count: int, modbits: int, mod) -> dict:
     """roofline.traffic: fabric bytes per launch of the bench kernel from the
     committed rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate --pmc runs of
-    the bench command over the current kernel, tools/gpu_pmc2.sh). rocprofv3 cannot run
+    the bench command over the current kernel, tools/gpu.sh pmc). rocprofv3 cannot run
     inside the timed process. Only reported for the workload those passes
     measured (65,536 operands, 4096-bit modulus, 4x37 quad geometry); null
     otherwise. The algorithmic I/O is 1 KB per operand (base in, result out).

@@ -55,7 +55,7 @@
 #define MPCX_SQR_B2 1  // k_modexp / k_prime2c squarings read 2*b from LDS (no per-iteration doubling)
 #endif
 #ifndef MPCX_FB_PREFETCH
-#define MPCX_FB_PREFETCH 1  // k_fixedbase loads the next table entry during the current product
+#define MPCX_FB_PREFETCH 0  // 1: k_fixedbase loads the next table entry during the current product (measured slower)
 #endif
 #ifndef MPCX_BLOCK_FENCE
 #define MPCX_BLOCK_FENCE 0  // scheduling fence between montmul's P blocks (the prime kernels' TU sets 1)
@@ -653,10 +653,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     lds_store_digits<K>(bl, p, t);
   };
   // ONE montmul call site (three would triple the unrolled product and its
-  // register allocation). The next product's multiplier (a table entry: one
-  // scattered 304-B read per operand, mostly from HBM for a 12-bit table) is
-  // loaded into registers while the current product runs, so the load latency
-  // hides behind the Montgomery work instead of stalling every product.
+  // register allocation). MPCX_FB_PREFETCH=1 loads the next product's table
+  // entry (one scattered 304-B read per operand) into registers while the
+  // current product runs; measured 6% slower on config 5 than loading it
+  // after the product (profiles/r03/fb_prefetch), so it is off.
   uint32_t t = 0, j = 0;  // next window: base t, window j
   uint32_t nx[K];         // the next product's B digits, in flight
   // nx <- the next window with bits in some operand of the wave, else the exit
