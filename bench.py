@@ -489,9 +489,11 @@ def safeprime_line(num: int, seed: int, cpu: bool, info: dict, world: int = 1, r
         dist.all_reduce(t)  # whole-job candidate / test counts (gloo, host tensors)
         st = dict(zip(acc, (int(x) for x in t)))
     else:
+        _kernel_stats_reset()
         t0 = time.perf_counter()
         res, st = mhost.safe_primes(1024, num, seed=seed)
         el = time.perf_counter() - t0
+        kr = _kernel_roofline()
     for p, q, _ in res:  # untimed: p = 2q + 1, both prime (CPython pow MR spot check)
         if p != 2 * q + 1 or pow(2, p - 1, p) != 1 or pow(3, q - 1, q) != 1 or q.bit_length() != 1023:
             raise SystemExit("safe-prime line: bad prime")
@@ -503,6 +505,19 @@ def safeprime_line(num: int, seed: int, cpu: bool, info: dict, world: int = 1, r
             "n_gpus": world, "scaling": "strong", "first_index": res[0][2], "last_index": res[-1][2],
             "roofline": _job_roofline((st["fermat_tests"] + st["mr_tests"]) * alg_macs(1024, 1023), el, world),
             "cpu_baseline": None}
+    if world == 1:
+        # the dominant kernel's own roofline: k_prime2c's Go-equivalent work
+        # (2^(p-1) mod p per sieve survivor, 2^d mod q per ride-along q) over
+        # its summed launch time (HIP events on its stream)
+        pk = [k for k in kr["kernels"] if k["kind"] == "prime2c"]
+        if pk and pk[0]["kernel_ms"] > 0:
+            k = pk[0]
+            ach = k["alg_ops"] / (k["kernel_ms"] / 1e3)
+            line["kernel_roofline"] = {"kernel": "k_prime2c", "bound": "valu", "achieved": ach / 1e12,
+                                       "peak": PEAK_INT32_NOMINAL / 1e12, "unit": "TOP/s",
+                                       "frac": ach / PEAK_INT32_NOMINAL, "launches": k["launches"],
+                                       "tests": k["operands"], "kernel_ms": k["kernel_ms"],
+                                       "gpu_busy_s_instrumented": kr["gpu_busy_s"]}
     if cpu:
         b = cpu_baseline_fermat(8.0, info)
         if b:

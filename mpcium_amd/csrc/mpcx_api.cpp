@@ -267,6 +267,16 @@ void kstat_end(Lane& l, int slot, const Device& d, int dev, const char* kind, in
   p.alg = alg;
 }
 
+// work of a launch whose operand count is known only after it ran (the
+// safe-prime step's sieve survivors): added to its kind without a launch
+void kstat_credit(const char* kind, int geom, uint64_t ops, double alg) {
+  if (!g_kstats.load(std::memory_order_relaxed)) return;
+  std::lock_guard<std::mutex> lk(g_kmu);
+  KAgg& a = g_kagg[{kind, geom}];
+  a.ops += ops;
+  a.alg += alg;
+}
+
 // after the lane's stream drained: every pending pair has completed
 void kstat_resolve(Lane& l) {
   std::lock_guard<std::mutex> lk(g_kmu);
@@ -801,6 +811,8 @@ int mpcx_device_count(int* out_count) {
 static void read_env_options() {
   const char* sp = std::getenv("MPCX_SPLIT");
   if (sp) g_split = sp[0] != '0';
+  const char* nr = std::getenv("MPCX_NARROW_ROUNDS");  // percent of a main round
+  if (nr) g_narrow_rounds = std::max(0, std::min(100, std::atoi(nr))) / 100.0;
   const char* mr = std::getenv("MPCX_MID_ROUNDS");  // percent of a main round
   if (mr) g_mid_rounds = std::max(0, std::min(400, std::atoi(mr))) / 100.0;
   const char* pc = std::getenv("MPCX_PRIME_COOP");
@@ -2195,8 +2207,10 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
     pa.r1 = (uint32_t*)sv[6].ptr;
     pa.meta = (uint32_t*)sv[7].ptr;
     if (count || n_sprp) {
+      const int ks = kstat_begin(l);
       e = mpcx_launch_prime2c(&pa, l.st);
       if (e != hipSuccess) return hip_fail(e, "launch k_prime2c");
+      kstat_end(l, ks, g_devs[di], di, "prime2c", -1, 0, 0.0);  // work credited below from the survivor count
     }
   } else {
     const uint32_t blocks = pa.f_blocks + (n_sprp + 63) / 64;
@@ -2209,6 +2223,9 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
   if ((rc = d2h_sync(cnt2, dm, 8, l))) return rc;
   const uint32_t ns = cnt2[0], np = cnt2[1];
   if (ns > count || np > ns) return fail(MPCX_EHIP, "safe-prime step counters %u/%u out of range (%u)", ns, np, count);
+  if (g_prime_coop)  // Go-equivalent work: 2^(p-1) mod p per survivor, 2^d mod q per ride-along q
+    kstat_credit("prime2c", -1, (uint64_t)ns + n_sprp, (double)ns * go_macs(q_bits + 1, q_bits + 1) +
+                                                           (double)n_sprp * go_macs(q_bits, q_bits));
   if (np > max_pass) return fail(MPCX_ENOMEM, "%u Fermat passes > max_pass %u", np, max_pass);
   std::vector<uint32_t> pidx(np), pp((size_t)np * W);
   if (np) {

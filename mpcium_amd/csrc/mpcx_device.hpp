@@ -58,7 +58,7 @@
 #define MPCX_FB_PREFETCH 0  // 1: k_fixedbase loads the next table entry during the current product (measured slower)
 #endif
 #ifndef MPCX_BLOCK_FENCE
-#define MPCX_BLOCK_FENCE 0  // scheduling fence between montmul's P blocks (the prime kernels' TU sets 1)
+#define MPCX_BLOCK_FENCE 0  // scheduling fence between montmul's P blocks (1: all, 2: K >= 16; the prime kernels' TU sets 1)
 #endif
 #ifndef MPCX_MID_CARRY
 #define MPCX_MID_CARRY 0  // montmul: an extra carry pass half-way through the L iterations (not needed, see montmul)
@@ -275,12 +275,10 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
     // fold: < 2^62.8 for K <= 37. profiles/r03/kernel_ab: dropping the pass
     // took the config-2 kernel from 176.3 to 171.7 ms.
     if (MPCX_MID_CARRY && o == P / 2 - 1) carry_pass64<P, K>(acc);
-#if MPCX_BLOCK_FENCE
     // block boundary as a scheduling fence (mpcx_prime.hip: without it
     // k_prime2c's live ranges grew past its 3-wave budget and spilled; the
-    // k_modexp geometries fit better without it)
-    __builtin_amdgcn_sched_barrier(0);
-#endif
+    // k_modexp geometries fit better without it). 2: long blocks only (K >= 16).
+    if constexpr (MPCX_BLOCK_FENCE == 1 || (MPCX_BLOCK_FENCE == 2 && K >= 16)) __builtin_amdgcn_sched_barrier(0);
   }
   carry_pass64<P, K>(acc);
   // digits are now < 2^28 + 2^37: one more pass brings them to <= 2^28 + 2^10

@@ -2,7 +2,9 @@
 // DRBG, sieve, base-2 Fermat / strong tests, Miller-Rabin, strong Lucas;
 // thread per candidate), the shared-exponent window schedule (k_expsched) and
 // the device self-test.
+#ifndef MPCX_BLOCK_FENCE
 #define MPCX_BLOCK_FENCE 1  // see montmul: keeps k_prime2c within its register budget
+#endif
 #include "mpcx_device.hpp"
 
 namespace mpcx {
