@@ -36,11 +36,18 @@
 #ifndef MPCX_WPE_MULTI
 #define MPCX_WPE_MULTI MPCX_WPE
 #endif
+// the single-batch k_modexp's budget (A/B: -DMPCX_WPE_SINGLE_G1=n)
+#if MPCX_GEOM_ID == 1 && defined(MPCX_WPE_SINGLE_G1)
+#define MPCX_WPE_SINGLE MPCX_WPE_SINGLE_G1
+#endif
+#ifndef MPCX_WPE_SINGLE
+#define MPCX_WPE_SINGLE MPCX_WPE
+#endif
 
 #define MPCX_CAT2(a, b) a##b
 #define MPCX_CAT(a, b) MPCX_CAT2(a, b)
 #define MPCX_THIS_KERNEL \
-  mpcx::k_modexp<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID), MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>
+  mpcx::k_modexp<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID), MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE_SINGLE>
 
 extern "C" {
 
