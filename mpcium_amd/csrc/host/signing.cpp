@@ -647,14 +647,16 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
     r4 += c4 - c3;
   };
 
-  // Chunking: three concurrent third-wallet pipelines for 2 signers (2 ordered
-  // pairs leave the GPU idle while every chain is in a host phase; the
-  // pipelines' phases interleave), one for more signers (their 6+ chains keep
-  // the GPU busy, and smaller launches cost more GPU time): measured on MI355X,
-  // three vs two pipelines mean 6,036 vs 5,770 sigs/s over four alternating
-  // pairs, then 6,187 vs 5,766 (profiles/r02/pipe_ab/). MPCX_SIGN_PIPELINE =
-  // "chunks,workers" overrides (A/B runs).
-  size_t n_chunks = pairs.size() <= 2 ? 3 : 1, n_workers = n_chunks;
+  // Chunking: concurrent wallet pipelines whose host phases fall into each
+  // other's GPU launches. 2 signers (2 ordered pairs): three pipelines --
+  // three vs two mean 6,036 vs 5,770 sigs/s over four alternating pairs, then
+  // 6,187 vs 5,766 (profiles/r02/pipe_ab/); round 3 re-measured 6,441 vs
+  // 6,367, within the spread (profiles/r03/pipe_ab/). 3+ signers (6+ pairs):
+  // two pipelines since round 3's coalesced launches and lighter host work --
+  // 2,859 vs 2,673 sigs/s over seven runs each, t = 3.6 (profiles/r03/pipes3/,
+  // profiles/r03/pipe_ab/, profiles/r03/lanes_ab/); round 2 measured them 15%
+  // slower. MPCX_SIGN_PIPELINE = "chunks,workers" overrides (A/B runs).
+  size_t n_chunks = pairs.size() <= 2 ? 3 : 2, n_workers = n_chunks;
   if (const char* e = std::getenv("MPCX_SIGN_PIPELINE")) {
     unsigned a = 0, b = 0;
     if (std::sscanf(e, "%u,%u", &a, &b) == 2 && a > 0 && b > 0) {
