@@ -407,7 +407,10 @@ Engine::Fixed Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
   auto key = std::make_pair(m.limbs(), base.limbs());
   auto it = fixed_.find(key);
   if (it != fixed_.end() && it->second->max_bits >= need_bits) return it->second;
-  if (it != fixed_.end()) fixed_.erase(it);  // grow: rebuild for the longer exponent
+  if (it != fixed_.end()) {  // grow: rebuild for the longer exponent
+    fixed_bytes_ -= std::min(fixed_bytes_, it->second->bytes);
+    fixed_.erase(it);
+  }
   // bound the device footprint (~320 MB per 12-bit table): drop every cached
   // table past kFixedMaxBytes (handles in use keep theirs alive)
   if (fixed_bytes_ >= kFixedMaxBytes || fixed_.size() >= 256) {
@@ -424,8 +427,7 @@ Engine::Fixed Engine::fixed(const Nat& m, const Nat& base, uint32_t need_bits) {
   int rc = mpcx_fixedbase_register(md.h, bw.data(), md.class_words, bits, &f->h);
   if (rc) throw_last(rc, "mpcx_fixedbase_register");
   f->max_bits = bits;
-  size_t tb = 0;
-  if (mpcx_fixedbase_info(f->h, nullptr, &tb) == MPCX_OK) fixed_bytes_ += tb;
+  if (mpcx_fixedbase_info(f->h, nullptr, &f->bytes) == MPCX_OK) fixed_bytes_ += f->bytes;
   fixed_.emplace(key, f);
   return f;
 }

@@ -121,6 +121,7 @@ class Engine {
   struct FixedTable {
     mpcx_fb_t h = nullptr;
     uint32_t max_bits = 0;
+    size_t bytes = 0;  // device footprint (mpcx_fixedbase_info)
     ~FixedTable() {
       if (h) mpcx_fixedbase_release(h);
     }
