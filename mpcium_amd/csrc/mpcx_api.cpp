@@ -43,8 +43,8 @@
   hipError_t mpcx_launch_modexp_multi_g##g(const mpcx::ModexpArgs* segs, const uint32_t* first,      \
                                            uint32_t nsegs, uint32_t waves, hipStream_t st);          \
   hipError_t mpcx_modexp_occupancy_g##g(int* blocks_per_cu);
-#define MPCX_FOR_EACH_GEOM(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6)
-static_assert(MPCX_NUM_GEOMS == 7, "update MPCX_FOR_EACH_GEOM and build.py GEOMS");
+#define MPCX_FOR_EACH_GEOM(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
+static_assert(MPCX_NUM_GEOMS == 8, "update MPCX_FOR_EACH_GEOM and build.py GEOMS");
 extern "C" {
 MPCX_FOR_EACH_GEOM(MPCX_GEOM_DECL)
 hipError_t mpcx_launch_prime2(const mpcx::Prime2Args* a, uint32_t blocks, hipStream_t st);
@@ -821,6 +821,8 @@ static void read_env_options() {
   if (gp) g_geom_policy = std::max(0, std::min(2, std::atoi(gp)));
   const char* ln = std::getenv("MPCX_LANES");
   if (ln && g_ndev.load() == 0) g_lanes = std::max(1, std::min(kMaxLanes, std::atoi(ln)));
+  const char* g0 = std::getenv("MPCX_MAIN_GEOM0");  // main geometry of the 1024-bit class (0 or 7)
+  if (g0 && (std::atoi(g0) == 0 || std::atoi(g0) == 7)) g_main_geom[0] = std::atoi(g0);
   const char* fw = std::getenv("MPCX_FB_WINDOW");  // fixed-base comb width of new tables
   if (fw) g_fb_window = std::max(4, std::min(MPCX_FB_MAX_WINDOW_BITS, std::atoi(fw)));
 }

@@ -29,11 +29,16 @@
 //   5: 3 x 25, 21, class 1  7-lane/3-lane groups, m_i by ds_bpermute (round-1 main)
 //   6: 8 x 19,  8, class 2  mid: batches of a fraction of a main round (twice the main
 //                           geometry's wavefronts, 3 per SIMD); m_i by quad_perm + row_shr:4
-#define MPCX_NUM_GEOMS 7
-#define MPCX_GEOM_P(g) ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 16 : (g) == 4 ? 32 : (g) == 5 ? 3 : 8)
-#define MPCX_GEOM_K(g) ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 5 : (g) == 5 ? 25 : 19)
-#define MPCX_GEOM_G(g) ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 2 : (g) == 5 ? 21 : 8)
-#define MPCX_GEOM_CLASS(g) ((g) == 0 ? 0 : ((g) == 1 || (g) == 3 || (g) == 5) ? 1 : 2)
+//   7: 2 x 19, 32, class 0  lane pair per operand (the k_prime2c layout): m_i by quad_perm
+//                           [0,0,2,2]; 3 waves per SIMD instead of geometry 0's lone serial chain
+#define MPCX_NUM_GEOMS 8
+#define MPCX_GEOM_P(g) \
+  ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 16 : (g) == 4 ? 32 : (g) == 5 ? 3 : (g) == 6 ? 8 : 2)
+#define MPCX_GEOM_K(g) \
+  ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 5 : (g) == 5 ? 25 : 19)
+#define MPCX_GEOM_G(g) \
+  ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 2 : (g) == 5 ? 21 : (g) == 6 ? 8 : 32)
+#define MPCX_GEOM_CLASS(g) (((g) == 0 || (g) == 7) ? 0 : ((g) == 1 || (g) == 3 || (g) == 5) ? 1 : 2)
 #define MPCX_GEOM_L(g) (MPCX_GEOM_P(g) * MPCX_GEOM_K(g))
 // default main (throughput) and narrow geometry of each class
 #define MPCX_MAIN_GEOM(c) ((c) == 0 ? 0 : (c) == 1 ? 1 : 2)

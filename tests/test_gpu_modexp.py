@@ -145,12 +145,13 @@ def test_exp_mul_and_mulmod(gpu, paillier_key):
         mod.release()
 
 
-@pytest.mark.parametrize("geom", [1, 2, 3, 4, 5, 6])
+@pytest.mark.parametrize("geom", [1, 2, 3, 4, 5, 6, 7])
 def test_each_geometry_forced(gpu, paillier_key, geom):
     """Every geometry of the 2048-bit (1, 3, 5) and 4096-bit (2, 4, 6) classes:
-    quad-per-operand main, narrow, and the 3/7-lane-group (bpermute) layouts."""
+    quad-per-operand main, narrow, and the 3/7-lane-group (bpermute) layouts;
+    and the 1024-bit class's lane-pair geometry 7 (modulus P)."""
     N = paillier_key["N"]
-    m = N * N if geom in (2, 4, 6) else N
+    m = N * N if geom in (2, 4, 6) else paillier_key["P"] if geom == 7 else N
     rng = random.Random(geom)
     gpu.set_option("force_geom", geom)
     try:
