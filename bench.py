@@ -385,17 +385,18 @@ def cpu_baseline_paillier(N: int, seconds: float, info: dict):
             **info}
 
 
-def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict):
+def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: int = 1, rank: int = 0):
     """Config 1 (BASELINE.json): tss-lib paillier Encrypt + HomoMult over a
     batch of `batch` ops, 2048-bit N, through the host mirror of
     crypto/paillier (libmpcx_host.so -> libmpcx.so; host buffers, so the rate
-    includes PCIe and the Python<->words conversion)."""
+    includes PCIe and the Python<->words conversion). world > 1: every rank
+    runs its own batches (weak scaling); value = all ranks' ops / max time."""
     import random
     from mpcium_amd import host as mhost
     from oracle import gomath as gm
     mhost.init(gpu_index())
     pk = mhost.PublicKey(N)
-    rng = random.Random(0x6D706331)
+    rng = random.Random(0x6D706331 + 7919 * rank)
     Q = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
     ms = [rng.randrange(N) for _ in range(batch)]
     rs = [rng.randrange(1, N) for _ in range(batch)]
@@ -408,14 +409,20 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict):
         if cs[i] != gm.paillier_encrypt(N, ms[i], rs[i]) or out[i] != gm.paillier_homo_mult(N, bs[i], cs[i]):
             raise SystemExit(f"paillier line: mismatch at {i}")
     _kernel_stats_reset()
+    if world > 1:
+        import torch.distributed as dist
+        from mpcium_amd.shard import max_over_ranks
+        dist.barrier()
     t0 = time.perf_counter()
     for _ in range(reps):
         cs, _ = pk.encrypt(ms, rs)
         pk.homo_mult(bs, cs)
     el = time.perf_counter() - t0
+    if world > 1:
+        el = max_over_ranks([el], world)[0]
     line = {"metric": "tss-lib paillier Encrypt+HomoMult ops/s (config 1: batch of 1024 ops, 2048-bit N)",
-            "value": batch * reps / el, "unit": "Encrypt+HomoMult ops/s", "batch": batch, "reps": reps,
-            "seconds": el, "n_gpus": 1,
+            "value": batch * reps * world / el, "unit": "Encrypt+HomoMult ops/s", "batch": batch, "reps": reps,
+            "seconds": el, "n_gpus": world, "scaling": "weak",
             "note": "host-buffer API end to end (Python ints -> words -> PCIe -> GPU -> back); Encrypt's Gamma^m "
                     "is the bit-exact 1 + mN shortcut, r^N a shared-exponent GPU batch, c^b per-operand",
             "cpu_baseline": None}
@@ -424,7 +431,7 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict):
     L2 = 2 * 128 * 128
     alg = sum((2048 + 512) * L2 + (b.bit_length() + (b.bit_length() + 3) // 4) * L2 for b in bs) * reps
     line["roofline"] = _kernel_roofline()
-    line["job_roofline"] = _job_roofline(alg, el)
+    line["job_roofline"] = _job_roofline(alg, el, world)
     line["job_roofline"]["scope"] = "end to end (host buffers, Python conversions); batch of 1,024 = latency-bound"
     line["alg_ops_per_op"] = alg / (batch * reps)
     if cpu:
@@ -503,7 +510,7 @@ def safeprime_line(num: int, seed: int, cpu: bool, info: dict, world: int = 1, r
             "sieved_out": st["sieved_out"], "fermat_tests": st["fermat_tests"], "mr_tests": st["mr_tests"],
             "lucas_tests": st.get("lucas_tests", 0),
             "n_gpus": world, "scaling": "strong", "first_index": res[0][2], "last_index": res[-1][2],
-            "roofline": _job_roofline((st["fermat_tests"] + st["mr_tests"]) * alg_macs(1024, 1023), el, world),
+            "roofline": _job_roofline((st["fermat_tests"] + st["mr_tests"]) * alg_macs(1024, 1023) / world, el, world),
             "cpu_baseline": None}
     if world == 1:
         # the dominant kernel's own roofline: k_prime2c's Go-equivalent work
@@ -658,12 +665,14 @@ def cpu_baseline_keygen(seconds: float, info: dict, parties: int):
                       f"Jacobi symbols run in Python); one_core = 1 / CPU-s per session"}
 
 
-def keygen_line(args):
+def keygen_line(args, world: int = 1, rank: int = 0):
     """Config 5 (BASELINE.json): keygen / reshare proof work under load --
     every party of every session proves DLN x2 + Mod + Fac per peer and
     verifies all peers' proofs (csrc/host/keygenload.hpp), 5 parties (3-of-5),
     on one GPU. Parties: the 3 fixture nodes plus 2 generated here by the GPU
-    GeneratePreParams (untimed)."""
+    GeneratePreParams (untimed). world > 1: every rank runs its own
+    `keygen_sessions` sessions (weak scaling); value = all ranks' sessions /
+    max time."""
     from mpcium_amd import host as mhost
     from mpcium_amd import proofs as mproofs
     mhost.init(gpu_index())
@@ -682,21 +691,28 @@ def keygen_line(args):
     import resource
     rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
     _kernel_stats_reset()
-    st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67, wave=wave)
+    if world > 1:
+        import torch.distributed as dist
+        from mpcium_amd.shard import max_over_ranks
+        dist.barrier()
+    st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67 + 7919 * rank, wave=wave)
     rss1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
     if st["failures"]:
-        raise SystemExit(f"keygen proofs: {st}")
+        raise SystemExit(f"rank {rank}: keygen proofs: {st}")
+    total_s = st["total_s"]
+    if world > 1:
+        total_s = max_over_ranks([total_s], world)[0]
     line = {"metric": f"{len(parties)}-party keygen/reshare sessions/s (config 5: DLN x2 + Mod + Fac proofs per party, "
                       f"every peer verified, {args.keygen_sessions} sessions)",
-            "value": st["sessions"] / st["total_s"], "unit": "sessions/s", "n_gpus": 1,
+            "value": st["sessions"] * world / total_s, "unit": "sessions/s", "n_gpus": world, "scaling": "weak",
             "sessions": int(st["sessions"]), "parties": len(parties), "proofs": int(st["proofs"]),
             "verifications": int(st["verifications"]), "seconds": st["total_s"], "prove_s": st["prove_s"],
             "verify_s": st["verify_s"], "engine_busy_s": st["engine_busy_s"],
             "waves": int(st["waves"]), "wave_sessions": int(st["wave_sessions"]), "max_wave_s": st["max_wave_s"],
             "host_max_rss_mb": rss1 / 1024.0, "host_max_rss_mb_before": rss0 / 1024.0,
-            "verifications_per_s": st["verifications"] / st["total_s"], "checked": "every verification passes",
+            "verifications_per_s": st["verifications"] * world / total_s, "checked": "every verification passes",
             "roofline": _kernel_roofline(),
-            "job_roofline": _job_roofline(st["alg_macs"], st["total_s"]),
+            "job_roofline": _job_roofline(st["alg_macs"], total_s, world),
             "cpu_baseline": None}
     return line
 
@@ -850,6 +866,85 @@ def signing_line(args, world, rank, signers: int):
     return line
 
 
+LINE_MAX_BYTES = 4096  # the driver keeps a bounded tail of stdout: the result line must fit in it whole
+
+# sub-line key of the detail dict -> short key in the printed line
+_SUBLINES = (("paillier_batch", "c1_paillier"), ("safe_prime", "c3_safe_primes"), ("signing", "c4_sign"),
+             ("signing_3_signers", "c4_sign_3_signers"), ("keygen", "c5_keygen"))
+
+
+def _r(x, nd=4):
+    """Round a float to `nd` significant digits (None passes through)."""
+    if x is None or not isinstance(x, float):
+        return x
+    return float(f"{x:.{nd}g}")
+
+
+def compact_line(result: dict, detail_path: str | None) -> dict:
+    """The ONE line bench.py prints: the contract keys, the headline roofline
+    and cpu_baseline, and per config {value, unit, frac, cpu, cores}. Every
+    other field (per-step times, telemetry, per-kernel lists, samples, notes,
+    host profiles) stays in the detail file the line names. Guaranteed to
+    serialise to at most LINE_MAX_BYTES (tests/test_bench_line.py)."""
+    keep = ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype")
+    line = {k: _r(result.get(k), 6) for k in keep}
+    line["data"] = "synthetic (seeded bases < N^2; N = tests/golden/paillier_key_2048.json)"
+    c = result.get("config") or {}
+    line["config"] = {k: c.get(k) for k in ("workload", "operands_per_gpu", "modulus_bits", "exp_bits",
+                                             "parallelism") if k in c}
+    r = result.get("roofline") or {}
+    line["roofline"] = {"bound": r.get("bound"), "achieved": _r(r.get("achieved")), "peak": _r(r.get("peak")),
+                        "unit": r.get("unit"), "frac": _r(r.get("frac")), "traffic": r.get("traffic"),
+                        "kernel_ms": _r(r.get("kernel_ms"), 5)}
+    if r.get("frac_at_measured_clock") is not None:
+        line["roofline"]["frac_at_clock"] = _r(r["frac_at_measured_clock"])
+    cb = result.get("cpu_baseline")
+    line["cpu_baseline"] = None if not cb else {
+        "value": _r(cb.get("value")), "unit": cb.get("unit"), "cores": cb.get("cores"), "kind": cb.get("kind"),
+        "sample": "Go expNNMontgomery restated in C (64-bit Words), x^N mod N^2 on the host's usable threads"}
+    dg = result.get("batch_digest")
+    if dg is not None:
+        line["digest_match"] = bool(dg.get("match"))
+    cfg = {}
+    po = result.get("config2_per_operand_exponents") or []
+    for s in po:
+        cfg[f"c2_per_op_{s['exp_bits']}"] = {"value": _r(s.get("value")), "unit": s.get("unit"),
+                                             "frac": _r((s.get("roofline") or {}).get("frac"), 3)}
+    for src, dst in _SUBLINES:
+        s = result.get(src)
+        if not s:
+            continue
+        fr = (s.get("kernel_roofline") or s.get("roofline") or {}).get("frac")
+        sb = s.get("cpu_baseline") or {}
+        cpu = sb.get("safe_primes_per_s_equiv", sb.get("value"))  # config 3: in the line's own unit
+        cfg[dst] = {"value": _r(s.get("value")), "unit": s.get("unit"), "n_gpus": s.get("n_gpus"),
+                    "frac": _r(fr, 3), "cpu": _r(cpu), "cores": sb.get("cores")}
+    line["configs"] = cfg
+    line["detail"] = detail_path
+    # last resort: never exceed the driver's tail (drop the configs, which are in the detail file)
+    if len(json.dumps(line)) > LINE_MAX_BYTES:
+        line["configs"] = {k: {"value": v["value"], "unit": v["unit"]} for k, v in cfg.items()}
+    if len(json.dumps(line)) > LINE_MAX_BYTES:
+        line.pop("configs")
+    return line
+
+
+def relaunch_under_torchrun(args, argv) -> int:
+    """--gpus N > 1 without a launcher: start torchrun with N local ranks as a
+    CHILD process (nothing in this process has touched the GPU yet) and return
+    its exit code; rank 0 of the child prints the line."""
+    import socket
+    import subprocess
+    with socket.socket() as s:  # a free port on the loopback interface
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    print(f"[bench] --gpus {args.gpus} without WORLD_SIZE: running {' '.join(cmd)}", file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -877,7 +972,14 @@ def main():
                     help="config 3: 1024-bit safe primes to find (256: steady state, ~4 steps per GPU at N = 8)")
     ap.add_argument("--modbits", type=int, default=4096, choices=(2048, 4096),
                     help="4096: x^N mod N^2 (config 2, the bench line); 2048: x^N mod N (Paillier N / N~ class)")
+    ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
+                    help="file for the full result (per-step times, telemetry, per-kernel lists, samples); "
+                         "the printed line names it")
     args = ap.parse_args()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(relaunch_under_torchrun(args, sys.argv[1:]))
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={os.environ.get('WORLD_SIZE')} but --gpus {args.gpus}")
     # progress lines on stderr (stdout carries the one JSON line): phases
     # here, keygen waves from the C++ driver
     os.environ.setdefault("MPCX_PROGRESS", "1")
@@ -1129,16 +1231,19 @@ def main():
     if args.extra_lines:
         cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
         progress("config 1 and 3: Paillier batch, safe primes")
-        if world == 1:
-            result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, info)
+        result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, info, world, rank)
         result["safe_prime"] = safeprime_line(args.safe_primes, 0x5AFE, cpu, info, world, rank)
-    if args.keygen_sessions > 0 and world == 1:
-        progress(f"config 5: keygen/reshare proofs, {args.keygen_sessions} sessions")
-        result["keygen"] = keygen_line(args)
+    if args.keygen_sessions > 0:
+        progress(f"config 5: keygen/reshare proofs, {args.keygen_sessions} sessions per GPU")
+        result["keygen"] = keygen_line(args, world, rank)
         result["keygen"]["cpu_baseline"] = keygen_cpu
     progress("done")
     if rank == 0:
-        print(json.dumps(result), flush=True)
+        detail = os.path.abspath(args.detail)
+        os.makedirs(os.path.dirname(detail), exist_ok=True)
+        with open(detail, "w") as f:
+            json.dump(result, f, indent=1)
+        print(json.dumps(compact_line(result, os.path.relpath(detail, ROOT))), flush=True)
     if world > 1:
         dist.destroy_process_group()
 

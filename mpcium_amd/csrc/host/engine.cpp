@@ -227,10 +227,24 @@ class Coalescer {
         }
         ++inflight_;
         lk.unlock();
-        std::vector<mpcx_modexp_group_t> gs;
-        for (Req* b : batch) gs.push_back(b->g);
-        const int rc = mpcx_modexp_multi_batch((uint32_t)gs.size(), gs.data());
-        const std::string err = rc ? mpcx_last_error() : std::string();
+        // whatever happens in the launch, every member of the batch gets an
+        // rc and done, and inflight_ drops again (a throw here would
+        // otherwise leave the followers waiting forever)
+        int rc = MPCX_OK;
+        std::string err;
+        try {
+          std::vector<mpcx_modexp_group_t> gs;
+          gs.reserve(batch.size());
+          for (Req* b : batch) gs.push_back(b->g);
+          rc = mpcx_modexp_multi_batch((uint32_t)gs.size(), gs.data());
+          if (rc) err = mpcx_last_error();
+        } catch (const std::bad_alloc&) {
+          rc = MPCX_ENOMEM;
+          err = "host allocation failed in a coalesced launch";
+        } catch (const std::exception& ex) {
+          rc = MPCX_EHIP;
+          err = std::string("coalesced launch: ") + ex.what();
+        }
         lk.lock();
         --inflight_;
         for (Req* b : batch) {

@@ -104,6 +104,7 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
   std::atomic<uint64_t> fails{0};
   std::mutex tm;
   double last_prove = 0, max_wave = 0;
+  size_t waves_done = 0;  // under tm
   // lane budget of this workload (MPCX_KEYGEN_LANES, default 8: its many small
   // independent chains overlap better; measured +10-15% over 4), restored after
   const char* kl = std::getenv("MPCX_KEYGEN_LANES");
@@ -217,13 +218,15 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
     }
     std::lock_guard<std::mutex> lk(tm);
     max_wave = std::max(max_wave, now() - w0);
-    // MPCX_PROGRESS=1: one line per finished wave on stderr (long runs are
-    // otherwise silent for minutes)
+    // MPCX_PROGRESS=1: a line on stderr every 10 finished waves and at the end
+    // (long runs are otherwise silent for minutes)
     static const bool progress = [] {
       const char* e = std::getenv("MPCX_PROGRESS");
       return e && e[0] == '1';
     }();
-    if (progress) std::fprintf(stderr, "[keygenload] wave %zu/%zu done (%.1f s)\n", w + 1, n_waves, now() - w0);
+    const size_t finished = ++waves_done;
+    if (progress && (finished % 10 == 0 || finished == n_waves))
+      std::fprintf(stderr, "[keygenload] %zu/%zu waves done (last %.1f s)\n", finished, n_waves, now() - w0);
   };
 
   Engine::get().reset_busy();

@@ -421,7 +421,10 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
           Signer& s = at(x, i);
           for (size_t pj = 0, j = 0; j < S; ++j) {
             if (j == i) continue;
-            if (!secp::Equal(r5[(x * S + i) * (P + 1) + pj], at(x, j).a4) || at(x, j).t4.is_zero()) s.ok = false;
+            // tss-lib's ZKProof.Verify fails when alpha + cX is the point at
+            // infinity; with tG - cX == alpha that is t = 0 mod q
+            if (!secp::Equal(r5[(x * S + i) * (P + 1) + pj], at(x, j).a4) || (at(x, j).t4 % q).is_zero())
+              s.ok = false;
             ++pj;
           }
           s.R = r5[(x * S + i) * (P + 1) + P];
@@ -531,7 +534,12 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
             if (j == i) continue;
             const Signer& o = at(x, j);
             const size_t e = (x * S + i) * P + pj;
-            if (!secp::Equal(r7[base + 2 * pj], o.aA) || !secp::Equal(r7[base + 2 * pj + 1], o.aV) || o.tA.is_zero())
+            // ZKProof: alpha + cA = infinity iff tA = 0 mod q (as in round 5).
+            // ZKVProof: tss-lib fails when tR + uG is infinity; without the
+            // discrete log of R (nobody knows k) that takes tV = uV = 0 mod q
+            // (alpha = -cV otherwise needs a fixed point of the challenge hash)
+            if (!secp::Equal(r7[base + 2 * pj], o.aA) || !secp::Equal(r7[base + 2 * pj + 1], o.aV) ||
+                (o.tA % q).is_zero() || ((o.tV % q).is_zero() && (o.uV % q).is_zero()))
               s.ok = false;
             V = secp::Add(V, Vj[e]);
             A = secp::Add(A, Aj[e]);

@@ -416,9 +416,13 @@ def exp_batch(m: int, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> 
         mod.release()
 
 
+SECP_N = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141  # secp256k1 group order
+
+
 def ec_combine_batch(items) -> list:
     """secp256k1 a G + b P + c Q per item (a, b, c, P, Q), points as (x, y)
-    tuples or None (infinity) -> list of (x, y) or None."""
+    tuples or None (infinity) -> list of (x, y) or None. Scalars are any
+    integers, taken mod the group order n (as the C++ CombineBatch does)."""
     n = len(items)
     if n == 0:
         return []
@@ -426,7 +430,8 @@ def ec_combine_batch(items) -> list:
     pt = np.zeros((n, 32), dtype="<u4")
     mask = (1 << 256) - 1
     for i, (a, b, c, P, Q) in enumerate(items):
-        sc[i] = int_to_words((a & mask) | ((b & mask) << 256) | ((c & mask) << 512), 24)
+        a, b, c = a % SECP_N, b % SECP_N, c % SECP_N
+        sc[i] = int_to_words(a | (b << 256) | (c << 512), 24)
         px = (P[0] | (P[1] << 256)) if P is not None else 0
         qx = (Q[0] | (Q[1] << 256)) if Q is not None else 0
         pt[i] = int_to_words(px | (qx << 512), 32)

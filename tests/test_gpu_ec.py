@@ -74,6 +74,8 @@ def test_edge_cases(mx):
         (5, 0, 7, None, P),               # only Q
         (5, 9, 7, P, None),               # Q infinite with c != 0
         (0, 2 ** 255 + 3, 1, G, G),
+        (2 ** 256 + 7, 0, 0, None, None),  # scalars >= 2^256 and negative: mod n
+        (-5, 2 ** 300 + 1, -(2 ** 260), P, G),
     ]
     got = mx.ec_combine_batch(items)
     assert got == [ref(*it) for it in items]

@@ -93,6 +93,40 @@ def test_paillier_random_roundtrip(host, paillier_key):
     assert dm == ms
 
 
+def test_config1_full_batch_matches_c_oracle(host, paillier_key):
+    """BASELINE config 1 at its stated size: one batch of 1,024 Encrypt +
+    HomoMult ops (the bench's paillier line: m < N, r < N, b < q) through
+    crypto/paillier's host mirror, EVERY output compared with tss-lib's
+    formulas evaluated by the C restatement of Go's expNN (Gamma^m as a full
+    Exp, as tss-lib computes it, not the GPU's 1 + mN shortcut)."""
+    from concurrent.futures import ThreadPoolExecutor
+    from oracle import crosscheck as cc
+    lib = cc.load_c_oracle(64)
+    if lib is None:
+        pytest.skip("oracle/libgomodexp64.so not built")
+    N = paillier_key["N"]
+    N2 = N * N
+    pk = host.PublicKey(N)
+    rng = random.Random(0x6D706331)  # bench.py paillier_line's draws
+    n = 1024
+    ms = [rng.randrange(N) for _ in range(n)]
+    rs = [rng.randrange(1, N) for _ in range(n)]
+    bs = [rng.randrange(gm.SECP256K1_N) for _ in range(n)]
+    cs, err = pk.encrypt(ms, rs)
+    assert err == [0] * n
+    hm, err = pk.homo_mult(bs, cs)
+    assert err == [0] * n
+
+    def want(i):
+        c = cc.c_expnn(lib, N + 1, ms[i], N2) * cc.c_expnn(lib, rs[i], N, N2) % N2
+        return c, cc.c_expnn(lib, c, bs[i], N2)
+
+    with ThreadPoolExecutor(8) as ex:  # ctypes releases the GIL
+        ref = list(ex.map(want, range(n)))
+    assert cs == [c for c, _ in ref]
+    assert hm == [h for _, h in ref]
+
+
 def test_safe_primes_match_oracle_stream(host):
     for v in load_golden("safeprime_vectors.json")["primes"]:
         got, stats = host.safe_primes(v["bits"], 1, seed=v["seed"])

@@ -50,11 +50,12 @@ def fast_exp():
     M._pw = old
 
 
-@pytest.mark.parametrize("signers,wallets,trace", [(2, 10000, 6), (3, 1000, 3)])
+@pytest.mark.parametrize("signers,wallets,trace", [(2, 10000, 6), (3, 10000, 6)])
 def test_signing_wallets_match_oracle(drv, nodes, fast_exp, signers, wallets, trace):
-    """Config 4 at its stated size for 2 signers (10,000 wallets, three
-    concurrent wallet pipelines by default): traced wallets are spread over the
-    batch, so every pipeline's sessions are compared with the oracle."""
+    """Config 4 at its stated size, 10,000 wallets, for 2 signers (three
+    concurrent wallet pipelines by default) and 3 signers (mpcium's default,
+    every ready peer; two pipelines): traced wallets are spread over the batch,
+    so every pipeline's sessions are compared with the oracle."""
     seed = 0x516E + signers
     st, tr = drv.bench_signing(nodes, signers, wallets, seed=seed, trace_wallets=trace)
     assert st["errors"] == 0 and st["relation_failures"] == 0
@@ -64,6 +65,8 @@ def test_signing_wallets_match_oracle(drv, nodes, fast_exp, signers, wallets, tr
     assert tr["wallets"] == [t * wallets // trace for t in range(trace)]
     if signers == 2:  # one traced wallet in each third (the default pipelines' chunks)
         assert {wi * 3 // wallets for wi in tr["wallets"]} == {0, 1, 2}
+    else:  # and in each half
+        assert {wi * 2 // wallets for wi in tr["wallets"]} == {0, 1}
     assert st["aborted"] == 0
     for t, wi in enumerate(tr["wallets"]):
         pairs, sig, ok, gg18 = S.sign_wallet(nodes, signers, seed, wi)
@@ -136,3 +139,30 @@ def test_keygen_reshare_waves_match_oracle(five_parties):
     assert st1["failures"] == 0 and st1["waves"] == 1
     assert tr1[0]["session"] == tr[0]["session"] == 0
     assert tr1[0]["digests"] == tr[0]["digests"]
+
+
+def test_keygen_bench_wave_size_matches_oracle(five_parties):
+    """Config 5 at the bench's wave size: one wave of 1,024 concurrent
+    sessions (bench.py keygen_line's default), every proof of every session
+    verified by every peer, and the wave's traced session recomputed by the
+    oracle proof by proof."""
+    from mpcium_amd import proofs as mproofs
+    from oracle import keygen_ref as KR
+    from oracle import proofs_ref as PR
+    lib = cc.load_c_oracle(64)
+    if lib is None:
+        pytest.skip("oracle/libgomodexp64.so not built")
+    n, sessions, seed = 5, 1024, 0x6B6A
+    st, tr = mproofs.bench_keygen_proofs(five_parties, sessions, seed=seed, wave=sessions, trace=True)
+    assert st["failures"] == 0
+    assert st["waves"] == 1 and st["wave_sessions"] == sessions
+    assert st["verifications"] == sessions * n * (n - 1) * 4
+    (t,) = tr
+    old = PR._pw
+    PR._pw = lambda x, y, m: cc.c_expnn(lib, x % m, y, m)
+    try:
+        want, passed = KR.session_digests(five_parties, seed, t["session"])
+    finally:
+        PR._pw = old
+    assert t["digests"] == want, t["session"]
+    assert t["verified"] == passed == n * (n - 1) * 4

@@ -43,26 +43,26 @@ suite)
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.txt 2>&1 || { tail $O/smoke.txt; exit 1; }
   tail -2 $O/smoke.txt ;;
 bench)
-  timeout -k 10 900 python3 bench.py "$@" > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
-  summ $O/bench.json ;;
+  timeout -k 10 900 python3 bench.py --detail $O/bench_detail.json "$@" > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+  wc -c $O/bench.json; summ $O/bench_detail.json ;;
 trace)
-  timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py "$@" \
-      > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
-  summ $O/bench.json
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o bench -- python3 bench.py \
+      --detail $O/bench_detail.json "$@" > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; }
+  summ $O/bench_detail.json
   f=$(find $O/prof -name '*kernel_trace.csv' | head -1)
   python3 tools/trace_segments.py $f > $O/trace_segments.txt && head -60 $O/trace_segments.txt
   find $O/prof -name '*kernel_stats*' -exec cp {} $O/kernel_stats.csv \; ;;
 pmc)
   ctr=$1; shift
-  timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $O/prof -o pmc -- python3 bench.py "$@" \
+  timeout -s KILL 300 rocprofv3 --pmc $ctr --output-format csv -d $O/prof -o pmc -- python3 bench.py --detail $O/bench_detail.json "$@" \
       > $O/bench.json 2> $O/bench.err || { tail $O/bench.err; exit 1; } ;;
 ab)
   n=$1; la=$2; lb=$3; shift 3
   for i in $(seq 1 $n); do
     for lib in $la $lb; do
       [ $lib = $la ] && tag=A_$i || tag=B_$i
-      MPCX_LIB_PATH=$(realpath $lib) timeout -k 10 300 python3 bench.py "$@" > $O/ab_$tag.json 2> $O/ab_$tag.err \
-          || { tail $O/ab_$tag.err; exit 1; }
+      MPCX_LIB_PATH=$(realpath $lib) timeout -k 10 300 python3 bench.py --detail $O/ab_$tag.json "$@" > $O/ab_$tag.line \
+          2> $O/ab_$tag.err || { tail $O/ab_$tag.err; exit 1; }
       echo -n "$lib run $i: "; summ $O/ab_$tag.json short
     done
   done ;;
@@ -75,7 +75,7 @@ abswap)
     for lib in $la $lb; do
       [ $lib = $la ] && tag=A_$i || tag=B_$i
       cp $lib mpcium_amd/libmpcx.so.tmp && mv mpcium_amd/libmpcx.so.tmp mpcium_amd/libmpcx.so
-      timeout -k 10 600 python3 bench.py "$@" > $O/ab_$tag.json 2> $O/ab_$tag.err
+      timeout -k 10 600 python3 bench.py --detail $O/ab_$tag.json "$@" > $O/ab_$tag.line 2> $O/ab_$tag.err
       rc=$?
       cp $O/orig_libmpcx.so mpcium_amd/libmpcx.so
       [ $rc -eq 0 ] || { tail $O/ab_$tag.err; exit 1; }
@@ -92,7 +92,7 @@ abn)
     for lib in ${libs//,/ }; do
       k=$((k+1)); tag=L${k}_$i
       cp $lib mpcium_amd/libmpcx.so.tmp && mv mpcium_amd/libmpcx.so.tmp mpcium_amd/libmpcx.so
-      timeout -k 10 600 python3 bench.py "$@" > $O/ab_$tag.json 2> $O/ab_$tag.err
+      timeout -k 10 600 python3 bench.py --detail $O/ab_$tag.json "$@" > $O/ab_$tag.line 2> $O/ab_$tag.err
       rc=$?
       cp $O/orig_libmpcx.so mpcium_amd/libmpcx.so
       [ $rc -eq 0 ] || { tail $O/ab_$tag.err; exit 1; }
@@ -105,7 +105,7 @@ envab)
   for i in $(seq 1 $n); do
     for e in A B; do
       [ $e = A ] && ev="$ea" || ev="$eb"
-      env $ev timeout -k 10 600 python3 bench.py "$@" > $O/ab_${e}_$i.json 2> $O/ab_${e}_$i.err \
+      env $ev timeout -k 10 600 python3 bench.py --detail $O/ab_${e}_$i.json "$@" > $O/ab_${e}_$i.line 2> $O/ab_${e}_$i.err \
           || { tail $O/ab_${e}_$i.err; exit 1; }
       echo "== $e ($ev) run $i"; summ $O/ab_${e}_$i.json
     done
