@@ -1040,7 +1040,7 @@ def main():
     N = load_key()
     N2 = N * N if args.modbits == 4096 else N  # the modulus
     mod = mpcx.Modulus(N2)
-    words = mod.class_words  # 128 for the 4096-bit class
+    words = mod.words  # 128 for N^2; 64 for a 2048-bit N (operands below the lane-pair geometry's R)
     count = args.count
     bases = synth_bases(N2, count, 0x6D706332 + rank, words)
     exp = mpcx.int_to_words(N, mpcx.nwords(N))

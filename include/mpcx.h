@@ -326,6 +326,27 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
                              const uint32_t* muls, uint32_t mul_words,
                              uint32_t* out, uint32_t out_words);
 
+/* Several comb batches in ONE launch (kernel k_fixedbase_multi): each group is
+ * exactly one mpcx_fixedbase_exp_batch call (its own tables -- any moduli of
+ * one size class --, exponents, multipliers, output). Concurrent callers'
+ * batches (h1, h2 of every peer's N~ in every wallet pipeline) become the
+ * segments of one launch that fills the GPU, instead of many launches of a
+ * fraction of a resident round each (the replaced surface is the same
+ * common.ModInt.Exp on h1/h2, up:crypto/mta/range_proof.go). Synchronous. */
+#define MPCX_FB_MAX_BASES 2
+typedef struct {
+  uint32_t nbases;                          /* 1 or 2 tables of one modulus */
+  mpcx_fb_t fbs[MPCX_FB_MAX_BASES];
+  uint32_t count;
+  const uint32_t* exps[MPCX_FB_MAX_BASES];  /* count x exp_words[t] words */
+  uint32_t exp_words[MPCX_FB_MAX_BASES];
+  const uint32_t* muls;                     /* NULL: no multiplier */
+  uint32_t mul_words;
+  uint32_t* out;
+  uint32_t out_words;
+} mpcx_fixedbase_group_t;
+int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* groups);
+
 /* Device memory helpers for callers without their own HIP allocator. */
 int mpcx_dev_alloc(size_t bytes, void** out_ptr);
 int mpcx_dev_free(void* ptr);
@@ -342,43 +363,44 @@ int mpcx_stream_sync(void* stream);
 /* SURVEY.md 8(b) name of mpcx_stream_sync. */
 int mpcx_sync(void* stream);
 
-/* Tuning knobs (process-wide):
- *   "split"      0 (default) / 1: run the partial last round of resident
- *                wavefronts of a large batch in the class's narrow geometry
- *                (more lanes per operand, shorter wavefronts). Batches under
- *                "narrow_rounds"/100 of a round always use the narrow geometry.
- *   "narrow_rounds" 0..100 (default 15): that threshold, in hundredths of a
- *                round of resident wavefronts in the main geometry.
- *   "force_geom" -1 (default) or a geometry id (0..6, see mpcx_internal.h) to
- *                run every batch of the matching class in that geometry.
- *   "main_geom"  geometry id: make it the main (throughput) geometry of its
- *                class (A/B of kernel layouts).
- *   "sched_width" 0..6 (default 6): cap on the sliding-window width used for
- *                shared exponents; 0 selects Go's 4-bit fixed window.
- *   "device_split_min" operands (default 4096): smallest per-device slice
- *                of a host-buffer batch split across the bound devices
- *                (0: never split).
+/* Tuning knobs (process-wide). Every default is the winner of a measured,
+ * interleaved A/B on MI355X (DESIGN.md section 6 cites each):
+ *   "narrow_rounds" 0..100 (default 15): batches under this many hundredths of
+ *                a resident round of the main geometry run in the class's
+ *                narrow geometry (3 was slower for signing, profiles/r03/narrow_ab).
  *   "geom_policy" 1 (default): 4096-bit batches pick the main, mid (8 x 19)
  *                or narrow geometry by a measured launch-time model of
- *                wavefronts per SIMD; 0: the "narrow_rounds" / "mid_rounds"
- *                thresholds only; 2: every batch in its class's main geometry.
- *   "duplicate_device" 0 (default) / 1 (test hook): mpcx_init of an already
- *                bound ordinal binds it again as another logical device (own
- *                lanes, constants, workspaces), so the multi-device split and
- *                gather run concurrently on a one-GPU box.
- *   "kernel_stats" 0 (default) / 1: time every batch-entry-point launch
- *                with an event pair for mpcx_kernel_stats.
- *   "mid_rounds" 0..400 (default 0): with geom_policy 0, 4096-bit batches
- *                under mid_rounds/100 of a main round run in the mid geometry.
+ *                wavefronts per SIMD; 0: the "narrow_rounds" threshold only;
+ *                2: every batch in its class's main geometry.
+ *   "main_geom"  geometry id: make it the main (throughput) geometry of its
+ *                class (A/B of kernel layouts: 5 vs 1 for the 2048-bit class).
+ *   "sched_width" 0..6 (default 6): cap on the sliding-window width used for
+ *                shared exponents; 0 selects Go's 4-bit fixed window.
  *   "fixed_window" 4 or 5 (default 5): widest fixed window for per-operand
  *                exponents (5 bits above 1024-bit exponents, else Go's 4).
+ *   "fb_window"  4..12 (default 12): window width of comb tables registered
+ *                from now on.
  *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
  *                thread per candidate.
  *   "lanes"      1..8 (default 6, or MPCX_LANES): execution lanes (streams
  *                with their own workspaces) per device used from now on.
+ *   "device_split_min" operands (default 4096): smallest per-device slice
+ *                of a host-buffer batch split across the bound devices
+ *                (0: never split).
+ * Test and measurement hooks:
+ *   "force_geom" -1 (default) or a geometry id (0..6, see mpcx_internal.h) to
+ *                run every batch of the matching class in that geometry (a
+ *                geometry that cannot serve a modulus or its operands falls
+ *                back to the class's full-width geometry).
+ *   "duplicate_device" 0 (default) / 1: mpcx_init of an already bound
+ *                ordinal binds it again as another logical device (own lanes,
+ *                constants, workspaces), so the multi-device split and gather
+ *                run concurrently on a one-GPU box.
+ *   "kernel_stats" 0 (default) / 1: time every batch-entry-point launch
+ *                with an event pair for mpcx_kernel_stats.
  * Environment, read at mpcx_init / mpcx_init_devices: MPCX_LANES (1..8,
- * default 6: execution lanes per device), MPCX_GEOM_POLICY, MPCX_MID_ROUNDS,
- * MPCX_SPLIT. */
+ * default 6: execution lanes per device), MPCX_GEOM_POLICY, MPCX_NARROW_ROUNDS,
+ * MPCX_PRIME_COOP, MPCX_FB_WINDOW. */
 int mpcx_set_option(const char* key, int value);
 
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):

@@ -16,7 +16,7 @@ CSRC = os.path.join(HERE, "csrc")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 ARCH = "gfx950"
 
-NUM_GEOMS = 8  # kernel geometries (mpcx_internal.h), one translation unit each
+NUM_GEOMS = 7  # kernel geometries (mpcx_internal.h), one translation unit each
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
 KERNEL_HDRS = ["mpcx_device.hpp", "mpcx_internal.h"]
 HOST_SRCS = ["host/bignum.cpp", "host/engine.cpp", "host/modint.cpp", "host/paillier.cpp", "host/safeprime.cpp",

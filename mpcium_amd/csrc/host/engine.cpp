@@ -197,10 +197,11 @@ namespace {
 // mpcx_modexp_multi_batch launch; the others wait for their results. Under
 // load the GPU thus receives few large launches (the main geometry's
 // throughput) instead of many narrow ones; alone, a call dispatches at once.
-class Coalescer {
+template <class Group, int (*Launch)(uint32_t, const Group*)>
+class CoalescerT {
  public:
   struct Req {
-    mpcx_modexp_group_t g{};
+    Group g{};
     bool taken = false, done = false;
     int rc = MPCX_OK;
     std::string err;
@@ -233,10 +234,10 @@ class Coalescer {
         int rc = MPCX_OK;
         std::string err;
         try {
-          std::vector<mpcx_modexp_group_t> gs;
+          std::vector<Group> gs;
           gs.reserve(batch.size());
           for (Req* b : batch) gs.push_back(b->g);
-          rc = mpcx_modexp_multi_batch((uint32_t)gs.size(), gs.data());
+          rc = Launch((uint32_t)gs.size(), gs.data());
           if (rc) err = mpcx_last_error();
         } catch (const std::bad_alloc&) {
           rc = MPCX_ENOMEM;
@@ -267,9 +268,18 @@ class Coalescer {
   int inflight_ = 0;
 };
 
+using Coalescer = CoalescerT<mpcx_modexp_group_t, mpcx_modexp_multi_batch>;
+// comb launches: concurrent fixed-base batches (h1, h2 of every peer's N~ in
+// every wallet pipeline, proof chain) as the segments of one k_fixedbase_multi
+using FixedCoalescer = CoalescerT<mpcx_fixedbase_group_t, mpcx_fixedbase_multi_batch>;
+
 Coalescer& coalescer(uint32_t class_words) {
   static Coalescer c[3];
   return c[class_words <= 32 ? 0 : class_words <= 65 ? 1 : 2];
+}
+FixedCoalescer& fixed_coalescer(uint32_t class_words) {
+  static FixedCoalescer c[2];
+  return c[class_words <= 32 ? 0 : 1];
 }
 
 // MPCX_COALESCE = max coalesced dispatches in flight per bound device (0: off,
@@ -280,9 +290,17 @@ int coalesce_inflight() {
     return e ? std::atoi(e) : kCoalesceInflight;
   }();
   if (v <= 0) return 0;
-  int dev = 1;
+  int dev = 1;  // per bound device
   if (mpcx_bound_devices(&dev, nullptr, 0) != MPCX_OK || dev < 1) dev = 1;
   return v * dev;
+}
+// MPCX_FIXED_COALESCE=0: every comb batch its own launch (A/B runs)
+bool fixed_coalesce_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("MPCX_FIXED_COALESCE");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 }  // namespace
 
@@ -459,20 +477,29 @@ std::vector<Nat> Engine::fixed_exp(const Nat& m, const Nat& base, const std::vec
 
 void Engine::fixed_exp_into(const Nat& m, const Nat& base, size_t n, const Nat* const* exps, const Nat* const* muls,
                             Nat* const* outs) {
+  const Nat* bases[1] = {&base};
+  const Nat* const* ex[1] = {exps};
+  fixed_multi_into(m, 1, bases, n, ex, muls, outs);
+}
+
+void Engine::fixed_multi_into(const Nat& m, size_t nb, const Nat* const* bases, size_t n,
+                              const Nat* const* const* exps, const Nat* const* muls, Nat* const* outs) {
+  if (nb == 0 || nb > kFixedMaxBases) throw std::invalid_argument("fixed_multi_into: 1 or 2 bases");
   if (!n) return;
   Mod md;
   {
     std::lock_guard<std::mutex> lk(mu_);
     md = modulus(m);
   }
-  uint32_t ew = 1, need = 1;
-  for (size_t i = 0; i < n; ++i) {
-    ew = std::max<uint32_t>(ew, (uint32_t)exps[i]->words());
-    need = std::max<uint32_t>(need, exps[i]->bit_len());
-  }
-  const Nat b = base.words() > md.class_words || base >= m ? base % m : base;
-  HostBuf E(n * ew), Mw(muls ? n * md.class_words : 1), out(n * md.words);
-  pack_ptrs(exps, n, ew, E.p);
+  uint32_t ew[kFixedMaxBases] = {1, 1}, need[kFixedMaxBases] = {1, 1};
+  for (size_t t = 0; t < nb; ++t)
+    for (size_t i = 0; i < n; ++i) {
+      ew[t] = std::max<uint32_t>(ew[t], (uint32_t)exps[t][i]->words());
+      need[t] = std::max<uint32_t>(need[t], exps[t][i]->bit_len());
+    }
+  HostBuf E0(n * ew[0]), E1(nb > 1 ? n * ew[1] : 1), Mw(muls ? n * md.class_words : 1), out(n * md.words);
+  pack_ptrs(exps[0], n, ew[0], E0.p);
+  if (nb > 1) pack_ptrs(exps[1], n, ew[1], E1.p);
   if (muls) {
     par_chunks(n, [&](size_t lo, size_t hi) {
       for (size_t i = lo; i < hi; ++i) {
@@ -487,21 +514,46 @@ void Engine::fixed_exp_into(const Nat& m, const Nat& base, size_t n, const Nat* 
       }
     });
   }
-  Fixed f;
-  {
+  Fixed f[kFixedMaxBases];
+  mpcx_fb_t h[kFixedMaxBases] = {nullptr, nullptr};
+  for (size_t t = 0; t < nb; ++t) {
+    const Nat& base = *bases[t];
+    const Nat b = base.words() > md.class_words || base >= m ? base % m : base;
     // look up (or build) under the lock; the shared handle keeps the table
     // alive while this batch uses it, even if another thread evicts it
     std::lock_guard<std::mutex> lk(mu_);
-    f = fixed(m, b, need);
+    f[t] = fixed(m, b, need[t]);
+    h[t] = f[t]->h;
   }
-  const uint32_t* ep = E.p;
-  count_work(m, exps, n, n);
+  const uint32_t* ep[kFixedMaxBases] = {E0.p, E1.p};
+  for (size_t t = 0; t < nb; ++t) count_work(m, exps[t], n, n);
   int rc;
   {
     MPCX_PROF("engine.fixed.gpu");
     enter_call();
-    rc = mpcx_fixedbase_exp_batch(1, &f->h, (uint32_t)n, &ep, &ew, muls ? Mw.p : nullptr, muls ? md.class_words : 0,
-                                  out.p, md.words);
+    const int inflight = coalesce_inflight();
+    if (inflight > 0 && n < kCoalesceAloneOps && fixed_coalesce_on()) {
+      FixedCoalescer::Req r;
+      r.g.nbases = (uint32_t)nb;
+      r.g.count = (uint32_t)n;
+      for (size_t t = 0; t < nb; ++t) {
+        r.g.fbs[t] = h[t];
+        r.g.exps[t] = ep[t];
+        r.g.exp_words[t] = ew[t];
+      }
+      r.g.muls = muls ? Mw.p : nullptr;
+      r.g.mul_words = muls ? md.class_words : 0;
+      r.g.out = out.p;
+      r.g.out_words = md.words;
+      rc = fixed_coalescer(md.class_words).run(r, inflight, kCoalesceMaxOps);
+      if (rc) {
+        leave_call();
+        throw EngineError(rc, "mpcx_fixedbase_multi_batch: " + r.err);
+      }
+    } else {
+      rc = mpcx_fixedbase_exp_batch((uint32_t)nb, h, (uint32_t)n, ep, ew, muls ? Mw.p : nullptr,
+                                    muls ? md.class_words : 0, out.p, md.words);
+    }
     leave_call();
   }
   if (rc) throw_last(rc, "mpcx_fixedbase_exp_batch");

@@ -49,6 +49,7 @@ class Engine {
   // one adversarial proof can neither force a huge table build nor fail the
   // whole batch.
   static constexpr uint32_t kFixedMaxBits = 5120;
+  static constexpr size_t kFixedMaxBases = 2;  // tables per comb launch (mpcx_fixedbase_exp_batch)
 
   // out[i] = (muls ? muls[i] : 1) * bases[i]^e_i mod m, m odd, 1 <= m < 2^4096.
   // exps.size() == 1: shared exponent; else one per base. Bases of any size
@@ -68,6 +69,10 @@ class Engine {
                              const std::vector<Nat>* muls = nullptr);
   void fixed_exp_into(const Nat& m, const Nat& base, size_t n, const Nat* const* exps, const Nat* const* muls,
                       Nat* const* outs);
+  // out[i] = (muls ? muls[i] : 1) * prod_t bases[t]^exps[t][i] mod m for nb <= 2
+  // recurring bases, one comb launch (each base's table cached as above)
+  void fixed_multi_into(const Nat& m, size_t nb, const Nat* const* bases, size_t n, const Nat* const* const* exps,
+                        const Nat* const* muls, Nat* const* outs);
   // fixed-base path usable for m (odd, <= 2080 bits) and enabled
   // (environment MPCX_FIXED_BASE=0 turns it off, for A/B runs)
   bool fixed_base_ok(const Nat& m) const;

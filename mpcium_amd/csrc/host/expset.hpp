@@ -65,7 +65,14 @@ class ExpSet {
   void add(const Nat& base, const Nat& e, Nat* out, const Nat* mul = nullptr) {
     reqs_.push_back({&base, &e, mul, out});
   }
-  size_t size() const { return reqs_.size(); }
+  // out = (mul ? mul : 1) * b1^e1 * b2^e2 mod m: two recurring bases (h1^x h2^y
+  // of the range proofs) in ONE comb launch, both exponents' windows chained
+  // into one accumulator (k_fixedbase with two tables), instead of a launch per
+  // base with the second waiting on the first
+  void add2(const Nat& b1, const Nat& e1, const Nat& b2, const Nat& e2, Nat* out, const Nat* mul = nullptr) {
+    reqs2_.push_back({&b1, &e1, &b2, &e2, mul, out});
+  }
+  size_t size() const { return reqs_.size() + reqs2_.size(); }
   // Every launch of the pending requests, concurrently; the set is empty after.
   void run() {
     std::vector<std::function<void()>> fs;
@@ -76,6 +83,7 @@ class ExpSet {
   // Appends one closure per launch of the pending requests (run them, e.g. with
   // run_concurrently together with other sets' launches, then clear()).
   void collect(std::vector<std::function<void()>>& fs) {
+    collect2(fs);
     if (reqs_.empty()) return;
     // A base recurring across many requests (h1, h2 of N~ in every session's
     // range proof) goes to the fixed-base comb path: no squarings, one
@@ -121,7 +129,10 @@ class ExpSet {
       g0 = g1;
     }
   }
-  void clear() { reqs_.clear(); }
+  void clear() {
+    reqs_.clear();
+    reqs2_.clear();
+  }
 
  private:
   struct Req {
@@ -130,6 +141,80 @@ class ExpSet {
     const Nat* mul;
     Nat* out;
   };
+  struct Req2 {
+    const Nat *b1, *e1, *b2, *e2, *mul;
+    Nat* out;
+  };
+  // two-base requests: per (b1, b2) pair one two-table comb launch when the
+  // comb path takes them; otherwise b1^e1 first, then b2^e2 times it
+  void collect2(std::vector<std::function<void()>>& fs) {
+    if (reqs2_.empty()) return;
+    std::map<std::pair<const Nat*, const Nat*>, std::vector<size_t>> by_b;
+    for (size_t i = 0; i < reqs2_.size(); ++i) by_b[{reqs2_[i].b1, reqs2_[i].b2}].push_back(i);
+    const bool comb = Engine::get().fixed_base_ok(m_);
+    for (auto& kv : by_b) {
+      auto idx = kv.second;
+      bool fits = comb && idx.size() >= kFixedMin;
+      for (size_t i : idx)
+        fits = fits && reqs2_[i].e1->bit_len() <= Engine::kFixedMaxBits &&
+               reqs2_[i].e2->bit_len() <= Engine::kFixedMaxBits;
+      if (fits) {
+        std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+          return std::max(reqs2_[a].e1->bit_len(), reqs2_[a].e2->bit_len()) <
+                 std::max(reqs2_[b].e1->bit_len(), reqs2_[b].e2->bit_len());
+        });
+        fs.push_back([this, idx] { launch_fixed2(idx); });
+      } else {
+        fs.push_back([this, idx] { launch_two_step(idx); });
+      }
+    }
+  }
+  void launch_fixed2(const std::vector<size_t>& idx) {
+    MPCX_PROF("expset.launch_fixed2");
+    const size_t n = idx.size();
+    std::vector<const Nat*> e1(n), e2(n), muls;
+    std::vector<Nat*> outs(n);
+    bool any_mul = false;
+    for (size_t i : idx) any_mul |= reqs2_[i].mul != nullptr;
+    if (any_mul) muls.resize(n);
+    for (size_t j = 0; j < n; ++j) {
+      const Req2& r = reqs2_[idx[j]];
+      e1[j] = r.e1;
+      e2[j] = r.e2;
+      outs[j] = r.out;
+      if (any_mul) muls[j] = r.mul;
+    }
+    const Nat* bases[2] = {reqs2_[idx[0]].b1, reqs2_[idx[0]].b2};
+    const Nat* const* exps[2] = {e1.data(), e2.data()};
+    Engine::get().fixed_multi_into(m_, 2, bases, n, exps, any_mul ? muls.data() : nullptr, outs.data());
+  }
+  void launch_two_step(const std::vector<size_t>& idx) {
+    MPCX_PROF("expset.launch_two_step");
+    const size_t n = idx.size();
+    std::vector<Nat> t(n);
+    std::vector<const Nat*> b(n), e(n), muls;
+    std::vector<Nat*> outs(n);
+    bool any_mul = false;
+    for (size_t i : idx) any_mul |= reqs2_[i].mul != nullptr;
+    for (size_t j = 0; j < n; ++j) {
+      b[j] = reqs2_[idx[j]].b1;
+      e[j] = reqs2_[idx[j]].e1;
+      outs[j] = &t[j];
+    }
+    if (any_mul) {
+      muls.resize(n);
+      for (size_t j = 0; j < n; ++j) muls[j] = reqs2_[idx[j]].mul;
+    }
+    Engine::get().exp_into(m_, n, b.data(), e.data(), n, any_mul ? muls.data() : nullptr, outs.data());
+    std::vector<const Nat*> tm(n);
+    for (size_t j = 0; j < n; ++j) {
+      b[j] = reqs2_[idx[j]].b2;
+      e[j] = reqs2_[idx[j]].e2;
+      tm[j] = &t[j];
+      outs[j] = reqs2_[idx[j]].out;
+    }
+    Engine::get().exp_into(m_, n, b.data(), e.data(), n, tm.data(), outs.data());
+  }
   static constexpr size_t kFixedMin = 64;  // requests on one base before a comb table pays
   // the requests' own operands and outputs, through pointers: no copies
   void launch_fixed(const std::vector<size_t>& idx) {
@@ -168,6 +253,7 @@ class ExpSet {
   }
   const Nat m_;  // by value: callers pass temporaries (pk.NSquare())
   std::vector<Req> reqs_;
+  std::vector<Req2> reqs2_;
 };
 
 // Every launch of several sets (one protocol step's moduli: N^2, N~, N) at once.

@@ -42,7 +42,7 @@ Nat affine_y(const secp::Affine& p) { return secp::FeToNat(p.y); }
 // ---- ProveRangeAlice in stages (shared by ProveRangeAliceBatch and AliceInitBatch)
 struct RangeProveState {
   Nat alpha, beta, gamma, rho;
-  Nat gam_alpha, t1, t2, e;
+  Nat gam_alpha, e;
 };
 
 // steps 1-4 for every session, in each reader's draw order: alpha < q^3,
@@ -86,16 +86,11 @@ void range_prove_core(const paillier::PublicKey& pk, const DLNParams& dln, const
   for (size_t i = 0; i < n; ++i) {
     auto& s = st[i];
     auto& o = (*out)[i];
-    eN2.add(s.beta, pk.N, &o.U, &s.gam_alpha);  // 6. u = Gamma^alpha beta^N mod N^2
-    eNt.add(dln.h1, m[i], &s.t1);               // 5. h1^m
-    eNt.add(dln.h1, s.alpha, &s.t2);            // 7. h1^alpha
+    eN2.add(s.beta, pk.N, &o.U, &s.gam_alpha);               // 6. u = Gamma^alpha beta^N mod N^2
+    eNt.add2(dln.h1, m[i], dln.h2, s.rho, &o.Z);             // 5. z = h1^m h2^rho mod N~
+    eNt.add2(dln.h1, s.alpha, dln.h2, s.gamma, &o.W);        // 7. w = h1^alpha h2^gamma mod N~
   }
   run_all({&eN2, &eNt});
-  for (size_t i = 0; i < n; ++i) {
-    eNt.add(dln.h2, st[i].rho, &(*out)[i].Z, &st[i].t1);    // 5. z = h1^m h2^rho mod N~
-    eNt.add(dln.h2, st[i].gamma, &(*out)[i].W, &st[i].t2);  // 7. w = h1^alpha h2^gamma mod N~
-  }
-  eNt.run();
   const Nat gamma = pk.Gamma();
   parallel_for(n, [&](size_t i) {  // 8-9. e = RejectionSample(q, SHA512_256i(N, Gamma, c, z, u, w))
     auto& o = (*out)[i];
@@ -131,7 +126,7 @@ std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const 
   const Nat N2 = pk.NSquare();
   const Nat gamma = pk.Gamma();
   std::vector<uint8_t> ok(n, 0);
-  std::vector<Nat> e(n), gs1(n), L1(n), R1(n), t(n), L2(n), R2(n), cr(n);
+  std::vector<Nat> e(n), gs1(n), L1(n), R1(n), L2(n), R2(n), cr(n);
   parallel_for(n, [&](size_t i) {
     MPCX_PROF("mta.verify_range.checks");
     const auto& p = pf[i];
@@ -171,13 +166,10 @@ std::vector<uint8_t> VerifyRangeAliceBatch(const paillier::PublicKey& pk, const 
     const auto& p = pf[i];
     eN2.add(cr[i], e[i], &L1[i], &p.U);     // u c^e
     eN2.add(p.S, pk.N, &R1[i], &gs1[i]);    // Gamma^s1 s^N
-    eNt.add(dln.h1, p.S1, &t[i]);           // h1^s1
-    eNt.add(p.Z, e[i], &L2[i], &p.W);       // w z^e
+    eNt.add2(dln.h1, p.S1, dln.h2, p.S2, &R2[i]);  // h1^s1 h2^s2
+    eNt.add(p.Z, e[i], &L2[i], &p.W);             // w z^e
   }
   run_all({&eN2, &eNt});
-  for (size_t i = 0; i < n; ++i)
-    if (ok[i]) eNt.add(dln.h2, pf[i].S2, &R2[i], &t[i]);  // h1^s1 h2^s2
-  eNt.run();
   for (size_t i = 0; i < n; ++i) ok[i] = ok[i] && L1[i] == R1[i] && L2[i] == R2[i];
   return ok;
 }
@@ -187,7 +179,7 @@ namespace {
 struct BobProveState {
   Nat alpha, rho, sigma, tau, rhoPrm, beta, gamma;
   secp::Affine u;
-  Nat bg, a1, a2, a3, a4, e;
+  Nat bg, e;
   bool wc = false;  // ProveBobWC (u = alpha*G)
 };
 
@@ -224,25 +216,20 @@ void bob_draw(std::vector<BobProveState>& st, const std::vector<size_t>& js, con
   for (size_t k = 0; k < wc.size(); ++k) st[wc[k]].u = u[k];
 }
 
-// stage A of ProveBob: N^2 -> bg = Gamma^gamma beta^N ; N~ -> h1^x, h1^alpha, h1^y, h1^gamma
+// stage A of ProveBob: N^2 -> bg = Gamma^gamma beta^N ; N~ -> z, z', t, w (6-8, 10.),
+// each h1^x h2^y one two-table comb product
 void bob_stage_a(BobProveState& s, const paillier::PublicKey& pk, const DLNParams& dln, const Nat& x, const Nat& y,
-                 ExpSet& eN2, ExpSet& eNt, Nat* gam_gamma) {
+                 ExpSet& eN2, ExpSet& eNt, Nat* gam_gamma, ProofBob& o) {
   *gam_gamma = gamma_pow(s.gamma, pk.N);
   eN2.add(s.beta, pk.N, &s.bg, gam_gamma);
-  eNt.add(dln.h1, x, &s.a1);
-  eNt.add(dln.h1, s.alpha, &s.a2);
-  eNt.add(dln.h1, y, &s.a3);
-  eNt.add(dln.h1, s.gamma, &s.a4);
+  eNt.add2(dln.h1, x, dln.h2, s.rho, &o.Z);           // z = h1^x h2^rho
+  eNt.add2(dln.h1, s.alpha, dln.h2, s.rhoPrm, &o.ZPrm);  // z' = h1^alpha h2^rhoPrm
+  eNt.add2(dln.h1, y, dln.h2, s.sigma, &o.T);          // t = h1^y h2^sigma
+  eNt.add2(dln.h1, s.gamma, dln.h2, s.tau, &o.W);      // w = h1^gamma h2^tau
 }
 
-// stage B: v = c1^alpha Gamma^gamma beta^N (9.), z, z', t, w (6-8, 10.)
-void bob_stage_b(BobProveState& s, const DLNParams& dln, const Nat& c1, ExpSet& eN2, ExpSet& eNt, ProofBob& o) {
-  eN2.add(c1, s.alpha, &o.V, &s.bg);
-  eNt.add(dln.h2, s.rho, &o.Z, &s.a1);
-  eNt.add(dln.h2, s.rhoPrm, &o.ZPrm, &s.a2);
-  eNt.add(dln.h2, s.sigma, &o.T, &s.a3);
-  eNt.add(dln.h2, s.tau, &o.W, &s.a4);
-}
+// stage B: v = c1^alpha Gamma^gamma beta^N (9.)
+void bob_stage_b(BobProveState& s, const Nat& c1, ExpSet& eN2, ProofBob& o) { eN2.add(c1, s.alpha, &o.V, &s.bg); }
 
 // 11-12. e = RejectionSample(q, SHA512_256i_TAGGED(Session, N, Gamma, [X.x, X.y,] c1, c2, [u.x, u.y,] z, z', t, v, w))
 Nat bob_challenge(const Bytes& session, const paillier::PublicKey& pk, const Nat& gamma, const secp::Affine* X,
@@ -287,10 +274,10 @@ void ProveBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey&
     bob_draw(st, js, rd, pk, dln);
   }
   ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
-  for (size_t i = 0; i < n; ++i) bob_stage_a(st[i], pk, dln, x[i], y[i], eN2, eNt, &gg[i]);
+  for (size_t i = 0; i < n; ++i) bob_stage_a(st[i], pk, dln, x[i], y[i], eN2, eNt, &gg[i], (*out)[i]);
   run_all({&eN2, &eNt});
-  for (size_t i = 0; i < n; ++i) bob_stage_b(st[i], dln, c1[i], eN2, eNt, (*out)[i]);
-  run_all({&eN2, &eNt});
+  for (size_t i = 0; i < n; ++i) bob_stage_b(st[i], c1[i], eN2, (*out)[i]);
+  eN2.run();
   parallel_for(n, [&](size_t i) {
     (*out)[i].U = st[i].u;
     st[i].e = bob_challenge(session[i], pk, gamma, X ? &(*X)[i] : nullptr, c1[i], c2[i], (*out)[i]);
@@ -311,7 +298,7 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
   const size_t n = c1.size();
   const Nat N2 = pk.NSquare(), gamma = pk.Gamma();
   std::vector<uint8_t> ok(n, 0);
-  std::vector<Nat> e(n), gt1(n), p1(n), p2(n), r1(n), r2(n), q1(n), r3(n), l1(n), l2(n), l3(n);
+  std::vector<Nat> e(n), gt1(n), r1(n), r2(n), q1(n), r3(n), l1(n), l2(n), l3(n);
   parallel_for(n, [&](size_t i) {
     MPCX_PROF("mta.verify_bob.checks");
     const auto& p = *pfp[i];
@@ -408,8 +395,8 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
     const auto& p = *pfp[i];
-    eNt.add(dln.h1, p.S1, &p1[i]);          // 5. h1^s1
-    eNt.add(dln.h1, p.T1, &p2[i]);          // 6. h1^t1
+    eNt.add2(dln.h1, p.S1, dln.h2, p.S2, &l1[i]);  // 5. h1^s1 h2^s2
+    eNt.add2(dln.h1, p.T1, dln.h2, p.T2, &l2[i]);  // 6. h1^t1 h2^t2
     eNt.add(p.Z, e[i], &r1[i], &p.ZPrm);    // 5. z^e z'
     eNt.add(p.T, e[i], &r2[i], &p.W);       // 6. t^e w
     if (crt) {
@@ -425,8 +412,6 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
   run_all({&eN2, &eQ2, &eNt});
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
-    eNt.add(dln.h2, pfp[i]->S2, &l1[i], &p1[i]);  // 5. h1^s1 h2^s2
-    eNt.add(dln.h2, pfp[i]->T2, &l2[i], &p2[i]);  // 6. h1^t1 h2^t2
     if (crt) {
       eN2.add(rp[i].c1, pfp[i]->S1, &l3[i], &q1[i]);   // 7. c1^s1 s^N Gamma^t1 mod P^2
       eQ2.add(rq[i].c1, pfp[i]->S1, &l3q[i], &q1q[i]);  //    and mod Q^2
@@ -434,7 +419,7 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
       eN2.add(*c1[i], pfp[i]->S1, &l3[i], &q1[i]);  // 7. c1^s1 s^N Gamma^t1
     }
   }
-  run_all({&eN2, &eQ2, &eNt});
+  run_all({&eN2, &eQ2});
   for (size_t i = 0; i < n; ++i)
     ok[i] = ok[i] && l1[i] == r1[i] && l2[i] == r2[i] && l3[i] == r3[i] && (!crt || l3q[i] == r3q[i]);
   return ok;
@@ -588,16 +573,16 @@ void bob_mid_halves(const std::vector<Bytes>& session, const paillier::PublicKey
   for (size_t j = 0; j < k; ++j) {
     if (!live[j]) continue;
     eN2.add(cRand[j], pkA.N, &cbp[j], &gbp[j]);  // cBetaPrm = Gamma^betaPrm r^N
-    bob_stage_a(st[j], pkA, dlnA, *h[j].b, h[j].out->betaPrm, eN2, eNt, &gg[j]);
+    bob_stage_a(st[j], pkA, dlnA, *h[j].b, h[j].out->betaPrm, eN2, eNt, &gg[j], h[j].out->pf);
   }
   run_all({&eN2, &eNt});
   for (size_t j = 0; j < k; ++j) {
     if (!live[j]) continue;
     const Nat& c = cA[h[j].i];
     eN2.add(c, *h[j].b, &h[j].out->cB, &cbp[j]);  // cB = HomoAdd(HomoMult(b, cA), cBetaPrm)
-    bob_stage_b(st[j], dlnA, c, eN2, eNt, h[j].out->pf);
+    bob_stage_b(st[j], c, eN2, h[j].out->pf);
   }
-  run_all({&eN2, &eNt});
+  eN2.run();
   parallel_for(k, [&](size_t j) {
     if (!live[j]) return;
     auto& o = *h[j].out;

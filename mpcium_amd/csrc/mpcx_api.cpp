@@ -43,8 +43,8 @@
   hipError_t mpcx_launch_modexp_multi_g##g(const mpcx::ModexpArgs* segs, const uint32_t* first,      \
                                            uint32_t nsegs, uint32_t waves, hipStream_t st);          \
   hipError_t mpcx_modexp_occupancy_g##g(int* blocks_per_cu);
-#define MPCX_FOR_EACH_GEOM(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6) X(7)
-static_assert(MPCX_NUM_GEOMS == 8, "update MPCX_FOR_EACH_GEOM and build.py GEOMS");
+#define MPCX_FOR_EACH_GEOM(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6)
+static_assert(MPCX_NUM_GEOMS == 7, "update MPCX_FOR_EACH_GEOM and build.py GEOMS");
 extern "C" {
 MPCX_FOR_EACH_GEOM(MPCX_GEOM_DECL)
 hipError_t mpcx_launch_prime2(const mpcx::Prime2Args* a, uint32_t blocks, hipStream_t st);
@@ -58,6 +58,10 @@ hipError_t mpcx_launch_lucasc_wide(const mpcx::LucasArgs* a, hipStream_t st);
 hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_g1(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_multi_g0(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
+                                          uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_multi_g1(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
+                                          uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_sieve(const mpcx::SieveArgs* a, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 hipError_t mpcx_launch_ec_combine(const uint32_t* sc, const uint32_t* pts, uint32_t* out, const uint32_t* gtab,
@@ -85,7 +89,11 @@ struct mpcx_fixedbase_s {
   int geom;                          // main geometry of the modulus class (table layout)
   uint32_t nwin;                     // windows: exponents of up to wbits*nwin bits
   uint32_t wbits;                    // window width (entries per window: 2^wbits)
-  std::vector<uint32_t> host_table;  // nwin x 2^wbits entries x L digits ([k][p] interleaved)
+  // nwin x 2^wbits entries x L digits ([k][p] interleaved); held only until the
+  // first device has its copy (a 12-bit table is ~320 MB): further devices copy
+  // it device to device
+  std::vector<uint32_t> host_table;
+  size_t table_words = 0;
   std::mutex mu;
   uint32_t* d_table[kMaxDevices] = {};
 };
@@ -97,10 +105,8 @@ constexpr uint32_t kM28 = (1u << kDigitBits) - 1u;
 
 thread_local std::string g_err;
 std::mutex g_mu;  // options, device binding, shutdown
-bool g_split = false;                    // narrow-geometry tail launch (measured slower: off)
 int g_force_geom = -1;                   // mpcx_set_option("force_geom", g): one geometry for everything
 double g_narrow_rounds = 0.15;           // mpcx_set_option("narrow_rounds", 100x): narrow-geometry threshold
-double g_mid_rounds = 0.0;               // mpcx_set_option("mid_rounds", 100x): mid-geometry threshold
 int g_geom_policy = 1;                   // 1: 4096-bit class by the launch-time model; 0: thresholds only
 int g_fixed_win = 5;                     // widest fixed window for per-operand exponents (4 or 5)
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
@@ -661,10 +667,19 @@ int fb_table(mpcx_fb_t fb, int di, const uint32_t** out) {
   std::lock_guard<std::mutex> lk(fb->mu);
   if (!fb->d_table[di]) {
     uint32_t* p = nullptr;
-    const size_t bytes = fb->host_table.size() * sizeof(uint32_t);
+    const size_t bytes = fb->table_words * sizeof(uint32_t);
     hipError_t e = hipMalloc((void**)&p, bytes);
     if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(fixed-base table %zu B)", bytes);
-    e = hipMemcpy(p, fb->host_table.data(), bytes, hipMemcpyHostToDevice);
+    if (!fb->host_table.empty()) {
+      e = hipMemcpy(p, fb->host_table.data(), bytes, hipMemcpyHostToDevice);
+      if (e == hipSuccess) std::vector<uint32_t>().swap(fb->host_table);  // the device copy is the master now
+    } else {
+      int src = -1;
+      for (int j = 0; j < kMaxDevices && src < 0; ++j)
+        if (fb->d_table[j]) src = j;
+      e = src < 0 ? hipErrorInvalidValue
+                  : hipMemcpyPeer(p, g_devs[di].ordinal, fb->d_table[src], g_devs[src].ordinal, bytes);
+    }
     if (e != hipSuccess) {
       (void)hipFree(p);
       return hip_fail(e, "upload fixed-base table");
@@ -728,6 +743,37 @@ int run_sliced(uint32_t count, uint32_t min_slice, const std::function<int(int, 
   return MPCX_OK;
 }
 
+// Can geometry g serve modulus mod? R = 2^(28 L) > 4m, and every base and
+// multiplier below R (almost-Montgomery entry mont(x, R^2) < 2m needs x < R).
+// The class width is 2^(32 class words); a geometry whose R is below it (the
+// lane-pair geometry 5: 2^2072 in a 2080-bit class) needs the caller's check of
+// the operands (ops_fit).
+bool geom_serves(int g, const mpcx_modulus_s* mod, bool ops_fit) {
+  const uint32_t rb = (uint32_t)MPCX_GEOM_RBITS(g);
+  if (mod->bits + 2u > rb) return false;
+  return ops_fit || rb >= 32u * (uint32_t)MPCX_CLASS_WORDS(mod->cls);
+}
+
+// every one of count operands of `words` words below 2^rbits (null: none)
+bool host_ops_below(const uint32_t* x, uint32_t count, uint32_t words, uint32_t rbits) {
+  if (!x || 32u * words <= rbits) return true;
+  const uint32_t w0 = rbits / 32u, sh = rbits % 32u;
+  for (uint32_t i = 0; i < count; ++i) {
+    const uint32_t* v = x + (size_t)i * words;
+    if (sh && (v[w0] >> sh)) return false;
+    for (uint32_t w = w0 + (sh ? 1u : 0u); w < words; ++w)
+      if (v[w]) return false;
+  }
+  return true;
+}
+
+// the main geometry of mod's class, or the class's full-width geometry when
+// the main one cannot serve this modulus / these operands
+int main_geom_for(const mpcx_modulus_s* mod, bool ops_fit) {
+  const int g = g_main_geom[mod->cls];
+  return geom_serves(g, mod, ops_fit) ? g : MPCX_FULL_GEOM(mod->cls);
+}
+
 }  // namespace
 
 extern "C" {
@@ -737,9 +783,7 @@ int mpcx_version(void) { return 200; }
 int mpcx_set_option(const char* key, int value) {
   if (!key) return fail(MPCX_EINVAL, "null option");
   std::lock_guard<std::mutex> lk(g_mu);
-  if (std::strcmp(key, "split") == 0) {
-    g_split = value != 0;
-  } else if (std::strcmp(key, "force_geom") == 0) {
+  if (std::strcmp(key, "force_geom") == 0) {
     if (value < -1 || value >= MPCX_NUM_GEOMS) return fail(MPCX_EINVAL, "force_geom %d out of range", value);
     g_force_geom = value;
   } else if (std::strcmp(key, "sched_width") == 0) {
@@ -750,11 +794,6 @@ int mpcx_set_option(const char* key, int value) {
     // batches below value/100 of a resident round run in the narrow geometry
     if (value < 0 || value > 100) return fail(MPCX_EINVAL, "narrow_rounds %d out of range", value);
     g_narrow_rounds = value / 100.0;
-  } else if (std::strcmp(key, "mid_rounds") == 0) {
-    // batches from narrow_rounds up to value/100 of a main-geometry round run in
-    // the class's mid geometry (twice the wavefronts per operand count)
-    if (value < 0 || value > 400) return fail(MPCX_EINVAL, "mid_rounds %d out of range", value);
-    g_mid_rounds = value / 100.0;
   } else if (std::strcmp(key, "fb_window") == 0) {
     // window width of fixed-base tables registered from now on (4..12; one
     // product per window, 2^w entries per window)
@@ -809,20 +848,14 @@ int mpcx_device_count(int* out_count) {
 
 // launch-policy overrides from the environment (A/B runs of whole drivers)
 static void read_env_options() {
-  const char* sp = std::getenv("MPCX_SPLIT");
-  if (sp) g_split = sp[0] != '0';
   const char* nr = std::getenv("MPCX_NARROW_ROUNDS");  // percent of a main round
   if (nr) g_narrow_rounds = std::max(0, std::min(100, std::atoi(nr))) / 100.0;
-  const char* mr = std::getenv("MPCX_MID_ROUNDS");  // percent of a main round
-  if (mr) g_mid_rounds = std::max(0, std::min(400, std::atoi(mr))) / 100.0;
   const char* pc = std::getenv("MPCX_PRIME_COOP");
   if (pc) g_prime_coop = pc[0] != '0';
   const char* gp = std::getenv("MPCX_GEOM_POLICY");
   if (gp) g_geom_policy = std::max(0, std::min(2, std::atoi(gp)));
   const char* ln = std::getenv("MPCX_LANES");
   if (ln && g_ndev.load() == 0) g_lanes = std::max(1, std::min(kMaxLanes, std::atoi(ln)));
-  const char* g0 = std::getenv("MPCX_MAIN_GEOM0");  // main geometry of the 1024-bit class (0 or 7)
-  if (g0 && (std::atoi(g0) == 0 || std::atoi(g0) == 7)) g_main_geom[0] = std::atoi(g0);
   const char* fw = std::getenv("MPCX_FB_WINDOW");  // fixed-base comb width of new tables
   if (fw) g_fb_window = std::max(4, std::min(MPCX_FB_MAX_WINDOW_BITS, std::atoi(fw)));
 }
@@ -1018,7 +1051,7 @@ int mpcx_modulus_info(mpcx_mod_t mod, uint32_t* out_bits, uint32_t* out_class_wo
 
 int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K, uint32_t* G) {
   if (!mod) return fail(MPCX_EINVAL, "null modulus");
-  const int g = g_main_geom[mod->cls];
+  const int g = main_geom_for(mod, true);
   if (L) *L = (uint32_t)MPCX_GEOM_L(g);
   if (P) *P = (uint32_t)MPCX_GEOM_P(g);
   if (K) *K = (uint32_t)MPCX_GEOM_K(g);
@@ -1066,22 +1099,25 @@ static int fastest_geom(int cls, uint32_t count, int nsimd) {
 // forced geometry, or policy 2's main, or policy 1's launch-time model, or
 // the thresholds) -- the multi-batch launch takes one geometry for all its
 // segments.
-static int choose_geom(const Device& dev, int cls, uint32_t count) {
-  const int gm = g_main_geom[cls], gn = MPCX_NARROW_GEOM(cls), gmid = MPCX_MID_GEOM(cls);
-  if (g_force_geom >= 0 && MPCX_GEOM_CLASS(g_force_geom) == cls) return g_force_geom;
+static int choose_geom(const Device& dev, int cls, uint32_t count, bool main_serves, bool forced_serves) {
+  const int gm = main_serves ? g_main_geom[cls] : MPCX_FULL_GEOM(cls);
+  const int gn = MPCX_NARROW_GEOM(cls), gmid = MPCX_MID_GEOM(cls);
+  if (g_force_geom >= 0 && MPCX_GEOM_CLASS(g_force_geom) == cls)
+    return forced_serves ? g_force_geom : MPCX_FULL_GEOM(cls);
   if (g_geom_policy == 2) return gm;
   if (g_geom_policy == 1 && gmid >= 0 && gn >= 0) return fastest_geom(cls, count, dev.num_cus * 4);
   const uint32_t G = (uint32_t)MPCX_GEOM_G(gm);
   const double rounds = (double)((count + G - 1) / G) / (double)std::max(1, dev.geom_slots[gm]);
   if (gn >= 0 && rounds < g_narrow_rounds) return gn;
-  if (gmid >= 0 && rounds < g_mid_rounds) return gmid;
   return gm;
 }
 
+// ops_fit: every base and multiplier is below 2^MPCX_GEOM_RBITS of the class's
+// main geometry (host_ops_below; see geom_serves).
 static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases,
                           uint32_t base_words, const uint32_t* d_exps, uint32_t exp_words, int exp_shared,
                           uint32_t exp_bits, const uint32_t* d_muls, uint32_t mul_words, uint32_t* d_out,
-                          uint32_t out_words, double alg_macs = -1.0) {
+                          uint32_t out_words, bool ops_fit, double alg_macs = -1.0) {
   const Device& dev = g_devs[di];
   hipStream_t st = lane.st;
   const uint32_t class_words = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
@@ -1102,18 +1138,17 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     uint32_t first, count;
   } parts[2];
   int nparts = 0;
-  const int gm = g_main_geom[mod->cls], gn = MPCX_NARROW_GEOM(mod->cls);
+  const int gm = main_geom_for(mod, ops_fit), gn = MPCX_NARROW_GEOM(mod->cls);
   if (g_force_geom >= 0 && MPCX_GEOM_CLASS(g_force_geom) == mod->cls) {
-    parts[nparts++] = {g_force_geom, 0, count};
+    parts[nparts++] = {geom_serves(g_force_geom, mod, ops_fit) ? g_force_geom : MPCX_FULL_GEOM(mod->cls), 0, count};
   } else {
     const uint32_t G = (uint32_t)MPCX_GEOM_G(gm);
     const double waves = (double)((count + G - 1) / G);
     const double rounds = waves / (double)std::max(1, dev.geom_slots[gm]);
-    const double full = std::floor(rounds), frac = rounds - full;
     // Measured on MI355X (profiles/r01): a lone wavefront issues v_mad_u64_u32
     // at ~45% of SIMD peak, so tiny batches (< 0.15 of a round) finish sooner
     // spread over the narrow geometry's 3x more wavefronts; from ~0.3 rounds up
-    // the main geometry wins, and a narrow tail launch did not pay.
+    // the main geometry wins, and a narrow tail launch did not pay (round 1).
     const int gmid = MPCX_MID_GEOM(mod->cls);
     if (g_geom_policy == 2) {
       // throughput: the main geometry at every size (concurrent launches from
@@ -1123,14 +1158,8 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
       parts[nparts++] = {fastest_geom(mod->cls, count, dev.num_cus * 4), 0, count};
     } else if (gn >= 0 && rounds < g_narrow_rounds) {
       parts[nparts++] = {gn, 0, count};
-    } else if (gmid >= 0 && rounds < g_mid_rounds) {
-      parts[nparts++] = {gmid, 0, count};
-    } else if (!g_split || gn < 0 || rounds < 1.0 || frac == 0.0 || frac > 0.75) {
-      parts[nparts++] = {gm, 0, count};
     } else {
-      const uint32_t nmain = (uint32_t)full * (uint32_t)dev.geom_slots[gm] * G;
-      parts[nparts++] = {gm, 0, nmain};
-      parts[nparts++] = {gn, nmain, count - nmain};
+      parts[nparts++] = {gm, 0, count};
     }
   }
   size_t ws_words = 0;
@@ -1220,6 +1249,8 @@ static int modexp_host_range(int di, mpcx_mod_t mod, uint32_t count, const uint3
   if ((rc = h2d(sg[0].ptr, bases, bb, l.st)) || (rc = h2d(sg[1].ptr, exps, n_exp_words * 4, l.st)) ||
       (muls && (rc = h2d(sg[3].ptr, muls, mb, l.st))))
     return rc;
+  const uint32_t rb = (uint32_t)MPCX_GEOM_RBITS(g_main_geom[mod->cls]);
+  const bool ops_fit = host_ops_below(bases, count, base_words, rb) && host_ops_below(muls, count, mul_words, rb);
   double alg = -1.0;
   if (!exp_shared && exp_words) {  // the operands' own exponent lengths (launch log)
     alg = 0.0;
@@ -1228,7 +1259,7 @@ static int modexp_host_range(int di, mpcx_mod_t mod, uint32_t count, const uint3
   }
   rc = modexp_enqueue(di, l, mod, count, (const uint32_t*)sg[0].ptr, base_words, (const uint32_t*)sg[1].ptr,
                       exp_words, exp_shared, exp_bits, muls ? (const uint32_t*)sg[3].ptr : nullptr, mul_words,
-                      (uint32_t*)sg[2].ptr, out_words, alg);
+                      (uint32_t*)sg[2].ptr, out_words, ops_fit, alg);
   if (rc) return rc;
   return d2h_sync(out, sg[2].ptr, ob, l);
 }
@@ -1304,8 +1335,10 @@ int mpcx_modexp_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_b
   if (int rc = selected(&dev)) return rc;
   Lane& l = stream_lane(*dev, (hipStream_t)stream);
   std::lock_guard<std::mutex> lk(l.mu);
+  // device buffers are not scanned: operands fit when their width does
+  const bool ops_fit = 32u * base_words <= (uint32_t)MPCX_GEOM_RBITS(g_main_geom[mod->cls]);
   return modexp_enqueue((int)(dev - g_devs), l, mod, count, d_bases, base_words, d_exps, exp_words, exp_shared,
-                        exp_bits, nullptr, 0, d_out, out_words);
+                        exp_bits, nullptr, 0, d_out, out_words, ops_fit);
 }
 
 int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t* d_bases, uint32_t base_words,
@@ -1318,8 +1351,10 @@ int mpcx_modexp_mul_batch_device(mpcx_mod_t mod, uint32_t count, const uint32_t*
   if (int rc = selected(&dev)) return rc;
   Lane& l = stream_lane(*dev, (hipStream_t)stream);
   std::lock_guard<std::mutex> lk(l.mu);
+  const uint32_t rb = (uint32_t)MPCX_GEOM_RBITS(g_main_geom[mod->cls]);
+  const bool ops_fit = 32u * base_words <= rb && 32u * mul_words <= rb;
   return modexp_enqueue((int)(dev - g_devs), l, mod, count, d_bases, base_words, d_exps, exp_words, exp_shared,
-                        exp_bits, d_muls, mul_words, d_out, out_words);
+                        exp_bits, d_muls, mul_words, d_out, out_words, ops_fit);
 }
 
 int mpcx_modexp_batch(mpcx_mod_t mod, uint32_t count, const uint32_t* bases, uint32_t base_words,
@@ -1415,7 +1450,24 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
   Device& dev = g_devs[di];
   int rc = bind(dev);
   if (rc) return rc;
-  const int geom = choose_geom(dev, cls, (uint32_t)total);
+  bool main_ok = true, forced_ok = true;  // every segment's modulus and operands fit the geometry
+  {
+    const int gf = g_force_geom >= 0 && MPCX_GEOM_CLASS(g_force_geom) == cls ? g_force_geom : -1;
+    const uint32_t rb = (uint32_t)MPCX_GEOM_RBITS(g_main_geom[cls]);
+    for (uint32_t i = 0; i < n_groups && (main_ok || forced_ok); ++i) {
+      const mpcx_modexp_group_t& g = gs[i];
+      if (g.count == 0) continue;
+      const bool fit = host_ops_below(g.bases, g.count, g.base_words, rb) &&
+                       host_ops_below(g.muls, g.count, g.mul_words, rb);
+      main_ok = main_ok && geom_serves(g_main_geom[cls], g.mod, fit);
+      if (gf >= 0) {
+        const uint32_t rf = (uint32_t)MPCX_GEOM_RBITS(gf);
+        forced_ok = forced_ok && geom_serves(gf, g.mod, host_ops_below(g.bases, g.count, g.base_words, rf) &&
+                                                            host_ops_below(g.muls, g.count, g.mul_words, rf));
+      }
+    }
+  }
+  const int geom = choose_geom(dev, cls, (uint32_t)total, main_ok, forced_ok);
   const uint32_t G = (uint32_t)MPCX_GEOM_G(geom), K = (uint32_t)MPCX_GEOM_K(geom), L = (uint32_t)MPCX_GEOM_L(geom);
   // host-side layout of the packed inputs and outputs (words)
   struct Seg {
@@ -1862,7 +1914,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   std::lock_guard<std::mutex> blk(bl.mu);
   int rc;
   if ((rc = lane_stream(bl))) return rc;
-  const int geom = MPCX_MAIN_GEOM(mod->cls);
+  const int geom = MPCX_FULL_GEOM(mod->cls);  // the comb tables' layout
   const uint32_t L = (uint32_t)MPCX_GEOM_L(geom), P = (uint32_t)MPCX_GEOM_P(geom), K = (uint32_t)MPCX_GEOM_K(geom);
   // window width: the configured one, narrowed until the table fits
   // MPCX_FB_MAX_TABLE_BYTES (one product per window; 2^w entries per window)
@@ -1911,7 +1963,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     cleanup();
     return hip_fail(e, "upload fixed-base inputs");
   }
-  rc = modexp_enqueue(di, bl, mod, nwin, d_b, cw, d_e1, ew1, 0, wb * (nwin - 1) + 1, nullptr, 0, d_bj, cw);
+  rc = modexp_enqueue(di, bl, mod, nwin, d_b, cw, d_e1, ew1, 0, wb * (nwin - 1) + 1, nullptr, 0, d_bj, cw, false);
   // T(j, v) = R * b_j^v: operand i = j*nv + (v-1) takes base b_j -> replicate b_j rows
   std::vector<uint32_t> hbj((size_t)nwin * cw), hb2;
   if (!rc) rc = d2h_sync(hbj.data(), d_bj, hbj.size() * 4, bl);
@@ -1929,7 +1981,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     for (size_t off = 0; off < n2 && !rc; off += kFbBuildSlice) {
       const uint32_t cnt = (uint32_t)std::min<size_t>(kFbBuildSlice, n2 - off);
       rc = modexp_enqueue(di, bl, mod, cnt, d_b + off * cw, cw, d_e2 + off, 1, 0, wb, d_m + off * mod->words,
-                          mod->words, d_t + off * cw, cw);
+                          mod->words, d_t + off * cw, cw, false);
     }
   std::vector<uint32_t> ht(n2 * cw);
   if (!rc) rc = d2h_sync(ht.data(), d_t, ht.size() * 4, bl);
@@ -1943,7 +1995,8 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   // digits, [k][p] interleaved per entry
   const size_t ent_words = L;
   auto& tab = fb->host_table;
-  tab.assign((size_t)nwin * entries * ent_words, 0);
+  fb->table_words = (size_t)nwin * entries * ent_words;
+  tab.assign(fb->table_words, 0);
   auto put = [&](size_t ent, const std::vector<uint32_t>& words) {
     const std::vector<uint32_t> d = to_digits(words, L);
     uint32_t* dst = &tab[ent * ent_words];
@@ -2058,7 +2111,7 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     a.n0inv = mod->n0inv;
     const uint32_t waves = (n + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
     const int ks = kstat_begin(l);
-    hipError_t e = geom == MPCX_MAIN_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
+    hipError_t e = geom == MPCX_FULL_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
                                              : mpcx_launch_fixedbase_g1(&a, waves, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
@@ -2082,6 +2135,165 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     }
     return d2h_sync(out + (size_t)first * out_words, sg[2].ptr, ob, l);
   });
+}
+
+// One comb group's checks (mpcx_fixedbase_exp_batch's rules) and the windows
+// its launch processes per base (the longest exponent's).
+static int fb_group_check(const mpcx_fixedbase_group_t& g, uint32_t gi, uint32_t* nwin) {
+  if (g.nbases == 0 || g.nbases > MPCX_FB_MAX_BASES)
+    return fail(MPCX_EINVAL, "group %u: nbases %u outside [1, %d]", gi, g.nbases, MPCX_FB_MAX_BASES);
+  for (uint32_t t = 0; t < g.nbases; ++t) {
+    if (!g.fbs[t]) return fail(MPCX_EINVAL, "group %u: null fixed base %u", gi, t);
+    if (g.fbs[t]->mod != g.fbs[0]->mod) return fail(MPCX_EINVAL, "group %u: fixed bases of different moduli", gi);
+  }
+  mpcx_mod_t mod = g.fbs[0]->mod;
+  const uint32_t cw = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
+  if (g.out_words < mod->words) return fail(MPCX_EINVAL, "group %u: out_words < modulus words", gi);
+  if (g.muls && (g.mul_words == 0 || g.mul_words > cw)) return fail(MPCX_EINVAL, "group %u: mul_words", gi);
+  if (g.count && !g.out) return fail(MPCX_EINVAL, "group %u: null output", gi);
+  for (uint32_t t = 0; t < g.nbases; ++t) {
+    if (g.exp_words[t] && !g.exps[t]) return fail(MPCX_EINVAL, "group %u: null exponents %u", gi, t);
+    uint32_t bits = 0;
+    for (uint32_t i = 0; i < g.count && g.exp_words[t]; ++i)
+      bits = std::max(bits, bit_length_words(g.exps[t] + (size_t)i * g.exp_words[t], g.exp_words[t]));
+    const uint32_t wb = g.fbs[t]->wbits;
+    if (bits > g.fbs[t]->nwin * wb)
+      return fail(MPCX_EINVAL, "group %u: exponent of %u bits > fixed-base table's %u", gi, bits, g.fbs[t]->nwin * wb);
+    nwin[t] = (bits + wb - 1) / wb;
+  }
+  return MPCX_OK;
+}
+
+int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* gs) {
+  if (n_groups == 0) return MPCX_OK;
+  if (!gs) return fail(MPCX_EINVAL, "null groups");
+  const int n = ndev_or_fail();
+  if (n < 0) return -n;
+  int cls = -1, rc;
+  uint64_t total = 0;
+  std::vector<uint32_t> nwin((size_t)n_groups * MPCX_FB_MAX_BASES, 0);
+  for (uint32_t i = 0; i < n_groups; ++i) {
+    if ((rc = fb_group_check(gs[i], i, &nwin[(size_t)i * MPCX_FB_MAX_BASES]))) return rc;
+    const int c = gs[i].fbs[0]->mod->cls;
+    if (cls < 0) cls = c;
+    if (c != cls) return fail(MPCX_EINVAL, "group %u: modulus class differs from group 0's", i);
+    total += gs[i].count;
+  }
+  if (total == 0) return MPCX_OK;
+  if (total > 0xFFFFFFFFull) return fail(MPCX_EINVAL, "too many operands");
+  const int di = (int)(g_dev_rr.fetch_add(1, std::memory_order_relaxed) % (unsigned)n);
+  Device& dev = g_devs[di];
+  if ((rc = bind(dev))) return rc;
+  const int geom = MPCX_FULL_GEOM(cls);  // the tables' layout
+  const uint32_t G = (uint32_t)MPCX_GEOM_G(geom), L = (uint32_t)MPCX_GEOM_L(geom);
+  struct Seg {
+    uint32_t gi, waves;
+    size_t in_e[MPCX_FB_MAX_BASES], in_m, out_o;
+  };
+  std::vector<Seg> segs;
+  size_t in_words = 0, out_words = 0;
+  for (uint32_t i = 0; i < n_groups; ++i) {
+    const mpcx_fixedbase_group_t& g = gs[i];
+    if (g.count == 0) continue;
+    Seg sg{};
+    sg.gi = i;
+    sg.waves = (g.count + G - 1) / G;
+    for (uint32_t t = 0; t < g.nbases; ++t) {
+      sg.in_e[t] = in_words;
+      in_words += (size_t)g.count * g.exp_words[t];
+    }
+    sg.in_m = in_words;
+    if (g.muls) in_words += (size_t)g.count * g.mul_words;
+    sg.out_o = out_words;
+    out_words += (size_t)g.count * g.out_words;
+    segs.push_back(sg);
+  }
+  const size_t nseg = segs.size();
+  const size_t seg_bytes = nseg * sizeof(mpcx::FixedBaseArgs), first_bytes = (nseg + 1) * sizeof(uint32_t);
+  std::unique_lock<std::mutex> lk;
+  Lane& l = acquire_lane(dev, lk);
+  if ((rc = lane_stream(l))) return rc;
+  if ((rc = ensure_buffer(l.stage[0], std::max<size_t>(in_words * 4, 4))) ||
+      (rc = ensure_buffer(l.stage[2], out_words * 4)) || (rc = ensure_buffer(l.stage[3], seg_bytes + first_bytes)))
+    return rc;
+  uint32_t* d_in = (uint32_t*)l.stage[0].ptr;
+  uint32_t* d_out = (uint32_t*)l.stage[2].ptr;
+  std::vector<mpcx::FixedBaseArgs> args(nseg);
+  std::vector<uint32_t> first(nseg + 1, 0);
+  for (size_t k = 0; k < nseg; ++k) {
+    const Seg& sg = segs[k];
+    const mpcx_fixedbase_group_t& g = gs[sg.gi];
+    mpcx_mod_t mod = g.fbs[0]->mod;
+    for (uint32_t t = 0; t < g.nbases; ++t)
+      if ((rc = h2d(d_in + sg.in_e[t], g.exps[t], (size_t)g.count * g.exp_words[t] * 4, l.st))) return rc;
+    if (g.muls && (rc = h2d(d_in + sg.in_m, g.muls, (size_t)g.count * g.mul_words * 4, l.st))) return rc;
+    const uint32_t* dconst = nullptr;
+    if ((rc = mod_const(mod, di, &dconst))) return rc;
+    mpcx::FixedBaseArgs& a = args[k];
+    a.nd = dconst + mod->const_off[geom];
+    a.r1d = a.nd + L;
+    a.r2d = a.nd + 2 * L;
+    for (uint32_t t = 0; t < g.nbases; ++t) {
+      const uint32_t* dt = nullptr;
+      if ((rc = fb_table(g.fbs[t], di, &dt))) return rc;
+      a.tables[t] = dt;
+      a.exps[t] = d_in + sg.in_e[t];
+      a.exp_words[t] = g.exp_words[t];
+      a.nwin[t] = nwin[(size_t)sg.gi * MPCX_FB_MAX_BASES + t];
+      a.wbits[t] = g.fbs[t]->wbits;
+    }
+    a.nbases = g.nbases;
+    a.mul = g.muls ? d_in + sg.in_m : nullptr;
+    a.mul_words = g.muls ? g.mul_words : 0;
+    a.out = d_out + sg.out_o;
+    a.out_words = g.out_words;
+    a.count = g.count;
+    a.n0inv = mod->n0inv;
+    first[k + 1] = first[k] + sg.waves;
+  }
+  if ((rc = h2d(l.stage[3].ptr, args.data(), seg_bytes, l.st)) ||
+      (rc = h2d((char*)l.stage[3].ptr + seg_bytes, first.data(), first_bytes, l.st)))
+    return rc;
+  const int ks = kstat_begin(l);
+  const mpcx::FixedBaseArgs* dsegs = (const mpcx::FixedBaseArgs*)l.stage[3].ptr;
+  const uint32_t* dfirst = (const uint32_t*)((const char*)l.stage[3].ptr + seg_bytes);
+  hipError_t e = geom == MPCX_FULL_GEOM(0)
+                     ? mpcx_launch_fixedbase_multi_g0(dsegs, dfirst, (uint32_t)nseg, first[nseg], l.st)
+                     : mpcx_launch_fixedbase_multi_g1(dsegs, dfirst, (uint32_t)nseg, first[nseg], l.st);
+  if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase_multi");
+  dev.launches.fetch_add(1, std::memory_order_relaxed);
+  {
+    // as mpcx_fixedbase_exp_batch: Go-equivalent work per base exponent (launch
+    // log), executed products x 2 L^2 (kernel stats)
+    double alg_all = 0.0, exec = 0.0;
+    uint32_t ops = 0;
+    for (const auto& sg : segs) {
+      const mpcx_fixedbase_group_t& g = gs[sg.gi];
+      mpcx_mod_t mod = g.fbs[0]->mod;
+      const double l2 = 2.0 * (double)((mod->bits + 31) / 32) * (double)((mod->bits + 31) / 32);
+      double alg = 0.0;
+      uint32_t eb_max = 0;
+      for (uint32_t t = 0; t < g.nbases; ++t)
+        for (uint32_t i = 0; i < g.count && g.exp_words[t]; ++i) {
+          const uint32_t b = bit_length_words(g.exps[t] + (size_t)i * g.exp_words[t], g.exp_words[t]);
+          alg += go_macs(mod->bits, b);
+          exec += (double)((b + g.fbs[t]->wbits - 1) / g.fbs[t]->wbits) * l2;
+          eb_max = std::max(eb_max, b);
+        }
+      if (g.muls) exec += (double)g.count * l2;
+      launch_log("fixedbase_multi", geom, g.count, mod->bits, eb_max, alg);
+      alg_all += alg;
+      ops += g.count;
+    }
+    (void)alg_all;
+    kstat_end(l, ks, dev, di, "fixedbase_multi", geom, ops, exec);
+  }
+  for (const auto& sg : segs) {  // results straight into each group's buffer
+    const mpcx_fixedbase_group_t& g = gs[sg.gi];
+    e = hipMemcpyAsync(g.out, d_out + sg.out_o, (size_t)g.count * g.out_words * 4, hipMemcpyDeviceToHost, l.st);
+    if (e != hipSuccess) return hip_fail(e, "copy results");
+  }
+  return lane_wait(l);
 }
 
 // ------------------------------------------------------------ safe-prime sieve

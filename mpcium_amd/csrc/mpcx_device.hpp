@@ -54,14 +54,8 @@
 #ifndef MPCX_SQR_B2
 #define MPCX_SQR_B2 1  // k_modexp / k_prime2c squarings read 2*b from LDS (no per-iteration doubling)
 #endif
-#ifndef MPCX_FB_PREFETCH
-#define MPCX_FB_PREFETCH 0  // 1: k_fixedbase loads the next table entry during the current product (measured slower)
-#endif
 #ifndef MPCX_BLOCK_FENCE
 #define MPCX_BLOCK_FENCE 0  // scheduling fence between montmul's P blocks (1: all, 2: K >= 16; the prime kernels' TU sets 1)
-#endif
-#ifndef MPCX_MID_CARRY
-#define MPCX_MID_CARRY 0  // montmul: an extra carry pass half-way through the L iterations (not needed, see montmul)
 #endif
 #ifndef MPCX_PRIME2C_DBL_FOLD
 #define MPCX_PRIME2C_DBL_FOLD 1  // k_prime2c: the square-and-double step as one product with B = 2^bit x
@@ -274,7 +268,6 @@ __device__ __forceinline__ void montmul(uint32_t (&A)[K], const uint32_t* bl, co
     // squaring row of k_prime2c, whose digits reach 2^30.01) plus a < 2^35
     // fold: < 2^62.8 for K <= 37. profiles/r03/kernel_ab: dropping the pass
     // took the config-2 kernel from 176.3 to 171.7 ms.
-    if (MPCX_MID_CARRY && o == P / 2 - 1) carry_pass64<P, K>(acc);
     // block boundary as a scheduling fence (mpcx_prime.hip: without it
     // k_prime2c's live ranges grew past its 3-wave budget and spilled; the
     // k_modexp geometries fit better without it). 2: long blocks only (K >= 16).
@@ -627,8 +620,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 // for the same Exp. Every operand multiplies in every window (v = 0 reads
 // the Montgomery one), so the wave never diverges; windows above every
 // operand's exponent are skipped by a wave-uniform ballot.
-template <int P, int K, int G, int WPE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase(const FixedBaseArgs a) {
+template <int P, int K, int G>
+__device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uint32_t blk) {
   constexpr int L = P * K;
   __shared__ uint32_t lds[(G + 1) * L + 2];
   const int lane = threadIdx.x;
@@ -636,7 +629,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   const bool idle = g_raw >= G;
   const int g = idle ? G : g_raw;
   const int p = lane - g_raw * P;
-  const uint32_t op = blockIdx.x * G + (idle ? 0 : g_raw);
+  const uint32_t op = blk * G + (idle ? 0 : g_raw);
   const bool active = !idle && op < a.count;
   uint32_t* bl = lds + g * L;
   const int m_src_addr = (idle ? lane : g_raw * P) * 4;
@@ -651,10 +644,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     lds_store_digits<K>(bl, p, t);
   };
   // ONE montmul call site (three would triple the unrolled product and its
-  // register allocation). MPCX_FB_PREFETCH=1 loads the next product's table
-  // entry (one scattered 304-B read per operand) into registers while the
-  // current product runs; measured 6% slower on config 5 than loading it
-  // after the product (profiles/r03/fb_prefetch), so it is off.
+  // register allocation). The next product's table entry is loaded after the
+  // current product: loading it during the product (registers held across it)
+  // measured 6% slower on config 5 (profiles/r03/fb_prefetch).
   uint32_t t = 0, j = 0;  // next window: base t, window j
   uint32_t nx[K];         // the next product's B digits, in flight
   // nx <- the next window with bits in some operand of the wave, else the exit
@@ -708,12 +700,30 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
     if (!b_in_lds) lds_store_digits<K>(bl, p, nx);
     b_in_lds = false;
     wave_lds_fence();
-    if (MPCX_FB_PREFETCH) more = fetch();  // the following B's loads overlap this product
     montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
     wave_lds_fence();
-    if (!MPCX_FB_PREFETCH) more = fetch();
+    more = fetch();
   }
   store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
+}
+
+template <int P, int K, int G, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase(const FixedBaseArgs a) {
+  fixedbase_wave<P, K, G>(a, blockIdx.x);
+}
+
+// Several comb batches in one launch (mpcx_fixedbase_multi_batch: concurrent
+// callers' batches -- other tables, other moduli of the class, muls or not):
+// segment s owns wavefronts [first[s], first[s+1]) and its own FixedBaseArgs,
+// read wave-uniformly, as k_modexp_multi does for exponentiations.
+template <int P, int K, int G, int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase_multi(
+    const FixedBaseArgs* __restrict__ segs, const uint32_t* __restrict__ first, uint32_t nsegs) {
+  const uint32_t b = blockIdx.x;
+  uint32_t s = 0;
+  while (s + 1u < nsegs && __builtin_amdgcn_readfirstlane(first[s + 1u]) <= b) ++s;
+  s = __builtin_amdgcn_readfirstlane(s);
+  fixedbase_wave<P, K, G>(segs[s], b - __builtin_amdgcn_readfirstlane(first[s]));
 }
 
 // ------------------------------------------- per-candidate-modulus helpers

@@ -17,7 +17,7 @@
 #elif MPCX_GEOM_ID == 3 || MPCX_GEOM_ID == 4
 #define MPCX_WPE 8
 #elif MPCX_GEOM_ID == 5
-#define MPCX_WPE 2
+#define MPCX_WPE 2  // K = 37 per lane, as geometry 2
 #else
 #define MPCX_WPE 3
 #endif
@@ -66,13 +66,22 @@ __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_mul
   return hipGetLastError();
 }
 
-#if MPCX_GEOM_ID == MPCX_MAIN_GEOM(0) || MPCX_GEOM_ID == MPCX_MAIN_GEOM(1)
+#if MPCX_GEOM_ID == MPCX_FULL_GEOM(0) || MPCX_GEOM_ID == MPCX_FULL_GEOM(1)
 // fixed-base comb kernel: main geometry of the <= 2080-bit classes (N~, N; tables are laid out for it)
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_fixedbase_g, MPCX_GEOM_ID)(
     const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st) {
   hipLaunchKernelGGL((mpcx::k_fixedbase<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
                                         MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>),
                      dim3(waves), dim3(64), 0, st, *a);
+  return hipGetLastError();
+}
+
+// several comb batches in one launch: segs / first are device arrays of nsegs entries
+__attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_fixedbase_multi_g, MPCX_GEOM_ID)(
+    const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs, uint32_t waves, hipStream_t st) {
+  hipLaunchKernelGGL((mpcx::k_fixedbase_multi<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
+                                              MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>),
+                     dim3(waves), dim3(64), 0, st, segs, first, nsegs);
   return hipGetLastError();
 }
 #endif

@@ -20,30 +20,37 @@
 #define MPCX_CLASS_MAXBITS(c) (32 * MPCX_CLASS_WORDS(c))
 
 // Geometries (id: P x K, G, class):
-//   0: 1 x 37, 64, class 0  thread per operand (1024-bit safe-prime candidates)
-//   1: 4 x 19, 16, class 1  quad per operand: m_i broadcast by DPP quad_perm (N, N~)
+//   0: 1 x 37, 64, class 0  thread per operand (1024-bit safe-prime candidates, CRT halves)
+//   1: 4 x 19, 16, class 1  quad per operand: m_i broadcast by DPP quad_perm (moduli of
+//                           2071..2080 bits; fixed-base comb tables)
 //   2: 4 x 37, 16, class 2  quad per operand (Paillier N^2)
 //   3: 16 x 5,  4, class 1  narrow: small latency-bound batches; one DPP row per operand,
 //                           m_i broadcast by DPP row_newbcast
 //   4: 32 x 5,  2, class 2  narrow; two DPP rows per operand, m_i by row_newbcast + row_bcast:15
-//   5: 3 x 25, 21, class 1  7-lane/3-lane groups, m_i by ds_bpermute (round-1 main)
+//   5: 2 x 37, 32, class 1  lane pair per operand, m_i by DPP quad_perm [0,0,2,2]: the 2048-bit
+//                           main geometry (N, N~). L = 74 < the class's L_min: R = 2^2072 > 4m
+//                           needs m < 2^2070 and operands < 2^2072 (MPCX_GEOM_RBITS), checked
+//                           per launch; otherwise geometry 1 serves the launch
 //   6: 8 x 19,  8, class 2  mid: batches of a fraction of a main round (twice the main
 //                           geometry's wavefronts, 3 per SIMD); m_i by quad_perm + row_shr:4
-//   7: 2 x 19, 32, class 0  lane pair per operand (the k_prime2c layout): m_i by quad_perm
-//                           [0,0,2,2]; 3 waves per SIMD instead of geometry 0's lone serial chain
-#define MPCX_NUM_GEOMS 8
+#define MPCX_NUM_GEOMS 7
 #define MPCX_GEOM_P(g) \
-  ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 16 : (g) == 4 ? 32 : (g) == 5 ? 3 : (g) == 6 ? 8 : 2)
+  ((g) == 0 ? 1 : (g) == 1 ? 4 : (g) == 2 ? 4 : (g) == 3 ? 16 : (g) == 4 ? 32 : (g) == 5 ? 2 : 8)
 #define MPCX_GEOM_K(g) \
-  ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 5 : (g) == 5 ? 25 : 19)
+  ((g) == 0 ? 37 : (g) == 1 ? 19 : (g) == 2 ? 37 : (g) == 3 ? 5 : (g) == 4 ? 5 : (g) == 5 ? 37 : 19)
 #define MPCX_GEOM_G(g) \
-  ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 2 : (g) == 5 ? 21 : (g) == 6 ? 8 : 32)
-#define MPCX_GEOM_CLASS(g) (((g) == 0 || (g) == 7) ? 0 : ((g) == 1 || (g) == 3 || (g) == 5) ? 1 : 2)
+  ((g) == 0 ? 64 : (g) == 1 ? 16 : (g) == 2 ? 16 : (g) == 3 ? 4 : (g) == 4 ? 2 : (g) == 5 ? 32 : 8)
+#define MPCX_GEOM_CLASS(g) ((g) == 0 ? 0 : ((g) == 1 || (g) == 3 || (g) == 5) ? 1 : 2)
 #define MPCX_GEOM_L(g) (MPCX_GEOM_P(g) * MPCX_GEOM_K(g))
+// bits of R = 2^(28 L): a geometry serves moduli m with 4m < R and operands below R
+#define MPCX_GEOM_RBITS(g) (28 * MPCX_GEOM_L(g))
 // default main (throughput) and narrow geometry of each class
-#define MPCX_MAIN_GEOM(c) ((c) == 0 ? 0 : (c) == 1 ? 1 : 2)
+#define MPCX_MAIN_GEOM(c) ((c) == 0 ? 0 : (c) == 1 ? 5 : 2)
 #define MPCX_NARROW_GEOM(c) ((c) == 1 ? 3 : (c) == 2 ? 4 : -1)
 #define MPCX_MID_GEOM(c) ((c) == 2 ? 6 : -1)
+// the geometry every modulus of the class can use (L >= L_min), and the layout of
+// the class's fixed-base comb tables
+#define MPCX_FULL_GEOM(c) ((c) == 0 ? 0 : (c) == 1 ? 1 : 2)
 // 1024-bit class used by the Fermat / Miller-Rabin kernels (thread per operand)
 #define MPCX_C0_K 37
 
@@ -102,7 +109,9 @@ struct ModexpArgs {
 #define MPCX_FB_WINDOW_BITS 12      // default width (option "fb_window")
 #define MPCX_FB_MAX_WINDOW_BITS 12
 #define MPCX_FB_MAX_TABLE_BYTES (512ull << 20)  // narrower windows above this per table
-#define MPCX_FB_MAX_BASES 2
+#ifndef MPCX_FB_MAX_BASES
+#define MPCX_FB_MAX_BASES 2  // also in include/mpcx.h
+#endif
 
 struct FixedBaseArgs {
   const uint32_t* nd;   // L digits of m

@@ -64,6 +64,7 @@ SIGNATURES = [
     ("mpcx_fixedbase_exp_batch", ctypes.c_int, [ctypes.c_uint32, ctypes.POINTER(_vp), ctypes.c_uint32,
                                                 ctypes.POINTER(_vp), _u32p, _vp, ctypes.c_uint32, _vp,
                                                 ctypes.c_uint32]),
+    ("mpcx_fixedbase_multi_batch", ctypes.c_int, [ctypes.c_uint32, _vp]),
     ("mpcx_lucas_batch", ctypes.c_int, [ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, _vp]),
     ("mpcx_safeprime_step", ctypes.c_int, [ctypes.c_uint64, _vp, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
                                            _vp, ctypes.c_uint32, ctypes.c_uint32, _u32p, _u32p, _vp, _vp, _vp]),
@@ -406,6 +407,46 @@ def fixedbase_exp(fbs: Sequence[FixedBase], exps: Sequence[Sequence[int]],
     _check(lib().mpcx_fixedbase_exp_batch(nb, hs, count, eps, ews, Mu.ctypes.data if Mu is not None else None,
                                           Mu.shape[1] if Mu is not None else 0, out.ctypes.data, mod.words))
     return words_to_ints(out)
+
+
+class FixedBaseGroup(ctypes.Structure):
+    """mpcx_fixedbase_group_t"""
+    _fields_ = [("nbases", ctypes.c_uint32), ("fbs", _vp * 2), ("count", ctypes.c_uint32), ("exps", _vp * 2),
+                ("exp_words", ctypes.c_uint32 * 2), ("muls", _vp), ("mul_words", ctypes.c_uint32), ("out", _vp),
+                ("out_words", ctypes.c_uint32)]
+
+
+def fixedbase_multi(groups) -> List[List[int]]:
+    """Several comb batches in one launch (mpcx_fixedbase_multi_batch): groups
+    of (fixed bases, exps[t][i], muls or None) -> [[mul_i * prod_t b_t^e_t,i mod m]
+    per group]; the groups' moduli share one size class."""
+    keep, outs = [], []
+    arr = (FixedBaseGroup * max(1, len(groups)))()
+    for i, (fbs, exps, muls) in enumerate(groups):
+        nb = len(fbs)
+        if nb != len(exps) or not 1 <= nb <= 2:
+            raise ValueError("one exponent list per fixed base (1 or 2)")
+        count = len(exps[0])
+        mod = fbs[0].mod
+        g = FixedBaseGroup()
+        g.nbases, g.count = nb, count
+        for t in range(nb):
+            E = ints_to_words(exps[t], max([nwords(v) for v in exps[t]] + [1]))
+            keep.append(E)
+            g.fbs[t] = fbs[t].handle
+            g.exps[t] = E.ctypes.data if count else None
+            g.exp_words[t] = E.shape[1]
+        Mu = mod._operands(muls, "muls") if muls is not None else None
+        keep.append(Mu)
+        g.muls = Mu.ctypes.data if Mu is not None else None
+        g.mul_words = mod.class_words if Mu is not None else 0
+        out = np.zeros((count, mod.words), dtype="<u4")
+        outs.append(out)
+        g.out = out.ctypes.data if count else None
+        g.out_words = mod.words
+        arr[i] = g
+    _check(lib().mpcx_fixedbase_multi_batch(len(groups), arr))
+    return [words_to_ints(o) if o.shape[0] else [] for o in outs]
 
 
 def exp_batch(m: int, bases: Sequence[int], exps: Union[int, Sequence[int]]) -> List[int]:

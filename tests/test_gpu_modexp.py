@@ -145,13 +145,14 @@ def test_exp_mul_and_mulmod(gpu, paillier_key):
         mod.release()
 
 
-@pytest.mark.parametrize("geom", [1, 2, 3, 4, 5, 6, 7])
+@pytest.mark.parametrize("geom", [1, 2, 3, 4, 5, 6])
 def test_each_geometry_forced(gpu, paillier_key, geom):
     """Every geometry of the 2048-bit (1, 3, 5) and 4096-bit (2, 4, 6) classes:
-    quad-per-operand main, narrow, and the 3/7-lane-group (bpermute) layouts;
-    and the 1024-bit class's lane-pair geometry 7 (modulus P)."""
+    quad-per-operand, lane-pair (5: the 2048-bit main geometry), narrow and
+    mid layouts, each forced for shared and per-operand exponents and the
+    fused multiplier."""
     N = paillier_key["N"]
-    m = N * N if geom in (2, 4, 6) else paillier_key["P"] if geom == 7 else N
+    m = N * N if geom in (2, 4, 6) else N
     rng = random.Random(geom)
     gpu.set_option("force_geom", geom)
     try:
@@ -163,6 +164,31 @@ def test_each_geometry_forced(gpu, paillier_key, geom):
         cs = [rng.randrange(m) for _ in xs]
         assert mod.exp_mul(xs, es, cs) == [c * pow(x, e, m) % m for x, e, c in zip(xs, es, cs)]
         mod.release()
+    finally:
+        gpu.set_option("force_geom", -1)
+
+
+@pytest.mark.parametrize("force", [-1, 5])
+def test_lane_pair_geometry_limits(gpu, paillier_key, force):
+    """Geometry 5 (2 x 37 digits, R = 2^2072) serves moduli below 2^2070 with
+    operands below 2^2072; a wider modulus of the class (up to 2080 bits), or
+    bases / multipliers of 2072..2080 bits (allowed by the class width, not
+    reduced by the caller), must run on geometry 1 instead -- default and
+    forced alike -- with results equal to pow()."""
+    N = paillier_key["N"]
+    rng = random.Random(2072)
+    gpu.set_option("force_geom", force)
+    try:
+        for m in (N, (1 << 2079) + rng.getrandbits(2078) | 1, (1 << 2069) + 1 + 2 * rng.getrandbits(2060)):
+            mod = gpu.Modulus(m)
+            top = 1 << (32 * mod.class_words)
+            xs = [rng.randrange(m) for _ in range(33)] + [top - 1 - rng.getrandbits(20) for _ in range(3)]
+            es = [rng.getrandbits(rng.choice([1, 64, 2048])) for _ in xs]
+            assert mod.exp(xs, N) == [pow(x, N, m) for x in xs], m.bit_length()
+            assert mod.exp(xs, es) == [pow(x, e, m) for x, e in zip(xs, es)], m.bit_length()
+            cs = [rng.randrange(m) for _ in xs[:-1]] + [top - 5]
+            assert mod.exp_mul(xs, es, cs) == [c * pow(x, e, m) % m for x, e, c in zip(xs, es, cs)]
+            mod.release()
     finally:
         gpu.set_option("force_geom", -1)
 
@@ -276,6 +302,49 @@ def test_fixed_base_tables(gpu, paillier_key, wbits):
     f2.release()
     f1.release()
     mod.release()
+
+
+def test_fixed_base_multi_batch(gpu, paillier_key):
+    """mpcx_fixedbase_multi_batch: comb groups of two different 2048-bit moduli
+    (other tables, one and two bases, with and without multipliers, an empty
+    and a one-operand group) as the segments of ONE launch equal pow(); groups
+    of two classes are refused; a group's exponent past its table fails."""
+    N, P = paillier_key["N"], paillier_key["P"]
+    rng = random.Random(4242)
+    m2 = rng.getrandbits(2046) | 1 | (1 << 2045)
+    mods = [gpu.Modulus(N), gpu.Modulus(m2)]
+    hs = [(rng.randrange(N), rng.randrange(N)), (rng.randrange(m2), rng.randrange(m2))]
+    fbs = [(gpu.FixedBase(mods[0], hs[0][0], 2816), gpu.FixedBase(mods[0], hs[0][1], 2816)),
+           (gpu.FixedBase(mods[1], hs[1][0], 1024), gpu.FixedBase(mods[1], hs[1][1], 1024))]
+    groups, want = [], []
+    for k, (count, nb, mul) in enumerate([(70, 2, False), (0, 1, False), (33, 1, True), (1, 2, True), (200, 2, True)]):
+        mi = k % 2
+        m = mods[mi].m
+        bits = 2816 if mi == 0 else 1024
+        es = [[rng.getrandbits(rng.choice([0, 5, bits // 2, bits])) for _ in range(count)] for _ in range(nb)]
+        cs = [rng.randrange(m) for _ in range(count)] if mul else None
+        groups.append((list(fbs[mi][:nb]), es, cs))
+        w = []
+        for i in range(count):
+            v = cs[i] if mul else 1
+            for t in range(nb):
+                v = v * pow(hs[mi][t], es[t][i], m) % m
+            w.append(v)
+        want.append(w)
+    assert gpu.fixedbase_multi(groups) == want
+    pm = gpu.Modulus(P)
+    fp = gpu.FixedBase(pm, 5, 64)
+    with pytest.raises(gpu.MpcxError):  # 1024-bit and 2048-bit classes in one launch
+        gpu.fixedbase_multi([([fp], [[3]], None), ([fbs[0][0]], [[3]], None)])
+    with pytest.raises(gpu.MpcxError):
+        gpu.fixedbase_multi([([fbs[1][0]], [[1 << 1100]], None)])
+    fp.release()
+    pm.release()
+    for pair in fbs:
+        for f in pair:
+            f.release()
+    for md in mods:
+        md.release()
 
 
 def test_multi_batch_groups_of_different_moduli(gpu):

@@ -9,6 +9,7 @@
 #   bash tools/gpu.sh ab     OUT N LIB_A LIB_B [bench args]  N interleaved config-2 runs per libmpcx build
 #   bash tools/gpu.sh abswap OUT N LIB_A LIB_B [bench args]  N interleaved full-bench runs, LIB swapped in place
 #   bash tools/gpu.sh envab  OUT N "ENV_A" "ENV_B" [bench args]  N interleaved runs under two environments
+#   bash tools/gpu.sh argab  OUT N "ARGS_A" "ARGS_B" [bench args]  N interleaved runs with two bench.py argument sets
 #   bash tools/gpu.sh py     OUT script.py [args]            any python tool (tools/*.py) under a 600 s limit
 set -o pipefail
 mode=$1; O=gpurun_out/$2; shift 2
@@ -108,6 +109,17 @@ envab)
       env $ev timeout -k 10 600 python3 bench.py --detail $O/ab_${e}_$i.json "$@" > $O/ab_${e}_$i.line 2> $O/ab_${e}_$i.err \
           || { tail $O/ab_${e}_$i.err; exit 1; }
       echo "== $e ($ev) run $i"; summ $O/ab_${e}_$i.json
+    done
+  done ;;
+argab)
+  # N interleaved runs of bench.py with two extra-argument strings A and B (same build)
+  n=$1; aa=$2; ab=$3; shift 3
+  for i in $(seq 1 $n); do
+    for e in A B; do
+      [ $e = A ] && ex="$aa" || ex="$ab"
+      timeout -k 10 600 python3 bench.py --detail $O/ab_${e}_$i.json $ex "$@" > $O/ab_${e}_$i.line 2> $O/ab_${e}_$i.err \
+          || { tail $O/ab_${e}_$i.err; exit 1; }
+      echo "== $e ($ex) run $i"; summ $O/ab_${e}_$i.json
     done
   done ;;
 py)
