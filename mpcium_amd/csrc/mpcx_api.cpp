@@ -1992,7 +1992,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   fb->geom = geom;
   fb->nwin = nwin;
   fb->wbits = wb;
-  // digits, [k][p] interleaved per entry
+  // digits per entry: natural order (MPCX_FB_DMA) or [k][p] interleaved
   const size_t ent_words = L;
   auto& tab = fb->host_table;
   fb->table_words = (size_t)nwin * entries * ent_words;
@@ -2000,8 +2000,12 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   auto put = [&](size_t ent, const std::vector<uint32_t>& words) {
     const std::vector<uint32_t> d = to_digits(words, L);
     uint32_t* dst = &tab[ent * ent_words];
-    for (uint32_t pp = 0; pp < P; ++pp)
-      for (uint32_t k = 0; k < K; ++k) dst[k * P + pp] = d[pp * K + k];
+    if (MPCX_FB_DMA) {  // natural digit order: one LDS-DMA dword per digit
+      std::memcpy(dst, d.data(), (size_t)L * 4);
+    } else {
+      for (uint32_t pp = 0; pp < P; ++pp)
+        for (uint32_t k = 0; k < K; ++k) dst[k * P + pp] = d[pp * K + k];
+    }
   };
   // 2^w entries per window: the conversion to interleaved digits runs on the
   // host threads (a 12-bit table is ~1M entries)
@@ -2150,7 +2154,8 @@ static int fb_group_check(const mpcx_fixedbase_group_t& g, uint32_t gi, uint32_t
   const uint32_t cw = (uint32_t)MPCX_CLASS_WORDS(mod->cls);
   if (g.out_words < mod->words) return fail(MPCX_EINVAL, "group %u: out_words < modulus words", gi);
   if (g.muls && (g.mul_words == 0 || g.mul_words > cw)) return fail(MPCX_EINVAL, "group %u: mul_words", gi);
-  if (g.count && !g.out) return fail(MPCX_EINVAL, "group %u: null output", gi);
+  if (g.count == 0) return MPCX_OK;  // an empty group's buffers may be null
+  if (!g.out) return fail(MPCX_EINVAL, "group %u: null output", gi);
   for (uint32_t t = 0; t < g.nbases; ++t) {
     if (g.exp_words[t] && !g.exps[t]) return fail(MPCX_EINVAL, "group %u: null exponents %u", gi, t);
     uint32_t bits = 0;
