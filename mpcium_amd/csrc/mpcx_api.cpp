@@ -1992,7 +1992,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   fb->geom = geom;
   fb->nwin = nwin;
   fb->wbits = wb;
-  // digits per entry: natural order (MPCX_FB_DMA) or [k][p] interleaved
+  // digits, [k][p] interleaved per entry (a group's P lanes read P consecutive words per slot)
   const size_t ent_words = L;
   auto& tab = fb->host_table;
   fb->table_words = (size_t)nwin * entries * ent_words;
@@ -2000,12 +2000,8 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   auto put = [&](size_t ent, const std::vector<uint32_t>& words) {
     const std::vector<uint32_t> d = to_digits(words, L);
     uint32_t* dst = &tab[ent * ent_words];
-    if (MPCX_FB_DMA) {  // natural digit order: one LDS-DMA dword per digit
-      std::memcpy(dst, d.data(), (size_t)L * 4);
-    } else {
-      for (uint32_t pp = 0; pp < P; ++pp)
-        for (uint32_t k = 0; k < K; ++k) dst[k * P + pp] = d[pp * K + k];
-    }
+    for (uint32_t pp = 0; pp < P; ++pp)
+      for (uint32_t k = 0; k < K; ++k) dst[k * P + pp] = d[pp * K + k];
   };
   // 2^w entries per window: the conversion to interleaved digits runs on the
   // host threads (a 12-bit table is ~1M entries)

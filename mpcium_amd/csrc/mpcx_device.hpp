@@ -620,7 +620,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 // for the same Exp. Every operand multiplies in every window (v = 0 reads
 // the Montgomery one), so the wave never diverges; windows above every
 // operand's exponent are skipped by a wave-uniform ballot.
-#if !MPCX_FB_DMA
 template <int P, int K, int G>
 __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uint32_t blk) {
   constexpr int L = P * K;
@@ -646,8 +645,10 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
   };
   // ONE montmul call site (three would triple the unrolled product and its
   // register allocation). The next product's table entry is loaded after the
-  // current product: loading it during the product (registers held across it)
-  // measured 6% slower on config 5 (profiles/r03/fb_prefetch).
+  // current product: loading it during the product into registers measured 6%
+  // slower on config 5 (profiles/r03/fb_prefetch), and staging it into a second
+  // LDS row set by LDS DMA (global_load_lds) 5-15% slower in isolation
+  // (profiles/r04/fb_dma_ab/isolated).
   uint32_t t = 0, j = 0;  // next window: base t, window j
   uint32_t nx[K];         // the next product's B digits, in flight
   // nx <- the next window with bits in some operand of the wave, else the exit
@@ -707,125 +708,6 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
   }
   store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
 }
-#else
-// LDS-DMA version (MPCX_FB_DMA, default): the next product's table entries go
-// straight from memory into the other half of a double-buffered LDS row set
-// (global_load_lds_dword, no VGPRs held) while the current product runs, so the
-// scattered 304-B entry reads no longer stall every product. Tables are in
-// natural digit order (entry word d = digit d), so LDS slot g*L + d of the wave's
-// row set is one lane's dword: G*L/64 DMA instructions per product.
-template <int P, int K, int G>
-__device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uint32_t blk) {
-  constexpr int L = P * K;
-  constexpr int ROW = (G + 1) * L + 2;       // one row set (+2: the b prefetch reads past a row)
-  constexpr int NDMA = (G * L + 63) / 64;    // DMA instructions per row set
-  static_assert(64 < 2 * L, "one wrap of the slot walk per DMA instruction step");
-  __shared__ uint32_t lds[2 * ROW];
-  __shared__ uint32_t vsh[G];                // the groups' window values of the staged product
-  const int lane = threadIdx.x;
-  const int g_raw = lane / P;
-  const bool idle = g_raw >= G;
-  const int g = idle ? G : g_raw;
-  const int p = lane - g_raw * P;
-  const uint32_t op = blk * G + (idle ? 0 : g_raw);
-  const bool active = !idle && op < a.count;
-  const int m_src_addr = (idle ? lane : g_raw * P) * 4;
-  auto row = [&](int c) __attribute__((always_inline)) { return lds + c * ROW + g * L; };
-
-  uint32_t Nd[K], A[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) Nd[k] = idle ? 0u : a.nd[p * K + k];
-
-  uint32_t t = 0, j = 0;  // next window: base t, window j
-  bool fin = false;
-  // stage the next product's B into row set c: the DMA of the next window
-  // with bits in some operand of the wave (true), else once the exit
-  // multiplier 1 (true), else nothing (false)
-  auto stage = [&](int c) __attribute__((always_inline)) -> bool {
-    for (; t < a.nbases; ++t, j = 0) {
-      const uint32_t ew = a.exp_words[t], wb = a.wbits[t];
-      const uint32_t* ex = a.exps[t] + (size_t)(active ? op : 0) * ew;
-      for (; j < a.nwin[t]; ++j) {
-        const uint32_t v = (active && ew) ? window_of(ex, j, wb, ew) : 0u;
-        if (__ballot(v != 0u) == 0ull) continue;  // no operand of the wave has bits here
-        if (!idle && p == 0) vsh[g] = v;
-        wave_lds_fence();
-        const uint32_t* tb = a.tables[t] + ((size_t)j << wb) * L;
-        uint32_t* dst = lds + c * ROW;
-        int gg = lane / L, d = lane - (lane / L) * L;  // slot jj*64 + lane = gg*L + d
-        // a rolled loop: unrolled, the scheduler batches every instruction's
-        // address math ahead of the DMAs and the kernel spills
-#pragma nounroll
-        for (int jj = 0; jj < NDMA; ++jj) {
-          const uint32_t vv = vsh[gg < G ? gg : G - 1];
-          __builtin_amdgcn_global_load_lds(tb + (size_t)vv * L + d,
-                                           (__attribute__((address_space(3))) void*)(dst + jj * 64), 4, 0, 0);
-          d += 64;
-          if (d >= L) {
-            d -= L;
-            ++gg;
-          }
-          if (d >= L) {
-            d -= L;
-            ++gg;
-          }
-        }
-        ++j;
-        return true;
-      }
-    }
-    if (fin) return false;
-    fin = true;  // leave the Montgomery domain: z = mont(z R, 1) <= m
-    uint32_t one[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
-    lds_store_digits<K>(row(c), p, one);
-    return true;
-  };
-
-  // B of the first product: R^2 (z = mul R = mont(mul, R^2)), or the first staged entry
-  int cur = 0;
-  bool more = true;
-  if (a.mul) {
-    uint32_t r2[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) r2[k] = idle ? 0u : a.r2d[p * K + k];
-    lds_store_digits<K>(row(0), p, r2);
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const uint32_t bit = (uint32_t)(p * K + k) * DB;
-      const uint32_t w = bit >> 5, sh = bit & 31u;
-      uint64_t v = 0;
-      if (active) {
-        const uint32_t* x = a.mul + (size_t)op * a.mul_words;
-        const uint32_t lo = w < a.mul_words ? x[w] : 0u;
-        const uint32_t hi = (w + 1) < a.mul_words ? x[w + 1] : 0u;
-        v = ((uint64_t)hi << 32) | lo;
-      }
-      A[k] = (uint32_t)(v >> sh) & M28;
-    }
-  } else {
-#pragma unroll
-    for (int k = 0; k < K; ++k) A[k] = idle ? 0u : a.r1d[p * K + k];  // z = R mod m
-    more = stage(0);
-  }
-  // every load so far has landed (the first staged entries, and N's digits:
-  // with one of those loads still counted as pending on some path into the
-  // loop, the compiler's wait for it lands inside montmul and would then also
-  // wait for each in-flight DMA)
-  __builtin_amdgcn_s_waitcnt(0);
-  wave_lds_fence();
-  while (more) {
-    const bool next = stage(cur ^ 1);  // its DMA overlaps this product
-    montmul<P, K, false>(A, row(cur), Nd, a.n0inv, m_src_addr, p);
-    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
-    wave_lds_fence();
-    more = next;
-    cur ^= 1;
-  }
-  store_result<P, K>(A, Nd, row(cur), p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
-}
-#endif
 
 template <int P, int K, int G, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase(const FixedBaseArgs a) {

@@ -109,12 +109,6 @@ struct ModexpArgs {
 #define MPCX_FB_WINDOW_BITS 12      // default width (option "fb_window")
 #define MPCX_FB_MAX_WINDOW_BITS 12
 #define MPCX_FB_MAX_TABLE_BYTES (512ull << 20)  // narrower windows above this per table
-// 1 (default): k_fixedbase stages the next product's table entries by LDS DMA
-// and tables are in natural digit order; 0: register loads, tables [slot k][lane p]
-// interleaved (round 3)
-#ifndef MPCX_FB_DMA
-#define MPCX_FB_DMA 1
-#endif
 #ifndef MPCX_FB_MAX_BASES
 #define MPCX_FB_MAX_BASES 2  // also in include/mpcx.h
 #endif
