@@ -1074,6 +1074,12 @@ int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K,
 // per wavefront) trade per-operand work for a finer split. x^N mod N^2 for
 // 1.25K / 5K / 10K / 20K / 30K / 40K operands: main 49 / 49 / 50 / 91 / 93 / 135 ms,
 // mid 32 / 32 / 55 / 83 / 107 / 134 ms, narrow 20 / 41 / 65 / 119 / 175 / 230 ms.
+//
+// The 2048-bit class keeps the narrow_rounds threshold: the same kind of model
+// fitted to its geometries (tools/geom_sweep.py --class 1,
+// profiles/r04/geom_sweep_c1/: lane pair 25.4 ms per wavefront-per-SIMD step,
+// 4 x 19 at 0.556 and 16 x 5 at 0.226 of it) sent mid-size batches to 4 x 19 and
+// measured 7% slower on config 5's concurrent load (profiles/r04/c1model_ab/).
 static int fastest_geom(int cls, uint32_t count, int nsimd) {
   struct M {
     int g;
