@@ -172,3 +172,36 @@ def test_two_logical_devices(gpu):
     assert s["errors"] == 0 and s["relation_failures"] == 0 and s["verified"] == 300 and s["aborted"] == 0
     assert out["keygen"]["failures"] == 0 and out["keygen"]["waves"] == 2
     assert all(n > 0 for n in out["work_launches"]), out["work_launches"]
+
+
+def test_bench_two_ranks(gpu, tmp_path):
+    """The driver's N-GPU bench path end to end, at small sizes: `bench.py
+    --gpus 2` without a launcher re-launches itself under torchrun (two ranks;
+    LOCAL_RANK wraps onto this box's GPU), every rank runs its own config-2
+    batch (checked against pow on a sample inside bench.py), signing wallets,
+    config-1 batches and config-5 sessions, the safe-prime search is sharded,
+    and rank 0 prints ONE parseable line with n_gpus 2 and every config."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    detail = tmp_path / "detail.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
+           "--count", "4096", "--wallets", "300", "--keygen-sessions", "64", "--keygen-wave", "32",
+           "--safe-primes", "8", "--no-cpu-baseline", "--no-smi", "--detail", str(detail)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert len(lines[0]) <= 4096
+    assert line["n_gpus"] == 2 and line["scaling"] == "weak"
+    assert line["value"] > 0 and line["roofline"]["frac"] > 0
+    for k in ("c1_paillier", "c3_safe_primes", "c4_sign", "c4_sign_3_signers", "c5_keygen"):
+        assert line["configs"][k]["n_gpus"] == 2, k
+        assert line["configs"][k]["value"] > 0, k
+    full = json.load(open(detail))
+    assert full["signing"]["signatures_verified"] == 600
+    assert full["keygen"]["sessions"] == 64
