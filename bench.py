@@ -40,7 +40,7 @@ PEAK_MAD_MEASURED = 33.8e12            # tools/microbench/valu_rates.hip, 8 wave
 
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r03", "pmc", "config2_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04", "pmc", "config2_traffic.json")
 
 
 def pmc_traffic(count: int, modbits: int, mod) -> dict:
