@@ -206,33 +206,11 @@ class CoalescerT {
     int rc = MPCX_OK;
     std::string err;
   };
-  // hold_us > 0: while another dispatch is in flight and fewer than min_ops
-  // operands are pending, a would-be leader waits up to hold_us for more groups
-  // (a fuller launch) before it dispatches
-  int run(Req& r, int max_inflight, uint64_t max_ops, uint64_t min_ops = 0, int hold_us = 0) {
+  int run(Req& r, int max_inflight, uint64_t max_ops) {
     std::unique_lock<std::mutex> lk(mu_);
     q_.push_back(&r);
-    if (hold_us > 0) cv_.notify_all();  // a held leader re-counts the pending operands
-    bool holding = false;
-    std::chrono::steady_clock::time_point hold_end{};
     while (!r.done) {
       if (!r.taken && inflight_ < max_inflight) {
-        if (hold_us > 0 && inflight_ > 0) {
-          uint64_t pend = 0;
-          for (const Req* q : q_)
-            if (!q->taken) pend += q->g.count;
-          if (pend < min_ops) {
-            const auto now = std::chrono::steady_clock::now();
-            if (!holding) {
-              holding = true;
-              hold_end = now + std::chrono::microseconds(hold_us);
-            }
-            if (now < hold_end) {
-              cv_.wait_until(lk, hold_end);
-              continue;
-            }
-          }
-        }
         std::vector<Req*> batch{&r};  // the leader's own group first, then arrival order
         r.taken = true;
         uint64_t ops = r.g.count;
@@ -304,22 +282,6 @@ FixedCoalescer& fixed_coalescer(uint32_t class_words) {
   return c[class_words <= 32 ? 0 : 1];
 }
 
-// MPCX_COALESCE_HOLD_US: the coalescers' hold (0, default: dispatch at once)
-int coalesce_hold_us() {
-  static const int v = [] {
-    const char* e = std::getenv("MPCX_COALESCE_HOLD_US");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
-  return v;
-}
-// operands of one resident round at one wavefront per SIMD in the class's main
-// geometry (1,024 SIMDs): the fill a held dispatch waits for
-uint64_t round_ops(uint32_t class_words, bool comb) {
-  if (class_words <= 32) return 64u * 1024u;
-  if (class_words <= 65) return (comb ? 16u : 32u) * 1024u;
-  return 16u * 1024u;
-}
-
 // MPCX_COALESCE = max coalesced dispatches in flight per bound device (0: off,
 // each exp() call is its own launch); default kCoalesceInflight
 int coalesce_inflight() {
@@ -331,14 +293,6 @@ int coalesce_inflight() {
   int dev = 1;  // per bound device
   if (mpcx_bound_devices(&dev, nullptr, 0) != MPCX_OK || dev < 1) dev = 1;
   return v * dev;
-}
-// MPCX_FIXED_COALESCE=0: every comb batch its own launch (A/B runs)
-bool fixed_coalesce_on() {
-  static const bool on = [] {
-    const char* e = std::getenv("MPCX_FIXED_COALESCE");
-    return !(e && e[0] == '0');
-  }();
-  return on;
 }
 }  // namespace
 
@@ -452,8 +406,7 @@ void Engine::exp_into(const Nat& m, size_t n, const Nat* const* bases, const Nat
       r.g.mul_words = muls ? md.class_words : 0;
       r.g.out = out.p;
       r.g.out_words = md.words;
-      rc = coalescer(md.class_words).run(r, inflight, kCoalesceMaxOps, round_ops(md.class_words, false),
-                                         coalesce_hold_us());
+      rc = coalescer(md.class_words).run(r, inflight, kCoalesceMaxOps);
       if (rc) {
         leave_call();
         throw EngineError(rc, "mpcx_modexp_multi_batch: " + r.err);
@@ -571,7 +524,7 @@ void Engine::fixed_multi_into(const Nat& m, size_t nb, const Nat* const* bases, 
     MPCX_PROF("engine.fixed.gpu");
     enter_call();
     const int inflight = coalesce_inflight();
-    if (inflight > 0 && n < kCoalesceAloneOps && fixed_coalesce_on()) {
+    if (inflight > 0 && n < kCoalesceAloneOps) {
       FixedCoalescer::Req r;
       r.g.nbases = (uint32_t)nb;
       r.g.count = (uint32_t)n;
@@ -584,8 +537,7 @@ void Engine::fixed_multi_into(const Nat& m, size_t nb, const Nat* const* bases, 
       r.g.mul_words = muls ? md.class_words : 0;
       r.g.out = out.p;
       r.g.out_words = md.words;
-      rc = fixed_coalescer(md.class_words).run(r, inflight, kCoalesceMaxOps, round_ops(md.class_words, true),
-                                               coalesce_hold_us());
+      rc = fixed_coalescer(md.class_words).run(r, inflight, kCoalesceMaxOps);
       if (rc) {
         leave_call();
         throw EngineError(rc, "mpcx_fixedbase_multi_batch: " + r.err);
