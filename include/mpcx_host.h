@@ -260,8 +260,9 @@ int mpcxh_bench_signing(uint32_t w, const mpcxh_paillier_t* sks, const mpcxh_dln
  * n_parties nodes (csrc/host/keygenload.hpp): every party proves DLN x2,
  * Paillier-Blum Mod, and a Fac proof to each peer; every party verifies
  * every peer's proofs. Integers are w words wide (w >= 64). Sessions stream in
- * waves of wave_sessions (0: 1024), two waves in flight: host memory is bounded
- * by the waves, not by `sessions`.
+ * waves of wave_sessions (0: 1024), two waves in flight, every proof chain of a
+ * wave (each party's proofs and their verification by every peer) at once:
+ * host memory is bounded by the waves, not by `sessions`.
  * stats_out[MPCXH_KEYGEN_STATS]: prove_s, verify_s, total_s, sessions, parties,
  * proofs, verifications, failures, engine_busy_s, alg_macs, waves,
  * wave_sessions, max_wave_s.
