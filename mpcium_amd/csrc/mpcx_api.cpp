@@ -62,6 +62,9 @@ hipError_t mpcx_launch_fixedbase_multi_g0(const mpcx::FixedBaseArgs* segs, const
                                           uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_multi_g1(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
                                           uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_g5(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_multi_g5(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
+                                          uint32_t waves, hipStream_t st);
 hipError_t mpcx_launch_sieve(const mpcx::SieveArgs* a, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 hipError_t mpcx_launch_ec_combine(const uint32_t* sc, const uint32_t* pts, uint32_t* out, const uint32_t* gtab,
@@ -677,8 +680,12 @@ int fb_table(mpcx_fb_t fb, int di, const uint32_t** out) {
       int src = -1;
       for (int j = 0; j < kMaxDevices && src < 0; ++j)
         if (fb->d_table[j]) src = j;
+      // device-to-device copies return before they complete, and the lanes'
+      // non-blocking streams are not ordered after the null stream: wait for
+      // the copy before any launch may read the table
       e = src < 0 ? hipErrorInvalidValue
-                  : hipMemcpyPeer(p, g_devs[di].ordinal, fb->d_table[src], g_devs[src].ordinal, bytes);
+                  : hipMemcpyPeerAsync(p, g_devs[di].ordinal, fb->d_table[src], g_devs[src].ordinal, bytes, nullptr);
+      if (e == hipSuccess) e = hipStreamSynchronize(nullptr);
     }
     if (e != hipSuccess) {
       (void)hipFree(p);
@@ -772,6 +779,27 @@ bool host_ops_below(const uint32_t* x, uint32_t count, uint32_t words, uint32_t 
 int main_geom_for(const mpcx_modulus_s* mod, bool ops_fit) {
   const int g = g_main_geom[mod->cls];
   return geom_serves(g, mod, ops_fit) ? g : MPCX_FULL_GEOM(mod->cls);
+}
+
+// The layout (geometry) of a modulus's comb tables: the lane pair for moduli
+// below 2^2070 (MPCX_FB_LANEPAIR), else the class's full-width geometry. A
+// lane-pair table needs every multiplier below 2^2072 (geom_serves).
+#ifndef MPCX_FB_LANEPAIR
+#define MPCX_FB_LANEPAIR 1
+#endif
+int fb_geom_for(const mpcx_modulus_s* mod) {
+  if (MPCX_FB_LANEPAIR && mod->cls == 1 && geom_serves(5, mod, true)) return 5;
+  return MPCX_FULL_GEOM(mod->cls);
+}
+hipError_t launch_fixedbase(int geom, const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st) {
+  return geom == 0 ? mpcx_launch_fixedbase_g0(a, waves, st)
+                   : geom == 5 ? mpcx_launch_fixedbase_g5(a, waves, st) : mpcx_launch_fixedbase_g1(a, waves, st);
+}
+hipError_t launch_fixedbase_multi(int geom, const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
+                                  uint32_t waves, hipStream_t st) {
+  return geom == 0   ? mpcx_launch_fixedbase_multi_g0(segs, first, nsegs, waves, st)
+         : geom == 5 ? mpcx_launch_fixedbase_multi_g5(segs, first, nsegs, waves, st)
+                     : mpcx_launch_fixedbase_multi_g1(segs, first, nsegs, waves, st);
 }
 
 }  // namespace
@@ -1920,7 +1948,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   std::lock_guard<std::mutex> blk(bl.mu);
   int rc;
   if ((rc = lane_stream(bl))) return rc;
-  const int geom = MPCX_FULL_GEOM(mod->cls);  // the comb tables' layout
+  const int geom = fb_geom_for(mod);  // the comb tables' layout
   const uint32_t L = (uint32_t)MPCX_GEOM_L(geom), P = (uint32_t)MPCX_GEOM_P(geom), K = (uint32_t)MPCX_GEOM_K(geom);
   // window width: the configured one, narrowed until the table fits
   // MPCX_FB_MAX_TABLE_BYTES (one product per window; 2^w entries per window)
@@ -2065,6 +2093,10 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
   if (muls && (mul_words == 0 || mul_words > cw)) return fail(MPCX_EINVAL, "mul_words %u outside [1, %u]", mul_words, cw);
   if (count == 0) return MPCX_OK;
   if (!out) return fail(MPCX_EINVAL, "null output");
+  if (muls && !geom_serves(fbs[0]->geom, mod, host_ops_below(muls, count, mul_words,
+                                                               (uint32_t)MPCX_GEOM_RBITS(fbs[0]->geom))))
+    return fail(MPCX_EINVAL, "multiplier of %u+ bits for a lane-pair comb table: reduce it mod m first",
+                (unsigned)MPCX_GEOM_RBITS(fbs[0]->geom));
   uint32_t nwin[MPCX_FB_MAX_BASES] = {0, 0};
   for (uint32_t t = 0; t < nbases; ++t) {
     if (exp_words[t] && !exps[t]) return fail(MPCX_EINVAL, "null exponents %u", t);
@@ -2117,8 +2149,7 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     a.n0inv = mod->n0inv;
     const uint32_t waves = (n + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
     const int ks = kstat_begin(l);
-    hipError_t e = geom == MPCX_FULL_GEOM(0) ? mpcx_launch_fixedbase_g0(&a, waves, l.st)
-                                             : mpcx_launch_fixedbase_g1(&a, waves, l.st);
+    hipError_t e = launch_fixedbase(geom, &a, waves, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
     {
@@ -2191,7 +2222,16 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
   const int di = (int)(g_dev_rr.fetch_add(1, std::memory_order_relaxed) % (unsigned)n);
   Device& dev = g_devs[di];
   if ((rc = bind(dev))) return rc;
-  const int geom = MPCX_FULL_GEOM(cls);  // the tables' layout
+  int geom = -1;  // the tables' layout: one per launch
+  for (uint32_t i = 0; i < n_groups; ++i) {
+    if (gs[i].count == 0) continue;
+    const int g = gs[i].fbs[0]->geom;
+    if (geom < 0) geom = g;
+    if (g != geom) return fail(MPCX_EINVAL, "group %u: comb table layout differs from group 0's", i);
+    if (gs[i].muls && !geom_serves(g, gs[i].fbs[0]->mod, host_ops_below(gs[i].muls, gs[i].count, gs[i].mul_words,
+                                                                          (uint32_t)MPCX_GEOM_RBITS(g))))
+      return fail(MPCX_EINVAL, "group %u: multiplier too wide for a lane-pair comb table", i);
+  }
   const uint32_t G = (uint32_t)MPCX_GEOM_G(geom), L = (uint32_t)MPCX_GEOM_L(geom);
   struct Seg {
     uint32_t gi, waves;
@@ -2264,9 +2304,7 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
   const int ks = kstat_begin(l);
   const mpcx::FixedBaseArgs* dsegs = (const mpcx::FixedBaseArgs*)l.stage[3].ptr;
   const uint32_t* dfirst = (const uint32_t*)((const char*)l.stage[3].ptr + seg_bytes);
-  hipError_t e = geom == MPCX_FULL_GEOM(0)
-                     ? mpcx_launch_fixedbase_multi_g0(dsegs, dfirst, (uint32_t)nseg, first[nseg], l.st)
-                     : mpcx_launch_fixedbase_multi_g1(dsegs, dfirst, (uint32_t)nseg, first[nseg], l.st);
+  hipError_t e = launch_fixedbase_multi(geom, dsegs, dfirst, (uint32_t)nseg, first[nseg], l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase_multi");
   dev.launches.fetch_add(1, std::memory_order_relaxed);
   {

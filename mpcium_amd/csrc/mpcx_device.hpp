@@ -650,9 +650,9 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
   // LDS row set by LDS DMA (global_load_lds) 5-15% slower in isolation
   // (profiles/r04/fb_dma_ab/isolated).
   uint32_t t = 0, j = 0;  // next window: base t, window j
-  uint32_t nx[K];         // the next product's B digits, in flight
-  // nx <- the next window with bits in some operand of the wave, else the exit
-  // multiplier 1; false once the exit product has been handed out
+  // the LDS row <- the next window's entry (some operand of the wave has bits
+  // there), else the exit multiplier 1; false once the exit product has been
+  // handed out. Stored at once: no digits held in registers across a product.
   bool fin = false;
   auto fetch = [&] __attribute__((always_inline))() -> bool {
     for (; t < a.nbases; ++t, j = 0) {
@@ -662,22 +662,26 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
         const uint32_t v = (active && ew) ? window_of(ex, j, wb, ew) : 0u;
         if (__ballot(v != 0u) == 0ull) continue;  // no operand of the wave has bits here
         const uint32_t* e = a.tables[t] + (((size_t)j << wb) + v) * L;
+        uint32_t nx[K];
 #pragma unroll
         for (int k = 0; k < K; ++k) nx[k] = idle ? 0u : e[k * P + p];
+        lds_store_digits<K>(bl, p, nx);
         ++j;
         return true;
       }
     }
     if (fin) return false;
     fin = true;  // leave the Montgomery domain: z = mont(z R, 1) <= m
+    uint32_t one[K];
 #pragma unroll
-    for (int k = 0; k < K; ++k) nx[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
+    for (int k = 0; k < K; ++k) one[k] = (p == 0 && k == 0 && !idle) ? 1u : 0u;
+    lds_store_digits<K>(bl, p, one);
     return true;
   };
 
   // B of the first product: R^2 already in LDS (z = mul R = mont(mul, R^2)),
   // or the first fetched entry
-  bool more = true, b_in_lds = a.mul != nullptr;
+  bool more = true;
   if (a.mul) {
     lds_digits(a.r2d);
 #pragma unroll
@@ -699,8 +703,6 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
     more = fetch();
   }
   while (more) {
-    if (!b_in_lds) lds_store_digits<K>(bl, p, nx);
-    b_in_lds = false;
     wave_lds_fence();
     montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
     wave_lds_fence();

@@ -66,8 +66,9 @@ __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_mul
   return hipGetLastError();
 }
 
-#if MPCX_GEOM_ID == MPCX_FULL_GEOM(0) || MPCX_GEOM_ID == MPCX_FULL_GEOM(1)
-// fixed-base comb kernel: main geometry of the <= 2080-bit classes (N~, N; tables are laid out for it)
+#if MPCX_GEOM_ID == MPCX_FULL_GEOM(0) || MPCX_GEOM_ID == MPCX_FULL_GEOM(1) || MPCX_GEOM_ID == 5
+// fixed-base comb kernel: the comb-table layouts (full-width geometries of the <= 2080-bit classes, and the
+// 2048-bit lane pair)
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_fixedbase_g, MPCX_GEOM_ID)(
     const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st) {
   hipLaunchKernelGGL((mpcx::k_fixedbase<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),

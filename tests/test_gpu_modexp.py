@@ -291,6 +291,9 @@ def test_fixed_base_tables(gpu, paillier_key, wbits):
     assert gpu.fixedbase_exp([f1], [edge]) == [pow(h1, x, N) for x in edge]
     with pytest.raises(gpu.MpcxError):
         gpu.fixedbase_exp([f2], [[1 << cap(300)]])
+    # a lane-pair table (N < 2^2070) takes multipliers below 2^2072 only
+    with pytest.raises(gpu.MpcxError):
+        gpu.fixedbase_exp([f1], [[5]], [1 << 2075])
     # N~-shape modulus from the node fixtures and the 1024-bit class
     for m in (paillier_key["P"], rng.getrandbits(1500) | 1 | (1 << 1499)):
         md = gpu.Modulus(m)
