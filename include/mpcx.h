@@ -380,6 +380,10 @@ int mpcx_sync(void* stream);
  *                exponents (5 bits above 1024-bit exponents, else Go's 4).
  *   "fb_window"  4..12 (default 12): window width of comb tables registered
  *                from now on.
+ *   "fb_lanepair" 0 (default) / 1: comb tables of moduli below 2^2070
+ *                registered from now on take the lane-pair (2 x 37) layout:
+ *                faster for batches of >= ~64k operands, slower below
+ *                (profiles/r04/fblp); their multipliers must be below 2^2072.
  *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
  *                thread per candidate.
  *   "lanes"      1..8 (default 6, or MPCX_LANES): execution lanes (streams

@@ -115,6 +115,7 @@ int g_fixed_win = 5;                     // widest fixed window for per-operand 
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 int g_fb_window = MPCX_FB_WINDOW_BITS;  // mpcx_set_option("fb_window", w): fixed-base comb width of new tables
+int g_fb_lanepair = 0;  // mpcx_set_option("fb_lanepair", 1): lane-pair layout for new 2048-bit tables
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
 bool g_prime_coop = true;                // mpcx_set_option("prime_coop", 0): thread-per-candidate prime kernels
 bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 1): test hook, see below
@@ -781,14 +782,14 @@ int main_geom_for(const mpcx_modulus_s* mod, bool ops_fit) {
   return geom_serves(g, mod, ops_fit) ? g : MPCX_FULL_GEOM(mod->cls);
 }
 
-// The layout (geometry) of a modulus's comb tables: the lane pair for moduli
-// below 2^2070 (MPCX_FB_LANEPAIR), else the class's full-width geometry. A
-// lane-pair table needs every multiplier below 2^2072 (geom_serves).
-#ifndef MPCX_FB_LANEPAIR
-#define MPCX_FB_LANEPAIR 1
-#endif
+// The layout (geometry) of a modulus's comb tables: the class's full-width
+// geometry, or with option "fb_lanepair" the lane pair for moduli below 2^2070
+// (a lane-pair table needs every multiplier below 2^2072, geom_serves). The
+// lane pair is 10% faster at 131k operands but 24-30% slower at 16k (half the
+// lanes per operand leave SIMDs idle) and neutral end to end, where the comb
+// batches are small (profiles/r04/fblp/): off by default.
 int fb_geom_for(const mpcx_modulus_s* mod) {
-  if (MPCX_FB_LANEPAIR && mod->cls == 1 && geom_serves(5, mod, true)) return 5;
+  if (g_fb_lanepair && mod->cls == 1 && geom_serves(5, mod, true)) return 5;
   return MPCX_FULL_GEOM(mod->cls);
 }
 hipError_t launch_fixedbase(int geom, const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st) {
@@ -827,6 +828,10 @@ int mpcx_set_option(const char* key, int value) {
     // product per window, 2^w entries per window)
     if (value < 4 || value > MPCX_FB_MAX_WINDOW_BITS) return fail(MPCX_EINVAL, "fb_window %d out of range", value);
     g_fb_window = value;
+  } else if (std::strcmp(key, "fb_lanepair") == 0) {
+    // 1: comb tables of 2048-bit moduli registered from now on use the lane pair
+    if (value < 0 || value > 1) return fail(MPCX_EINVAL, "fb_lanepair %d out of range", value);
+    g_fb_lanepair = value;
   } else if (std::strcmp(key, "fixed_window") == 0) {
     // widest fixed window of per-operand exponents: 4 (Go's) or 5 (above 320 bits)
     if (value != 4 && value != 5) return fail(MPCX_EINVAL, "fixed_window %d not 4 or 5", value);
