@@ -380,6 +380,10 @@ int mpcx_sync(void* stream);
  *                exponents (5 bits above 1024-bit exponents, else Go's 4).
  *   "fb_window"  4..12 (default 12): window width of comb tables registered
  *                from now on.
+ *   "fb_split"   0 (default), 1, 2 or 4: wavefronts sharing one comb
+ *                operand's windows (each takes every S-th window; wave 0
+ *                multiplies the partials in); 0 picks the largest that keeps a
+ *                launch within 4 wavefronts per SIMD.
  *   "fb_lanepair" 0 (default) / 1: comb tables of moduli below 2^2070
  *                registered from now on take the lane-pair (2 x 37) layout:
  *                faster for batches of >= ~64k operands, slower below

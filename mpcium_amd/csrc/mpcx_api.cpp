@@ -56,15 +56,15 @@ hipError_t mpcx_launch_mrc(const mpcx::MrArgs* a, hipStream_t st);
 hipError_t mpcx_launch_lucasc(const mpcx::LucasArgs* a, hipStream_t st);
 hipError_t mpcx_launch_lucasc_wide(const mpcx::LucasArgs* a, hipStream_t st);
 hipError_t mpcx_launch_expsched(const mpcx::ExpSchedArgs* a, hipStream_t st);
-hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
-hipError_t mpcx_launch_fixedbase_g1(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_g0(const mpcx::FixedBaseArgs* a, uint32_t blocks, uint32_t split, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_g1(const mpcx::FixedBaseArgs* a, uint32_t blocks, uint32_t split, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_multi_g0(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
-                                          uint32_t waves, hipStream_t st);
+                                          uint32_t blocks, uint32_t split, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_multi_g1(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
-                                          uint32_t waves, hipStream_t st);
-hipError_t mpcx_launch_fixedbase_g5(const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st);
+                                          uint32_t blocks, uint32_t split, hipStream_t st);
+hipError_t mpcx_launch_fixedbase_g5(const mpcx::FixedBaseArgs* a, uint32_t blocks, uint32_t split, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_multi_g5(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
-                                          uint32_t waves, hipStream_t st);
+                                          uint32_t blocks, uint32_t split, hipStream_t st);
 hipError_t mpcx_launch_sieve(const mpcx::SieveArgs* a, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 hipError_t mpcx_launch_ec_combine(const uint32_t* sc, const uint32_t* pts, uint32_t* out, const uint32_t* gtab,
@@ -115,6 +115,10 @@ int g_fixed_win = 5;                     // widest fixed window for per-operand 
 int g_sched_width = MPCX_SCHED_MAX_WIDTH;  // mpcx_set_option("sched_width", w): 0 = Go's fixed window
 int g_main_geom[MPCX_NUM_CLASSES] = {MPCX_MAIN_GEOM(0), MPCX_MAIN_GEOM(1), MPCX_MAIN_GEOM(2)};
 int g_fb_window = MPCX_FB_WINDOW_BITS;  // mpcx_set_option("fb_window", w): fixed-base comb width of new tables
+#ifndef MPCX_FB_SPLIT_DEFAULT
+#define MPCX_FB_SPLIT_DEFAULT 0  // A/B builds: -DMPCX_FB_SPLIT_DEFAULT=1 (no window split)
+#endif
+int g_fb_split = MPCX_FB_SPLIT_DEFAULT;  // mpcx_set_option("fb_split", s): comb waves per workgroup (0: by size)
 int g_fb_lanepair = 0;  // mpcx_set_option("fb_lanepair", 1): lane-pair layout for new 2048-bit tables
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
 bool g_prime_coop = true;                // mpcx_set_option("prime_coop", 0): thread-per-candidate prime kernels
@@ -792,15 +796,28 @@ int fb_geom_for(const mpcx_modulus_s* mod) {
   if (g_fb_lanepair && mod->cls == 1 && geom_serves(5, mod, true)) return 5;
   return MPCX_FULL_GEOM(mod->cls);
 }
-hipError_t launch_fixedbase(int geom, const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st) {
-  return geom == 0 ? mpcx_launch_fixedbase_g0(a, waves, st)
-                   : geom == 5 ? mpcx_launch_fixedbase_g5(a, waves, st) : mpcx_launch_fixedbase_g1(a, waves, st);
+hipError_t launch_fixedbase(int geom, const mpcx::FixedBaseArgs* a, uint32_t blocks, uint32_t split, hipStream_t st) {
+  return geom == 0   ? mpcx_launch_fixedbase_g0(a, blocks, split, st)
+         : geom == 5 ? mpcx_launch_fixedbase_g5(a, blocks, split, st)
+                     : mpcx_launch_fixedbase_g1(a, blocks, split, st);
 }
 hipError_t launch_fixedbase_multi(int geom, const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
-                                  uint32_t waves, hipStream_t st) {
-  return geom == 0   ? mpcx_launch_fixedbase_multi_g0(segs, first, nsegs, waves, st)
-         : geom == 5 ? mpcx_launch_fixedbase_multi_g5(segs, first, nsegs, waves, st)
-                     : mpcx_launch_fixedbase_multi_g1(segs, first, nsegs, waves, st);
+                                  uint32_t blocks, uint32_t split, hipStream_t st) {
+  return geom == 0   ? mpcx_launch_fixedbase_multi_g0(segs, first, nsegs, blocks, split, st)
+         : geom == 5 ? mpcx_launch_fixedbase_multi_g5(segs, first, nsegs, blocks, split, st)
+                     : mpcx_launch_fixedbase_multi_g1(segs, first, nsegs, blocks, split, st);
+}
+
+// Wavefronts per comb workgroup (k_fixedbase's window split): the largest of
+// 4, 2, 1 that keeps a launch of `blocks` workgroups within kFbSplitWaves
+// wavefronts per SIMD, or option "fb_split" when set.
+constexpr uint32_t kFbSplitWaves = 4;
+uint32_t fb_split_for(const Device& dev, uint32_t blocks) {
+  if (g_fb_split) return (uint32_t)g_fb_split;
+  const uint64_t cap = (uint64_t)std::max(1, dev.num_cus) * 4u * kFbSplitWaves;
+  for (uint32_t s = MPCX_FB_MAX_SPLIT; s > 1; s >>= 1)
+    if ((uint64_t)blocks * s <= cap) return s;
+  return 1;
 }
 
 }  // namespace
@@ -828,6 +845,10 @@ int mpcx_set_option(const char* key, int value) {
     // product per window, 2^w entries per window)
     if (value < 4 || value > MPCX_FB_MAX_WINDOW_BITS) return fail(MPCX_EINVAL, "fb_window %d out of range", value);
     g_fb_window = value;
+  } else if (std::strcmp(key, "fb_split") == 0) {
+    // wavefronts sharing one comb operand's windows: 1, 2, 4; 0 picks by launch size
+    if (value != 0 && value != 1 && value != 2 && value != 4) return fail(MPCX_EINVAL, "fb_split %d not 0/1/2/4", value);
+    g_fb_split = value;
   } else if (std::strcmp(key, "fb_lanepair") == 0) {
     // 1: comb tables of 2048-bit moduli registered from now on use the lane pair
     if (value < 0 || value > 1) return fail(MPCX_EINVAL, "fb_lanepair %d out of range", value);
@@ -2152,9 +2173,10 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     a.out_words = out_words;
     a.count = n;
     a.n0inv = mod->n0inv;
-    const uint32_t waves = (n + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
+    const uint32_t blocks = (n + MPCX_GEOM_G(geom) - 1) / MPCX_GEOM_G(geom);
+    const uint32_t split = fb_split_for(g_devs[di], blocks);
     const int ks = kstat_begin(l);
-    hipError_t e = launch_fixedbase(geom, &a, waves, l.st);
+    hipError_t e = launch_fixedbase(geom, &a, blocks, split, l.st);
     if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase");
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
     {
@@ -2309,7 +2331,8 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
   const int ks = kstat_begin(l);
   const mpcx::FixedBaseArgs* dsegs = (const mpcx::FixedBaseArgs*)l.stage[3].ptr;
   const uint32_t* dfirst = (const uint32_t*)((const char*)l.stage[3].ptr + seg_bytes);
-  hipError_t e = launch_fixedbase_multi(geom, dsegs, dfirst, (uint32_t)nseg, first[nseg], l.st);
+  hipError_t e = launch_fixedbase_multi(geom, dsegs, dfirst, (uint32_t)nseg, first[nseg],
+                                        fb_split_for(dev, first[nseg]), l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_fixedbase_multi");
   dev.launches.fetch_add(1, std::memory_order_relaxed);
   {

@@ -620,18 +620,35 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 // for the same Exp. Every operand multiplies in every window (v = 0 reads
 // the Montgomery one), so the wave never diverges; windows above every
 // operand's exponent are skipped by a wave-uniform ballot.
+//
+// Window split: a workgroup is S = blockDim.x / 64 wavefronts (1, 2 or 4) for
+// the SAME G operands; wave w takes windows j = w, w + S, ... of every base
+// (interleaved: balanced for short exponents too), waves 1..S-1 leave their
+// partial products (Montgomery form) in their LDS rows, and wave 0 multiplies
+// them in before leaving the Montgomery domain: S - 1 extra products per
+// operand for S times the wavefronts of a launch below a resident round.
+// LDS: S slices of (G + 1) L + 2 words (dynamic, sized by the launch).
+template <int P, int K, int G>
+constexpr uint32_t fb_lds_slice_words() {
+  return (uint32_t)((G + 1) * P * K + 2);
+}
+
 template <int P, int K, int G>
 __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uint32_t blk) {
   constexpr int L = P * K;
-  __shared__ uint32_t lds[(G + 1) * L + 2];
-  const int lane = threadIdx.x;
+  constexpr uint32_t kSlice = fb_lds_slice_words<P, K, G>();
+  extern __shared__ uint32_t fb_lds[];
+  const uint32_t S = __builtin_amdgcn_readfirstlane(blockDim.x >> 6);
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  // lane id from mbcnt: threadIdx.x & 63 made these kernels spill 48-264 B
+  const int lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
   const int g_raw = lane / P;
   const bool idle = g_raw >= G;
   const int g = idle ? G : g_raw;
   const int p = lane - g_raw * P;
   const uint32_t op = blk * G + (idle ? 0 : g_raw);
   const bool active = !idle && op < a.count;
-  uint32_t* bl = lds + g * L;
+  uint32_t* bl = fb_lds + wv * kSlice + g * L;
   const int m_src_addr = (idle ? lane : g_raw * P) * 4;
 
   uint32_t Nd[K], A[K];
@@ -644,21 +661,24 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
     lds_store_digits<K>(bl, p, t);
   };
   // ONE montmul call site (three would triple the unrolled product and its
-  // register allocation). The next product's table entry is loaded after the
-  // current product: loading it during the product into registers measured 6%
-  // slower on config 5 (profiles/r03/fb_prefetch), and staging it into a second
-  // LDS row set by LDS DMA (global_load_lds) 5-15% slower in isolation
-  // (profiles/r04/fb_dma_ab/isolated).
-  uint32_t t = 0, j = 0;  // next window: base t, window j
-  // the LDS row <- the next window's entry (some operand of the wave has bits
-  // there), else the exit multiplier 1; false once the exit product has been
-  // handed out. Stored at once: no digits held in registers across a product.
-  bool fin = false;
+  // register allocation); its B operand is this wave's LDS row. The next
+  // product's table entry is
+  // loaded after the current product: loading it during the product into
+  // registers measured 6% slower on config 5 (profiles/r03/fb_prefetch), and
+  // staging it into a second LDS row set by LDS DMA (global_load_lds) 5-15%
+  // slower in isolation (profiles/r04/fb_dma_ab/isolated).
+  uint32_t t = 0, j = wv;  // next window: base t, window j
+  uint32_t part = 1;  // wave 0: next partial to multiply in
+  bool own = true, fin = false;
+  // B <- the next window's entry (some operand of the wave has bits there),
+  // then the other waves' partials (wave 0), then the exit multiplier 1; false
+  // once the exit product has been handed out (waves > 0: once their windows
+  // are done). Stored at once: no digits held in registers across a product.
   auto fetch = [&] __attribute__((always_inline))() -> bool {
-    for (; t < a.nbases; ++t, j = 0) {
+    for (; t < a.nbases; ++t, j = wv) {
       const uint32_t ew = a.exp_words[t], wb = a.wbits[t];
       const uint32_t* ex = a.exps[t] + (size_t)(active ? op : 0) * ew;
-      for (; j < a.nwin[t]; ++j) {
+      for (; j < a.nwin[t]; j += S) {
         const uint32_t v = (active && ew) ? window_of(ex, j, wb, ew) : 0u;
         if (__ballot(v != 0u) == 0ull) continue;  // no operand of the wave has bits here
         const uint32_t* e = a.tables[t] + (((size_t)j << wb) + v) * L;
@@ -666,9 +686,26 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
 #pragma unroll
         for (int k = 0; k < K; ++k) nx[k] = idle ? 0u : e[k * P + p];
         lds_store_digits<K>(bl, p, nx);
-        ++j;
+        j += S;
         return true;
       }
+    }
+    if (own) {  // this wave's windows are done
+      own = false;
+      if (S > 1u) {
+        if (wv) lds_store_digits<K>(bl, p, A);  // the partial, for wave 0
+        __syncthreads();
+        if (wv) return false;
+      }
+    }
+    if (part < S) {  // wave 0: B <- wave part's partial (copied into this wave's row)
+      const uint32_t* src = fb_lds + part * kSlice + g * L;
+      uint32_t nx[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) nx[k] = src[p * K + k];
+      lds_store_digits<K>(bl, p, nx);
+      ++part;
+      return true;
     }
     if (fin) return false;
     fin = true;  // leave the Montgomery domain: z = mont(z R, 1) <= m
@@ -679,10 +716,10 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
     return true;
   };
 
-  // B of the first product: R^2 already in LDS (z = mul R = mont(mul, R^2)),
-  // or the first fetched entry
+  // B of the first product: R^2 already in LDS (z = mul R = mont(mul, R^2),
+  // wave 0), or the first fetched entry
   bool more = true;
-  if (a.mul) {
+  if (a.mul && wv == 0u) {
     lds_digits(a.r2d);
 #pragma unroll
     for (int k = 0; k < K; ++k) {
@@ -708,20 +745,22 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
     wave_lds_fence();
     more = fetch();
   }
-  store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
+  if (wv == 0u)
+    store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
 }
 
 template <int P, int K, int G, int WPE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase(const FixedBaseArgs a) {
+__global__ __launch_bounds__(64 * MPCX_FB_MAX_SPLIT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase(
+    const FixedBaseArgs a) {
   fixedbase_wave<P, K, G>(a, blockIdx.x);
 }
 
 // Several comb batches in one launch (mpcx_fixedbase_multi_batch: concurrent
 // callers' batches -- other tables, other moduli of the class, muls or not):
-// segment s owns wavefronts [first[s], first[s+1]) and its own FixedBaseArgs,
+// segment s owns workgroups [first[s], first[s+1]) and its own FixedBaseArgs,
 // read wave-uniformly, as k_modexp_multi does for exponentiations.
 template <int P, int K, int G, int WPE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase_multi(
+__global__ __launch_bounds__(64 * MPCX_FB_MAX_SPLIT) __attribute__((amdgpu_waves_per_eu(WPE))) void k_fixedbase_multi(
     const FixedBaseArgs* __restrict__ segs, const uint32_t* __restrict__ first, uint32_t nsegs) {
   const uint32_t b = blockIdx.x;
   uint32_t s = 0;

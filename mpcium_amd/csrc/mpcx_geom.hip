@@ -68,23 +68,25 @@ __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_mul
 
 #if MPCX_GEOM_ID == MPCX_FULL_GEOM(0) || MPCX_GEOM_ID == MPCX_FULL_GEOM(1) || MPCX_GEOM_ID == 5
 // fixed-base comb kernel: the comb-table layouts (full-width geometries of the <= 2080-bit classes, and the
-// 2048-bit lane pair)
+// 2048-bit lane pair); `split` wavefronts per workgroup share its G operands' windows
+#define MPCX_FB_ARGS MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID), MPCX_GEOM_G(MPCX_GEOM_ID)
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_fixedbase_g, MPCX_GEOM_ID)(
-    const mpcx::FixedBaseArgs* a, uint32_t waves, hipStream_t st) {
-  hipLaunchKernelGGL((mpcx::k_fixedbase<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
-                                        MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>),
-                     dim3(waves), dim3(64), 0, st, *a);
+    const mpcx::FixedBaseArgs* a, uint32_t blocks, uint32_t split, hipStream_t st) {
+  const size_t lds = (size_t)mpcx::fb_lds_slice_words<MPCX_FB_ARGS>() * 4u * split;
+  hipLaunchKernelGGL((mpcx::k_fixedbase<MPCX_FB_ARGS, MPCX_WPE>), dim3(blocks), dim3(64 * split), lds, st, *a);
   return hipGetLastError();
 }
 
 // several comb batches in one launch: segs / first are device arrays of nsegs entries
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_fixedbase_multi_g, MPCX_GEOM_ID)(
-    const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs, uint32_t waves, hipStream_t st) {
-  hipLaunchKernelGGL((mpcx::k_fixedbase_multi<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
-                                              MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE>),
-                     dim3(waves), dim3(64), 0, st, segs, first, nsegs);
+    const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs, uint32_t blocks, uint32_t split,
+    hipStream_t st) {
+  const size_t lds = (size_t)mpcx::fb_lds_slice_words<MPCX_FB_ARGS>() * 4u * split;
+  hipLaunchKernelGGL((mpcx::k_fixedbase_multi<MPCX_FB_ARGS, MPCX_WPE>), dim3(blocks), dim3(64 * split), lds, st,
+                     segs, first, nsegs);
   return hipGetLastError();
 }
+#undef MPCX_FB_ARGS
 #endif
 
 // resident 64-thread blocks (= wavefronts) per CU

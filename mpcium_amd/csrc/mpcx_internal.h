@@ -109,6 +109,8 @@ struct ModexpArgs {
 #define MPCX_FB_WINDOW_BITS 12      // default width (option "fb_window")
 #define MPCX_FB_MAX_WINDOW_BITS 12
 #define MPCX_FB_MAX_TABLE_BYTES (512ull << 20)  // narrower windows above this per table
+// most wavefronts one comb operand's windows are split over (k_fixedbase)
+#define MPCX_FB_MAX_SPLIT 4
 #ifndef MPCX_FB_MAX_BASES
 #define MPCX_FB_MAX_BASES 2  // also in include/mpcx.h
 #endif

@@ -341,6 +341,42 @@ def test_fixed_base_lane_pair_tables(gpu, paillier_key):
         mod.release()
 
 
+@pytest.mark.parametrize("split", [1, 2, 4, 0])
+def test_fixed_base_window_split(gpu, paillier_key, split):
+    """Option "fb_split": 1, 2 or 4 wavefronts share one comb operand's
+    windows (j = w, w + S, ...; partials multiplied in by wave 0), 0 picks by
+    launch size. Products equal pow() for one and two bases, multipliers,
+    exponents shorter than S windows, zero exponents, ragged batches, and the
+    multi-segment launch; the 1024-bit class (thread-per-operand layout) too."""
+    N, P = paillier_key["N"], paillier_key["P"]
+    rng = random.Random(900 + split)
+    mod, modp = gpu.Modulus(N), gpu.Modulus(P)
+    h1, h2, hp = rng.randrange(N), rng.randrange(N), rng.randrange(P)
+    f1, f2, fp = gpu.FixedBase(mod, h1, 2816), gpu.FixedBase(mod, h2, 2048), gpu.FixedBase(modp, hp, 1024)
+    gpu.set_option("fb_split", split)
+    try:
+        for count in (1, 17, 100, 3000):
+            a = [rng.getrandbits(rng.choice([0, 5, 12, 13, 30, 2048, 2816])) for _ in range(count)]
+            b = [rng.getrandbits(rng.choice([0, 24, 2048])) for _ in range(count)]
+            cs = [rng.randrange(N) for _ in range(count)]
+            assert gpu.fixedbase_exp([f1], [a]) == [pow(h1, x, N) for x in a], count
+            want = [c * pow(h1, x, N) * pow(h2, y, N) % N for c, x, y in zip(cs, a, b)]
+            assert gpu.fixedbase_exp([f1, f2], [a, b], cs) == want, count
+            ep = [rng.getrandbits(rng.choice([0, 11, 1024])) for _ in range(count)]
+            assert gpu.fixedbase_exp([fp], [ep]) == [pow(hp, x, P) for x in ep], count
+        got = gpu.fixedbase_multi([([f1], [[3, 0, 1 << 2000]], None), ([f2, f1], [[7] * 40, list(range(40))], None)])
+        assert got[0] == [pow(h1, e, N) for e in (3, 0, 1 << 2000)]
+        assert got[1] == [pow(h2, 7, N) * pow(h1, e, N) % N for e in range(40)]
+    finally:
+        gpu.set_option("fb_split", 0)
+        for f in (fp, f2, f1):
+            f.release()
+        modp.release()
+        mod.release()
+    with pytest.raises(gpu.MpcxError):
+        gpu.set_option("fb_split", 3)
+
+
 def test_fixed_base_multi_batch(gpu, paillier_key):
     """mpcx_fixedbase_multi_batch: comb groups of two different 2048-bit moduli
     (other tables, one and two bases, with and without multipliers, an empty

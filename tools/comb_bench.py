@@ -21,15 +21,18 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--sizes", default="2048,16384,131072")
+    ap.add_argument("--split", type=int, default=None, help="option fb_split (0: by launch size)")
     args = ap.parse_args()
     from mpcium_amd import mpcx
     mpcx.init(0)
+    if args.split is not None:
+        mpcx.set_option("fb_split", args.split)
     nodes = json.load(open(os.path.join(ROOT, "tests", "golden", "node_preparams.json")))["nodes"]
     Nt, h1, h2 = (int(nodes[0][k], 16) for k in ("NTildei", "H1i", "H2i"))
     mod = mpcx.Modulus(Nt)
     f1, f2 = mpcx.FixedBase(mod, h1, 3072), mpcx.FixedBase(mod, h2, 3072)
     rng = random.Random(5)
-    out = {"lib": os.environ.get("MPCX_LIB_PATH", "mpcium_amd/libmpcx.so"), "rows": []}
+    out = {"lib": os.environ.get("MPCX_LIB_PATH", "mpcium_amd/libmpcx.so"), "split": args.split, "rows": []}
     for n in (int(x) for x in args.sizes.split(",")):
         for bits, nb in ((2048, 1), (2816, 2)):
             es = [[rng.getrandbits(bits) for _ in range(n)] for _ in range(nb)]
