@@ -384,10 +384,6 @@ int mpcx_sync(void* stream);
  *                operand's windows (each takes every S-th window; wave 0
  *                multiplies the partials in); 0 picks the largest that keeps a
  *                launch within 4 wavefronts per SIMD.
- *   "fb_lanepair" 0 (default) / 1: comb tables of moduli below 2^2070
- *                registered from now on take the lane-pair (2 x 37) layout:
- *                faster for batches of >= ~64k operands, slower below
- *                (profiles/r04/fblp); their multipliers must be below 2^2072.
  *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
  *                thread per candidate.
  *   "lanes"      1..8 (default 6, or MPCX_LANES): execution lanes (streams

@@ -62,9 +62,6 @@ hipError_t mpcx_launch_fixedbase_multi_g0(const mpcx::FixedBaseArgs* segs, const
                                           uint32_t blocks, uint32_t split, hipStream_t st);
 hipError_t mpcx_launch_fixedbase_multi_g1(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
                                           uint32_t blocks, uint32_t split, hipStream_t st);
-hipError_t mpcx_launch_fixedbase_g5(const mpcx::FixedBaseArgs* a, uint32_t blocks, uint32_t split, hipStream_t st);
-hipError_t mpcx_launch_fixedbase_multi_g5(const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
-                                          uint32_t blocks, uint32_t split, hipStream_t st);
 hipError_t mpcx_launch_sieve(const mpcx::SieveArgs* a, hipStream_t st);
 hipError_t mpcx_launch_selftest(uint32_t* d_out, hipStream_t st);
 hipError_t mpcx_launch_ec_combine(const uint32_t* sc, const uint32_t* pts, uint32_t* out, const uint32_t* gtab,
@@ -119,7 +116,6 @@ int g_fb_window = MPCX_FB_WINDOW_BITS;  // mpcx_set_option("fb_window", w): fixe
 #define MPCX_FB_SPLIT_DEFAULT 0  // A/B builds: -DMPCX_FB_SPLIT_DEFAULT=1 (no window split)
 #endif
 int g_fb_split = MPCX_FB_SPLIT_DEFAULT;  // mpcx_set_option("fb_split", s): comb waves per workgroup (0: by size)
-int g_fb_lanepair = 0;  // mpcx_set_option("fb_lanepair", 1): lane-pair layout for new 2048-bit tables
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
 bool g_prime_coop = true;                // mpcx_set_option("prime_coop", 0): thread-per-candidate prime kernels
 bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 1): test hook, see below
@@ -786,26 +782,18 @@ int main_geom_for(const mpcx_modulus_s* mod, bool ops_fit) {
   return geom_serves(g, mod, ops_fit) ? g : MPCX_FULL_GEOM(mod->cls);
 }
 
-// The layout (geometry) of a modulus's comb tables: the class's full-width
-// geometry, or with option "fb_lanepair" the lane pair for moduli below 2^2070
-// (a lane-pair table needs every multiplier below 2^2072, geom_serves). The
-// lane pair is 10% faster at 131k operands but 24-30% slower at 16k (half the
-// lanes per operand leave SIMDs idle) and neutral end to end, where the comb
-// batches are small (profiles/r04/fblp/): off by default.
-int fb_geom_for(const mpcx_modulus_s* mod) {
-  if (g_fb_lanepair && mod->cls == 1 && geom_serves(5, mod, true)) return 5;
-  return MPCX_FULL_GEOM(mod->cls);
-}
+// The layout (geometry) of a modulus's comb tables: its class's full-width
+// geometry. (A lane-pair layout for 2048-bit moduli was 10% faster at 131k
+// operands but 24-30% slower at 16k and neutral end to end, where the comb
+// batches are small: profiles/r04/fblp/; removed.)
+int fb_geom_for(const mpcx_modulus_s* mod) { return MPCX_FULL_GEOM(mod->cls); }
 hipError_t launch_fixedbase(int geom, const mpcx::FixedBaseArgs* a, uint32_t blocks, uint32_t split, hipStream_t st) {
-  return geom == 0   ? mpcx_launch_fixedbase_g0(a, blocks, split, st)
-         : geom == 5 ? mpcx_launch_fixedbase_g5(a, blocks, split, st)
-                     : mpcx_launch_fixedbase_g1(a, blocks, split, st);
+  return geom == 0 ? mpcx_launch_fixedbase_g0(a, blocks, split, st) : mpcx_launch_fixedbase_g1(a, blocks, split, st);
 }
 hipError_t launch_fixedbase_multi(int geom, const mpcx::FixedBaseArgs* segs, const uint32_t* first, uint32_t nsegs,
                                   uint32_t blocks, uint32_t split, hipStream_t st) {
-  return geom == 0   ? mpcx_launch_fixedbase_multi_g0(segs, first, nsegs, blocks, split, st)
-         : geom == 5 ? mpcx_launch_fixedbase_multi_g5(segs, first, nsegs, blocks, split, st)
-                     : mpcx_launch_fixedbase_multi_g1(segs, first, nsegs, blocks, split, st);
+  return geom == 0 ? mpcx_launch_fixedbase_multi_g0(segs, first, nsegs, blocks, split, st)
+                   : mpcx_launch_fixedbase_multi_g1(segs, first, nsegs, blocks, split, st);
 }
 
 // Wavefronts per comb workgroup (k_fixedbase's window split): the largest of
@@ -849,10 +837,6 @@ int mpcx_set_option(const char* key, int value) {
     // wavefronts sharing one comb operand's windows: 1, 2, 4; 0 picks by launch size
     if (value != 0 && value != 1 && value != 2 && value != 4) return fail(MPCX_EINVAL, "fb_split %d not 0/1/2/4", value);
     g_fb_split = value;
-  } else if (std::strcmp(key, "fb_lanepair") == 0) {
-    // 1: comb tables of 2048-bit moduli registered from now on use the lane pair
-    if (value < 0 || value > 1) return fail(MPCX_EINVAL, "fb_lanepair %d out of range", value);
-    g_fb_lanepair = value;
   } else if (std::strcmp(key, "fixed_window") == 0) {
     // widest fixed window of per-operand exponents: 4 (Go's) or 5 (above 320 bits)
     if (value != 4 && value != 5) return fail(MPCX_EINVAL, "fixed_window %d not 4 or 5", value);
@@ -2119,10 +2103,6 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
   if (muls && (mul_words == 0 || mul_words > cw)) return fail(MPCX_EINVAL, "mul_words %u outside [1, %u]", mul_words, cw);
   if (count == 0) return MPCX_OK;
   if (!out) return fail(MPCX_EINVAL, "null output");
-  if (muls && !geom_serves(fbs[0]->geom, mod, host_ops_below(muls, count, mul_words,
-                                                               (uint32_t)MPCX_GEOM_RBITS(fbs[0]->geom))))
-    return fail(MPCX_EINVAL, "multiplier of %u+ bits for a lane-pair comb table: reduce it mod m first",
-                (unsigned)MPCX_GEOM_RBITS(fbs[0]->geom));
   uint32_t nwin[MPCX_FB_MAX_BASES] = {0, 0};
   for (uint32_t t = 0; t < nbases; ++t) {
     if (exp_words[t] && !exps[t]) return fail(MPCX_EINVAL, "null exponents %u", t);
@@ -2255,9 +2235,6 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
     const int g = gs[i].fbs[0]->geom;
     if (geom < 0) geom = g;
     if (g != geom) return fail(MPCX_EINVAL, "group %u: comb table layout differs from group 0's", i);
-    if (gs[i].muls && !geom_serves(g, gs[i].fbs[0]->mod, host_ops_below(gs[i].muls, gs[i].count, gs[i].mul_words,
-                                                                          (uint32_t)MPCX_GEOM_RBITS(g))))
-      return fail(MPCX_EINVAL, "group %u: multiplier too wide for a lane-pair comb table", i);
   }
   const uint32_t G = (uint32_t)MPCX_GEOM_G(geom), L = (uint32_t)MPCX_GEOM_L(geom);
   struct Seg {

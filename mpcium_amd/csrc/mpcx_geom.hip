@@ -66,9 +66,9 @@ __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_mul
   return hipGetLastError();
 }
 
-#if MPCX_GEOM_ID == MPCX_FULL_GEOM(0) || MPCX_GEOM_ID == MPCX_FULL_GEOM(1) || MPCX_GEOM_ID == 5
-// fixed-base comb kernel: the comb-table layouts (full-width geometries of the <= 2080-bit classes, and the
-// 2048-bit lane pair); `split` wavefronts per workgroup share its G operands' windows
+#if MPCX_GEOM_ID == MPCX_FULL_GEOM(0) || MPCX_GEOM_ID == MPCX_FULL_GEOM(1)
+// fixed-base comb kernel: the comb-table layouts (full-width geometries of the <= 2080-bit classes);
+// `split` wavefronts per workgroup share its G operands' windows
 #define MPCX_FB_ARGS MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID), MPCX_GEOM_G(MPCX_GEOM_ID)
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_fixedbase_g, MPCX_GEOM_ID)(
     const mpcx::FixedBaseArgs* a, uint32_t blocks, uint32_t split, hipStream_t st) {

@@ -307,40 +307,6 @@ def test_fixed_base_tables(gpu, paillier_key, wbits):
     mod.release()
 
 
-def test_fixed_base_lane_pair_tables(gpu, paillier_key):
-    """Option "fb_lanepair": tables of a modulus below 2^2070 in the lane-pair
-    (2 x 37) layout give the same products as pow(), alone, as two bases and
-    as segments of one multi-batch launch; a multiplier of 2072+ bits is
-    refused for such a table (the layout's R = 2^2072)."""
-    N = paillier_key["N"]
-    rng = random.Random(2070)
-    mod = gpu.Modulus(N)
-    h1, h2 = rng.randrange(N), rng.randrange(N)
-    gpu.set_option("fb_lanepair", 1)
-    try:
-        f1, f2 = gpu.FixedBase(mod, h1, 2816), gpu.FixedBase(mod, h2, 2048)
-    finally:
-        gpu.set_option("fb_lanepair", 0)
-    try:
-        for count in (1, 31, 33, 1000):
-            a = [rng.getrandbits(rng.choice([0, 1, 12, 2048, 2816])) for _ in range(count)]
-            b = [rng.getrandbits(rng.choice([0, 7, 2048])) for _ in range(count)]
-            cs = [rng.randrange(N) for _ in range(count)]
-            assert gpu.fixedbase_exp([f1], [a]) == [pow(h1, x, N) for x in a], count
-            want = [c * pow(h1, x, N) * pow(h2, y, N) % N for c, x, y in zip(cs, a, b)]
-            assert gpu.fixedbase_exp([f1, f2], [a, b], cs) == want, count
-        groups = [([f1], [[3, 4, 5]], None), ([f2, f1], [[7] * 40, list(range(40))], None)]
-        got = gpu.fixedbase_multi(groups)
-        assert got[0] == [pow(h1, e, N) for e in (3, 4, 5)]
-        assert got[1] == [pow(h2, 7, N) * pow(h1, e, N) % N for e in range(40)]
-        with pytest.raises(gpu.MpcxError):
-            gpu.fixedbase_exp([f1], [[5]], [1 << 2075])
-    finally:
-        f2.release()
-        f1.release()
-        mod.release()
-
-
 @pytest.mark.parametrize("split", [1, 2, 4, 0])
 def test_fixed_base_window_split(gpu, paillier_key, split):
     """Option "fb_split": 1, 2 or 4 wavefronts share one comb operand's
