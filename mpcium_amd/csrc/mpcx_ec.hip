@@ -115,8 +115,23 @@ __device__ __forceinline__ Fe fe_sub(const Fe& a, const Fe& b) {
   return r;
 }
 __device__ __forceinline__ Fe fe_dbl(const Fe& a) { return fe_add(a, a); }
-// a * b mod p: 8 x 8 schoolbook rows into 16 limbs, then two folds of the
-// high half by 2^256 = 2^32 + 977
+// t (512 bits, 16 limbs) mod p: two folds of the high half by
+// 2^256 = 2^32 + 977
+__device__ __forceinline__ Fe fe_reduce512(const uint32_t (&t)[16]) {
+  // r = lo + hi * 977 + (hi << 32)
+  Fe r;
+  uint64_t c = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    c += (uint64_t)t[i] + (uint64_t)t[8 + i] * 977u + (i ? t[7 + i] : 0u);
+    r.v[i] = (uint32_t)c;
+    c >>= 32;
+  }
+  c += t[15];  // the last shifted limb
+  fe_fold(r, c);
+  return r;
+}
+// a * b mod p: 8 x 8 schoolbook rows into 16 limbs, then the fold
 __device__ __forceinline__ Fe fe_mul(const Fe& a, const Fe& b) {
   uint32_t t[16];
 #pragma unroll
@@ -132,34 +147,69 @@ __device__ __forceinline__ Fe fe_mul(const Fe& a, const Fe& b) {
     }
     t[i + 8] = (uint32_t)c;
   }
-  // r = lo + hi * 977 + (hi << 32)
-  Fe r;
+  return fe_reduce512(t);
+}
+// a^2 mod p: the 28 products a_i a_j (i < j) once, doubled by a shift, plus
+// the 8 squares on the diagonal (36 limb products against fe_mul's 64)
+__device__ __forceinline__ Fe fe_sqr(const Fe& a) {
+  uint32_t t[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) t[i] = 0;
+#pragma unroll
+  for (int i = 0; i < 7; ++i) {
+    uint64_t c = 0;
+#pragma unroll
+    for (int j = i + 1; j < 8; ++j) {
+      c += (uint64_t)a.v[i] * a.v[j] + t[i + j];
+      t[i + j] = (uint32_t)c;
+      c >>= 32;
+    }
+    t[i + 8] = (uint32_t)c;  // no earlier row reaches limb i + 8
+  }
+  uint32_t top = 0;  // off-diagonal sum < 2^511: doubling fits 16 limbs
+#pragma unroll
+  for (int k = 0; k < 16; ++k) {
+    const uint32_t v = t[k];
+    t[k] = (v << 1) | top;
+    top = v >> 31;
+  }
   uint64_t c = 0;
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
-    c += (uint64_t)t[i] + (uint64_t)t[8 + i] * 977u + (i ? t[7 + i] : 0u);
-    r.v[i] = (uint32_t)c;
+    const uint64_t sq = (uint64_t)a.v[i] * a.v[i];
+    c += (uint64_t)t[2 * i] + (uint32_t)sq;
+    t[2 * i] = (uint32_t)c;
+    c >>= 32;
+    c += (uint64_t)t[2 * i + 1] + (sq >> 32);
+    t[2 * i + 1] = (uint32_t)c;
     c >>= 32;
   }
-  c += t[15];  // the last shifted limb
-  fe_fold(r, c);
+  return fe_reduce512(t);
+}
+__device__ Fe fe_sqr_n(Fe r, int n) {
+  for (int i = 0; i < n; ++i) r = fe_sqr(r);
   return r;
 }
-__device__ __forceinline__ Fe fe_sqr(const Fe& a) { return fe_mul(a, a); }
-// a^(p-2): p - 2 = 2^256 - 2^32 - 979 -- bits 255..33 set, bit 32 clear,
-// bits 31..0 = 0xFFFFFC2D
+// a^(p-2) by an addition chain: p - 2 = 2^256 - 2^32 - 979 is 223 ones, a
+// zero, then 0xFFFFFC2D = 22 ones, 00001, 011, 01. x_k = a^(2^k - 1) built
+// up to x223 (x_{i+j} = x_i^(2^j) x_j), then the low 33 bits appended:
+// 255 squarings and 15 multiplications (square-and-multiply: 255 + 238)
 __device__ Fe fe_inv(const Fe& a) {
-  Fe r = a;
-  for (int i = 254; i >= 33; --i) {  // the top 223 ones (bit 255 is the initial r)
-    r = fe_sqr(r);
-    r = fe_mul(r, a);
-  }
-  r = fe_sqr(r);  // bit 32 = 0
-  const uint32_t low = 0xFFFFFC2Du;
-  for (int i = 31; i >= 0; --i) {
-    r = fe_sqr(r);
-    if ((low >> i) & 1u) r = fe_mul(r, a);
-  }
+  const Fe x2 = fe_mul(fe_sqr(a), a);
+  const Fe x3 = fe_mul(fe_sqr(x2), a);
+  const Fe x6 = fe_mul(fe_sqr_n(x3, 3), x3);
+  const Fe x9 = fe_mul(fe_sqr_n(x6, 3), x3);
+  const Fe x11 = fe_mul(fe_sqr_n(x9, 2), x2);
+  const Fe x22 = fe_mul(fe_sqr_n(x11, 11), x11);
+  const Fe x44 = fe_mul(fe_sqr_n(x22, 22), x22);
+  const Fe x88 = fe_mul(fe_sqr_n(x44, 44), x44);
+  const Fe x176 = fe_mul(fe_sqr_n(x88, 88), x88);
+  const Fe x220 = fe_mul(fe_sqr_n(x176, 44), x44);
+  const Fe x223 = fe_mul(fe_sqr_n(x220, 3), x3);
+  Fe r = fe_mul(fe_sqr_n(x223, 23), x22);  // 223 ones, 0, 22 ones
+  r = fe_mul(fe_sqr_n(r, 5), a);           // 00001
+  r = fe_mul(fe_sqr_n(r, 3), x2);          // 011
+  r = fe_mul(fe_sqr_n(r, 2), a);           // 01
   return r;
 }
 
