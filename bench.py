@@ -385,7 +385,8 @@ def cpu_baseline_paillier(N: int, seconds: float, info: dict):
             **info}
 
 
-def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: int = 1, rank: int = 0):
+def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: int = 1, rank: int = 0,
+                  inflight: int = 16):
     """Config 1 (BASELINE.json): tss-lib paillier Encrypt + HomoMult over a
     batch of `batch` ops, 2048-bit N, through the host mirror of
     crypto/paillier (libmpcx_host.so -> libmpcx.so; host buffers, so the rate
@@ -419,8 +420,12 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: i
     el_seq = time.perf_counter() - t0
     # the same batches, `inflight` at a time from their own threads (a node's
     # concurrent sessions; the host mirror's Engine coalesces their launches):
-    # every batch is still 1,024 Encrypt + HomoMult ops
-    inflight = 4
+    # every batch is still 1,024 Encrypt + HomoMult ops. A batch alone is bound
+    # by one wavefront's serial chain (~25 ms for Encrypt in the narrow
+    # geometry); concurrent batches merge into mid / main geometry launches
+    # (tools/paillier_probe.py: 4 in flight 58.7K ops/s, 8: 69.5K, 16: 97-103K,
+    # 32: 129-135K; the default 16 is one batch per usable host thread)
+    inflight = max(1, inflight)
 
     def worker(k):
         for _ in range(reps):
@@ -986,6 +991,8 @@ def main():
     ap.add_argument("--keygen-wave", type=int, default=0,
                     help="config 5: sessions per bounded-memory wave (0: the driver's 1024)")
     ap.add_argument("--parties", type=int, default=5)
+    ap.add_argument("--paillier-inflight", type=int, default=16,
+                    help="config 1: batches of 1,024 in flight from their own threads (concurrent sessions)")
     ap.add_argument("--extra-lines", type=int, default=1,
                     help="1: add the config-1 (Paillier batch) and config-3 (safe primes) objects at N=1")
     ap.add_argument("--cpu-sign-seconds", type=float, default=15.0)
@@ -1252,7 +1259,7 @@ def main():
     if args.extra_lines:
         cpu = rank == 0 and world == 1 and not args.no_cpu_baseline
         progress("config 1 and 3: Paillier batch, safe primes")
-        result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, info, world, rank)
+        result["paillier_batch"] = paillier_line(N, 1024, 20, cpu, info, world, rank, args.paillier_inflight)
         result["safe_prime"] = safeprime_line(args.safe_primes, 0x5AFE, cpu, info, world, rank)
     if args.keygen_sessions > 0:
         progress(f"config 5: keygen/reshare proofs, {args.keygen_sessions} sessions per GPU")
