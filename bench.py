@@ -413,24 +413,33 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: i
         import torch.distributed as dist
         from mpcium_amd.shard import max_over_ranks
         dist.barrier()
+    # value: BASELINE.json configs[0] as stated -- ONE batch of 1,024 Encrypt +
+    # HomoMult ops at a time, repeated `reps` times
+    _kernel_stats_reset()
     t0 = time.perf_counter()
     for _ in range(reps):
         cs, _ = pk.encrypt(ms, rs)
         pk.homo_mult(bs, cs)
     el_seq = time.perf_counter() - t0
-    # the same batches, `inflight` at a time from their own threads (a node's
-    # concurrent sessions; the host mirror's Engine coalesces their launches):
-    # every batch is still 1,024 Encrypt + HomoMult ops. A batch alone is bound
-    # by one wavefront's serial chain (~25 ms for Encrypt in the narrow
-    # geometry); concurrent batches merge into mid / main geometry launches
-    # (tools/paillier_probe.py: 4 in flight 58.7K ops/s, 8: 69.5K, 16: 97-103K,
-    # 32: 129-135K; the default 16 is one batch per usable host thread)
+    seq_roof = _kernel_roofline()
+    # a second, separately labelled shape: `inflight` such batches at once from
+    # their own threads (a node's concurrent sessions; the Engine coalesces their
+    # launches). Every batch is still 1,024 ops; worker errors fail the run and
+    # one worker's last outputs are checked against the oracle formulas.
     inflight = max(1, inflight)
+    errors, last = [], {}
 
     def worker(k):
-        for _ in range(reps):
-            c, _ = pk.encrypt(ms, rs)
-            pk.homo_mult(bs, c)
+        try:
+            for _ in range(reps):
+                c, e1 = pk.encrypt(ms, rs)
+                o, e2 = pk.homo_mult(bs, c)
+                if any(e1) or any(e2):
+                    raise RuntimeError(f"worker {k}: error codes")
+            if k == 0:
+                last["c"], last["o"] = c, o
+        except BaseException as ex:  # noqa: BLE001 -- reported below
+            errors.append(f"{type(ex).__name__}: {ex}")
     if world > 1:
         dist.barrier()
     _kernel_stats_reset()
@@ -441,23 +450,32 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: i
     for th in ths:
         th.join()
     el = time.perf_counter() - t0
+    if errors:
+        raise SystemExit(f"paillier line: {len(errors)} worker(s) failed: {errors[0]}")
+    for i in range(0, batch, max(1, batch // 16)):
+        if last["c"][i] != gm.paillier_encrypt(N, ms[i], rs[i]) or \
+                last["o"][i] != gm.paillier_homo_mult(N, bs[i], last["c"][i]):
+            raise SystemExit(f"paillier line: in-flight worker 0 mismatch at {i}")
+    flight_roof = _kernel_roofline()
     if world > 1:
         el, el_seq = max_over_ranks([el, el_seq], world)
-    line = {"metric": "tss-lib paillier Encrypt+HomoMult ops/s (config 1: batches of 1024 ops, 2048-bit N)",
-            "value": batch * reps * inflight * world / el, "unit": "Encrypt+HomoMult ops/s", "batch": batch,
-            "reps": reps, "batches_in_flight": inflight, "seconds": el, "n_gpus": world, "scaling": "weak",
-            "one_batch_at_a_time": {"value": batch * reps * world / el_seq, "seconds": el_seq, "reps": reps},
+    line = {"metric": "tss-lib paillier Encrypt+HomoMult ops/s (config 1: one batch of 1024 ops at a time, 2048-bit N)",
+            "value": batch * reps * world / el_seq, "unit": "Encrypt+HomoMult ops/s", "batch": batch,
+            "reps": reps, "seconds": el_seq, "n_gpus": world, "scaling": "weak",
+            "batches_in_flight": {"batches": inflight, "value": batch * reps * inflight * world / el,
+                                  "seconds": el, "kernel_roofline": flight_roof,
+                                  "checked": "worker 0's last batch, 64 outputs vs oracle/gomath.py"},
             "note": "host-buffer API end to end (Python ints -> words -> PCIe -> GPU -> back); Encrypt's Gamma^m "
-                    "is the bit-exact 1 + mN shortcut, r^N a shared-exponent GPU batch, c^b per-operand; value: "
-                    f"{inflight} batches in flight from their own threads, one_batch_at_a_time: the latency-bound "
-                    "sequential rate",
+                    "is the bit-exact 1 + mN shortcut, r^N a shared-exponent GPU batch, c^b per-operand; value: one "
+                    "1,024-op batch at a time (BASELINE configs[0]); batches_in_flight: a different shape, "
+                    f"{inflight} such batches concurrently from their own threads",
             "cpu_baseline": None}
     # Go-equivalent work per op (SURVEY.md 8(d) W = (E + E/4) 2 L^2, L = 128 words of N^2): r^N (E = 2048) + c^b
     # (E = bit length of b < q); a 1,024-op batch is a small latency-bound launch pair, not a throughput shape
     L2 = 2 * 128 * 128
-    alg = sum((2048 + 512) * L2 + (b.bit_length() + (b.bit_length() + 3) // 4) * L2 for b in bs) * reps * inflight
-    line["roofline"] = _kernel_roofline()
-    line["job_roofline"] = _job_roofline(alg, el, world)
+    alg = sum((2048 + 512) * L2 + (b.bit_length() + (b.bit_length() + 3) // 4) * L2 for b in bs) * reps
+    line["roofline"] = seq_roof
+    line["job_roofline"] = _job_roofline(alg, el_seq, world)
     line["job_roofline"]["scope"] = "end to end (host buffers, Python conversions); batch of 1,024 = latency-bound"
     line["alg_ops_per_op"] = alg / (batch * reps)
     if cpu:
@@ -946,6 +964,13 @@ def compact_line(result: dict, detail_path: str | None) -> dict:
         cpu = sb.get("safe_primes_per_s_equiv", sb.get("value"))  # config 3: in the line's own unit
         cfg[dst] = {"value": _r(s.get("value")), "unit": s.get("unit"), "n_gpus": s.get("n_gpus"),
                     "frac": _r(fr, 3), "cpu": _r(cpu), "cores": sb.get("cores")}
+        bif = s.get("batches_in_flight")
+        if isinstance(bif, dict):  # config 1's second shape, labelled
+            cfg[dst]["batches_in_flight"] = bif.get("batches")
+            cfg[dst]["in_flight_value"] = _r(bif.get("value"))
+        for k in ("sessions", "concurrent_sessions", "reshare_value", "keygen_value", "host_rss_gb"):
+            if s.get(k) is not None:
+                cfg[dst][k] = _r(s[k]) if isinstance(s[k], float) else s[k]
     line["configs"] = cfg
     line["detail"] = detail_path
     # last resort: never exceed the driver's tail (drop the configs, which are in the detail file)
@@ -1013,8 +1038,21 @@ def main():
     os.environ.setdefault("MPCX_PROGRESS", "1")
     t_start = time.time()
 
+    # a native crash prints every thread's Python stack, and the module map
+    # (rewritten at every phase, so it lists each library loaded so far) lets
+    # a native stack's addresses be resolved afterwards
+    import faulthandler
+    faulthandler.enable()
+    maps_path = os.path.abspath(args.detail) + f".maps.rank{os.environ.get('RANK', '0')}.txt"
+
     def progress(msg):
         print(f"[bench {time.time() - t_start:7.1f} s] {msg}", file=sys.stderr, flush=True)
+        try:
+            os.makedirs(os.path.dirname(maps_path), exist_ok=True)
+            with open("/proc/self/maps") as fi, open(maps_path, "w") as fo:
+                fo.write(fi.read())
+        except OSError:
+            pass
 
     import torch
     import torch.distributed as dist
@@ -1266,6 +1304,15 @@ def main():
         result["keygen"] = keygen_line(args, world, rank)
         result["keygen"]["cpu_baseline"] = keygen_cpu
     progress("done")
+    result["host_copies"] = {"libmpcx": mpcx.copy_stats(), "maps": os.path.relpath(maps_path, ROOT),
+                             "note": "direct: DMA from/to mpcx_host_alloc blocks; bounced: copied by libmpcx through "
+                                     "its lanes' pinned buffers (no pageable pointer reaches hipMemcpyAsync)"}
+    try:
+        from mpcium_amd import host as mhost
+        if mhost._lib is not None:
+            result["host_copies"]["engine_pinned_pool"] = mhost.pinned_pool_stats()
+    except Exception as ex:  # noqa: BLE001 -- diagnostics only
+        result["host_copies"]["engine_pinned_pool"] = f"unavailable: {ex}"
     if rank == 0:
         detail = os.path.abspath(args.detail)
         os.makedirs(os.path.dirname(detail), exist_ok=True)

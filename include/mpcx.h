@@ -351,10 +351,17 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
 int mpcx_dev_alloc(size_t bytes, void** out_ptr);
 int mpcx_dev_free(void* ptr);
 /* Page-locked host memory (portable across the bound devices): host-buffer
- * batches staged here are copied by DMA, without the runtime's CPU bounce
- * copy of pageable memory. */
+ * batches staged here are copied by DMA. Every other host range a call reads
+ * or writes goes through the lane's own page-locked bounce buffer, copied by
+ * libmpcx in the calling thread: no pageable pointer reaches the HIP runtime's
+ * copy engine. A range that starts inside an mpcx_host_alloc block and runs
+ * past its end is rejected with MPCX_EINVAL. */
 int mpcx_host_alloc(size_t bytes, void** out_ptr);
 int mpcx_host_free(void* ptr);
+/* Host-copy counters since load: bytes DMA'd directly from/to mpcx_host_alloc
+ * blocks, bytes bounced through the lanes' pinned buffers, and bounce-buffer
+ * (re)allocations. Any pointer may be NULL. */
+int mpcx_copy_stats(uint64_t* direct_bytes, uint64_t* bounced_bytes, uint64_t* bounce_allocs);
 int mpcx_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes);
 int mpcx_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes);
 int mpcx_stream_create(void** out_stream);

@@ -322,6 +322,11 @@ int mpcxh_profile_report(char* buf, size_t cap, int reset);
  * (MPCX_HOST_THREADS, else min(usable CPUs, 16 per bound GPU)); *usable = the
  * CPUs this process may run on (affinity mask capped by the cgroup CPU quota). */
 int mpcxh_host_threads(int* threads, int* usable);
+/* The engine's page-locked staging pool (no GPU needed): bytes held (in use +
+ * cached), peak bytes in use, and the pageable fallbacks taken when pinning
+ * failed (count, bytes; each is also logged to stderr). Any pointer may be NULL. */
+int mpcxh_pinned_pool_stats(uint64_t* held_bytes, uint64_t* peak_in_use_bytes, uint64_t* fallbacks,
+                            uint64_t* fallback_bytes);
 /* Pool self-test (no GPU): `tasks` threads each run a parallel loop of `outer`
  * indices, each index a nested parallel loop of `inner` indices adding
  * (task+1)(o+1)(i+1); *sum = the total. */

@@ -346,6 +346,11 @@ int mpcxh_host_threads(int* threads, int* usable) {
   });
 }
 
+int mpcxh_pinned_pool_stats(uint64_t* held_bytes, uint64_t* peak_in_use_bytes, uint64_t* fallbacks,
+                            uint64_t* fallback_bytes) {
+  return guard([&] { pinned_pool_stats(held_bytes, peak_in_use_bytes, fallbacks, fallback_bytes); });
+}
+
 int mpcxh_nat_arith(int op, const uint32_t* a, uint32_t na, const uint32_t* b, uint32_t nb, uint32_t* out,
                     uint32_t nout, uint32_t* out_words) {
   return guard([&] {

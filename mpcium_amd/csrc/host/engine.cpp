@@ -2,6 +2,7 @@
 #include "engine.hpp"
 
 #include <condition_variable>
+#include <cstdio>
 #include <deque>
 #include <malloc.h>
 #include <string>
@@ -123,12 +124,16 @@ static void par_chunks(size_t n, const std::function<void(size_t, size_t)>& fn) 
 
 namespace {
 // Pool of page-locked host buffers (mpcx_host_alloc) for the batches' inputs
-// and outputs: copies from pageable memory go through the runtime's CPU
-// bounce buffer in the calling thread, which a signing run's concurrent tasks
-// then also contend for. Buffers are reused across calls (size classes of
-// powers of two) and never returned to the system.
+// and outputs: libmpcx DMAs them directly (anything else it bounces through
+// its lanes' own pinned buffers with a CPU copy). Buffers are reused across
+// calls (size classes of powers of two); free buffers beyond kCacheMax bytes
+// are returned to the system. A failed pinned allocation first releases every
+// cached free buffer and retries; only then does the batch fall back to a
+// pageable buffer -- counted, and logged to stderr (the first 8 times, then
+// every 1000th), never silent.
 class PinnedPool {
  public:
+  static constexpr size_t kCacheMax = size_t(8) << 30;
   static PinnedPool& get() {
     static PinnedPool p;
     return p;
@@ -142,31 +147,86 @@ class PinnedPool {
       if (!fl.empty()) {
         uint32_t* p = fl.back();
         fl.pop_back();
+        cached_bytes_ -= cls * 4;
+        note_use(cls * 4);
         return p;
       }
     }
     void* p = nullptr;
-    if (mpcx_host_alloc(cls * 4, &p) != MPCX_OK) return nullptr;
+    if (mpcx_host_alloc(cls * 4, &p) != MPCX_OK) {
+      release_cached();
+      if (mpcx_host_alloc(cls * 4, &p) != MPCX_OK) return nullptr;
+    }
     std::lock_guard<std::mutex> lk(mu_);
     size_of_[(uint32_t*)p] = cls;
+    held_bytes_ += cls * 4;
+    note_use(cls * 4);
     return (uint32_t*)p;
   }
   void release(uint32_t* p) {
     if (!p) return;
+    std::unique_lock<std::mutex> lk(mu_);
+    const size_t cls = size_of_.at(p);
+    in_use_bytes_ -= cls * 4;
+    if (cached_bytes_ + cls * 4 > kCacheMax) {
+      size_of_.erase(p);
+      held_bytes_ -= cls * 4;
+      lk.unlock();
+      mpcx_host_free(p);
+      return;
+    }
+    free_[cls].push_back(p);
+    cached_bytes_ += cls * 4;
+  }
+  void note_fallback(size_t words) {
+    const uint64_t k = fallbacks_.fetch_add(1) + 1;
+    fallback_bytes_ += words * 4;
+    if (k <= 8 || k % 1000 == 0)
+      std::fprintf(stderr, "[mpcx engine] pinned host allocation of %zu B failed (%s): pageable buffer #%llu\n",
+                   words * 4, mpcx_last_error(), (unsigned long long)k);
+  }
+  void stats(uint64_t* held, uint64_t* peak_in_use, uint64_t* fallbacks, uint64_t* fallback_bytes) {
     std::lock_guard<std::mutex> lk(mu_);
-    free_[size_of_.at(p)].push_back(p);
+    if (held) *held = held_bytes_;
+    if (peak_in_use) *peak_in_use = peak_in_use_;
+    if (fallbacks) *fallbacks = fallbacks_.load();
+    if (fallback_bytes) *fallback_bytes = fallback_bytes_.load();
   }
 
  private:
+  void note_use(size_t bytes) {  // mu_ held
+    in_use_bytes_ += bytes;
+    peak_in_use_ = std::max(peak_in_use_, in_use_bytes_);
+  }
+  void release_cached() {
+    std::vector<uint32_t*> drop;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      for (auto& [cls, fl] : free_) {
+        for (uint32_t* p : fl) {
+          drop.push_back(p);
+          size_of_.erase(p);
+          held_bytes_ -= cls * 4;
+        }
+        fl.clear();
+      }
+      cached_bytes_ = 0;
+    }
+    for (uint32_t* p : drop) mpcx_host_free(p);
+  }
   std::mutex mu_;
   std::map<size_t, std::vector<uint32_t*>> free_;
   std::map<uint32_t*, size_t> size_of_;
+  size_t held_bytes_ = 0, cached_bytes_ = 0, in_use_bytes_ = 0, peak_in_use_ = 0;
+  std::atomic<uint64_t> fallbacks_{0}, fallback_bytes_{0};
 };
 
-// a pinned buffer of `words` words (pageable fallback if pinning fails)
+// a pinned buffer of `words` words (a counted, logged pageable fallback if
+// pinning fails: libmpcx then bounces it, so the batch stays correct)
 struct HostBuf {
   uint32_t* p = nullptr;
   std::vector<uint32_t> fallback;
+  bool pinned = false;
   explicit HostBuf(size_t words) {
     static const bool off = [] {  // MPCX_PINNED=0: pageable staging (A/B runs)
       const char* e = std::getenv("MPCX_PINNED");
@@ -174,6 +234,7 @@ struct HostBuf {
     }();
     p = off ? nullptr : PinnedPool::get().acquire(words);
     if (!p) {
+      if (!off) PinnedPool::get().note_fallback(words);
       fallback.resize(words);
       p = fallback.data();
     } else {
@@ -185,9 +246,13 @@ struct HostBuf {
   }
   HostBuf(const HostBuf&) = delete;
   HostBuf& operator=(const HostBuf&) = delete;
-  bool pinned = false;
 };
 }  // namespace
+
+void pinned_pool_stats(uint64_t* held_bytes, uint64_t* peak_in_use_bytes, uint64_t* fallbacks,
+                       uint64_t* fallback_bytes) {
+  PinnedPool::get().stats(held_bytes, peak_in_use_bytes, fallbacks, fallback_bytes);
+}
 
 namespace {
 // Launch coalescing across concurrent callers (ExpSets of different signer

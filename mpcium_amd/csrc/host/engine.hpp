@@ -153,4 +153,9 @@ class Engine {
 
 [[noreturn]] void throw_last(int rc, const char* what);
 
+// Engine's page-locked staging pool: bytes held (in use + cached), peak bytes
+// in use, and the pageable fallbacks taken when pinning failed (count, bytes).
+void pinned_pool_stats(uint64_t* held_bytes, uint64_t* peak_in_use_bytes, uint64_t* fallbacks,
+                       uint64_t* fallback_bytes);
+
 }  // namespace mpcx::host

@@ -153,20 +153,27 @@ class ExpSet {
     for (size_t i = 0; i < reqs2_.size(); ++i) by_b[{reqs2_[i].b1, reqs2_[i].b2}].push_back(i);
     const bool comb = Engine::get().fixed_base_ok(m_);
     for (auto& kv : by_b) {
-      auto idx = kv.second;
-      bool fits = comb && idx.size() >= kFixedMin;
-      for (size_t i : idx)
-        fits = fits && reqs2_[i].e1->bit_len() <= Engine::kFixedMaxBits &&
-               reqs2_[i].e2->bit_len() <= Engine::kFixedMaxBits;
-      if (fits) {
-        std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
-          return std::max(reqs2_[a].e1->bit_len(), reqs2_[a].e2->bit_len()) <
-                 std::max(reqs2_[b].e1->bit_len(), reqs2_[b].e2->bit_len());
-        });
-        fs.push_back([this, idx] { launch_fixed2(idx); });
-      } else {
+      // only the requests with an over-long (peer-supplied, unbounded) exponent
+      // leave the comb path; the rest of the group stays on it
+      std::vector<size_t> idx, longx;
+      for (size_t i : kv.second)
+        (reqs2_[i].e1->bit_len() <= Engine::kFixedMaxBits && reqs2_[i].e2->bit_len() <= Engine::kFixedMaxBits
+             ? idx
+             : longx)
+            .push_back(i);
+      if (!comb || idx.size() < kFixedMin) {
+        idx.insert(idx.end(), longx.begin(), longx.end());
+        longx.clear();
+        std::sort(idx.begin(), idx.end());
         fs.push_back([this, idx] { launch_two_step(idx); });
+        continue;
       }
+      std::stable_sort(idx.begin(), idx.end(), [&](size_t a, size_t b) {
+        return std::max(reqs2_[a].e1->bit_len(), reqs2_[a].e2->bit_len()) <
+               std::max(reqs2_[b].e1->bit_len(), reqs2_[b].e2->bit_len());
+      });
+      fs.push_back([this, idx] { launch_fixed2(idx); });
+      if (!longx.empty()) fs.push_back([this, longx] { launch_two_step(longx); });
     }
   }
   void launch_fixed2(const std::vector<size_t>& idx) {

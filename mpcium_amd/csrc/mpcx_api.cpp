@@ -30,6 +30,7 @@
 #include <map>
 #include <memory>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -160,6 +161,25 @@ struct Lane {
   };
   std::vector<KEv> kev_free;
   std::vector<KPend> kpend;
+  // Page-locked bounce buffers for host memory that is not a registered
+  // pinned allocation (mpcx_host_alloc): the call copies it here itself and
+  // DMAs from here, and D2H results land here and are copied out after the
+  // lane's host wait (`post`). No pageable pointer ever reaches
+  // hipMemcpyAsync, whose pageable path made a CPU read in the runtime that
+  // faulted once (profiles/r04/final3/segv/). Cursors reset at
+  // every completed wait; guarded by mu.
+  struct Bounce {
+    char* p = nullptr;
+    size_t cap = 0, used = 0;
+  };
+  Bounce hin, hout;
+  struct Post {
+    void* dst;
+    const void* src;
+    size_t bytes;
+  };
+  std::vector<Post> post;
+  bool pending = false;  // copies queued since the last completed wait
 };
 constexpr int kMaxLanes = 8;
 // lanes in use per device: MPCX_LANES (1..8, read at init) or the "lanes" option;
@@ -204,6 +224,38 @@ int fail(int code, const char* fmt, ...) {
 int hip_fail(hipError_t e, const char* what) {
   return fail(MPCX_EHIP, "%s: %s", what, hipGetErrorString(e));
 }
+
+// Registry of this library's page-locked allocations (mpcx_host_alloc):
+// [start, start + bytes). A host range entirely inside one is DMA'd
+// directly; a range that starts inside one and runs past its end is a caller
+// bug and fails loudly (the bounds check of VERDICT r4 item 1); anything
+// else is bounced through the lane's own pinned buffer.
+struct PinRegistry {
+  std::shared_mutex mu;
+  std::map<uintptr_t, size_t> ranges;
+  void add(const void* p, size_t bytes) {
+    std::unique_lock<std::shared_mutex> lk(mu);
+    ranges[(uintptr_t)p] = bytes;
+  }
+  void remove(const void* p) {
+    std::unique_lock<std::shared_mutex> lk(mu);
+    ranges.erase((uintptr_t)p);
+  }
+  // 1: inside one pinned allocation; 0: not pinned; -1: overruns one
+  int lookup(const void* p, size_t bytes) {
+    const uintptr_t a = (uintptr_t)p;
+    std::shared_lock<std::shared_mutex> lk(mu);
+    auto it = ranges.upper_bound(a);
+    if (it == ranges.begin()) return 0;
+    --it;
+    if (a >= it->first + it->second) return 0;
+    return a + bytes <= it->first + it->second ? 1 : -1;
+  }
+};
+PinRegistry g_pins;
+// copy statistics (mpcx_copy_stats): bytes DMA'd from/to registered pinned
+// memory, bytes bounced through the lanes' buffers, bounce-buffer growth
+std::atomic<uint64_t> g_cp_direct{0}, g_cp_bounced{0}, g_cp_bounce_grow{0};
 
 // Launch log (environment MPCX_LAUNCH_LOG=<path>): one CSV line per kernel
 // launch of the batch entry points -- kind, geometry, operands, modulus bits,
@@ -495,21 +547,154 @@ int lane_wait(Lane& l) {
       }
     }
   }
-  if (e != hipSuccess) return hip_fail(e, "lane wait");
+  if (e != hipSuccess) {
+    (void)hipStreamSynchronize(l.st);  // nothing of this call may still read or write host memory
+    l.post.clear();
+    l.hin.used = l.hout.used = 0;
+    l.pending = false;
+    return hip_fail(e, "lane wait");
+  }
+  // bounced results to their destinations, then the bounce buffers are free
+  for (const auto& p : l.post) std::memcpy(p.dst, p.src, p.bytes);
+  l.post.clear();
+  l.hin.used = l.hout.used = 0;
+  l.pending = false;
   if (!l.kpend.empty()) kstat_resolve(l);
   return MPCX_OK;
 }
 
-int h2d(void* d, const void* h, size_t bytes, hipStream_t st) {
+// A call that fails after queueing copies on its lane drains the lane before
+// it returns: those copies read or write the caller's buffers, which the
+// caller frees or reuses as soon as it sees the error (VERDICT r4 item 1,
+// ADVICE r4). Declared after the lane's lock, so it runs before the unlock.
+struct LaneDrain {
+  Lane& l;
+  explicit LaneDrain(Lane& lane) : l(lane) {}
+  ~LaneDrain() {
+    if (!l.pending) return;
+    if (l.st) (void)hipStreamSynchronize(l.st);
+    l.post.clear();  // the call failed: its results are not delivered
+    l.hin.used = l.hout.used = 0;
+    l.pending = false;
+  }
+  LaneDrain(const LaneDrain&) = delete;
+  LaneDrain& operator=(const LaneDrain&) = delete;
+};
+
+// `bytes` of lane bounce buffer b. When it is full, the lane's queued work
+// is waited for first (copies may still read the in-buffer; bounced results
+// are delivered), then the buffer grows if one request needs more.
+int bounce_reserve(Lane& l, Lane::Bounce& b, size_t bytes, char** out) {
+  const size_t need = (bytes + 255) & ~(size_t)255;
+  if (b.used + need > b.cap) {
+    if (l.hin.used || l.hout.used) {
+      hipError_t e = hipStreamSynchronize(l.st);
+      if (e != hipSuccess) return hip_fail(e, "bounce-buffer wait");
+      for (const auto& p : l.post) std::memcpy(p.dst, p.src, p.bytes);
+      l.post.clear();
+      l.hin.used = l.hout.used = 0;
+    }
+    if (need > b.cap) {
+      if (b.p) (void)hipHostFree(b.p);
+      b.p = nullptr;
+      b.cap = 0;
+      const size_t want = std::max<size_t>({need + need / 4, (size_t)1 << 20});
+      hipError_t e = hipHostMalloc((void**)&b.p, want, hipHostMallocPortable);
+      if (e != hipSuccess) {
+        b.p = nullptr;
+        return fail(MPCX_ENOMEM, "hipHostMalloc(bounce %zu): %s", want, hipGetErrorString(e));
+      }
+      b.cap = want;
+      g_cp_bounce_grow.fetch_add(1, std::memory_order_relaxed);
+    }
+  }
+  *out = b.p + b.used;
+  b.used += need;
+  return MPCX_OK;
+}
+
+// Host-to-device copy on lane l: straight from a registered pinned range,
+// else through the lane's bounce buffer (the copy into it is ours, in this
+// thread, within the caller's stated range).
+int h2d(Lane& l, void* d, const void* h, size_t bytes) {
   if (!bytes) return MPCX_OK;
-  hipError_t e = hipMemcpyAsync(d, h, bytes, hipMemcpyHostToDevice, st);
+  const int pin = g_pins.lookup(h, bytes);
+  if (pin < 0) return fail(MPCX_EINVAL, "host source of %zu B at %p overruns its pinned allocation", bytes, h);
+  const void* src = h;
+  if (pin == 0) {
+    char* b = nullptr;
+    if (int rc = bounce_reserve(l, l.hin, bytes, &b)) return rc;
+    std::memcpy(b, h, bytes);
+    src = b;
+    g_cp_bounced.fetch_add(bytes, std::memory_order_relaxed);
+  } else {
+    g_cp_direct.fetch_add(bytes, std::memory_order_relaxed);
+  }
+  l.pending = true;
+  hipError_t e = hipMemcpyAsync(d, src, bytes, hipMemcpyHostToDevice, l.st);
   return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy inputs");
 }
 
+// Device-to-host copy on lane l, complete after the lane's next successful
+// lane_wait (a bounced result is copied to h by that wait).
+int d2h(Lane& l, void* h, const void* d, size_t bytes) {
+  if (!bytes) return MPCX_OK;
+  const int pin = g_pins.lookup(h, bytes);
+  if (pin < 0) return fail(MPCX_EINVAL, "host destination of %zu B at %p overruns its pinned allocation", bytes, h);
+  void* dst = h;
+  if (pin == 0) {
+    char* b = nullptr;
+    if (int rc = bounce_reserve(l, l.hout, bytes, &b)) return rc;
+    dst = b;
+    l.post.push_back({h, b, bytes});
+    g_cp_bounced.fetch_add(bytes, std::memory_order_relaxed);
+  } else {
+    g_cp_direct.fetch_add(bytes, std::memory_order_relaxed);
+  }
+  l.pending = true;
+  hipError_t e = hipMemcpyAsync(dst, d, bytes, hipMemcpyDeviceToHost, l.st);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy results");
+}
+
 int d2h_sync(void* h, const void* d, size_t bytes, Lane& l) {
-  hipError_t e = bytes ? hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, l.st) : hipSuccess;
-  if (e != hipSuccess) return hip_fail(e, "copy results");
+  if (int rc = d2h(l, h, d, bytes)) return rc;
   return lane_wait(l);
+}
+
+// Synchronous copy of a large or one-off host buffer (modulus constants, comb
+// tables and their build inputs, the public mpcx_memcpy_* helpers) on stream
+// st, through a temporary pinned chunk unless the range is registered pinned.
+int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st) {
+  if (!bytes) return MPCX_OK;
+  const void* hp = kind == hipMemcpyHostToDevice ? src : dst;
+  const int pin = g_pins.lookup(hp, bytes);
+  if (pin < 0) return fail(MPCX_EINVAL, "host range of %zu B at %p overruns its pinned allocation", bytes, hp);
+  hipError_t e;
+  if (pin == 1) {
+    e = hipMemcpyAsync(dst, src, bytes, kind, st);
+    if (e == hipSuccess) e = hipStreamSynchronize(st);
+    return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy");
+  }
+  constexpr size_t kChunk = (size_t)16 << 20;
+  char* buf = nullptr;
+  const size_t cb = std::min(bytes, kChunk);
+  e = hipHostMalloc((void**)&buf, cb, hipHostMallocPortable);
+  if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipHostMalloc(copy chunk %zu): %s", cb, hipGetErrorString(e));
+  for (size_t off = 0; off < bytes && e == hipSuccess; off += cb) {
+    const size_t n = std::min(cb, bytes - off);
+    if (kind == hipMemcpyHostToDevice) {
+      std::memcpy(buf, (const char*)src + off, n);
+      e = hipMemcpyAsync((char*)dst + off, buf, n, kind, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+    } else {
+      e = hipMemcpyAsync(buf, (const char*)src + off, n, kind, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (e == hipSuccess) std::memcpy((char*)dst + off, buf, n);
+    }
+  }
+  (void)hipHostFree(buf);
+  g_cp_bounced.fetch_add(bytes, std::memory_order_relaxed);
+  return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy");
 }
 
 // Buffers grow with headroom: hipFree waits for the whole device, so a size
@@ -575,6 +760,12 @@ void drop_lane(Lane& l) {
     if (s.ptr) (void)hipFree(s.ptr);
     s = Staging{};
   }
+  for (Lane::Bounce* b : {&l.hin, &l.hout}) {
+    if (b->p) (void)hipHostFree(b->p);
+    *b = Lane::Bounce{};
+  }
+  l.post.clear();
+  l.pending = false;
 }
 
 // Device-buffer workspace of (device, caller stream).
@@ -595,7 +786,8 @@ int run_selftest() {
   if (e != hipSuccess) return hip_fail(e, "selftest alloc");
   e = mpcx_launch_selftest(d, nullptr);
   std::vector<uint32_t> h(256);
-  if (e == hipSuccess) e = hipMemcpy(h.data(), d, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost);
+  if (e == hipSuccess && copy_sync(h.data(), d, 256 * sizeof(uint32_t), hipMemcpyDeviceToHost, nullptr) != MPCX_OK)
+    e = hipErrorInvalidValue;
   (void)hipFree(d);
   if (e != hipSuccess) return hip_fail(e, "selftest");
   for (uint32_t l = 0; l < 64; ++l) {
@@ -656,10 +848,10 @@ int mod_const(mpcx_mod_t mod, int di, const uint32_t** out) {
     uint32_t* p = nullptr;
     hipError_t e = hipMalloc((void**)&p, mod->host_const.size() * sizeof(uint32_t));
     if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(modulus): %s", hipGetErrorString(e));
-    e = hipMemcpy(p, mod->host_const.data(), mod->host_const.size() * sizeof(uint32_t), hipMemcpyHostToDevice);
-    if (e != hipSuccess) {
+    if (int rc = copy_sync(p, mod->host_const.data(), mod->host_const.size() * sizeof(uint32_t),
+                           hipMemcpyHostToDevice, nullptr)) {
       (void)hipFree(p);
-      return hip_fail(e, "upload modulus");
+      return rc;
     }
     mod->d_const[di] = p;
   }
@@ -675,8 +867,9 @@ int fb_table(mpcx_fb_t fb, int di, const uint32_t** out) {
     hipError_t e = hipMalloc((void**)&p, bytes);
     if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(fixed-base table %zu B)", bytes);
     if (!fb->host_table.empty()) {
-      e = hipMemcpy(p, fb->host_table.data(), bytes, hipMemcpyHostToDevice);
-      if (e == hipSuccess) std::vector<uint32_t>().swap(fb->host_table);  // the device copy is the master now
+      const int rc = copy_sync(p, fb->host_table.data(), bytes, hipMemcpyHostToDevice, nullptr);
+      e = rc ? hipErrorInvalidValue : hipSuccess;
+      if (rc == MPCX_OK) std::vector<uint32_t>().swap(fb->host_table);  // the device copy is the master now
     } else {
       int src = -1;
       for (int j = 0; j < kMaxDevices && src < 0; ++j)
@@ -1284,14 +1477,15 @@ static int modexp_host_range(int di, mpcx_mod_t mod, uint32_t count, const uint3
                ob = (size_t)count * out_words * 4, mb = muls ? (size_t)count * mul_words * 4 : 0;
   std::unique_lock<std::mutex> lk;
   Lane& l = acquire_lane(g_devs[di], lk);
+  LaneDrain drain(l);
   int rc;
   if ((rc = lane_stream(l))) return rc;
   Staging* sg = l.stage;
   if ((rc = ensure_buffer(sg[0], bb)) || (rc = ensure_buffer(sg[1], eb)) || (rc = ensure_buffer(sg[2], ob)) ||
       (muls && (rc = ensure_buffer(sg[3], mb))))
     return rc;
-  if ((rc = h2d(sg[0].ptr, bases, bb, l.st)) || (rc = h2d(sg[1].ptr, exps, n_exp_words * 4, l.st)) ||
-      (muls && (rc = h2d(sg[3].ptr, muls, mb, l.st))))
+  if ((rc = h2d(l, sg[0].ptr, bases, bb)) || (rc = h2d(l, sg[1].ptr, exps, n_exp_words * 4)) ||
+      (muls && (rc = h2d(l, sg[3].ptr, muls, mb))))
     return rc;
   const uint32_t rb = (uint32_t)MPCX_GEOM_RBITS(g_main_geom[mod->cls]);
   const bool ops_fit = host_ops_below(bases, count, base_words, rb) && host_ops_below(muls, count, mul_words, rb);
@@ -1558,6 +1752,7 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
   const size_t seg_bytes = nseg * sizeof(mpcx::ModexpArgs), first_bytes = (nseg + 1) * sizeof(uint32_t);
   std::unique_lock<std::mutex> lk;
   Lane& l = acquire_lane(dev, lk);
+  LaneDrain drain(l);
   if ((rc = lane_stream(l))) return rc;
   if ((rc = ensure_buffer(l.stage[0], std::max<size_t>(in_words * 4, 4))) ||
       (rc = ensure_buffer(l.stage[2], out_words * 4)) || (rc = ensure_buffer(l.stage[3], seg_bytes + first_bytes)) ||
@@ -1570,9 +1765,9 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
   for (const auto& sg : segs) {
     const mpcx_modexp_group_t& g = gs[sg.gi];
     const size_t ne = g.exp_shared ? g.exp_words : (size_t)g.count * g.exp_words;
-    if ((rc = h2d((uint32_t*)l.stage[0].ptr + sg.in_b, g.bases, (size_t)g.count * g.base_words * 4, l.st)) ||
-        (rc = h2d((uint32_t*)l.stage[0].ptr + sg.in_e, g.exps, ne * 4, l.st)) ||
-        (g.muls && (rc = h2d((uint32_t*)l.stage[0].ptr + sg.in_m, g.muls, (size_t)g.count * g.mul_words * 4, l.st))))
+    if ((rc = h2d(l, (uint32_t*)l.stage[0].ptr + sg.in_b, g.bases, (size_t)g.count * g.base_words * 4)) ||
+        (rc = h2d(l, (uint32_t*)l.stage[0].ptr + sg.in_e, g.exps, ne * 4)) ||
+        (g.muls && (rc = h2d(l, (uint32_t*)l.stage[0].ptr + sg.in_m, g.muls, (size_t)g.count * g.mul_words * 4))))
       return rc;
   }
   std::vector<mpcx::ModexpArgs> args(nseg);
@@ -1612,8 +1807,8 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
     a.sched = sg.use_sched ? l.ws + sg.sched : nullptr;
     first[k + 1] = first[k] + sg.waves;
   }
-  if ((rc = h2d(l.stage[3].ptr, args.data(), seg_bytes, l.st)) ||
-      (rc = h2d((char*)l.stage[3].ptr + seg_bytes, first.data(), first_bytes, l.st)))
+  if ((rc = h2d(l, l.stage[3].ptr, args.data(), seg_bytes)) ||
+      (rc = h2d(l, (char*)l.stage[3].ptr + seg_bytes, first.data(), first_bytes)))
     return rc;
   const int ks = kstat_begin(l);
   hipError_t e = mpcx_launch_modexp_multi(geom, (const mpcx::ModexpArgs*)l.stage[3].ptr,
@@ -1633,8 +1828,7 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
   for (const auto& sg : segs) launch_log("modexp_multi", geom, gs[sg.gi].count, gs[sg.gi].mod->bits, sg.exp_bits, sg.alg);
   for (const auto& sg : segs) {  // results straight into each group's buffer
     const mpcx_modexp_group_t& g = gs[sg.gi];
-    e = hipMemcpyAsync(g.out, d_out + sg.out_o, (size_t)g.count * g.out_words * 4, hipMemcpyDeviceToHost, l.st);
-    if (e != hipSuccess) return hip_fail(e, "copy results");
+    if ((rc = d2h(l, g.out, d_out + sg.out_o, (size_t)g.count * g.out_words * 4))) return rc;
   }
   return lane_wait(l);
 }
@@ -1670,7 +1864,7 @@ int ec_gtab(Device& d, Lane& l, const uint32_t** out) {
     uint32_t* tab = nullptr;
     hipError_t e = hipMalloc((void**)&tab, (size_t)kEcTabEntries * 16u * 4u);
     if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(secp256k1 comb): %s", hipGetErrorString(e));
-    if ((rc = h2d(l.stage[0].ptr, sc.data(), sb, l.st)) || (rc = h2d(l.stage[1].ptr, pts.data(), pb, l.st))) {
+    if ((rc = h2d(l, l.stage[0].ptr, sc.data(), sb)) || (rc = h2d(l, l.stage[1].ptr, pts.data(), pb))) {
       (void)hipFree(tab);
       return rc;
     }
@@ -1694,6 +1888,7 @@ int ec_range(int di, uint32_t count, const uint32_t* scalars, const uint32_t* po
   Device& d = g_devs[di];
   std::unique_lock<std::mutex> lk;
   Lane& l = acquire_lane(d, lk);
+  LaneDrain drain(l);
   int rc;
   if ((rc = lane_stream(l))) return rc;
   const uint32_t* gtab = nullptr;
@@ -1702,7 +1897,7 @@ int ec_range(int di, uint32_t count, const uint32_t* scalars, const uint32_t* po
   if ((rc = ensure_buffer(l.stage[0], sb)) || (rc = ensure_buffer(l.stage[1], pb)) ||
       (rc = ensure_buffer(l.stage[2], ob)) || (rc = ensure_workspace(l, ec_ws_words(count) * 4)))
     return rc;
-  if ((rc = h2d(l.stage[0].ptr, scalars, sb, l.st)) || (rc = h2d(l.stage[1].ptr, points, pb, l.st))) return rc;
+  if ((rc = h2d(l, l.stage[0].ptr, scalars, sb)) || (rc = h2d(l, l.stage[1].ptr, points, pb))) return rc;
   const int ks = kstat_begin(l);
   hipError_t e = mpcx_launch_ec_combine((const uint32_t*)l.stage[0].ptr, (const uint32_t*)l.stage[1].ptr,
                                         (uint32_t*)l.stage[2].ptr, gtab, l.ws, count, l.st);
@@ -1737,6 +1932,7 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
   return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t n) {
     std::unique_lock<std::mutex> lk;
     Lane& l = acquire_lane(g_devs[di], lk);
+    LaneDrain drain(l);
     int rc;
     if ((rc = lane_stream(l))) return rc;
     const size_t pb = (size_t)n * p_words * 4;
@@ -1744,7 +1940,7 @@ int mpcx_fermat2_batch(uint32_t count, const uint32_t* p, uint32_t p_words, uint
         (g_prime_coop && ((rc = ensure_buffer(l.stage[1], (size_t)n * MPCX_PRIME_L * 4)) ||
                           (rc = ensure_buffer(l.stage[2], (size_t)n * 8)))))
       return rc;
-    if ((rc = h2d(l.stage[0].ptr, p + (size_t)first * p_words, pb, l.st))) return rc;
+    if ((rc = h2d(l, l.stage[0].ptr, p + (size_t)first * p_words, pb))) return rc;
     mpcx::Prime2Args a{};
     a.nf = (const uint32_t*)l.stage[0].ptr;
     a.count_f = n;
@@ -1779,6 +1975,7 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
   return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t cnt) {
     std::unique_lock<std::mutex> lk;
     Lane& l = acquire_lane(g_devs[di], lk);
+    LaneDrain drain(l);
     int rc;
     if ((rc = lane_stream(l))) return rc;
     const size_t nb = (size_t)cnt * n_words * 4;
@@ -1786,8 +1983,8 @@ int mpcx_mr_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const uin
         (rc = ensure_buffer(l.stage[3], cnt)) ||
         (g_prime_coop && (rc = ensure_buffer(l.stage[2], (size_t)cnt * (MPCX_MR_L + 2) * 4))))
       return rc;
-    if ((rc = h2d(l.stage[0].ptr, n + (size_t)first * n_words, nb, l.st)) ||
-        (rc = h2d(l.stage[1].ptr, bases + (size_t)first * n_words, nb, l.st)))
+    if ((rc = h2d(l, l.stage[0].ptr, n + (size_t)first * n_words, nb)) ||
+        (rc = h2d(l, l.stage[1].ptr, bases + (size_t)first * n_words, nb)))
       return rc;
     mpcx::MrArgs a{};
     a.n = (const uint32_t*)l.stage[0].ptr;
@@ -1827,6 +2024,7 @@ int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const 
   return run_sliced(count, g_split_min, [&](int di, uint32_t first, uint32_t cnt) {
     std::unique_lock<std::mutex> lk;
     Lane& l = acquire_lane(g_devs[di], lk);
+    LaneDrain drain(l);
     int rc;
     if ((rc = lane_stream(l))) return rc;
     const size_t nb = (size_t)cnt * n_words * 4;
@@ -1834,8 +2032,8 @@ int mpcx_lucas_batch(uint32_t count, const uint32_t* n, uint32_t n_words, const 
         (rc = ensure_buffer(l.stage[3], cnt)) ||
         ((g_prime_coop || wide) && (rc = ensure_buffer(l.stage[2], (size_t)cnt * (4 * cl + 2) * 4))))
       return rc;
-    if ((rc = h2d(l.stage[0].ptr, n + (size_t)first * n_words, nb, l.st)) ||
-        (rc = h2d(l.stage[1].ptr, P + first, (size_t)cnt * 4, l.st)))
+    if ((rc = h2d(l, l.stage[0].ptr, n + (size_t)first * n_words, nb)) ||
+        (rc = h2d(l, l.stage[1].ptr, P + first, (size_t)cnt * 4)))
       return rc;
     mpcx::LucasArgs a{};
     a.n = (const uint32_t*)l.stage[0].ptr;
@@ -1876,23 +2074,31 @@ int mpcx_host_alloc(size_t bytes, void** out_ptr) {
   if (int rc = selected(&dev)) return rc;
   hipError_t e = hipHostMalloc(out_ptr, std::max<size_t>(bytes, 1), hipHostMallocPortable);
   if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipHostMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  g_pins.add(*out_ptr, std::max<size_t>(bytes, 1));
   return MPCX_OK;
 }
 
 int mpcx_host_free(void* ptr) {
   if (!ptr) return MPCX_OK;
+  g_pins.remove(ptr);
   hipError_t e = hipHostFree(ptr);
   return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipHostFree");
 }
 
+int mpcx_copy_stats(uint64_t* direct_bytes, uint64_t* bounced_bytes, uint64_t* bounce_allocs) {
+  if (direct_bytes) *direct_bytes = g_cp_direct.load(std::memory_order_relaxed);
+  if (bounced_bytes) *bounced_bytes = g_cp_bounced.load(std::memory_order_relaxed);
+  if (bounce_allocs) *bounce_allocs = g_cp_bounce_grow.load(std::memory_order_relaxed);
+  return MPCX_OK;
+}
+
 int mpcx_memcpy_h2d(void* d_dst, const void* h_src, size_t bytes) {
-  hipError_t e = hipMemcpy(d_dst, h_src, bytes, hipMemcpyHostToDevice);
-  return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipMemcpy H2D");
+  // the null stream: ordered after earlier blocking-stream work (hipMemcpy's semantics)
+  return copy_sync(d_dst, h_src, bytes, hipMemcpyHostToDevice, nullptr);
 }
 
 int mpcx_memcpy_d2h(void* h_dst, const void* d_src, size_t bytes) {
-  hipError_t e = hipMemcpy(h_dst, d_src, bytes, hipMemcpyDeviceToHost);
-  return e == hipSuccess ? MPCX_OK : hip_fail(e, "hipMemcpy D2H");
+  return copy_sync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, nullptr);
 }
 
 int mpcx_stream_create(void** out_stream) {
@@ -1956,6 +2162,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
   const int di = (int)(dev - g_devs);
   Lane& bl = dev->build_lane;
   std::lock_guard<std::mutex> blk(bl.mu);
+  LaneDrain drain(bl);
   int rc;
   if ((rc = lane_stream(bl))) return rc;
   const int geom = fb_geom_for(mod);  // the comb tables' layout
@@ -1999,18 +2206,18 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     cleanup();
     return fail(MPCX_ENOMEM, "hipMalloc(fixed-base build)");
   }
-  hipError_t e = hipMemcpy(d_b, hb.data(), hb.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(d_e1, he1.data(), he1.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(d_e2, he2.data(), he2.size() * 4, hipMemcpyHostToDevice);
-  if (e == hipSuccess) e = hipMemcpy(d_m, hm.data(), hm.size() * 4, hipMemcpyHostToDevice);
-  if (e != hipSuccess) {
+  if ((rc = copy_sync(d_b, hb.data(), hb.size() * 4, hipMemcpyHostToDevice, bl.st)) ||
+      (rc = copy_sync(d_e1, he1.data(), he1.size() * 4, hipMemcpyHostToDevice, bl.st)) ||
+      (rc = copy_sync(d_e2, he2.data(), he2.size() * 4, hipMemcpyHostToDevice, bl.st)) ||
+      (rc = copy_sync(d_m, hm.data(), hm.size() * 4, hipMemcpyHostToDevice, bl.st))) {
     cleanup();
-    return hip_fail(e, "upload fixed-base inputs");
+    return rc;
   }
   rc = modexp_enqueue(di, bl, mod, nwin, d_b, cw, d_e1, ew1, 0, wb * (nwin - 1) + 1, nullptr, 0, d_bj, cw, false);
   // T(j, v) = R * b_j^v: operand i = j*nv + (v-1) takes base b_j -> replicate b_j rows
   std::vector<uint32_t> hbj((size_t)nwin * cw), hb2;
-  if (!rc) rc = d2h_sync(hbj.data(), d_bj, hbj.size() * 4, bl);
+  if (!rc) rc = lane_wait(bl);
+  if (!rc) rc = copy_sync(hbj.data(), d_bj, hbj.size() * 4, hipMemcpyDeviceToHost, bl.st);
   if (!rc) {
     hb2.resize(n2 * cw);
     for (size_t i = 0; i < n2; ++i) std::memcpy(&hb2[i * cw], &hbj[(i / nv) * cw], cw * 4);
@@ -2018,7 +2225,7 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
     d_b = nullptr;
     if (!alloc(&d_b, hb2.size())) rc = fail(MPCX_ENOMEM, "hipMalloc(fixed-base bases)");
   }
-  if (!rc) rc = h2d(d_b, hb2.data(), hb2.size() * 4, bl.st);
+  if (!rc) rc = copy_sync(d_b, hb2.data(), hb2.size() * 4, hipMemcpyHostToDevice, bl.st);
   if (!rc)
     // in slices: the build lane's window-table workspace grows with the
     // operands of one launch (a 12-bit table has ~1M entries)
@@ -2028,7 +2235,8 @@ int mpcx_fixedbase_register(mpcx_mod_t mod, const uint32_t* base, uint32_t base_
                           mod->words, d_t + off * cw, cw, false);
     }
   std::vector<uint32_t> ht(n2 * cw);
-  if (!rc) rc = d2h_sync(ht.data(), d_t, ht.size() * 4, bl);
+  if (!rc) rc = lane_wait(bl);
+  if (!rc) rc = copy_sync(ht.data(), d_t, ht.size() * 4, hipMemcpyDeviceToHost, bl.st);
   cleanup();
   if (rc) return rc;
   auto* fb = new mpcx_fixedbase_s();
@@ -2126,14 +2334,15 @@ int mpcx_fixedbase_exp_batch(uint32_t nbases, const mpcx_fb_t* fbs, uint32_t cou
     const size_t ob = (size_t)n * out_words * 4, mb = muls ? (size_t)n * mul_words * 4 : 0;
     std::unique_lock<std::mutex> lk;
     Lane& l = acquire_lane(g_devs[di], lk);
+    LaneDrain drain(l);
     if ((rc = lane_stream(l))) return rc;
     Staging* sg = l.stage;
     if ((rc = ensure_buffer(sg[0], eb[0])) || (rc = ensure_buffer(sg[1], eb[1])) ||
         (rc = ensure_buffer(sg[2], ob)) || (muls && (rc = ensure_buffer(sg[3], mb))))
       return rc;
     for (uint32_t t = 0; t < nbases; ++t)  // exps[t] exists only for t < nbases
-      if (eb[t] && (rc = h2d(sg[t].ptr, exps[t] + (size_t)first * exp_words[t], eb[t], l.st))) return rc;
-    if (muls && (rc = h2d(sg[3].ptr, muls + (size_t)first * mul_words, mb, l.st))) return rc;
+      if (eb[t] && (rc = h2d(l, sg[t].ptr, exps[t] + (size_t)first * exp_words[t], eb[t]))) return rc;
+    if (muls && (rc = h2d(l, sg[3].ptr, muls + (size_t)first * mul_words, mb))) return rc;
     const int geom = fbs[0]->geom;
     mpcx::FixedBaseArgs a{};
     a.nd = dconst + mod->const_off[geom];
@@ -2263,6 +2472,7 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
   const size_t seg_bytes = nseg * sizeof(mpcx::FixedBaseArgs), first_bytes = (nseg + 1) * sizeof(uint32_t);
   std::unique_lock<std::mutex> lk;
   Lane& l = acquire_lane(dev, lk);
+  LaneDrain drain(l);
   if ((rc = lane_stream(l))) return rc;
   if ((rc = ensure_buffer(l.stage[0], std::max<size_t>(in_words * 4, 4))) ||
       (rc = ensure_buffer(l.stage[2], out_words * 4)) || (rc = ensure_buffer(l.stage[3], seg_bytes + first_bytes)))
@@ -2276,8 +2486,8 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
     const mpcx_fixedbase_group_t& g = gs[sg.gi];
     mpcx_mod_t mod = g.fbs[0]->mod;
     for (uint32_t t = 0; t < g.nbases; ++t)
-      if ((rc = h2d(d_in + sg.in_e[t], g.exps[t], (size_t)g.count * g.exp_words[t] * 4, l.st))) return rc;
-    if (g.muls && (rc = h2d(d_in + sg.in_m, g.muls, (size_t)g.count * g.mul_words * 4, l.st))) return rc;
+      if ((rc = h2d(l, d_in + sg.in_e[t], g.exps[t], (size_t)g.count * g.exp_words[t] * 4))) return rc;
+    if (g.muls && (rc = h2d(l, d_in + sg.in_m, g.muls, (size_t)g.count * g.mul_words * 4))) return rc;
     const uint32_t* dconst = nullptr;
     if ((rc = mod_const(mod, di, &dconst))) return rc;
     mpcx::FixedBaseArgs& a = args[k];
@@ -2302,8 +2512,8 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
     a.n0inv = mod->n0inv;
     first[k + 1] = first[k] + sg.waves;
   }
-  if ((rc = h2d(l.stage[3].ptr, args.data(), seg_bytes, l.st)) ||
-      (rc = h2d((char*)l.stage[3].ptr + seg_bytes, first.data(), first_bytes, l.st)))
+  if ((rc = h2d(l, l.stage[3].ptr, args.data(), seg_bytes)) ||
+      (rc = h2d(l, (char*)l.stage[3].ptr + seg_bytes, first.data(), first_bytes)))
     return rc;
   const int ks = kstat_begin(l);
   const mpcx::FixedBaseArgs* dsegs = (const mpcx::FixedBaseArgs*)l.stage[3].ptr;
@@ -2340,8 +2550,7 @@ int mpcx_fixedbase_multi_batch(uint32_t n_groups, const mpcx_fixedbase_group_t* 
   }
   for (const auto& sg : segs) {  // results straight into each group's buffer
     const mpcx_fixedbase_group_t& g = gs[sg.gi];
-    e = hipMemcpyAsync(g.out, d_out + sg.out_o, (size_t)g.count * g.out_words * 4, hipMemcpyDeviceToHost, l.st);
-    if (e != hipSuccess) return hip_fail(e, "copy results");
+    if ((rc = d2h(l, g.out, d_out + sg.out_o, (size_t)g.count * g.out_words * 4))) return rc;
   }
   return lane_wait(l);
 }
@@ -2393,6 +2602,7 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
   static const TrialTables tt;
   std::unique_lock<std::mutex> lk;
   Lane& l = acquire_lane(g_devs[di], lk);
+  LaneDrain drain(l);
   int rc;
   if ((rc = lane_stream(l))) return rc;
   constexpr uint32_t W = MPCX_SIEVE_MAX_BYTES / 4;
@@ -2417,12 +2627,12 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
   std::copy(tt.start.begin(), tt.start.end(), misc.begin() + off_start);
   std::copy(tt.primes.begin(), tt.primes.end(), misc.begin() + off_primes);
   std::memcpy(misc.data() + off_inv, tt.inv.data(), ng * 8);
-  if ((rc = h2d(sv[2].ptr, misc.data(), misc_words * 4, l.st))) return rc;
+  if ((rc = h2d(l, sv[2].ptr, misc.data(), misc_words * 4))) return rc;
   uint32_t* dm = (uint32_t*)sv[2].ptr;
   hipError_t e;
   if (count) {
     if (raw) {
-      if ((rc = h2d(sg[0].ptr, raw, (size_t)count * nbytes, l.st))) return rc;
+      if ((rc = h2d(l, sg[0].ptr, raw, (size_t)count * nbytes))) return rc;
     } else {
       mpcx::DrbgArgs da{};
       da.seed = seed;
@@ -2450,7 +2660,7 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
   }
   uint32_t* d_sq = (uint32_t*)sv[5].ptr;
   uint8_t* d_sok = (uint8_t*)(d_sq + (size_t)n_sprp * W);
-  if (n_sprp && (rc = h2d(d_sq, sprp_q, (size_t)n_sprp * W * 4, l.st))) return rc;
+  if (n_sprp && (rc = h2d(l, d_sq, sprp_q, (size_t)n_sprp * W * 4))) return rc;
   mpcx::Prime2Args pa{};
   pa.nf = (const uint32_t*)sv[0].ptr;
   pa.count_f = count;
@@ -2492,23 +2702,15 @@ int safeprime_step_on(int di, uint64_t seed, const uint8_t* raw, uint64_t stream
                                                            (double)n_sprp * go_macs(q_bits, q_bits));
   if (np > max_pass) return fail(MPCX_ENOMEM, "%u Fermat passes > max_pass %u", np, max_pass);
   std::vector<uint32_t> pidx(np), pp((size_t)np * W);
-  if (np) {
-    e = hipMemcpyAsync(pidx.data(), sv[4].ptr, (size_t)np * 4, hipMemcpyDeviceToHost, l.st);
-    if (e == hipSuccess) e = hipMemcpyAsync(pp.data(), sv[3].ptr, pp.size() * 4, hipMemcpyDeviceToHost, l.st);
-    if (e != hipSuccess) return hip_fail(e, "copy passes");
-  }
-  if (n_sprp) {
-    e = hipMemcpyAsync(sprp_ok, d_sok, n_sprp, hipMemcpyDeviceToHost, l.st);
-    if (e != hipSuccess) return hip_fail(e, "copy strong-test verdicts");
-  }
+  if (np && ((rc = d2h(l, pidx.data(), sv[4].ptr, (size_t)np * 4)) || (rc = d2h(l, pp.data(), sv[3].ptr, pp.size() * 4))))
+    return rc;
+  if (n_sprp && (rc = d2h(l, sprp_ok, d_sok, n_sprp))) return rc;
   std::vector<uint32_t> aidx;
   std::vector<uint8_t> aok;
   if (all_ok && ns) {
     aidx.resize(ns);
     aok.resize(ns);
-    e = hipMemcpyAsync(aidx.data(), sv[1].ptr, (size_t)ns * 4, hipMemcpyDeviceToHost, l.st);
-    if (e == hipSuccess) e = hipMemcpyAsync(aok.data(), sg[3].ptr, ns, hipMemcpyDeviceToHost, l.st);
-    if (e != hipSuccess) return hip_fail(e, "copy survivors");
+    if ((rc = d2h(l, aidx.data(), sv[1].ptr, (size_t)ns * 4)) || (rc = d2h(l, aok.data(), sg[3].ptr, ns))) return rc;
   }
   if ((rc = lane_wait(l))) return rc;
   // stream order

@@ -68,6 +68,7 @@ SIGNATURES = [
     ("mpcxh_coprime_batch", _i, [_u32, _vp, _vp, _u32, _vp]),
     ("mpcxh_profile_report", _i, [ctypes.c_char_p, ctypes.c_size_t, _i]),
     ("mpcxh_host_threads", _i, [_vp, _vp]),
+    ("mpcxh_pinned_pool_stats", _i, [_vp, _vp, _vp, _vp]),
     ("mpcxh_pool_selftest", _i, [_u32, _u32, _u32, _vp]),
     ("mpcxh_nat_arith", _i, [_i, _vp, _u32, _vp, _u32, _vp, _u32, _vp]),
     ("mpcxh_drbg_read", _i, [_u64, _vp, ctypes.c_size_t]),
@@ -268,6 +269,15 @@ def profile_report(reset: bool = False) -> str:
     buf = ctypes.create_string_buffer(1 << 16)
     _check(lib().mpcxh_profile_report(buf, len(buf), 1 if reset else 0))
     return buf.value.decode()
+
+
+def pinned_pool_stats() -> dict:
+    """mpcxh_pinned_pool_stats: the engine's page-locked staging pool (bytes
+    held, peak bytes in use) and the pageable fallbacks taken when pinning failed."""
+    v = [ctypes.c_uint64(0) for _ in range(4)]
+    _check(lib().mpcxh_pinned_pool_stats(*(ctypes.byref(x) for x in v)))
+    return {"held_bytes": v[0].value, "peak_in_use_bytes": v[1].value, "fallbacks": v[2].value,
+            "fallback_bytes": v[3].value}
 
 
 def probably_prime(ns: Sequence[int], reps: int = 20) -> List[bool]:

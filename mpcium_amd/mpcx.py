@@ -74,6 +74,8 @@ SIGNATURES = [
     ("mpcx_dev_free", ctypes.c_int, [_vp]),
     ("mpcx_host_alloc", ctypes.c_int, [ctypes.c_size_t, ctypes.POINTER(ctypes.c_void_p)]),
     ("mpcx_host_free", ctypes.c_int, [_vp]),
+    ("mpcx_copy_stats", ctypes.c_int, [ctypes.POINTER(ctypes.c_uint64), ctypes.POINTER(ctypes.c_uint64),
+                                       ctypes.POINTER(ctypes.c_uint64)]),
     ("mpcx_memcpy_h2d", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
     ("mpcx_memcpy_d2h", ctypes.c_int, [_vp, _vp, ctypes.c_size_t]),
     ("mpcx_stream_create", ctypes.c_int, [ctypes.POINTER(_vp)]),
@@ -162,6 +164,14 @@ def kernel_stats(reset: bool = False) -> dict:
     buf = ctypes.create_string_buffer(1 << 16)
     _check(lib().mpcx_kernel_stats(buf, len(buf), 1 if reset else 0))
     return json.loads(buf.value.decode())
+
+
+def copy_stats() -> dict:
+    """mpcx_copy_stats: host bytes DMA'd directly from/to mpcx_host_alloc
+    blocks, bytes bounced through the lanes' pinned buffers, bounce allocations."""
+    v = [ctypes.c_uint64(0) for _ in range(3)]
+    _check(lib().mpcx_copy_stats(*(ctypes.byref(x) for x in v)))
+    return {"direct_bytes": v[0].value, "bounced_bytes": v[1].value, "bounce_allocs": v[2].value}
 
 
 def select_device(index: int):

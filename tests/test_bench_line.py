@@ -62,6 +62,24 @@ def test_compact_line_never_exceeds_limit():
     assert line["value"] == pytest.approx(full["value"], rel=1e-5)
 
 
+def test_config1_value_is_single_batch_and_in_flight_is_labelled():
+    """BASELINE configs[0] is ONE batch of 1,024 ops: c1_paillier.value is that
+    rate; the concurrent-batches rate is a second, labelled key (VERDICT r4
+    item 4)."""
+    full = _recorded()
+    full["paillier_batch"] = {
+        "value": 40000.0, "unit": "Encrypt+HomoMult ops/s", "n_gpus": 1,
+        "roofline": {"frac": 0.11}, "cpu_baseline": {"value": 550.0, "cores": 16},
+        "batches_in_flight": {"batches": 16, "value": 88000.0, "seconds": 3.7}}
+    line = bench.compact_line(full, "d.json")
+    c1 = line["configs"]["c1_paillier"]
+    assert c1["value"] == pytest.approx(40000.0)
+    assert c1["batches_in_flight"] == 16
+    assert c1["in_flight_value"] == pytest.approx(88000.0)
+    assert c1["frac"] == pytest.approx(0.11)
+    assert len(json.dumps(line)) <= bench.LINE_MAX_BYTES
+
+
 def test_world_size_mismatch_exits_nonzero():
     env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "1"], env=env,
