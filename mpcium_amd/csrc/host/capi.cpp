@@ -446,7 +446,8 @@ int mpcxh_mta_alice_init_batch(uint32_t w, const mpcxh_paillier_t* pkA, const mp
     std::vector<Nat> c;
     std::vector<mta::RangeProofAlice> p;
     std::vector<uint8_t> e;
-    mta::AliceInitBatch(sk.pub, nats(a, w, count), dln, rd, &c, &p, &e);
+    // a key with its factors (the caller is Alice): the CRT form
+    mta::AliceInitBatch(sk.pub, nats(a, w, count), dln, rd, &c, &p, &e, sk.P.is_zero() ? nullptr : &sk);
     store(c, cA, w);
     range_to(p, pf, w);
     std::memcpy(err, e.data(), count);

@@ -637,9 +637,10 @@ std::vector<uint8_t> Engine::fermat2(const std::vector<Nat>& cands) {
   if (cands.empty()) return {};
   uint32_t w = 1;
   for (const auto& c : cands) w = std::max<uint32_t>(w, (uint32_t)c.words());
-  auto P = pack(cands, w);
+  HostBuf P(cands.size() * w);  // pinned: DMA'd directly (MR / Lucas batches of ModProof verification are GBs)
+  pack_into(cands, w, P.p);
   std::vector<uint8_t> ok(cands.size());
-  int rc = mpcx_fermat2_batch((uint32_t)cands.size(), P.data(), w, ok.data());
+  int rc = mpcx_fermat2_batch((uint32_t)cands.size(), P.p, w, ok.data());
   if (rc) throw_last(rc, "mpcx_fermat2_batch");
   return ok;
 }
@@ -672,10 +673,11 @@ std::vector<uint8_t> Engine::lucas(const std::vector<Nat>& n, const std::vector<
   if (n.empty()) return {};
   uint32_t w = 1;
   for (const auto& c : n) w = std::max<uint32_t>(w, (uint32_t)c.words());
-  auto N = pack(n, w);
+  HostBuf N(n.size() * w);
+  pack_into(n, w, N.p);
   std::vector<uint8_t> ok(n.size());
   enter_call();
-  int rc = mpcx_lucas_batch((uint32_t)n.size(), N.data(), w, P.data(), ok.data());
+  int rc = mpcx_lucas_batch((uint32_t)n.size(), N.p, w, P.data(), ok.data());
   leave_call();
   if (rc) throw_last(rc, "mpcx_lucas_batch");
   return ok;
@@ -689,11 +691,12 @@ std::vector<uint8_t> Engine::strong_probable_prime(const std::vector<Nat>& n, co
   std::vector<Nat> b(bases);
   for (size_t i = 0; i < b.size(); ++i)
     if (b[i].words() > w) b[i] = b[i] % n[i];
-  auto N = pack(n, w);
-  auto A = pack(b, w);
+  HostBuf N(n.size() * w), A(n.size() * w);
+  pack_into(n, w, N.p);
+  pack_into(b, w, A.p);
   std::vector<uint8_t> ok(n.size());
   enter_call();
-  int rc = mpcx_mr_batch((uint32_t)n.size(), N.data(), w, A.data(), ok.data());
+  int rc = mpcx_mr_batch((uint32_t)n.size(), N.p, w, A.p, ok.data());
   leave_call();
   if (rc) throw_last(rc, "mpcx_mr_batch");
   return ok;

@@ -7,6 +7,7 @@
 #include <exception>
 #include <functional>
 #include <map>
+#include <memory>
 #include <stdexcept>
 #include <thread>
 
@@ -38,6 +39,101 @@ Nat gamma_pow(const Nat& k, const Nat& N) {
 
 Nat affine_x(const secp::Affine& p) { return secp::FeToNat(p.x); }
 Nat affine_y(const secp::Affine& p) { return secp::FeToNat(p.y); }
+
+// mul * r^N mod N^2 requests of one launch step (Encrypt's c = Gamma^m r^N,
+// the range proof's u = Gamma^alpha beta^N). With the key's factors at hand
+// (Alice's own key in AliceInit) each runs as r^N mod P^2 and mod Q^2 --
+// 2048-bit moduli, half the Montgomery work of one 4096-bit exponentiation,
+// in the 2048-bit main geometry -- and is recombined on the host
+// (x = x_Q + Q^2 ((x_P - x_Q) (Q^2)^-1 mod P^2)): the same residue mod N^2,
+// bit-exact. Without them, mod N^2 as before. MPCX_INIT_CRT=0: always mod N^2
+// (A/B runs).
+class N2Step {
+ public:
+  N2Step(const paillier::PublicKey& pk, const paillier::PrivateKey* own) : N_(pk.N), N2_(pk.NSquare()) {
+    static const bool on = [] {
+      const char* e = std::getenv("MPCX_INIT_CRT");
+      return !(e && e[0] == '0');
+    }();
+    crt_ = on && own && !own->P.is_zero() && !own->Q.is_zero() && own->P * own->Q == pk.N;
+    if (crt_) {
+      P2_ = own->P * own->P;
+      Q2_ = own->Q * own->Q;
+      if (!mod_inverse(Int(Q2_ % P2_), P2_, &q2inv_)) crt_ = false;
+    }
+    eN2_ = std::make_unique<ExpSet>(N2_);
+    if (crt_) {
+      eP2_ = std::make_unique<ExpSet>(P2_);
+      eQ2_ = std::make_unique<ExpSet>(Q2_);
+    }
+  }
+  // out = mul * r^N mod N^2; r, mul and out must outlive run()/finish()
+  void add(const Nat& r, const Nat& mul, Nat* out) { reqs_.push_back({&r, &mul, out}); }
+  // queue the launches (call run_all on sets() afterwards, then finish())
+  void prepare() {
+    if (!crt_) {
+      for (const Req& q : reqs_) eN2_->add(*q.r, N_, q.out, q.mul);
+      return;
+    }
+    const size_t n = reqs_.size();
+    red_.assign(n, Red{});
+    parallel_for(n, [&](size_t i) {
+      const Req& q = reqs_[i];
+      red_[i].rp = *q.r % P2_;
+      red_[i].rq = *q.r % Q2_;
+      red_[i].mp = *q.mul % P2_;
+      red_[i].mq = *q.mul % Q2_;
+    });
+    for (size_t i = 0; i < n; ++i) {
+      eP2_->add(red_[i].rp, N_, &red_[i].xp, &red_[i].mp);
+      eQ2_->add(red_[i].rq, N_, &red_[i].xq, &red_[i].mq);
+    }
+  }
+  std::vector<ExpSet*> sets() { return crt_ ? std::vector<ExpSet*>{eP2_.get(), eQ2_.get()} : std::vector<ExpSet*>{eN2_.get()}; }
+  void finish() {
+    if (crt_) {
+      parallel_for(reqs_.size(), [&](size_t i) {
+        const Red& r = red_[i];
+        const Nat xqp = r.xq % P2_;
+        const Nat d = r.xp < xqp ? r.xp + P2_ - xqp : r.xp - xqp;
+        *reqs_[i].out = r.xq + Q2_ * ((d * q2inv_) % P2_);
+      });
+    }
+    reqs_.clear();
+    red_.clear();
+  }
+
+ private:
+  struct Req {
+    const Nat *r, *mul;
+    Nat* out;
+  };
+  struct Red {
+    Nat rp, rq, mp, mq, xp, xq;
+  };
+  const Nat N_, N2_;
+  bool crt_ = false;
+  Nat P2_, Q2_, q2inv_;
+  std::unique_ptr<ExpSet> eN2_, eP2_, eQ2_;
+  std::vector<Req> reqs_;
+  std::vector<Red> red_;
+};
+
+// the launches of several sets and N2Steps of one protocol step at once
+void run_step(std::initializer_list<ExpSet*> sets, N2Step* n2) {
+  std::vector<std::function<void()>> fs;
+  for (ExpSet* x : sets) x->collect(fs);
+  if (n2) {
+    n2->prepare();
+    for (ExpSet* x : n2->sets()) x->collect(fs);
+  }
+  run_concurrently(fs);
+  for (ExpSet* x : sets) x->clear();
+  if (n2) {
+    for (ExpSet* x : n2->sets()) x->clear();
+    n2->finish();
+  }
+}
 
 // ---- ProveRangeAlice in stages (shared by ProveRangeAliceBatch and AliceInitBatch)
 struct RangeProveState {
@@ -79,18 +175,18 @@ namespace {
 // read only after them (the challenge hashes it).
 void range_prove_core(const paillier::PublicKey& pk, const DLNParams& dln, const std::vector<const Nat*>& c,
                       const std::vector<Nat>& m, const std::vector<Nat>& r, std::vector<RangeProveState>& st,
-                      ExpSet& eN2, std::vector<RangeProofAlice>* out) {
+                      N2Step& eN2, std::vector<RangeProofAlice>* out) {
   const size_t n = st.size();
   out->assign(n, RangeProofAlice{});
   ExpSet eNt(dln.NTilde), eN(pk.N);
   for (size_t i = 0; i < n; ++i) {
     auto& s = st[i];
     auto& o = (*out)[i];
-    eN2.add(s.beta, pk.N, &o.U, &s.gam_alpha);               // 6. u = Gamma^alpha beta^N mod N^2
+    eN2.add(s.beta, s.gam_alpha, &o.U);                      // 6. u = Gamma^alpha beta^N mod N^2
     eNt.add2(dln.h1, m[i], dln.h2, s.rho, &o.Z);             // 5. z = h1^m h2^rho mod N~
     eNt.add2(dln.h1, s.alpha, dln.h2, s.gamma, &o.W);        // 7. w = h1^alpha h2^gamma mod N~
   }
-  run_all({&eN2, &eNt});
+  run_step({&eNt}, &eN2);
   const Nat gamma = pk.Gamma();
   parallel_for(n, [&](size_t i) {  // 8-9. e = RejectionSample(q, SHA512_256i(N, Gamma, c, z, u, w))
     auto& o = (*out)[i];
@@ -115,7 +211,7 @@ void ProveRangeAliceBatch(const paillier::PublicKey& pk, const DLNParams& dln, c
   range_draw(st, pk, dln, rand);
   std::vector<const Nat*> cp(n);
   for (size_t i = 0; i < n; ++i) cp[i] = &c[i];
-  ExpSet eN2(pk.NSquare());
+  N2Step eN2(pk, nullptr);
   range_prove_core(pk, dln, cp, m, r, st, eN2, out);
 }
 
@@ -179,7 +275,7 @@ namespace {
 struct BobProveState {
   Nat alpha, rho, sigma, tau, rhoPrm, beta, gamma;
   secp::Affine u;
-  Nat bg, e;
+  Nat bg, c1a, e;  // Gamma^gamma beta^N, c1^alpha
   bool wc = false;  // ProveBobWC (u = alpha*G)
 };
 
@@ -216,20 +312,24 @@ void bob_draw(std::vector<BobProveState>& st, const std::vector<size_t>& js, con
   for (size_t k = 0; k < wc.size(); ++k) st[wc[k]].u = u[k];
 }
 
-// stage A of ProveBob: N^2 -> bg = Gamma^gamma beta^N ; N~ -> z, z', t, w (6-8, 10.),
+// the exponentiations of ProveBob before its challenge, one launch step:
+// N^2 -> bg = Gamma^gamma beta^N and c1^alpha; N~ -> z, z', t, w (6-9, 10.),
 // each h1^x h2^y one two-table comb product
-void bob_stage_a(BobProveState& s, const paillier::PublicKey& pk, const DLNParams& dln, const Nat& x, const Nat& y,
-                 ExpSet& eN2, ExpSet& eNt, Nat* gam_gamma, ProofBob& o) {
+void bob_stage_a(BobProveState& s, const paillier::PublicKey& pk, const DLNParams& dln, const Nat& c1, const Nat& x,
+                 const Nat& y, ExpSet& eN2, ExpSet& eNt, Nat* gam_gamma, ProofBob& o) {
   *gam_gamma = gamma_pow(s.gamma, pk.N);
   eN2.add(s.beta, pk.N, &s.bg, gam_gamma);
+  eN2.add(c1, s.alpha, &s.c1a);
   eNt.add2(dln.h1, x, dln.h2, s.rho, &o.Z);           // z = h1^x h2^rho
   eNt.add2(dln.h1, s.alpha, dln.h2, s.rhoPrm, &o.ZPrm);  // z' = h1^alpha h2^rhoPrm
   eNt.add2(dln.h1, y, dln.h2, s.sigma, &o.T);          // t = h1^y h2^sigma
   eNt.add2(dln.h1, s.gamma, dln.h2, s.tau, &o.W);      // w = h1^gamma h2^tau
 }
 
-// stage B: v = c1^alpha Gamma^gamma beta^N (9.)
-void bob_stage_b(BobProveState& s, const Nat& c1, ExpSet& eN2, ProofBob& o) { eN2.add(c1, s.alpha, &o.V, &s.bg); }
+// 9. v = c1^alpha Gamma^gamma beta^N: the two factors of stage A multiplied on
+// the host (a 4096-bit product) instead of a second launch step that waited
+// for bg (round 4)
+void bob_stage_b(BobProveState& s, const Nat& N2, ProofBob& o) { o.V = (s.c1a * s.bg) % N2; }
 
 // 11-12. e = RejectionSample(q, SHA512_256i_TAGGED(Session, N, Gamma, [X.x, X.y,] c1, c2, [u.x, u.y,] z, z', t, v, w))
 Nat bob_challenge(const Bytes& session, const paillier::PublicKey& pk, const Nat& gamma, const secp::Affine* X,
@@ -274,11 +374,10 @@ void ProveBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey&
     bob_draw(st, js, rd, pk, dln);
   }
   ExpSet eN2(N2), eNt(dln.NTilde), eN(pk.N);
-  for (size_t i = 0; i < n; ++i) bob_stage_a(st[i], pk, dln, x[i], y[i], eN2, eNt, &gg[i], (*out)[i]);
+  for (size_t i = 0; i < n; ++i) bob_stage_a(st[i], pk, dln, c1[i], x[i], y[i], eN2, eNt, &gg[i], (*out)[i]);
   run_all({&eN2, &eNt});
-  for (size_t i = 0; i < n; ++i) bob_stage_b(st[i], c1[i], eN2, (*out)[i]);
-  eN2.run();
   parallel_for(n, [&](size_t i) {
+    bob_stage_b(st[i], N2, (*out)[i]);
     (*out)[i].U = st[i].u;
     st[i].e = bob_challenge(session[i], pk, gamma, X ? &(*X)[i] : nullptr, c1[i], c2[i], (*out)[i]);
   });
@@ -288,13 +387,36 @@ void ProveBobBatch(const std::vector<Bytes>& session, const paillier::PublicKey&
 }
 
 namespace {
+// Decrypt(cB) mod q of every session whose proof verified
+void alice_decrypt(const paillier::PrivateKey& skA, const std::vector<const Nat*>& cB, const std::vector<uint8_t>& ok,
+                   const std::vector<Nat*>& alpha, const std::vector<uint8_t*>& err) {
+  std::vector<Int> cs;
+  std::vector<size_t> idx;
+  for (size_t i = 0; i < cB.size(); ++i) {
+    if (!ok[i]) {
+      *err[i] = ErrProofVerify;
+      continue;
+    }
+    idx.push_back(i);
+    cs.push_back(Int(*cB[i]));
+  }
+  std::vector<Nat> m;
+  std::vector<uint8_t> derr;
+  skA.DecryptBatch(cs, &m, &derr);
+  for (size_t j = 0; j < idx.size(); ++j) {
+    if (derr[j]) *err[idx[j]] = derr[j];
+    else *alpha[idx[j]] = m[j] % Q();
+  }
+}
 // ProofBob[WC].Verify of session i's proof *pfp[i], X[i] == nullptr for a
 // plain ProofBob: one batch may mix both kinds (AliceEnd and AliceEndWC of one
 // pair share every modulus).
 std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, const paillier::PublicKey& pk,
                                      const DLNParams& dln, const std::vector<const Nat*>& c1,
                                      const std::vector<const Nat*>& c2, const std::vector<const ProofBob*>& pfp,
-                                     const std::vector<const secp::Affine*>& X, const paillier::PrivateKey* own) {
+                                     const std::vector<const secp::Affine*>& X, const paillier::PrivateKey* own,
+                                     const std::vector<Nat*>* dec = nullptr,
+                                     const std::vector<uint8_t*>* dec_err = nullptr) {
   const size_t n = c1.size();
   const Nat N2 = pk.NSquare(), gamma = pk.Gamma();
   std::vector<uint8_t> ok(n, 0);
@@ -370,12 +492,22 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
     return !(e && e[0] == '0');
   }();
   const bool crt = crt_on && own && !own->P.is_zero() && !own->Q.is_zero();
-  const Nat P2 = crt ? own->P * own->P : Nat(), Q2 = crt ? own->Q * own->Q : Nat();
+  // With the key's factors every exponentiation of the verification -- and,
+  // when asked (AliceEnd), the CRT decryption of c2 -- is independent of the
+  // others: ONE launch step. c1^s1 runs without a multiplier and is multiplied
+  // into s^N Gamma^t1 on the host (a 2048-bit product per half), where the
+  // form below chains it behind the first step.
+  std::unique_ptr<paillier::CrtDecrypt> cd;
+  if (crt) cd = std::make_unique<paillier::CrtDecrypt>(*own);
+  const Nat& P2 = crt ? cd->P2 : N2;
+  const Nat& Q2 = crt ? cd->Q2 : N2;
+  const bool decrypt = crt && dec;
   struct Red {  // s, c1, c2, v, Gamma^t1 reduced mod P^2 and Q^2
     Nat s, c1, c2, v, g;
   };
   std::vector<Red> rp(crt ? n : 0), rq(crt ? n : 0);
-  std::vector<Nat> q1q(crt ? n : 0), r3q(crt ? n : 0), l3q(crt ? n : 0);
+  std::vector<Nat> q1q(crt ? n : 0), r3q(crt ? n : 0), l3q(crt ? n : 0), up(decrypt ? n : 0), uq(decrypt ? n : 0);
+  std::vector<uint8_t> dec_ok(decrypt ? n : 0, 0);  // c2 < N^2: Decrypt's range check
   if (crt) {
     parallel_for(n, [&](size_t i) {
       if (!ok[i]) return;
@@ -389,9 +521,10 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
         r.v = p.V % m;
         r.g = gt1[i] % m;
       }
+      if (decrypt) dec_ok[i] = *c2[i] < N2;
     });
   }
-  ExpSet eN2(crt ? P2 : N2), eQ2(crt ? Q2 : N2), eNt(dln.NTilde);
+  ExpSet eN2(P2), eQ2(Q2), eNt(dln.NTilde);
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
     const auto& p = *pfp[i];
@@ -402,26 +535,51 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
     if (crt) {
       eN2.add(rp[i].s, pk.N, &q1[i], &rp[i].g);   // 7. s^N Gamma^t1 mod P^2
       eN2.add(rp[i].c2, e[i], &r3[i], &rp[i].v);  // 7. c2^e v mod P^2
+      eN2.add(rp[i].c1, p.S1, &l3[i]);            // 7. c1^s1 mod P^2
       eQ2.add(rq[i].s, pk.N, &q1q[i], &rq[i].g);  //    and mod Q^2
       eQ2.add(rq[i].c2, e[i], &r3q[i], &rq[i].v);
+      eQ2.add(rq[i].c1, p.S1, &l3q[i]);
+      if (decrypt && dec_ok[i]) {
+        eN2.add(rp[i].c2, cd->Pm1, &up[i]);  // Decrypt(c2): c2^(P-1) mod P^2
+        eQ2.add(rq[i].c2, cd->Qm1, &uq[i]);  //              c2^(Q-1) mod Q^2
+      }
     } else {
       eN2.add(p.S, pk.N, &q1[i], &gt1[i]);    // 7. s^N Gamma^t1
       eN2.add(*c2[i], e[i], &r3[i], &p.V);    // 7. c2^e v
     }
   }
   run_all({&eN2, &eQ2, &eNt});
-  for (size_t i = 0; i < n; ++i) {
-    if (!ok[i]) continue;
-    if (crt) {
-      eN2.add(rp[i].c1, pfp[i]->S1, &l3[i], &q1[i]);   // 7. c1^s1 s^N Gamma^t1 mod P^2
-      eQ2.add(rq[i].c1, pfp[i]->S1, &l3q[i], &q1q[i]);  //    and mod Q^2
-    } else {
-      eN2.add(*c1[i], pfp[i]->S1, &l3[i], &q1[i]);  // 7. c1^s1 s^N Gamma^t1
-    }
+  if (crt) {
+    parallel_for(n, [&](size_t i) {  // 7. c1^s1 s^N Gamma^t1 mod P^2 and mod Q^2
+      if (!ok[i]) return;
+      l3[i] = (l3[i] * q1[i]) % P2;
+      l3q[i] = (l3q[i] * q1q[i]) % Q2;
+    });
+  } else {
+    for (size_t i = 0; i < n; ++i)
+      if (ok[i]) eN2.add(*c1[i], pfp[i]->S1, &l3[i], &q1[i]);  // 7. c1^s1 s^N Gamma^t1
+    eN2.run();
   }
-  run_all({&eN2, &eQ2});
   for (size_t i = 0; i < n; ++i)
     ok[i] = ok[i] && l1[i] == r1[i] && l2[i] == r2[i] && l3[i] == r3[i] && (!crt || l3q[i] == r3q[i]);
+  if (dec) {  // AliceEnd: Decrypt(c2) mod q of every session whose proof verified
+    if (decrypt) {
+      parallel_for(n, [&](size_t i) {
+        if (!ok[i]) {
+          *(*dec_err)[i] = ErrProofVerify;
+        } else if (!dec_ok[i]) {
+          *(*dec_err)[i] = ErrMessageTooLong;
+        } else {
+          Nat m;
+          const uint8_t de = cd->finish(up[i], uq[i], &m);
+          if (de) *(*dec_err)[i] = de;
+          else *(*dec)[i] = m % Q();
+        }
+      });
+    } else {
+      alice_decrypt(*own, c2, ok, *dec, *dec_err);
+    }
+  }
   return ok;
 }
 }  // namespace
@@ -451,7 +609,7 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
 // ================================================================ protocol
 void AliceInitBatch(const paillier::PublicKey& pkA, const std::vector<Nat>& a, const DLNParams& dlnB,
                     const std::vector<RandFn>& rand, std::vector<Nat>* cA, std::vector<RangeProofAlice>* pf,
-                    std::vector<uint8_t>* err) {
+                    std::vector<uint8_t>* err, const paillier::PrivateKey* skA) {
   const size_t n = a.size();
   if (rand.size() != n) throw std::invalid_argument("AliceInit: sizes");
   cA->assign(n, Nat());
@@ -482,10 +640,10 @@ void AliceInitBatch(const paillier::PublicKey& pkA, const std::vector<Nat>& a, c
   std::vector<RangeProveState> st(k);
   range_draw(st, pkA, dlnB, rd);
   parallel_for(k, [&](size_t j) { ga[j] = gamma_pow(m[j], pkA.N); });
-  ExpSet eN2(pkA.NSquare());
+  N2Step eN2(pkA, skA);  // Alice's own key: c and u by CRT mod P^2, Q^2
   std::vector<const Nat*> cp(k);
   for (size_t j = 0; j < k; ++j) {
-    eN2.add(r[j], pkA.N, &c[j], &ga[j]);  // c = Gamma^a r^N mod N^2
+    eN2.add(r[j], ga[j], &c[j]);  // c = Gamma^a r^N mod N^2
     cp[j] = &c[j];
   }
   std::vector<RangeProofAlice> p;
@@ -569,23 +727,24 @@ void bob_mid_halves(const std::vector<Bytes>& session, const paillier::PublicKey
     }
     bob_draw(st, js, rdj, pkA, dlnA);  // ProveBob[WC] steps 1-5
   }
+  // every exponentiation before the challenge in ONE launch step: Encrypt's
+  // r^N, HomoMult's cA^b and ProveBob's stage A (c^b and cA^alpha multiplied
+  // into their products on the host below)
+  std::vector<Nat> cab(k);
   ExpSet eN2(N2), eNt(dlnA.NTilde), eN(pkA.N);
   for (size_t j = 0; j < k; ++j) {
     if (!live[j]) continue;
+    const Nat& c = cA[h[j].i];
     eN2.add(cRand[j], pkA.N, &cbp[j], &gbp[j]);  // cBetaPrm = Gamma^betaPrm r^N
-    bob_stage_a(st[j], pkA, dlnA, *h[j].b, h[j].out->betaPrm, eN2, eNt, &gg[j], h[j].out->pf);
+    eN2.add(c, *h[j].b, &cab[j]);                // HomoMult(b, cA) = cA^b
+    bob_stage_a(st[j], pkA, dlnA, c, *h[j].b, h[j].out->betaPrm, eN2, eNt, &gg[j], h[j].out->pf);
   }
   run_all({&eN2, &eNt});
-  for (size_t j = 0; j < k; ++j) {
-    if (!live[j]) continue;
-    const Nat& c = cA[h[j].i];
-    eN2.add(c, *h[j].b, &h[j].out->cB, &cbp[j]);  // cB = HomoAdd(HomoMult(b, cA), cBetaPrm)
-    bob_stage_b(st[j], c, eN2, h[j].out->pf);
-  }
-  eN2.run();
   parallel_for(k, [&](size_t j) {
     if (!live[j]) return;
     auto& o = *h[j].out;
+    o.cB = (cab[j] * cbp[j]) % N2;  // cB = HomoAdd(HomoMult(b, cA), cBetaPrm)
+    bob_stage_b(st[j], N2, o.pf);
     o.beta = (Q() - o.betaPrm % Q()) % Q();  // beta = ModInt(q).Sub(0, betaPrm)
     o.pf.U = st[j].u;
     st[j].e = bob_challenge(session[h[j].i], pkA, gamma, h[j].B, cA[h[j].i], o.cB, o.pf);
@@ -660,47 +819,32 @@ void BobMidPairBatch(const std::vector<Bytes>& session, const paillier::PublicKe
   both([&] { bob_mid_halves(session, pkA, dlnA, cA, h); }, [&] { bob_mid_halves(session, pkA, dlnA, cA, hwc); });
 }
 
-namespace {
-// Decrypt(cB) mod q of every session whose proof verified
-void alice_decrypt(const paillier::PrivateKey& skA, const std::vector<const Nat*>& cB, const std::vector<uint8_t>& ok,
-                   const std::vector<Nat*>& alpha, const std::vector<uint8_t*>& err) {
-  std::vector<Int> cs;
-  std::vector<size_t> idx;
-  for (size_t i = 0; i < cB.size(); ++i) {
-    if (!ok[i]) {
-      *err[i] = ErrProofVerify;
-      continue;
-    }
-    idx.push_back(i);
-    cs.push_back(Int(*cB[i]));
-  }
-  std::vector<Nat> m;
-  std::vector<uint8_t> derr;
-  skA.DecryptBatch(cs, &m, &derr);
-  for (size_t j = 0; j < idx.size(); ++j) {
-    if (derr[j]) *err[idx[j]] = derr[j];
-    else *alpha[idx[j]] = m[j] % Q();
-  }
-}
-}  // namespace
-
 void AliceEndBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,
                    const std::vector<ProofBob>& pf, const DLNParams& dlnA, const std::vector<Nat>& cA,
                    const std::vector<Nat>& cB, const std::vector<secp::Affine>* B, std::vector<Nat>* alpha,
                    std::vector<uint8_t>* err) {
   const size_t n = cA.size();
-  const std::vector<uint8_t> ok = VerifyBobBatch(session, skA.pub, dlnA, cA, cB, pf, B, &skA);
+  if (session.size() != n || pf.size() != n || cB.size() != n || (B && B->size() != n))
+    throw std::invalid_argument("AliceEnd: sizes");
   alpha->assign(n, Nat());
   err->assign(n, OK);
-  std::vector<const Nat*> c(n);
+  std::vector<const Bytes*> sp(n);
+  std::vector<const Nat*> c1(n), c2(n);
+  std::vector<const ProofBob*> pp(n);
+  std::vector<const secp::Affine*> Xp(n, nullptr);
   std::vector<Nat*> a(n);
   std::vector<uint8_t*> e(n);
   for (size_t i = 0; i < n; ++i) {
-    c[i] = &cB[i];
+    sp[i] = &session[i];
+    c1[i] = &cA[i];
+    c2[i] = &cB[i];
+    pp[i] = &pf[i];
+    if (B) Xp[i] = &(*B)[i];
     a[i] = &(*alpha)[i];
     e[i] = &(*err)[i];
   }
-  alice_decrypt(skA, c, ok, a, e);
+  // ProofBob[WC].Verify, then Decrypt(cB) mod q: one launch step (verify_bob_core)
+  verify_bob_core(sp, skA.pub, dlnA, c1, c2, pp, Xp, &skA, &a, &e);
 }
 
 void AliceEndPairBatch(const std::vector<Bytes>& session, const paillier::PrivateKey& skA,
@@ -735,8 +879,7 @@ void AliceEndPairBatch(const std::vector<Bytes>& session, const paillier::Privat
       a[i] = &(*res)[i];
       e[i] = &(*er)[i];
     }
-    const std::vector<uint8_t> ok = verify_bob_core(sp, skA.pub, dlnA, c1, c2, pp, Xp, &skA);
-    alice_decrypt(skA, c2, ok, a, e);
+    verify_bob_core(sp, skA.pub, dlnA, c1, c2, pp, Xp, &skA, &a, &e);
   };
   both([&] { half(pf, cB, nullptr, alpha, err); }, [&] { half(pfwc, cBwc, Bwc.data(), mu, errwc); });
 }

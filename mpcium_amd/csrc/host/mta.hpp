@@ -85,10 +85,13 @@ std::vector<uint8_t> VerifyBobBatch(const std::vector<Bytes>& session, const pai
                                     const paillier::PrivateKey* own_sk = nullptr);
 
 // ---- protocol
-// AliceInit(ec, pkA, a, NTildeB, h1B, h2B, rand) -> (cA, pf, err)
+// AliceInit(ec, pkA, a, NTildeB, h1B, h2B, rand) -> (cA, pf, err). skA: Alice's
+// own private key when the caller holds it (it always does in tss-lib: AliceInit
+// runs on Alice's node): Encrypt's r^N and the proof's beta^N then run mod P^2 and
+// Q^2 with a CRT recombination -- bit-exact, half the GPU work.
 void AliceInitBatch(const paillier::PublicKey& pkA, const std::vector<Nat>& a, const DLNParams& dlnB,
                     const std::vector<RandFn>& rand, std::vector<Nat>* cA, std::vector<RangeProofAlice>* pf,
-                    std::vector<uint8_t>* err);
+                    std::vector<uint8_t>* err, const paillier::PrivateKey* skA = nullptr);
 
 struct BobMidResult {
   Nat beta, cB, betaPrm;

@@ -2,6 +2,7 @@
 #include "paillier.hpp"
 
 #include "engine.hpp"
+#include "expset.hpp"
 #include "tsscommon.hpp"
 
 namespace mpcx::host::paillier {
@@ -117,37 +118,48 @@ void PrivateKey::DecryptBatch(const std::vector<Int>& c, std::vector<Nat>* m, st
     for (size_t j = 0; j < idx.size(); ++j) (*m)[idx[j]] = r[j];
     return;
   }
-  // CRT form (same plaintext: every c in Z*_{N^2} is Gamma^m r^N for exactly one
-  // m in [0, N), and both formulas return that m). Per prime p of N:
-  //   m_p = L_p(c^(p-1) mod p^2) * h_p mod p,  L_p(u) = (u - 1) / p,
-  //   h_p = L_p(Gamma^(p-1) mod p^2)^-1 = ((p-1) * N / p mod p)^-1 mod p,
-  // then m = m_q + q * ((m_p - m_q) * q^-1 mod p). Two 1024-bit exponents mod
-  // 2048-bit moduli on the GPU instead of a 2047-bit exponent mod N^2: a
-  // quarter of the Montgomery work.
+  const CrtDecrypt cd(*this);
+  std::vector<Nat> up(cs.size()), uq(cs.size());
+  run_concurrently({[&] { up = Engine::get().exp(cd.P2, cs, {cd.Pm1}); },
+                    [&] { uq = Engine::get().exp(cd.Q2, cs, {cd.Qm1}); }});
+  parallel_for(idx.size(), [&](size_t j) {
+    const uint8_t e = cd.finish(up[j], uq[j], &(*m)[idx[j]]);
+    if (e) (*err)[idx[j]] = e;
+  });
+}
+
+// CRT form (same plaintext: every c in Z*_{N^2} is Gamma^m r^N for exactly one
+// m in [0, N), and both formulas return that m). Per prime p of N:
+//   m_p = L_p(c^(p-1) mod p^2) * h_p mod p,  L_p(u) = (u - 1) / p,
+//   h_p = L_p(Gamma^(p-1) mod p^2)^-1 = ((p-1) * N / p mod p)^-1 mod p,
+// then m = m_q + q * ((m_p - m_q) * q^-1 mod p). Two 1024-bit exponents mod
+// 2048-bit moduli on the GPU instead of a 2047-bit exponent mod N^2: a
+// quarter of the Montgomery work.
+CrtDecrypt::CrtDecrypt(const PrivateKey& sk) : P(sk.P), Q(sk.Q) {
   const Nat one(1);
-  const Nat Pm1 = P - one, Qm1 = Q - one;
+  P2 = P * P;
+  Q2 = Q * Q;
+  Pm1 = P - one;
+  Qm1 = Q - one;
   auto h_of = [&](const Nat& p, const Nat& pm1, const Nat& other) {
     Nat h;  // (1 + N)^(p-1) = 1 + (p-1) N mod p^2, so L_p = (p-1) * other mod p
     if (!mod_inverse(Int(mulmod(pm1, other % p, p)), p, &h)) throw EngineError(MPCX_EINVAL, "Paillier key: bad factor");
     return h;
   };
-  const Nat hP = h_of(P, Pm1, Q), hQ = h_of(Q, Qm1, P);
-  Nat qinv;
+  hP = h_of(P, Pm1, Q);
+  hQ = h_of(Q, Qm1, P);
   if (!mod_inverse(Int(Q % P), P, &qinv)) throw EngineError(MPCX_EINVAL, "Paillier key: P, Q not coprime");
-  std::vector<Nat> up = Engine::get().exp(P * P, cs, {Pm1});
-  std::vector<Nat> uq = Engine::get().exp(Q * Q, cs, {Qm1});
+}
+
+uint8_t CrtDecrypt::finish(const Nat& up, const Nat& uq, Nat* m) const {
   // p | c  <=>  c^(p-1) mod p^2 == 0 (p^2 | c^(p-1), p - 1 >= 2); otherwise it
   // is 1 mod p. tss-lib rejects such c (gcd(c, N^2) != 1) with ErrMessageMalFormed.
-  parallel_for(idx.size(), [&](size_t j) {
-    if (up[j].is_zero() || uq[j].is_zero()) {
-      (*err)[idx[j]] = ErrMessageMalFormed;
-      return;
-    }
-    const Nat mp = mulmod(L(up[j], P), hP, P), mq = mulmod(L(uq[j], Q), hQ, Q);
-    const Nat mqp = mq % P;
-    const Nat d = mp < mqp ? mp + P - mqp : mp - mqp;
-    (*m)[idx[j]] = mq + Q * mulmod(d, qinv, P);
-  });
+  if (up.is_zero() || uq.is_zero()) return ErrMessageMalFormed;
+  const Nat mp = mulmod(L(up, P), hP, P), mq = mulmod(L(uq, Q), hQ, Q);
+  const Nat mqp = mq % P;
+  const Nat d = mp < mqp ? mp + P - mqp : mp - mqp;
+  *m = mq + Q * mulmod(d, qinv, P);
+  return OK;
 }
 
 }  // namespace mpcx::host::paillier

@@ -47,6 +47,18 @@ struct PrivateKey {
   void DecryptBatch(const std::vector<Int>& c, std::vector<Nat>* m, std::vector<uint8_t>* err) const;
 };
 
+// The key holder's CRT decryption (DecryptBatch's CRT form) in two parts, so a
+// caller can put the two exponentiations up = c^(P-1) mod P^2 and
+// uq = c^(Q-1) mod Q^2 into a launch step it already runs (AliceEnd's
+// verification, mta.cpp) instead of a step of their own. Same plaintext as
+// tss-lib's L(c^lambda) * mu mod N for every c in Z*_{N^2}.
+struct CrtDecrypt {
+  Nat P, Q, P2, Q2, Pm1, Qm1, hP, hQ, qinv;
+  explicit CrtDecrypt(const PrivateKey& sk);  // requires the factors P, Q of N
+  // m from (up, uq); ErrMessageMalFormed when P | c or Q | c (gcd(c, N^2) != 1)
+  uint8_t finish(const Nat& up, const Nat& uq, Nat* m) const;
+};
+
 // L(u) = (u - 1) / N
 Nat L(const Nat& u, const Nat& N);
 

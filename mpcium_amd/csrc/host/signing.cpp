@@ -302,7 +302,8 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
         const double a0 = now();
         {  // round 1: AliceInit(k_i) to Bob j
           std::vector<uint8_t> err;
-          mta::AliceInitBatch(nodes[p.i].sk.pub, sl(k[p.i]), public_dln(nodes[p.j].dln), l.ra, &l.cA, &l.pfA, &err);
+          mta::AliceInitBatch(nodes[p.i].sk.pub, sl(k[p.i]), public_dln(nodes[p.j].dln), l.ra, &l.cA, &l.pfA, &err,
+                              &nodes[p.i].sk);
           count_err(err);
         }
         const double a1 = now();

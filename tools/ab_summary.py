@@ -22,6 +22,9 @@ FIELDS = (
     ("config2_kernel_ms", lambda d: round(d["roofline"]["kernel_ms"], 2)),
     ("per_operand_2048_kernel_ms", lambda d: round(d["config2_per_operand_exponents"][0]["kernel_ms"], 2)),
     ("paillier_batch", lambda d: d["paillier_batch"]["value"]),
+    ("signing_2_kernel_frac", lambda d: round(d["signing"]["roofline"]["frac"], 4)),
+    ("signing_3_kernel_frac", lambda d: round(d["signing_3_signers"]["roofline"]["frac"], 4)),
+    ("keygen_kernel_frac", lambda d: round(d["keygen"]["roofline"]["frac"], 4)),
 )
 
 
@@ -44,7 +47,7 @@ def main():
     runs, sides = [], {}
     for p in sorted(glob.glob(os.path.join(src, "ab_*.json"))):
         # ab_A_1 / ab_B_1 (ab, abswap, envab) or ab_L3_1 (abn: position in the build list)
-        m = re.search(r"ab_([AB]|L\d+)_(\d+)\.json$", p)
+        m = re.search(r"ab_([AB]|[LH]\d+)_(\d+)\.json$", p)
         if not m:
             continue
         tag = m.group(1)

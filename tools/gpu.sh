@@ -8,6 +8,7 @@
 #   bash tools/gpu.sh pmc    OUT COUNTERS [bench args]   one rocprofv3 --pmc pass (COUNTERS comma-free, space-joined in quotes)
 #   bash tools/gpu.sh ab     OUT N LIB_A LIB_B [bench args]  N interleaved config-2 runs per libmpcx build
 #   bash tools/gpu.sh abswap OUT N LIB_A LIB_B [bench args]  N interleaved full-bench runs, LIB swapped in place
+#   bash tools/gpu.sh abhost OUT N HOSTLIB_A,HOSTLIB_B [bench args]  N interleaved runs per libmpcx_host build
 #   bash tools/gpu.sh envab  OUT N "ENV_A" "ENV_B" [bench args]  N interleaved runs under two environments
 #   bash tools/gpu.sh argab  OUT N "ARGS_A" "ARGS_B" [bench args]  N interleaved runs with two bench.py argument sets
 #   bash tools/gpu.sh py     OUT script.py [args]            any python tool (tools/*.py) under a 600 s limit
@@ -101,6 +102,24 @@ abn)
     done
   done
   rm -f $O/orig_libmpcx.so ;;
+abhost)
+  # interleaved full-bench runs over host-library builds (comma-separated; see
+  # tools/build_host_variant.sh): each replaces mpcium_amd/libmpcx_host.so for its run
+  n=$1; libs=$2; shift 2
+  cp mpcium_amd/libmpcx_host.so $O/orig_libmpcx_host.so
+  for i in $(seq 1 $n); do
+    k=0
+    for lib in ${libs//,/ }; do
+      k=$((k+1)); tag=H${k}_$i
+      cp $lib mpcium_amd/libmpcx_host.so.tmp && mv mpcium_amd/libmpcx_host.so.tmp mpcium_amd/libmpcx_host.so
+      timeout -k 10 600 python3 bench.py --detail $O/ab_$tag.json "$@" > $O/ab_$tag.line 2> $O/ab_$tag.err
+      rc=$?
+      cp $O/orig_libmpcx_host.so mpcium_amd/libmpcx_host.so
+      [ $rc -eq 0 ] || { tail $O/ab_$tag.err; exit 1; }
+      echo "== $tag $lib"; summ $O/ab_$tag.json
+    done
+  done
+  rm -f $O/orig_libmpcx_host.so ;;
 envab)
   n=$1; ea=$2; eb=$3; shift 3
   for i in $(seq 1 $n); do
