@@ -1011,6 +1011,7 @@ def main():
     ap.add_argument("--wallets", type=int, default=10000,
                     help="config 4: wallets per GPU for the 2-of-3 signing MtA line (0: skip)")
     ap.add_argument("--signers", type=int, default=2)
+    ap.add_argument("--no-sign3", action="store_true", help="skip the 3-signer signing line (timeline runs)")
     ap.add_argument("--keygen-sessions", type=int, default=50000,
                     help="config 5: keygen/reshare sessions for the proof-work line (0: skip)")
     ap.add_argument("--keygen-wave", type=int, default=0,
@@ -1290,7 +1291,7 @@ def main():
         progress(f"config 4: signing, {args.signers} signers")
         result["signing"] = signing_line(args, world, rank, args.signers)
         result["signing"]["cpu_baseline"] = sign_cpu
-        if args.signers != 3:  # mpcium signs with every ready peer (/root/reference/pkg/mpc/node.go:148)
+        if args.signers != 3 and not args.no_sign3:  # mpcium signs with every ready peer (/root/reference/pkg/mpc/node.go:148)
             progress("config 4: signing, 3 signers")
             result["signing_3_signers"] = signing_line(args, world, rank, 3)
             result["signing_3_signers"]["cpu_baseline"] = sign3_cpu

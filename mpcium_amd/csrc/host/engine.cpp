@@ -453,6 +453,7 @@ void Engine::exp_into(const Nat& m, size_t n, const Nat* const* bases, const Nat
   int rc;
   {
     MPCX_PROF("engine.exp.gpu");
+    MPCX_TRACE(md.class_words <= 32 ? "gpu.exp1024" : md.class_words <= 65 ? "gpu.exp2048" : "gpu.exp4096", n);
     enter_call();
     const int inflight = coalesce_inflight();
     // a batch already wide enough to fill the GPU gains nothing from merging
@@ -587,6 +588,7 @@ void Engine::fixed_multi_into(const Nat& m, size_t nb, const Nat* const* bases, 
   int rc;
   {
     MPCX_PROF("engine.fixed.gpu");
+    MPCX_TRACE("gpu.comb", n);
     enter_call();
     const int inflight = coalesce_inflight();
     if (inflight > 0 && n < kCoalesceAloneOps) {

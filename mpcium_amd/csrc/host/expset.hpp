@@ -34,9 +34,11 @@ inline void run_concurrently(const std::vector<std::function<void()>>& fs) {
   }
   std::vector<std::exception_ptr> errs(fs.size());
   std::vector<std::thread> th;
+  const int chain = prof::chain();
   for (size_t i = 0; i + 1 < fs.size(); ++i)
-    th.emplace_back([&, i] {
+    th.emplace_back([&, i, chain] {
       MPCX_PROF_CPU("cpu.launch_threads");
+      prof::set_chain(chain);
       try {
         fs[i]();
       } catch (...) {

@@ -49,6 +49,39 @@ uint64_t thread_cpu_ns() {
   return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
 }
 
+namespace {
+thread_local int t_chain = -1;
+std::mutex g_tr_mu;
+FILE* trace_file() {
+  static FILE* f = [] {
+    const char* p = std::getenv("MPCX_HOST_TRACE");
+    FILE* h = p && *p ? std::fopen(p, "w") : nullptr;
+    if (h) std::fprintf(h, "chain,kind,n,t0_ns,t1_ns\n");
+    return h;
+  }();
+  return f;
+}
+}  // namespace
+
+bool trace_on() {
+  static const bool on = trace_file() != nullptr;
+  return on;
+}
+uint64_t now_ns() {
+  timespec ts{};
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+void set_chain(int c) { t_chain = c; }
+int chain() { return t_chain; }
+void trace(const char* kind, uint64_t t0, uint64_t t1, int64_t n) {
+  FILE* f = trace_file();
+  if (!f) return;
+  std::lock_guard<std::mutex> lk(g_tr_mu);
+  std::fprintf(f, "%d,%s,%lld,%llu,%llu\n", t_chain, kind, (long long)n, (unsigned long long)t0,
+               (unsigned long long)t1);
+}
+
 void add(int slot, uint64_t ns) {
   g_ns[slot].fetch_add(ns, std::memory_order_relaxed);
   g_calls[slot].fetch_add(1, std::memory_order_relaxed);

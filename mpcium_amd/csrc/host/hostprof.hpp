@@ -52,6 +52,29 @@ class ThreadCpu {
   uint64_t t0_;
 };
 
+// ---- timeline (MPCX_HOST_TRACE=<file>): one CSV line per traced interval,
+// "chain,kind,n,t0_ns,t1_ns" on the steady clock (CLOCK_MONOTONIC, the clock
+// libmpcx's MPCX_KTRACE kernel lines use), so a run's protocol chains can be
+// laid against the kernels they waited for (tools/timeline.py). The chain tag
+// is thread-local; run_concurrently hands it to its launch threads.
+bool trace_on();
+uint64_t now_ns();
+void set_chain(int chain);
+int chain();
+void trace(const char* kind, uint64_t t0_ns, uint64_t t1_ns, int64_t n);
+class TraceScope {
+ public:
+  TraceScope(const char* kind, int64_t n) : kind_(trace_on() ? kind : nullptr), n_(n), t0_(kind_ ? now_ns() : 0) {}
+  ~TraceScope() {
+    if (kind_) trace(kind_, t0_, now_ns(), n_);
+  }
+
+ private:
+  const char* kind_;
+  int64_t n_;
+  uint64_t t0_;
+};
+
 }  // namespace mpcx::host::prof
 
 #define MPCX_PROF_CAT2(a, b) a##b
@@ -60,6 +83,8 @@ class ThreadCpu {
 #define MPCX_PROF(label)                                                       \
   static const int MPCX_PROF_CAT(mpcx_prof_slot_, __LINE__) = ::mpcx::host::prof::slot_of(label); \
   ::mpcx::host::prof::Scope MPCX_PROF_CAT(mpcx_prof_scope_, __LINE__)(MPCX_PROF_CAT(mpcx_prof_slot_, __LINE__))
+// MPCX_TRACE("kind", n): a timeline interval over the rest of the scope
+#define MPCX_TRACE(kind, n) ::mpcx::host::prof::TraceScope MPCX_PROF_CAT(mpcx_trace_, __LINE__)(kind, (int64_t)(n))
 // MPCX_PROF_CPU("label"): this thread's CPU time over the rest of the scope
 #define MPCX_PROF_CPU(label)                                                   \
   static const int MPCX_PROF_CAT(mpcx_profc_slot_, __LINE__) = ::mpcx::host::prof::slot_of(label); \

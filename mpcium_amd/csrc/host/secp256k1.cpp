@@ -516,6 +516,7 @@ Affine Combine(const Nat& a, const Affine& P, const Nat& b, const Affine& Q, con
 }
 
 std::vector<Affine> CombineBatch(const std::vector<Comb>& items) {
+  MPCX_TRACE("gpu.ec", items.size());
   MPCX_PROF("ec.combine_batch");
   const size_t n = items.size();
   std::vector<Affine> out(n);

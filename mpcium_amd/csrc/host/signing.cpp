@@ -299,8 +299,10 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
       tasks.push_back([&, pi] {
         const Pair& p = pairs[pi];
         Local& l = L[pi];
+        prof::set_chain((int)(lo * 64 + pi));  // timeline tag: chunk start x 64 + ordered pair
         const double a0 = now();
         {  // round 1: AliceInit(k_i) to Bob j
+          MPCX_TRACE("round1", n);
           std::vector<uint8_t> err;
           mta::AliceInitBatch(nodes[p.i].sk.pub, sl(k[p.i]), public_dln(nodes[p.j].dln), l.ra, &l.cA, &l.pfA, &err,
                               &nodes[p.i].sk);
@@ -308,6 +310,7 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
         }
         const double a1 = now();
         {  // round 2: BobMid(gamma_j) + BobMidWC(w_j, W_j)
+          MPCX_TRACE("round2", n);
           std::vector<uint8_t> err, errwc;
           join_ec();
           const std::vector<secp::Affine> Wj = slp(Wp[p.j]);
@@ -318,6 +321,7 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
         }
         const double a2 = now();
         {  // round 3: AliceEnd + AliceEndWC
+          MPCX_TRACE("round3", n);
           std::vector<mta::ProofBob> pf(n), pfwc(n);
           std::vector<Nat> cB(n), cBwc(n);
           for (size_t x = 0; x < n; ++x) {
@@ -354,6 +358,8 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
     join_ec();
     {
       MPCX_PROF("sign.rounds4_9");
+      prof::set_chain((int)(lo * 64 + 63));
+      MPCX_TRACE("rounds4_9", n);
       auto at = [&](size_t x, size_t i) -> Signer& { return sg[(lo + x) * S + i]; };
       // round 3's outputs: delta_i = k_i gamma_i + sum_j (alpha_ij + beta_ji),
       // sigma_i = k_i w_i + sum_j (mu_ij + nu_ji); theta = sum delta_i

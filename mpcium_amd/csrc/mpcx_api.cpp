@@ -25,6 +25,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <ctime>
 #include <deque>
 #include <functional>
 #include <map>
@@ -295,6 +296,24 @@ struct KAgg {
 std::mutex g_kmu;
 std::map<std::pair<std::string, int>, KAgg> g_kagg;
 std::vector<std::pair<double, double>> g_kiv[8];  // per device: [start, end) ms from its kref
+// MPCX_KTRACE=<file>: one CSV line per timed launch, "dev,kind,geom,ops,t0_ns,t1_ns"
+// on the host's CLOCK_MONOTONIC (the kref event's completion time is taken as
+// its host time), for tools/timeline.py against libmpcx_host's MPCX_HOST_TRACE
+uint64_t g_kref_host_ns[8] = {};
+uint64_t mono_ns() {
+  timespec ts{};
+  clock_gettime(CLOCK_MONOTONIC, &ts);
+  return (uint64_t)ts.tv_sec * 1000000000ull + (uint64_t)ts.tv_nsec;
+}
+FILE* ktrace_file() {
+  static FILE* f = [] {
+    const char* p = std::getenv("MPCX_KTRACE");
+    FILE* h = p && *p ? std::fopen(p, "w") : nullptr;
+    if (h) std::fprintf(h, "dev,kind,geom,ops,t0_ns,t1_ns\n");
+    return h;
+  }();
+  return f;
+}
 
 int kstat_begin(Lane& l) {
   if (!g_kstats.load(std::memory_order_relaxed) || l.kpend.size() >= 512) return -1;
@@ -352,6 +371,11 @@ void kstat_resolve(Lane& l) {
       a.alg += p.alg;
       a.ms += ms;
       if (p.dev >= 0 && p.dev < 8) g_kiv[p.dev].push_back({(double)t0, (double)t0 + ms});
+      if (FILE* kf = ktrace_file(); kf && p.dev >= 0 && p.dev < 8) {
+        const uint64_t b = g_kref_host_ns[p.dev];
+        std::fprintf(kf, "%d,%s,%d,%u,%llu,%llu\n", p.dev, p.kind, p.geom, p.ops,
+                     (unsigned long long)(b + (uint64_t)(t0 * 1e6)), (unsigned long long)(b + (uint64_t)((t0 + ms) * 1e6)));
+      }
     }
     l.kev_free.push_back(p.ev);
   }
@@ -1183,6 +1207,7 @@ int mpcx_kernel_stats(char* buf, size_t cap, int reset) {
       if (e == hipSuccess) e = hipEventRecord(d.kref, nullptr);
       if (e == hipSuccess) e = hipEventSynchronize(d.kref);
       if (e != hipSuccess) return hip_fail(e, "kernel stats time origin");
+      if (i < 8) g_kref_host_ns[i] = mono_ns();
     }
   }
   if (buf && cap) {
