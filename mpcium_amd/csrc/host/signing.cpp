@@ -128,6 +128,7 @@ struct Signer {
 MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wallets, uint64_t seed,
                     size_t trace_wallets, std::vector<uint32_t>* trace, int64_t tamper_wallet, int tamper_kind) {
   if (signers < 2 || (size_t)signers > nodes.size()) throw std::invalid_argument("signers must be in [2, nodes]");
+  MPCX_TRACE("run", wallets);  // timeline window of this run
   const Nat& q = mta::Q();
   const size_t S = (size_t)signers, Wn = wallets;
   MtaStats st;

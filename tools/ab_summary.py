@@ -47,7 +47,7 @@ def main():
     runs, sides = [], {}
     for p in sorted(glob.glob(os.path.join(src, "ab_*.json"))):
         # ab_A_1 / ab_B_1 (ab, abswap, envab) or ab_L3_1 (abn: position in the build list)
-        m = re.search(r"ab_([AB]|[LH]\d+)_(\d+)\.json$", p)
+        m = re.search(r"ab_([AB]|[LHE]\d+)_(\d+)\.json$", p)
         if not m:
             continue
         tag = m.group(1)

@@ -10,6 +10,7 @@
 #   bash tools/gpu.sh abswap OUT N LIB_A LIB_B [bench args]  N interleaved full-bench runs, LIB swapped in place
 #   bash tools/gpu.sh abhost OUT N HOSTLIB_A,HOSTLIB_B [bench args]  N interleaved runs per libmpcx_host build
 #   bash tools/gpu.sh envab  OUT N "ENV_A" "ENV_B" [bench args]  N interleaved runs under two environments
+#   bash tools/gpu.sh envn   OUT N "ENV1;ENV2;..." [bench args]  N interleaved runs per environment
 #   bash tools/gpu.sh argab  OUT N "ARGS_A" "ARGS_B" [bench args]  N interleaved runs with two bench.py argument sets
 #   bash tools/gpu.sh py     OUT script.py [args]            any python tool (tools/*.py) under a 600 s limit
 set -o pipefail
@@ -128,6 +129,20 @@ envab)
       env $ev timeout -k 10 600 python3 bench.py --detail $O/ab_${e}_$i.json "$@" > $O/ab_${e}_$i.line 2> $O/ab_${e}_$i.err \
           || { tail $O/ab_${e}_$i.err; exit 1; }
       echo "== $e ($ev) run $i"; summ $O/ab_${e}_$i.json
+    done
+  done ;;
+envn)
+  # N interleaved runs over several environments (separated by ';'), tag E<k>
+  n=$1; envs=$2; shift 2
+  IFS=';' read -ra EV <<< "$envs"
+  for i in $(seq 1 $n); do
+    k=0
+    for ev in "${EV[@]}"; do
+      k=$((k+1)); tag=E${k}_$i
+      env $ev timeout -k 10 600 python3 bench.py --detail $O/ab_$tag.json "$@" > $O/ab_$tag.line 2> $O/ab_$tag.err \
+          || { tail $O/ab_$tag.err; exit 1; }
+      echo "== $tag ($ev)"; summ $O/ab_$tag.json short
+      python3 -c "import json,sys; d=json.load(open(sys.argv[1])); print('  ', {k: round(d[k]['value'],1) for k in ('signing','signing_3_signers','keygen','paillier_batch') if k in d})" $O/ab_$tag.json
     done
   done ;;
 argab)

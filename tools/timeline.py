@@ -48,10 +48,15 @@ def main():
         r["t0"], r["t1"], r["chain"] = int(r["t0_ns"]) / 1e9, int(r["t1_ns"]) / 1e9, int(r["chain"])
     for r in kern:
         r["t0"], r["t1"] = int(r["t0_ns"]) / 1e9, int(r["t1_ns"]) / 1e9
+    runs = [r for r in host if r["kind"] == "run"]
+    if runs:  # the last traced run only (a line's warm-up run comes first)
+        lo, hi = runs[-1]["t0"], runs[-1]["t1"]
+        host = [r for r in host if r["kind"] != "run" and r["t0"] >= lo and r["t1"] <= hi]
     rounds = [r for r in host if not r["kind"].startswith("gpu.")]
     if not rounds:
         sys.exit("no round intervals in the host trace")
-    lo, hi = min(r["t0"] for r in rounds), max(r["t1"] for r in rounds)
+    if not runs:
+        lo, hi = min(r["t0"] for r in rounds), max(r["t1"] for r in rounds)
     win = hi - lo
     kiv = clip([(r["t0"], r["t1"]) for r in kern], lo, hi)
     busy = length(union(kiv))
