@@ -284,6 +284,23 @@ typedef struct {
 } mpcxh_party_t;
 int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
                               uint64_t seed, uint32_t wave_sessions, double* stats_out, uint32_t* trace_out);
+/* Config 5 with resharing as mpcium runs it (two resharing sessions per node
+ * per wallet: old party and new party, /root/reference/pkg/eventconsumer/
+ * event_consumer.go:407-416): reshare_mix = 1 makes every odd wave a resharing
+ * wave -- the new committee's proof work (as keygen) plus the old committee's
+ * VSS of its Lagrange-weighted share with new threshold 2 and the new
+ * committee's decommitment, share and public-key checks (keygenload.hpp);
+ * 0: keygen waves only (= mpcxh_bench_keygen_proofs).
+ * stats_out[MPCXH_KEYGEN_RESHARE_STATS]: the MPCXH_KEYGEN_STATS values, then
+ * keygen_sessions, reshare_sessions, keygen_wave_s, reshare_wave_s (summed
+ * wave wall times per kind), vss_checks, vss_failures.
+ * trace_out: per wave the keygen trace words, then n*8 + 9 VSS words (per old
+ * party the 8-word digest of its commitment, points and shares; the digest of
+ * the new shares; the count of VSS checks that passed; zero on keygen waves). */
+#define MPCXH_KEYGEN_RESHARE_STATS 19
+int mpcxh_bench_keygen_reshare(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
+                               uint64_t seed, uint32_t wave_sessions, int reshare_mix, double* stats_out,
+                               uint32_t* trace_out);
 
 /* Host-side helpers of the MtA path, exported as test hooks (no GPU needed):
  * common.SHA512_256i / SHA512_256i_TAGGED (tag == NULL: untagged) over count

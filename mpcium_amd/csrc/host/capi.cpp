@@ -787,32 +787,58 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
 
 }  // extern "C"
 
+namespace {
+keygenload::ProofStats bench_config5(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
+                                     uint64_t seed, uint32_t wave_sessions, int mix, uint32_t* trace_out) {
+  if (w < 64) throw std::invalid_argument("party integer width must be >= 64 words");
+  if (!parties) throw std::invalid_argument("null argument");
+  std::vector<keygenload::PartyKeys> ps(n_parties);
+  for (uint32_t i = 0; i < n_parties; ++i) {
+    const mpcxh_party_t& a = parties[i];
+    if (!a.NTilde || !a.h1 || !a.h2 || !a.alpha || !a.beta || !a.p || !a.q)
+      throw std::invalid_argument("null party field");
+    ps[i].sk = paillier_from(&a.paillier, w);
+    ps[i].NTilde = Nat::from_words(a.NTilde, w);
+    ps[i].h1 = Nat::from_words(a.h1, w);
+    ps[i].h2 = Nat::from_words(a.h2, w);
+    ps[i].alpha = Nat::from_words(a.alpha, w);
+    ps[i].beta = Nat::from_words(a.beta, w);
+    ps[i].p = Nat::from_words(a.p, w);
+    ps[i].q = Nat::from_words(a.q, w);
+  }
+  std::vector<uint32_t> tr;
+  const auto st = keygenload::RunKeygenProofs(ps, sessions, seed, wave_sessions, trace_out ? &tr : nullptr, mix);
+  if (trace_out) std::memcpy(trace_out, tr.data(), tr.size() * sizeof(uint32_t));
+  return st;
+}
+void keygen_stats(const keygenload::ProofStats& st, double* v) {
+  const double a[MPCXH_KEYGEN_RESHARE_STATS] = {
+      st.prove_s, st.verify_s, st.total_s, (double)st.sessions, (double)st.parties, (double)st.proofs,
+      (double)st.verifications, (double)st.failures, st.engine_busy_s, st.alg_macs, (double)st.waves,
+      (double)st.wave_sessions, st.max_wave_s, (double)st.keygen_sessions, (double)st.reshare_sessions,
+      st.keygen_wave_s, st.reshare_wave_s, (double)st.vss_checks, (double)st.vss_failures};
+  std::memcpy(v, a, sizeof a);
+}
+}  // namespace
+
 int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
                               uint64_t seed, uint32_t wave_sessions, double* stats_out, uint32_t* trace_out) {
   return guard([&] {
-    if (w < 64) throw std::invalid_argument("party integer width must be >= 64 words");
-    if (!parties || !stats_out) throw std::invalid_argument("null argument");
-    std::vector<keygenload::PartyKeys> ps(n_parties);
-    for (uint32_t i = 0; i < n_parties; ++i) {
-      const mpcxh_party_t& a = parties[i];
-      if (!a.NTilde || !a.h1 || !a.h2 || !a.alpha || !a.beta || !a.p || !a.q)
-        throw std::invalid_argument("null party field");
-      ps[i].sk = paillier_from(&a.paillier, w);
-      ps[i].NTilde = Nat::from_words(a.NTilde, w);
-      ps[i].h1 = Nat::from_words(a.h1, w);
-      ps[i].h2 = Nat::from_words(a.h2, w);
-      ps[i].alpha = Nat::from_words(a.alpha, w);
-      ps[i].beta = Nat::from_words(a.beta, w);
-      ps[i].p = Nat::from_words(a.p, w);
-      ps[i].q = Nat::from_words(a.q, w);
-    }
-    std::vector<uint32_t> tr;
-    const auto st = keygenload::RunKeygenProofs(ps, sessions, seed, wave_sessions, trace_out ? &tr : nullptr);
-    const double v[MPCXH_KEYGEN_STATS] = {st.prove_s, st.verify_s, st.total_s, (double)st.sessions,
-                                          (double)st.parties, (double)st.proofs, (double)st.verifications,
-                                          (double)st.failures, st.engine_busy_s, st.alg_macs, (double)st.waves,
-                                          (double)st.wave_sessions, st.max_wave_s};
-    std::memcpy(stats_out, v, sizeof v);
-    if (trace_out) std::memcpy(trace_out, tr.data(), tr.size() * sizeof(uint32_t));
+    if (!stats_out) throw std::invalid_argument("null argument");
+    const auto st = bench_config5(w, parties, n_parties, sessions, seed, wave_sessions, 0, trace_out);
+    double v[MPCXH_KEYGEN_RESHARE_STATS];
+    keygen_stats(st, v);
+    std::memcpy(stats_out, v, MPCXH_KEYGEN_STATS * sizeof(double));
+  });
+}
+
+int mpcxh_bench_keygen_reshare(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
+                               uint64_t seed, uint32_t wave_sessions, int reshare_mix, double* stats_out,
+                               uint32_t* trace_out) {
+  return guard([&] {
+    if (!stats_out) throw std::invalid_argument("null argument");
+    if (reshare_mix != 0 && reshare_mix != 1) throw std::invalid_argument("reshare_mix: 0 or 1");
+    const auto st = bench_config5(w, parties, n_parties, sessions, seed, wave_sessions, reshare_mix, trace_out);
+    keygen_stats(st, stats_out);
   });
 }

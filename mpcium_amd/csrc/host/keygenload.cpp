@@ -17,6 +17,8 @@
 #include "engine.hpp"
 #include "hostprof.hpp"
 #include "proofs.hpp"
+#include "secp256k1.hpp"
+#include "tsscommon.hpp"
 
 namespace mpcx::host::keygenload {
 namespace {
@@ -85,10 +87,174 @@ Nat fac_digest(const proofs::FacProof& p) {
   return digest({&p.P, &p.Q, &p.A, &p.B, &p.T, &p.Sigma, &p.Z1, &p.Z2, &p.W1, &p.W2, &vabs, &vneg});
 }
 
+secp::Affine negate(const secp::Affine& P) {
+  if (P.inf) return P;
+  secp::Affine r = P;
+  const Nat y = secp::FeToNat(P.y);
+  r.y = secp::NatToFe(y.is_zero() ? y : secp::FieldP() - y);
+  return r;
+}
+
+// The old committee's side of a resharing wave [lo, hi) (keygenload.hpp) and
+// the new committee's checks of it: two GPU EC batches (k_ec_combine) plus
+// host hashing. vt: the traced session's TraceVssWords(n) words (or null).
+void vss_wave(size_t lo, size_t hi, size_t n, uint64_t seed, size_t ts, uint32_t* vt, std::atomic<uint64_t>& checks,
+              std::atomic<uint64_t>& fails) {
+  MPCX_PROF("keygen.vss");
+  constexpr size_t T = kReshareThreshold;
+  static_assert(T == 2, "the share check is one a*G + b*P + c*Q combination");
+  const size_t m = hi - lo;
+  const Nat& q = secp::CurveN();
+  // Lagrange coefficients of the old committee (ids 1..n) at 0
+  std::vector<Nat> lam(n);
+  for (size_t i = 0; i < n; ++i) {
+    Nat num(1), den(1);
+    for (size_t j = 0; j < n; ++j) {
+      if (j == i) continue;
+      num = (num * Nat(j + 1)) % q;
+      den = (den * ((Nat(j + 1) + q - Nat(i + 1)) % q)) % q;
+    }
+    Nat inv;
+    if (!mod_inverse(Int(den), q, &inv)) throw std::runtime_error("vss: Lagrange denominator");
+    lam[i] = (num * inv) % q;
+  }
+  struct Old {
+    std::vector<Nat> a, sh;  // coefficients a_0..a_T, shares s_i1..s_in
+    Nat r, C;
+    std::vector<secp::Affine> V;
+  };
+  std::vector<Nat> secret(m);
+  std::vector<std::vector<Old>> od(m, std::vector<Old>(n));
+  parallel_for(m, [&](size_t x) {
+    const size_t s = lo + x;
+    CounterDRBG wd(mix(seed, s, 0xEE, 0));  // the wallet's old sharing polynomial
+    const RandFn wr = wd.fn();
+    std::vector<Nat> c(T + 1);
+    for (auto& ck : c) ck = GetRandomPositiveInt(wr, q);
+    secret[x] = c[0];
+    for (size_t i = 0; i < n; ++i) {
+      Nat xi = c[T];  // x_i = f(i + 1) by Horner
+      for (size_t k = T; k-- > 0;) xi = (xi * Nat(i + 1) + c[k]) % q;
+      Old& o = od[x][i];
+      CounterDRBG d(mix(seed, s, i, 9));
+      const RandFn r = d.fn();
+      o.a.resize(T + 1);
+      o.a[0] = (lam[i] * xi) % q;  // w_i
+      for (size_t k = 1; k <= T; ++k) o.a[k] = GetRandomPositiveInt(r, q);
+      o.r = MustGetRandomInt(r, 256);
+      o.sh.resize(n);
+      for (size_t j = 0; j < n; ++j) {
+        Nat v = o.a[T];
+        for (size_t k = T; k-- > 0;) v = (v * Nat(j + 1) + o.a[k]) % q;
+        o.sh[j] = v;
+      }
+    }
+  });
+  // EC batch 1: X = secret G, V_ik = a_k G
+  std::vector<secp::Comb> c1(m * (1 + n * (T + 1)));
+  for (size_t x = 0; x < m; ++x) {
+    const size_t b = x * (1 + n * (T + 1));
+    c1[b].a = secret[x];
+    for (size_t i = 0; i < n; ++i)
+      for (size_t k = 0; k <= T; ++k) c1[b + 1 + i * (T + 1) + k].a = od[x][i].a[k];
+  }
+  const std::vector<secp::Affine> p1 = secp::CombineBatch(c1);
+  std::vector<secp::Affine> X(m);
+  parallel_for(m, [&](size_t x) {
+    const size_t b = x * (1 + n * (T + 1));
+    X[x] = p1[b];
+    for (size_t i = 0; i < n; ++i) {
+      Old& o = od[x][i];
+      o.V.assign(p1.begin() + (long)(b + 1 + i * (T + 1)), p1.begin() + (long)(b + 1 + (i + 1) * (T + 1)));
+      std::vector<Nat> flat{o.r};
+      for (const auto& v : o.V) {
+        flat.push_back(secp::FeToNat(v.x));
+        flat.push_back(secp::FeToNat(v.y));
+      }
+      std::vector<const Nat*> in;
+      for (const auto& f : flat) in.push_back(&f);
+      o.C = SHA512_256i(in);  // commitments.NewHashCommitment(rand, flatVs...)
+    }
+  });
+  // EC batch 2: new party j's share check of old party i:
+  // (q - s_ij) G + j V_i1 + j^2 V_i2 == -V_i0
+  std::vector<secp::Comb> c2(m * n * n);
+  std::vector<uint8_t> dec_ok(m * n * n, 0);
+  parallel_for(m, [&](size_t x) {
+    for (size_t i = 0; i < n; ++i) {
+      const Old& o = od[x][i];
+      std::vector<Nat> D{o.r};  // the decommitment as received, checked against C_i
+      for (const auto& v : o.V) {
+        D.push_back(secp::FeToNat(v.x));
+        D.push_back(secp::FeToNat(v.y));
+      }
+      std::vector<const Nat*> in;
+      for (const auto& f : D) in.push_back(&f);
+      const bool dc = SHA512_256i(in) == o.C;
+      for (size_t j = 0; j < n; ++j) {
+        secp::Comb& cb = c2[(x * n + i) * n + j];
+        const Nat& sij = o.sh[j];
+        cb.a = sij.is_zero() ? sij : q - sij;
+        cb.P = o.V[1];
+        cb.b = Nat(j + 1);
+        cb.Q = o.V[2];
+        cb.c = Nat((j + 1) * (j + 1));
+        dec_ok[(x * n + i) * n + j] = dc;
+      }
+    }
+  });
+  const std::vector<secp::Affine> p2 = secp::CombineBatch(c2);
+  std::atomic<uint64_t> ok_total{0}, bad_total{0};
+  parallel_for(m, [&](size_t x) {
+    uint64_t good = 0, bad = 0;
+    secp::Affine sumV;
+    for (size_t i = 0; i < n; ++i) {
+      const Old& o = od[x][i];
+      sumV = secp::Add(sumV, o.V[0]);
+      const secp::Affine nv0 = negate(o.V[0]);
+      for (size_t j = 0; j < n; ++j) {
+        const size_t k = (x * n + i) * n + j;
+        (dec_ok[k] && secp::Equal(p2[k], nv0) ? good : bad) += 1;
+      }
+    }
+    // every new party: sum_i V_i0 == X
+    (secp::Equal(sumV, X[x]) ? good : bad) += n;
+    ok_total += good;
+    bad_total += bad;
+    if (vt && lo + x == ts) {
+      uint32_t* d = vt;
+      for (size_t i = 0; i < n; ++i, d += 8) {
+        const Old& o = od[x][i];
+        std::vector<Nat> v{o.C};
+        for (const auto& pt : o.V) {
+          v.push_back(secp::FeToNat(pt.x));
+          v.push_back(secp::FeToNat(pt.y));
+        }
+        for (const auto& sh : o.sh) v.push_back(sh);
+        std::vector<const Nat*> in;
+        for (const auto& f : v) in.push_back(&f);
+        SHA512_256i(in).to_words(d, 8);
+      }
+      std::vector<Nat> xs(n);
+      for (size_t j = 0; j < n; ++j) {
+        Nat acc;
+        for (size_t i = 0; i < n; ++i) acc = acc + od[x][i].sh[j];
+        xs[j] = acc % q;  // x'_j
+      }
+      std::vector<const Nat*> in;
+      for (const auto& f : xs) in.push_back(&f);
+      SHA512_256i(in).to_words(d, 8);
+      d[8] = (uint32_t)good;
+    }
+  });
+  checks += ok_total.load() + bad_total.load();
+  fails += bad_total.load();
+}
+
 }  // namespace
 
 ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t sessions, uint64_t seed,
-                           size_t wave_sessions, std::vector<uint32_t>* trace) {
+                           size_t wave_sessions, std::vector<uint32_t>* trace, int reshare_mix) {
   const size_t n = parties.size();
   if (n < 2) throw std::invalid_argument("need at least two parties");
   const size_t W = wave_sessions ? wave_sessions : kDefaultWave;
@@ -100,9 +266,11 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
   st.wave_sessions = W;
   st.proofs = (uint64_t)sessions * n * (3 + (n - 1));
   st.verifications = (uint64_t)sessions * n * (n - 1) * 4;
-  const size_t tw = TraceSessionWords(n);
+  const size_t tk = TraceSessionWords(n), tw = tk + (reshare_mix ? TraceVssWords(n) : 0);
   if (trace) trace->assign(n_waves * tw, 0);
-  std::atomic<uint64_t> fails{0};
+  std::atomic<uint64_t> fails{0}, vss_checks{0}, vss_fails{0};
+  std::atomic<uint64_t> kg_sessions{0}, rs_sessions{0};
+  double kg_wave_s = 0, rs_wave_s = 0;  // under tm
   std::mutex tm;
   double last_prove = 0, max_wave = 0;
   size_t waves_done = 0;  // under tm
@@ -129,6 +297,7 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
   // when it returns.
   auto run_wave = [&](size_t w) {
     const size_t lo = w * W, hi = std::min(sessions, lo + W), m = hi - lo;
+    const bool reshare = reshare_mix && (w % 2 == 1);
     const double w0 = now();
     std::vector<proofs::Bytes> sess(m);  // SSID bytes shared by the parties of a session
     {
@@ -199,10 +368,16 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
         });
       }
     }
+    if (reshare)  // the old committee's VSS beside the new committee's proof chains
+      tasks.push_back([&, lo, hi] {
+        vss_wave(lo, hi, n, seed, TracedSession(w, lo, hi), trace ? trace->data() + w * tw + tk : nullptr, vss_checks,
+                 vss_fails);
+      });
     // every proof chain of the wave at once (35 for 5 parties): their small
     // per-pair batches meet in the coalescers; 8 at a time measured 5% slower
     // with twice the narrow-geometry share (profiles/r04/keygen_tasks_ab/)
     run_bounded(tasks, tasks.size());
+    (reshare ? rs_sessions : kg_sessions) += m;
     if (trace) {
       uint32_t* o = trace->data() + w * tw;
       o[0] = (uint32_t)(lo + ts);
@@ -222,6 +397,7 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
     }
     std::lock_guard<std::mutex> lk(tm);
     max_wave = std::max(max_wave, now() - w0);
+    (reshare ? rs_wave_s : kg_wave_s) += now() - w0;
     // MPCX_PROGRESS=1: a line on stderr every 10 finished waves and at the end
     // (long runs are otherwise silent for minutes)
     static const bool progress = [] {
@@ -256,6 +432,12 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
   st.failures = fails.load();
   st.engine_busy_s = Engine::get().busy_seconds();
   st.alg_macs = Engine::get().alg_macs();
+  st.keygen_sessions = kg_sessions.load();
+  st.reshare_sessions = rs_sessions.load();
+  st.keygen_wave_s = kg_wave_s;
+  st.reshare_wave_s = rs_wave_s;
+  st.vss_checks = vss_checks.load();
+  st.vss_failures = vss_fails.load();
   return st;
 }
 

@@ -43,7 +43,34 @@ struct ProofStats {
   uint64_t failures = 0;  // verifications that did not pass (honest proofs: must be 0)
   uint64_t waves = 0, wave_sessions = 0;
   double max_wave_s = 0;  // slowest wave, prove + verify
+  // mixed runs (reshare_mix): sessions and summed wave wall time per kind, and
+  // the old committee's VSS checks (decommitment + share + public key)
+  uint64_t keygen_sessions = 0, reshare_sessions = 0;
+  double keygen_wave_s = 0, reshare_wave_s = 0;
+  uint64_t vss_checks = 0, vss_failures = 0;
 };
+
+// ---- resharing as mpcium runs it: every node runs TWO resharing sessions per
+// wallet, as an old party and as a new party
+// (/root/reference/pkg/eventconsumer/event_consumer.go:407-416,
+// /root/reference/pkg/mpc/ecdsa_resharing_session.go:114-138). Old = new
+// committee = the n ready peers (ids 1..n), new threshold kReshareThreshold
+// (3-of-5). Per session, as recalled from tss-lib v2.0.2 up:ecdsa/resharing
+// (not vendored: "upstream, verify"):
+//   old party i: w_i = lambda_i x_i (its Lagrange-weighted share of the wallet
+//     key), vss.Create(t, w_i): coefficients a_1..a_t < q drawn from its
+//     reader, then a hash commitment to V_ik = a_k G (r = MustGetRandomInt(256)
+//     drawn after them); shares s_ij = f_i(j) to every new party j;
+//   new party j: the new-committee proof work (identical to keygen's: DLN x2,
+//     Mod, Fac per peer, proved and verified) and, for every old party i, the
+//     decommitment and s_ij G == sum_k V_ik j^k, then x'_j = sum_i s_ij and
+//     sum_i V_i0 == X (the wallet key).
+// The wallet's old shares are a degree-t polynomial of a seeded stream.
+constexpr size_t kReshareThreshold = 2;
+// extra trace words of a reshare wave's traced session: per old party an 8-word
+// SHA512_256i(C_i, V_i0.x, V_i0.y, .., V_it.y, s_i1 .. s_in), the 8-word digest
+// of the new shares x'_1 .. x'_n, and the number of VSS checks that passed
+inline size_t TraceVssWords(size_t n) { return n * 8 + 8 + 1; }
 
 // Sessions stream through in waves of `wave_sessions` (<= 0: kDefaultWave),
 // kWavesInFlight at a time: a wave's proofs are built, verified by every peer
@@ -66,7 +93,12 @@ constexpr size_t kWavesInFlight = 2;
 inline size_t TraceSessionWords(size_t n) { return 1 + n * (3 + (n - 1)) * 8 + 1; }
 inline size_t TracedSession(size_t wave, size_t lo, size_t hi) { return lo + (wave * 7919u) % (hi - lo); }
 
+// reshare_mix: 0 -- every wave a keygen wave; 1 -- odd waves are resharing
+// waves (the new committee's proof work + the old committee's VSS), so the two
+// waves in flight are one of each kind (config 5: "reshare + keygen under
+// load"). Trace: TraceSessionWords(n) + (reshare_mix ? TraceVssWords(n) : 0)
+// words per wave (the VSS words zero on keygen waves).
 ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t sessions, uint64_t seed,
-                           size_t wave_sessions = 0, std::vector<uint32_t>* trace = nullptr);
+                           size_t wave_sessions = 0, std::vector<uint32_t>* trace = nullptr, int reshare_mix = 0);
 
 }  // namespace mpcx::host::keygenload

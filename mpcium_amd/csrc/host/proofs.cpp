@@ -274,8 +274,7 @@ std::vector<FacProof> FacProveBatch(const std::vector<Bytes>& session, const Nat
   const Nat q3sqrtN0 = q3 * isqrt(N0);
   const Nat qNCap = Q_ * NCap, qN0NCap = qNCap * N0, q3NCap = q3 * NCap, q3N0NCap = q3NCap * N0;
   struct St {
-    Nat alpha, beta, mu, nu, sigma, r, x, y;
-    Nat sA, sB, qa, e;
+    Nat alpha, beta, mu, nu, sigma, r, x, y, e;
   };
   std::vector<St> st(n);
   std::vector<FacProof> out(n);
@@ -290,25 +289,27 @@ std::vector<FacProof> FacProveBatch(const std::vector<Bytes>& session, const Nat
     v.x = GetRandomPositiveInt(rand[i], q3NCap);
     v.y = GetRandomPositiveInt(rand[i], q3NCap);
   });
-  Nat sN0p, sN0q;
+  // Fig 28.1 compute, every value as ONE two-table comb product on (s, t) in
+  // ONE launch step (round 4: four steps, s^alpha / s^beta first, then the t
+  // products, then Q^alpha, then T):
+  //   P = s^N0p t^mu, Q = s^N0q t^nu, A = s^alpha t^x, B = s^beta t^y,
+  //   T = Q^alpha t^r = (s^N0q t^nu)^alpha t^r = s^(N0q alpha) t^(nu alpha + r)
+  // -- exponent identities of the group Z*_NCap (any commutative monoid), so
+  // the same residues bit for bit; the longest exponent, nu alpha + r, is
+  // < q^3 N0 NCap + q NCap q^3 sqrt(N0) < 2^4900, inside the comb tables'
+  // kFixedMaxBits (longer ones would take the per-operand path).
+  std::vector<Nat> ea(n), eb(n);
   ExpSet e(NCap);
-  e.add(s, N0p, &sN0p);  // shared by every proof of the batch
-  e.add(s, N0q, &sN0q);
   for (size_t i = 0; i < n; ++i) {
-    e.add(s, st[i].alpha, &st[i].sA);
-    e.add(s, st[i].beta, &st[i].sB);
+    auto& v = st[i];
+    ea[i] = N0q * v.alpha;
+    eb[i] = v.nu * v.alpha + v.r;
+    e.add2(s, N0p, t, v.mu, &out[i].P);
+    e.add2(s, N0q, t, v.nu, &out[i].Q);
+    e.add2(s, v.alpha, t, v.x, &out[i].A);
+    e.add2(s, v.beta, t, v.y, &out[i].B);
+    e.add2(s, ea[i], t, eb[i], &out[i].T);
   }
-  e.run();
-  for (size_t i = 0; i < n; ++i) {  // Fig 28.1 compute
-    e.add(t, st[i].mu, &out[i].P, &sN0p);      // P = s^N0p t^mu
-    e.add(t, st[i].nu, &out[i].Q, &sN0q);      // Q = s^N0q t^nu
-    e.add(t, st[i].x, &out[i].A, &st[i].sA);   // A = s^alpha t^x
-    e.add(t, st[i].y, &out[i].B, &st[i].sB);   // B = s^beta t^y
-  }
-  e.run();
-  for (size_t i = 0; i < n; ++i) e.add(out[i].Q, st[i].alpha, &st[i].qa);
-  e.run();
-  for (size_t i = 0; i < n; ++i) e.add(t, st[i].r, &out[i].T, &st[i].qa);  // T = Q^alpha t^r
   e.run();
   parallel_for(n, [&](size_t i) {
     auto& o = out[i];
@@ -360,13 +361,16 @@ std::vector<uint8_t> FacVerifyBatch(const std::vector<Bytes>& session, const Nat
   for (size_t i = 0; i < n; ++i) any_neg |= ok[i] && pf[i].V.neg;
   Nat tinv;
   const bool t_inv_ok = any_neg && mod_inverse(Int(t), NCap, &tinv);
+  // Every check's exponentiations in ONE launch step (round 4: three):
+  //   s^z1 t^w1 == A P^e,  s^z2 t^w2 == B Q^e,  Q^z1 t^v == T R^e with
+  //   R = s^N0 t^sigma, so R^e = s^(N0 e) t^(sigma e) -- a two-table comb
+  //   product with multiplier T instead of R first and R^e after it; Q^z1 and
+  //   t^v run side by side and are multiplied on the host (2048-bit product).
   struct St {
-    Nat sz1, sz2, pe, qe, tsig, qz1, L1, R1, L2, R2, R, L3, R3;
+    Nat qz1, tv, L1, R1, L2, R2, L3, R3, ne, se;
   };
   std::vector<St> st(n);
-  Nat sN0;
   ExpSet x(NCap);
-  x.add(s, N0, &sN0);  // s^N0, shared by the batch
   for (size_t i = 0; i < n; ++i) {
     if (!ok[i]) continue;
     const auto& p = pf[i];
@@ -374,25 +378,21 @@ std::vector<uint8_t> FacVerifyBatch(const std::vector<Bytes>& session, const Nat
       ok[i] = 0;
       continue;
     }
-    x.add(s, p.Z1, &st[i].sz1);
-    x.add(s, p.Z2, &st[i].sz2);
-    x.add(p.P, e[i], &st[i].R1, &p.A);  // A P^e
-    x.add(p.Q, e[i], &st[i].R2, &p.B);  // B Q^e
-    x.add(p.Q, p.Z1, &st[i].qz1);
+    auto& v = st[i];
+    v.ne = N0 * e[i];
+    v.se = p.Sigma * e[i];
+    x.add2(s, p.Z1, t, p.W1, &v.L1);       // s^z1 t^w1
+    x.add2(s, p.Z2, t, p.W2, &v.L2);       // s^z2 t^w2
+    x.add(p.P, e[i], &v.R1, &p.A);         // A P^e
+    x.add(p.Q, e[i], &v.R2, &p.B);         // B Q^e
+    x.add(p.Q, p.Z1, &v.qz1);              // Q^z1
+    x.add(p.V.neg ? tinv : t, p.V.mag, &v.tv);  // t^v
+    x.add2(s, v.ne, t, v.se, &v.R3, &p.T);  // T R^e = T s^(N0 e) t^(sigma e)
   }
   x.run();
-  for (size_t i = 0; i < n; ++i) {
-    if (!ok[i]) continue;
-    const auto& p = pf[i];
-    x.add(t, p.W1, &st[i].L1, &st[i].sz1);            // s^z1 t^w1
-    x.add(t, p.W2, &st[i].L2, &st[i].sz2);            // s^z2 t^w2
-    x.add(t, p.Sigma, &st[i].R, &sN0);                // R = s^N0 t^sigma
-    x.add(p.V.neg ? tinv : t, p.V.mag, &st[i].L3, &st[i].qz1);  // Q^z1 t^v
-  }
-  x.run();
-  for (size_t i = 0; i < n; ++i)
-    if (ok[i]) x.add(st[i].R, e[i], &st[i].R3, &pf[i].T);  // T R^e
-  x.run();
+  parallel_for(n, [&](size_t i) {
+    if (ok[i]) st[i].L3 = (st[i].qz1 * st[i].tv) % NCap;  // Q^z1 t^v
+  });
   for (size_t i = 0; i < n; ++i)
     ok[i] = ok[i] && st[i].L1 == st[i].R1 && st[i].L2 == st[i].R2 && st[i].L3 == st[i].R3;
   return ok;

@@ -28,6 +28,7 @@ SIGNATURES = [
     ("mpcxh_fac_prove_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("mpcxh_fac_verify_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("mpcxh_bench_keygen_proofs", _i, [_u32, _vp, _u32, _u32, _u64, _u32, _vp, _vp]),
+    ("mpcxh_bench_keygen_reshare", _i, [_u32, _vp, _u32, _u32, _u64, _u32, _i, _vp, _vp]),
 ]
 _bound = False
 
@@ -152,17 +153,23 @@ class _Party(ctypes.Structure):
 
 KEYGEN_STATS = ["prove_s", "verify_s", "total_s", "sessions", "parties", "proofs", "verifications", "failures",
                 "engine_busy_s", "alg_macs", "waves", "wave_sessions", "max_wave_s"]
+RESHARE_STATS = KEYGEN_STATS + ["keygen_sessions", "reshare_sessions", "keygen_wave_s", "reshare_wave_s",
+                                "vss_checks", "vss_failures"]
 
 
 def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B67, wave: int = 0,
-                        trace: bool = False):
+                        trace: bool = False, reshare: bool = False):
     """Config-5 driver (csrc/host/keygenload.hpp): the DLN / Mod / Fac proof
-    work of `sessions` keygen or reshare sessions of len(parties) nodes,
-    streamed in waves of `wave` sessions (0: the driver's default, 1024), two
-    waves in flight. parties: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i,
-    Alpha, Beta, p, q. trace: also return one traced session per wave --
-    [{"session": s, "digests": {(i, "dln1"|"dln2"|"mod"): d, (i, "fac", j): d},
-    "verified": count}]."""
+    work of `sessions` keygen sessions of len(parties) nodes, streamed in waves
+    of `wave` sessions (0: the driver's default, 1024), two waves in flight;
+    reshare=True: every odd wave is a resharing wave (the new committee's proof
+    work plus the old committee's VSS and its checks, mpcium's two resharing
+    sessions per node), so a keygen and a reshare wave are in flight together.
+    parties: dicts with N, LambdaN, P, Q, NTildei, H1i, H2i, Alpha, Beta, p, q.
+    trace: also return one traced session per wave -- [{"session": s,
+    "digests": {(i, "dln1"|"dln2"|"mod"): d, (i, "fac", j): d}, "verified":
+    count} + for reshare waves "vss": {"old": [d_i], "new_shares": d,
+    "passed": count}]."""
     keep = []
 
     def ptr(v):
@@ -174,16 +181,22 @@ def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B
     for k, n in enumerate(parties):
         arr[k] = _Party(ptr(n["N"]), ptr(n["LambdaN"]), ptr(n["P"]), ptr(n["Q"]), ptr(n["NTildei"]), ptr(n["H1i"]),
                         ptr(n["H2i"]), ptr(n["Alpha"]), ptr(n["Beta"]), ptr(n["p"]), ptr(n["q"]))
-    st = np.zeros(len(KEYGEN_STATS), dtype=np.float64)
+    names = RESHARE_STATS if reshare else KEYGEN_STATS
+    st = np.zeros(len(names), dtype=np.float64)
     n = len(parties)
     wv = wave or 1024
     n_waves = (sessions + wv - 1) // wv
-    tw = 1 + n * (3 + (n - 1)) * 8 + 1
+    tk = 1 + n * (3 + (n - 1)) * 8 + 1
+    tw = tk + (n * 8 + 9 if reshare else 0)
     tr = np.zeros(max(1, n_waves * tw), dtype="<u4")
-    rc = lib().mpcxh_bench_keygen_proofs(W, arr, n, sessions, seed, wave, st.ctypes.data,
-                                         tr.ctypes.data if trace else None)
+    if reshare:
+        rc = lib().mpcxh_bench_keygen_reshare(W, arr, n, sessions, seed, wave, 1, st.ctypes.data,
+                                              tr.ctypes.data if trace else None)
+    else:
+        rc = lib().mpcxh_bench_keygen_proofs(W, arr, n, sessions, seed, wave, st.ctypes.data,
+                                             tr.ctypes.data if trace else None)
     _host._check(rc)
-    stats = dict(zip(KEYGEN_STATS, [float(x) for x in st]))
+    stats = dict(zip(names, [float(x) for x in st]))
     if not trace:
         return stats
     out = []
@@ -198,5 +211,11 @@ def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B
                 if j != i:
                     d[(i, "fac", j)] = words_to_ints(o[k:k + 8].reshape(1, 8))[0]
                     k += 8
-        out.append({"session": int(o[0]), "digests": d, "verified": int(o[k])})
+        t = {"session": int(o[0]), "digests": d, "verified": int(o[k])}
+        if reshare and w % 2 == 1:
+            v = o[tk:]
+            t["vss"] = {"old": [words_to_ints(v[8 * i:8 * i + 8].reshape(1, 8))[0] for i in range(n)],
+                        "new_shares": words_to_ints(v[8 * n:8 * n + 8].reshape(1, 8))[0],
+                        "passed": int(v[8 * n + 8])}
+        out.append(t)
     return stats, out

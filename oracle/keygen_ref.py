@@ -60,3 +60,53 @@ def session_digests(parties: Sequence[Dict[str, int]], seed: int, s: int, verify
             if verify:
                 passed += PR.fac_verify(fp, ss, P["N"], V["NTildei"], V["H1i"], V["H2i"])
     return out, passed
+
+
+# ---------------------------------------------------------------- resharing
+RESHARE_THRESHOLD = 2  # keygenload.hpp kReshareThreshold (3-of-5)
+
+
+def _neg(P):
+    return None if P is None else (P[0], (-P[1]) % T.SECP_P)
+
+
+def reshare_vss(n: int, seed: int, s: int, t: int = RESHARE_THRESHOLD):
+    """The old committee's VSS of one resharing session and the new committee's
+    checks of it (keygenload.cpp vss_wave; tss-lib v2.0.2 up:ecdsa/resharing as
+    recalled, "upstream, verify"): the wallet's old shares x_i = f(i + 1) of a
+    degree-t polynomial drawn from CounterDRBG(mix(seed, s, 0xEE, 0)); old party
+    i shares w_i = lambda_i x_i with coefficients a_1..a_t < q and then the hash
+    commitment's r (MustGetRandomInt(256)) from CounterDRBG(mix(seed, s, i, 9));
+    V_ik = a_k G; s_ij = f_i(j + 1). -> ([digest per old party], digest of the
+    new shares x'_j = sum_i s_ij, VSS checks passed)."""
+    q = T.SECP_N
+    wr = T.Reader(mix(seed, s, 0xEE, 0))
+    c = [T.get_random_positive_int(wr, q) for _ in range(t + 1)]
+    X = T.scalar_base_mult(c[0])
+    olds, good = [], 0
+    sumV = None
+    for i in range(n):
+        xi = sum(ck * pow(i + 1, k, q) for k, ck in enumerate(c)) % q
+        lam = 1
+        for j in range(n):
+            if j != i:
+                lam = lam * (j + 1) * pow((j - i) % q, -1, q) % q
+        rd = T.Reader(mix(seed, s, i, 9))
+        a = [lam * xi % q] + [T.get_random_positive_int(rd, q) for _ in range(t)]
+        r = T.must_get_random_int(rd, 256)
+        V = [T.scalar_base_mult(ak) for ak in a]
+        flat = [r] + [v for P in V for v in P]
+        C = T.sha512_256i(*flat)
+        sh = [sum(ak * pow(j + 1, k, q) for k, ak in enumerate(a)) % q for j in range(n)]
+        olds.append((C, V, sh))
+        sumV = T.ec_add(sumV, V[0])
+        dc = T.sha512_256i(*flat) == C
+        for j in range(n):  # s_ij G == sum_k V_ik (j + 1)^k
+            rhs = None
+            for k, Vk in enumerate(V):
+                rhs = T.ec_add(rhs, T.ec_mul(pow(j + 1, k, q), Vk))
+            good += dc and T.scalar_base_mult(sh[j]) == rhs
+    good += n * (sumV == X)
+    digs = [T.sha512_256i(C, *[v for P in V for v in P], *sh) for C, V, sh in olds]
+    xs = [sum(o[2][j] for o in olds) % q for j in range(n)]
+    return digs, T.sha512_256i(*xs), good

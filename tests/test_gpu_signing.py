@@ -166,3 +166,39 @@ def test_keygen_bench_wave_size_matches_oracle(five_parties):
         PR._pw = old
     assert t["digests"] == want, t["session"]
     assert t["verified"] == passed == n * (n - 1) * 4
+
+
+def test_keygen_reshare_mix_matches_oracle(five_parties):
+    """Config 5 with resharing as mpcium runs it (an old-party and a new-party
+    session per node per wallet): odd waves are resharing waves -- the new
+    committee's proofs plus the old committee's VSS (commitments and shares on
+    the GPU EC kernel) and the new committee's decommitment, share and
+    public-key checks. One traced session per wave vs the oracle: every proof
+    digest, and on resharing waves the VSS digests, the new shares and the
+    count of passed checks (oracle/keygen_ref.py reshare_vss)."""
+    from mpcium_amd import proofs as mproofs
+    from oracle import keygen_ref as KR
+    from oracle import proofs_ref as PR
+    lib = cc.load_c_oracle(64)
+    if lib is None:
+        pytest.skip("oracle/libgomodexp64.so not built")
+    n, sessions, wave, seed = 5, 128, 32, 0x6B6B
+    st, tr = mproofs.bench_keygen_proofs(five_parties, sessions, seed=seed, wave=wave, trace=True, reshare=True)
+    assert st["failures"] == 0 and st["vss_failures"] == 0
+    assert st["keygen_sessions"] == st["reshare_sessions"] == sessions // 2
+    assert st["vss_checks"] == st["reshare_sessions"] * (n * n + n)
+    old = PR._pw
+    PR._pw = lambda x, y, m: cc.c_expnn(lib, x % m, y, m)
+    try:
+        for w, t in enumerate(tr):
+            want, passed = KR.session_digests(five_parties, seed, t["session"])
+            assert t["digests"] == want, t["session"]
+            assert t["verified"] == passed == n * (n - 1) * 4
+            if w % 2 == 1:
+                digs, shares, good = KR.reshare_vss(n, seed, t["session"])
+                assert t["vss"] == {"old": digs, "new_shares": shares, "passed": good}
+                assert good == n * n + n
+            else:
+                assert "vss" not in t
+    finally:
+        PR._pw = old
