@@ -729,8 +729,11 @@ def keygen_line(args, world: int = 1, rank: int = 0):
     # every party's N~ and their inverses) are built on first use, as a node
     # builds them once for its peers' preparams, not per session
     wave = args.keygen_wave or 1024
-    warm = mproofs.bench_keygen_proofs(parties, min(wave, args.keygen_sessions), seed=0x6B66, wave=wave)
-    if warm["failures"]:
+    mixed = bool(args.reshare_mix)
+    # (two waves when mixed: the resharing wave's EC paths warm up too)
+    warm = mproofs.bench_keygen_proofs(parties, min(wave * (2 if mixed else 1), args.keygen_sessions), seed=0x6B66,
+                                       wave=wave, reshare=mixed)
+    if warm["failures"] or warm.get("vss_failures"):
         raise SystemExit(f"keygen proofs warmup: {warm}")
     import resource
     rss0 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
@@ -739,25 +742,46 @@ def keygen_line(args, world: int = 1, rank: int = 0):
         import torch.distributed as dist
         from mpcium_amd.shard import max_over_ranks
         dist.barrier()
-    st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67 + 7919 * rank, wave=wave)
+    st = mproofs.bench_keygen_proofs(parties, args.keygen_sessions, seed=0x6B67 + 7919 * rank, wave=wave,
+                                     reshare=mixed)
     rss1 = resource.getrusage(resource.RUSAGE_SELF).ru_maxrss
-    if st["failures"]:
+    if st["failures"] or st.get("vss_failures"):
         raise SystemExit(f"rank {rank}: keygen proofs: {st}")
     total_s = st["total_s"]
     if world > 1:
         total_s = max_over_ranks([total_s], world)[0]
+    kind = ("keygen + resharing waves alternating (resharing: the new committee's proofs + the old committee's VSS, "
+            "mpcium's two sessions per node)" if mixed else "keygen waves only")
     line = {"metric": f"{len(parties)}-party keygen/reshare sessions/s (config 5: DLN x2 + Mod + Fac proofs per party, "
-                      f"every peer verified, {args.keygen_sessions} sessions)",
+                      f"every peer verified, {args.keygen_sessions} sessions, {kind})",
             "value": st["sessions"] * world / total_s, "unit": "sessions/s", "n_gpus": world, "scaling": "weak",
+            "concurrent_sessions": min(int(st["sessions"]), 2 * wave),
+            "host_rss_gb": rss1 / 1024.0 / 1024.0,
             "sessions": int(st["sessions"]), "parties": len(parties), "proofs": int(st["proofs"]),
             "verifications": int(st["verifications"]), "seconds": st["total_s"], "prove_s": st["prove_s"],
             "verify_s": st["verify_s"], "engine_busy_s": st["engine_busy_s"],
             "waves": int(st["waves"]), "wave_sessions": int(st["wave_sessions"]), "max_wave_s": st["max_wave_s"],
             "host_max_rss_mb": rss1 / 1024.0, "host_max_rss_mb_before": rss0 / 1024.0,
             "verifications_per_s": st["verifications"] * world / total_s, "checked": "every verification passes",
+            "concurrency_note": "sessions stream in waves of wave_sessions, two waves in flight: at most "
+                                "2 x wave_sessions sessions are concurrent (measured faster than larger waves, "
+                                "DESIGN.md 6)",
             "roofline": _kernel_roofline(),
             "job_roofline": _job_roofline(st["alg_macs"], total_s, world),
             "cpu_baseline": None}
+    if mixed:
+        # each kind's sessions over the time its waves were running (the two
+        # kinds share the GPU the whole time, so each is a rate within the mix)
+        ks, rs = st["keygen_sessions"], st["reshare_sessions"]
+        line["keygen_sessions"], line["reshare_sessions"] = int(ks), int(rs)
+        line["keygen_value"] = ks * world / total_s
+        line["reshare_value"] = rs * world / total_s
+        line["keygen_wave_s_mean"] = st["keygen_wave_s"] / max(1, (st["waves"] + 1) // 2)
+        line["reshare_wave_s_mean"] = st["reshare_wave_s"] / max(1, st["waves"] // 2)
+        line["vss_checks"], line["vss_failures"] = int(st["vss_checks"]), int(st["vss_failures"])
+        line["rates_note"] = ("keygen_value / reshare_value: each kind's sessions over the whole run (the kinds' waves "
+                              "alternate and share the GPU; value = their sum); *_wave_s_mean: one wave of that kind "
+                              "(wave_sessions sessions) while the other kind's wave runs beside it")
     return line
 
 
@@ -1017,6 +1041,9 @@ def main():
     ap.add_argument("--keygen-wave", type=int, default=0,
                     help="config 5: sessions per bounded-memory wave (0: the driver's 1024)")
     ap.add_argument("--parties", type=int, default=5)
+    ap.add_argument("--reshare-mix", type=int, default=1,
+                    help="config 5: 1 -- alternate keygen and resharing waves (mpcium's old + new party sessions); "
+                         "0 -- keygen waves only")
     ap.add_argument("--paillier-inflight", type=int, default=16,
                     help="config 1: batches of 1,024 in flight from their own threads (concurrent sessions)")
     ap.add_argument("--extra-lines", type=int, default=1,
