@@ -88,6 +88,8 @@ def lib():
             raise MpcxError(2, f"{_LIB_PATH} not built: run `python -m mpcium_amd.build`")
         l = ctypes.CDLL(_LIB_PATH)
         for name, res, args in SIGNATURES:
+            if not hasattr(l, name):  # an older build in an A/B run: its missing entries stay unbound
+                continue
             f = getattr(l, name)
             f.restype = res
             f.argtypes = args

@@ -38,6 +38,8 @@ def lib():
     l = _host.lib()
     if not _bound:
         for name, res, args in SIGNATURES:
+            if not hasattr(l, name):  # an older build in an A/B run: its missing entries stay unbound
+                continue
             f = getattr(l, name)
             f.restype, f.argtypes = res, args
         _bound = True
