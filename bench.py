@@ -532,7 +532,8 @@ def safeprime_line(num: int, seed: int, cpu: bool, info: dict, world: int = 1, r
 
         dist.barrier()
         t0 = time.perf_counter()
-        res = safe_primes_sharded(num, rank, world, fn)
+        sp_stats = {}
+        res = safe_primes_sharded(num, rank, world, fn, stats=sp_stats)
         el = time.perf_counter() - t0
         el = max_over_ranks([el], world)[0]
         import torch
@@ -556,6 +557,8 @@ def safeprime_line(num: int, seed: int, cpu: bool, info: dict, world: int = 1, r
             "n_gpus": world, "scaling": "strong", "first_index": res[0][2], "last_index": res[-1][2],
             "roofline": _job_roofline((st["fermat_tests"] + st["mr_tests"]) * alg_macs(1024, 1023) / world, el, world),
             "cpu_baseline": None}
+    if world > 1:
+        line["sharded_gathers"] = sp_stats  # one all-gather per group of rounds (shard.safe_primes_sharded)
     if world == 1:
         # the dominant kernel's own roofline: k_prime2c's Go-equivalent work
         # (2^(p-1) mod p per sieve survivor, 2^d mod q per ride-along q) over
@@ -1005,6 +1008,175 @@ def compact_line(result: dict, detail_path: str | None) -> dict:
     return line
 
 
+def node_main(args, progress) -> None:
+    """--node: mpcium's deployment shape -- ONE process per node drives every
+    GPU of the node (/root/reference/cmd/mpcium/main.go:150,
+    /root/reference/pkg/mpc/node.go:59-88: one preparams set shared by every
+    wallet session of the node). libmpcx binds the devices with
+    mpcx_init_devices; config 2 runs one resident batch per device, launched
+    from this one process onto each device's stream; configs 4 and 5 run
+    through the one Engine (libmpcx_host), whose batches spread over the
+    devices (split batches above device_split_min, round-robin otherwise).
+    Work per device is fixed (weak scaling): wallets and sessions scale with
+    the device count. --node-dup K rehearses K logical devices on one HIP
+    ordinal (mpcx_set_option "duplicate_device"): the node path end to end on a
+    one-GPU box, NOT a scaling measurement (the logical devices share one GPU).
+    Prints one JSON line (mode "node")."""
+    import torch
+    from mpcium_amd import host as mhost
+    from mpcium_amd import mpcx, mta, proofs as mproofs
+    if args.node_dup:
+        mpcx.set_option("duplicate_device", 1)
+        for _ in range(args.node_dup):
+            mhost.init(0)
+    else:
+        mhost.init_devices(args.node_devices)
+    devs = mpcx.bound_devices()
+    D = len(devs)
+    progress(f"node: {D} bound devices {devs}")
+    N = load_key()
+    N2 = N * N
+    mod = mpcx.Modulus(N2)
+    words, count = mod.words, args.count
+    exp = mpcx.int_to_words(N, mpcx.nwords(N))
+    L = mpcx.lib()
+    per = []
+    for d, ordinal in enumerate(devs):
+        dev = torch.device("cuda", ordinal)
+        bases = synth_bases(N2, count, 0x6D706332 + d, words)
+        per.append({"d": d, "dev": dev, "bases": bases, "st": torch.cuda.Stream(dev),
+                    "b": torch.from_numpy(bases.view(np.int32)).to(dev),
+                    "e": torch.from_numpy(exp.view(np.int32)).to(dev),
+                    "o": torch.zeros((count, words), dtype=torch.int32, device=dev)})
+
+    def launch(p):
+        mpcx.select_device(p["d"])
+        with torch.cuda.device(p["dev"]):
+            rc = L.mpcx_modexp_batch_device(mod.handle, count, p["b"].data_ptr(), words, p["e"].data_ptr(),
+                                            len(exp), 1, N.bit_length(), p["o"].data_ptr(), words,
+                                            p["st"].cuda_stream)
+        if rc != 0:
+            raise mpcx.MpcxError(rc, L.mpcx_last_error().decode())
+
+    def sync_all():
+        for p in per:
+            p["st"].synchronize()
+
+    progress("node: config 2 warm-up")
+    for _ in range(args.warmup):
+        for p in per:
+            launch(p)
+    sync_all()
+    l0 = [mpcx.device_launches(d) for d in range(D)]
+    for p in per:
+        p["ev"] = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+    t0 = time.perf_counter()
+    for p in per:
+        p["ev"][0].record(p["st"])
+    for _ in range(args.steps):  # every device's launches queued from this one thread
+        for p in per:
+            launch(p)
+    for p in per:
+        p["ev"][1].record(p["st"])
+    sync_all()
+    el = time.perf_counter() - t0
+    kms = [p["ev"][0].elapsed_time(p["ev"][1]) / max(1, args.steps) for p in per]
+    launches = [mpcx.device_launches(d) - l0[d] for d in range(D)]
+    bad = []
+    for p in per:  # untimed: sampled outputs of every device against pow()
+        out = p["o"].cpu().numpy().view(np.uint32)
+        idx = np.linspace(0, count - 1, max(2, args.verify)).astype(int)
+        xs, zs = mpcx.words_to_ints(p["bases"][idx]), mpcx.words_to_ints(out[idx])
+        bad += [(p["d"], int(i)) for i, x, z in zip(idx, xs, zs) if pow(x, N, N2) != z]
+    if bad:
+        raise SystemExit(f"node: config-2 results differ from pow() at {bad[:5]}")
+    digest = None
+    gd_path = os.path.join(ROOT, "tests", "golden", "batch_digest.json")
+    if os.path.exists(gd_path):
+        gd = json.load(open(gd_path))
+        if gd["count"] == count and gd["words"] == words and args.steps + args.warmup > 0:
+            import hashlib
+            got = hashlib.sha256(per[0]["o"].cpu().numpy().astype("<u4").tobytes()).hexdigest()
+            digest = {"match": got == gd["sha256"], "scope": "device 0's batch vs the C restatement"}
+            if not digest["match"]:
+                raise SystemExit("node: device 0 batch digest differs from the C restatement")
+    W = alg_macs(N2.bit_length(), N.bit_length())
+    result = {"metric": METRIC, "mode": "node", "value": count * D * args.steps / el, "unit": "modexp/s",
+              "n_gpus": D, "steps": args.steps, "warmup": args.warmup, "ms_per_step": el / max(1, args.steps) * 1e3,
+              "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "u32",
+              "data": "synthetic (seeded bases < N^2 per device; N = tests/golden/paillier_key_2048.json)",
+              "config": {"workload": "config2: x^N mod N^2, 4096-bit modulus, shared 2048-bit exponent y=N",
+                         "operands_per_gpu": count, "parallelism": f"node process x {D} devices (no collective)",
+                         "devices": devs, "duplicated_ordinal_rehearsal": bool(args.node_dup)},
+              "roofline": {"bound": "valu", "unit": "TOP/s", "peak": PEAK_INT32_NOMINAL / 1e12,
+                           "achieved": W * count / (max(kms) * 1e-3) / 1e12,
+                           "frac": W * count / (max(kms) * 1e-3) / PEAK_INT32_NOMINAL, "traffic": None,
+                           "kernel_ms_per_device": kms},
+              "device_launches": {"config2": launches}, "cpu_baseline": None}
+    if digest:
+        result["batch_digest"] = digest
+    nodes = load_nodes()
+    if args.wallets > 0:
+        progress(f"node: config 4 signing, {args.wallets * D} wallets over {D} devices")
+        wl = args.wallets * D
+        warm = mta.bench_signing(nodes, args.signers, wl, seed=0x5167)
+        if warm["errors"] or warm["verified"] != wl:
+            raise SystemExit(f"node: signing warm-up failed: {warm}")
+        l1 = [mpcx.device_launches(d) for d in range(D)]
+        _kernel_stats_reset()
+        t1 = time.perf_counter()
+        st = mta.bench_signing(nodes, args.signers, wl, seed=0x5168)
+        e1 = time.perf_counter() - t1
+        if st["errors"] or st["relation_failures"] or st["verified"] != wl or st["aborted"]:
+            raise SystemExit(f"node: signing failed: {st}")
+        result["signing"] = {"value": wl / e1, "unit": "sigs/s", "n_gpus": D, "wallets": wl, "seconds": e1,
+                             "signatures_verified": int(st["verified"]),
+                             "device_launches": [mpcx.device_launches(d) - l1[d] for d in range(D)],
+                             "roofline": _kernel_roofline(D)}
+    if args.keygen_sessions > 0:
+        parties = nodes
+        for seed in (0x6D706335, 0x6D706336)[:max(0, args.parties - len(parties))]:
+            pp, _ = mhost.generate_preparams(seed=seed)
+            parties.append(pp)
+        parties = parties[:args.parties]
+        ks = args.keygen_sessions * D
+        wave = args.keygen_wave or 1024
+        progress(f"node: config 5, {ks} keygen/reshare sessions over {D} devices")
+        mixed = bool(args.reshare_mix)
+        warm = mproofs.bench_keygen_proofs(parties, min(ks, wave * 2), seed=0x6B66, wave=wave, reshare=mixed)
+        if warm["failures"] or warm.get("vss_failures"):
+            raise SystemExit(f"node: keygen warm-up failed: {warm}")
+        l2 = [mpcx.device_launches(d) for d in range(D)]
+        _kernel_stats_reset()
+        st = mproofs.bench_keygen_proofs(parties, ks, seed=0x6B67, wave=wave, reshare=mixed)
+        if st["failures"] or st.get("vss_failures"):
+            raise SystemExit(f"node: keygen failed: {st}")
+        result["keygen"] = {"value": st["sessions"] / st["total_s"], "unit": "sessions/s", "n_gpus": D,
+                            "sessions": int(st["sessions"]), "seconds": st["total_s"],
+                            "reshare_sessions": int(st.get("reshare_sessions", 0)),
+                            "device_launches": [mpcx.device_launches(d) - l2[d] for d in range(D)],
+                            "roofline": _kernel_roofline(D)}
+    progress("node: done")
+    detail = os.path.abspath(args.detail)
+    os.makedirs(os.path.dirname(detail), exist_ok=True)
+    with open(detail, "w") as f:
+        json.dump(result, f, indent=1)
+    line = {k: result[k] for k in ("metric", "mode", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
+                                   "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
+    line["roofline"] = {k: _r(v) if isinstance(v, float) else v for k, v in result["roofline"].items()
+                        if k != "kernel_ms_per_device"}
+    line["cpu_baseline"] = None
+    line["device_launches"] = result["device_launches"]["config2"]
+    if digest:
+        line["digest_match"] = digest["match"]
+    for k, dst in (("signing", "c4_sign"), ("keygen", "c5_keygen")):
+        if k in result:
+            line.setdefault("configs", {})[dst] = {"value": _r(result[k]["value"]), "unit": result[k]["unit"],
+                                                   "n_gpus": D, "device_launches": result[k]["device_launches"]}
+    line["detail"] = os.path.relpath(detail, ROOT)
+    print(json.dumps(line), flush=True)
+
+
 def relaunch_under_torchrun(args, argv) -> int:
     """--gpus N > 1 without a launcher: start torchrun with N local ranks as a
     CHILD process (nothing in this process has touched the GPU yet) and return
@@ -1056,7 +1228,21 @@ def main():
     ap.add_argument("--detail", default=os.path.join("gpurun_out", "bench_detail.json"),
                     help="file for the full result (per-step times, telemetry, per-kernel lists, samples); "
                          "the printed line names it")
+    ap.add_argument("--node", action="store_true",
+                    help="one process drives every GPU of the node (mpcium's shape; see node_main)")
+    ap.add_argument("--node-devices", type=int, default=0, help="--node: GPUs to bind (0: all visible)")
+    ap.add_argument("--node-dup", type=int, default=0,
+                    help="--node rehearsal: bind HIP ordinal 0 this many times as logical devices")
     args = ap.parse_args()
+    if args.node:
+        if int(os.environ.get("WORLD_SIZE", "1")) != 1:
+            sys.exit("bench.py --node: one process per node (not under torchrun)")
+        t_node = time.time()
+
+        def progress_node(msg):
+            print(f"[bench {time.time() - t_node:7.1f} s] {msg}", file=sys.stderr, flush=True)
+        node_main(args, progress_node)
+        return
     if "WORLD_SIZE" not in os.environ and args.gpus > 1:
         sys.exit(relaunch_under_torchrun(args, sys.argv[1:]))
     if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:

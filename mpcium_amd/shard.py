@@ -50,30 +50,46 @@ def max_over_ranks(values: Sequence[float], world: int) -> List[float]:
 
 
 def safe_primes_sharded(num: int, rank: int, world: int, batch_fn: Callable[[int], List[Tuple[int, int, int]]],
-                        max_rounds: int = 1 << 20):
+                        max_rounds: int = 1 << 20, gather_every: int = 4, stats: dict | None = None):
     """Config-3 safe-prime search sharded over `world` GPUs:
     rank g tests stream batches b = r*world + g in round r (batch_fn(b) ->
-    [(p, q, stream index)] accepted in batch b, e.g. host.safe_prime_batch), and
-    after each round every rank all-gathers the (tiny) lists of accepted primes.
-    Once `num` are known, every batch below the round's end has been tested by
-    some rank, so the `num` smallest stream indices are exactly what a
-    single-GPU, stream-order search returns (tss-lib at concurrency 1). The only
-    exchange is that host-side gather of a few integers per round; no
-    collective touches the candidate data. Returns the same list on every rank."""
+    [(p, q, stream index)] accepted in batch b, e.g. host.safe_prime_batch).
+    The ranks exchange their (tiny) lists of accepted primes with ONE
+    all-gather per group of R rounds (round 4: one per round, an 8-rank host
+    sync per batch): R starts at 1 and then covers the rounds the observed
+    acceptance rate says are still needed, capped at `gather_every`. Once
+    `num` are known after a gather, every batch below that group's end has
+    been tested by some rank, so the `num` smallest stream indices are exactly
+    what a single-GPU, stream-order search returns (tss-lib at concurrency 1).
+    The only exchange is that host-side gather of a few integers; no
+    collective touches the candidate data. Returns the same list on every
+    rank; stats (optional dict) receives "rounds" and "gathers"."""
     if world <= 0 or not 0 <= rank < world:
         raise ValueError("bad rank/world")
     found: List[Tuple[int, int, int]] = []
-    for r in range(max_rounds):
-        mine = list(batch_fn(r * world + rank))
+    r, gathers, R = 0, 0, 1
+    while r < max_rounds:
+        mine: List[Tuple[int, int, int]] = []
+        for k in range(min(R, max_rounds - r)):
+            mine.extend(batch_fn((r + k) * world + rank))
+        r += min(R, max_rounds - r)
         if world == 1:
             parts = [mine]
         else:
             import torch.distributed as dist
             parts = [None] * world
             dist.all_gather_object(parts, mine)
+        gathers += 1
         for p in parts:
             found.extend(p)
         if len(found) >= num:
             found.sort(key=lambda t: t[2])
+            if stats is not None:
+                stats.update(rounds=r, gathers=gathers)
             return found[:num]
+        # every rank sees the same `found` and `r`: the same next R everywhere
+        per_round = len(found) / r
+        need = num - len(found)
+        R = max(1, min(gather_every, -(-need // per_round) if per_round > 0 else gather_every))
+        R = int(R)
     raise RuntimeError("safe prime search exhausted max_rounds")

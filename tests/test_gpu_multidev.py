@@ -205,3 +205,37 @@ def test_bench_two_ranks(gpu, tmp_path):
     full = json.load(open(detail))
     assert full["signing"]["signatures_verified"] == 600
     assert full["keygen"]["sessions"] == 64
+
+
+def test_bench_node_mode(gpu, tmp_path):
+    """`bench.py --node`: mpcium's one-process-per-node shape
+    (/root/reference/pkg/mpc/node.go:59-88) -- one process binds the node's
+    devices (here one HIP ordinal bound twice, the rehearsal hook) and runs
+    config 2 (one resident batch per device, device 0's whole batch checked
+    against the C restatement's digest, every device sampled against pow),
+    config 4 and config 5 through the one Engine: every device receives
+    launches in every config, and one parseable line reports mode "node"."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    detail = tmp_path / "node.json"
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--node", "--node-dup", "2", "--steps", "1",
+           "--warmup", "1", "--count", "65536", "--wallets", "300", "--keygen-sessions", "64", "--keygen-wave", "32",
+           "--detail", str(detail)]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=900, cwd=root)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [x for x in r.stdout.splitlines() if x.strip()]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["mode"] == "node" and line["n_gpus"] == 2 and line["value"] > 0
+    assert line["digest_match"] is True
+    assert all(n > 0 for n in line["device_launches"]), line["device_launches"]
+    for k in ("c4_sign", "c5_keygen"):
+        assert line["configs"][k]["value"] > 0
+        assert all(n > 0 for n in line["configs"][k]["device_launches"]), (k, line["configs"][k])
+    full = json.load(open(detail))
+    assert full["signing"]["signatures_verified"] == 600
+    assert full["keygen"]["sessions"] == 128 and full["keygen"]["reshare_sessions"] > 0

@@ -74,7 +74,9 @@ def _sp_worker(rank, world, port, q):
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     out = safe_primes_sharded(7, rank, world, _fake_batch)
-    q.put((rank, out))
+    st = {}
+    big = safe_primes_sharded(40, rank, world, _fake_batch, stats=st)
+    q.put((rank, (out, big, st)))
     dist.barrier()
     dist.destroy_process_group()
 
@@ -93,4 +95,11 @@ def test_safe_primes_sharded_world2_matches_stream_order():
     res = dict(q.get(timeout=100) for _ in range(2))
     for p in procs:
         p.join(timeout=60)
-    assert res[0] == single and res[1] == single
+    st1 = {}
+    big1 = safe_primes_sharded(40, 0, 1, _fake_batch, stats=st1)
+    for r in (0, 1):
+        out, big, st = res[r]
+        assert out == single
+        # batched gathers (one per group of rounds): the same stream-order result
+        assert big == big1 and [t[2] for t in big] == sorted(t[2] for t in big) and len(big) == 40
+        assert st["gathers"] < st["rounds"], st
