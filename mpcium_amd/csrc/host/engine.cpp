@@ -349,6 +349,16 @@ FixedCoalescer& fixed_coalescer(uint32_t class_words) {
 
 // MPCX_COALESCE = max coalesced dispatches in flight per bound device (0: off,
 // each exp() call is its own launch); default kCoalesceInflight
+// MPCX_COALESCE_MAXOPS: operands per merged launch (A/B runs); default kCoalesceMaxOps
+uint64_t coalesce_max_ops() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("MPCX_COALESCE_MAXOPS");
+    const long long x = e ? std::atoll(e) : 0;
+    return x > 0 ? (uint64_t)x : kCoalesceMaxOps;
+  }();
+  return v;
+}
+
 int coalesce_inflight() {
   static const int v = [] {
     const char* e = std::getenv("MPCX_COALESCE");
@@ -472,7 +482,7 @@ void Engine::exp_into(const Nat& m, size_t n, const Nat* const* bases, const Nat
       r.g.mul_words = muls ? md.class_words : 0;
       r.g.out = out.p;
       r.g.out_words = md.words;
-      rc = coalescer(md.class_words).run(r, inflight, kCoalesceMaxOps);
+      rc = coalescer(md.class_words).run(r, inflight, coalesce_max_ops());
       if (rc) {
         leave_call();
         throw EngineError(rc, "mpcx_modexp_multi_batch: " + r.err);
@@ -604,7 +614,7 @@ void Engine::fixed_multi_into(const Nat& m, size_t nb, const Nat* const* bases, 
       r.g.mul_words = muls ? md.class_words : 0;
       r.g.out = out.p;
       r.g.out_words = md.words;
-      rc = fixed_coalescer(md.class_words).run(r, inflight, kCoalesceMaxOps);
+      rc = fixed_coalescer(md.class_words).run(r, inflight, coalesce_max_ops());
       if (rc) {
         leave_call();
         throw EngineError(rc, "mpcx_fixedbase_multi_batch: " + r.err);

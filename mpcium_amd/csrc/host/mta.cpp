@@ -659,8 +659,10 @@ namespace {
 // f and g on two threads; rethrows the first failure
 void both(const std::function<void()>& f, const std::function<void()>& g) {
   std::exception_ptr ef, eg;
-  std::thread t([&] {
+  const int chain = prof::chain();
+  std::thread t([&, chain] {
     MPCX_PROF_CPU("cpu.mta_halves");
+    prof::set_chain(chain);
     try {
       g();
     } catch (...) {

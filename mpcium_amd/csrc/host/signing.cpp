@@ -687,8 +687,15 @@ MtaStats RunSigning(const std::vector<NodeKeys>& nodes, int signers, size_t wall
   {
     std::atomic<size_t> next{0};
     std::vector<std::function<void()>> workers;
+    // MPCX_SIGN_STAGGER_MS: worker t starts t x this many ms late (A/B runs:
+    // desynchronizes the pipelines' host and GPU phases)
+    static const int stagger_ms = [] {
+      const char* e = std::getenv("MPCX_SIGN_STAGGER_MS");
+      return e ? std::max(0, std::atoi(e)) : 0;
+    }();
     for (size_t t = 0; t < n_workers; ++t)
-      workers.push_back([&] {
+      workers.push_back([&, t] {
+        if (stagger_ms && t) std::this_thread::sleep_for(std::chrono::milliseconds(stagger_ms * (int)t));
         for (;;) {
           const size_t c = next.fetch_add(1);
           if (c >= n_chunks) return;
