@@ -40,7 +40,7 @@ PEAK_MAD_MEASURED = 33.8e12            # tools/microbench/valu_rates.hip, 8 wave
 
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r04", "pmc", "config2_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc", "config2_traffic.json")
 
 
 def pmc_traffic(count: int, modbits: int, mod) -> dict:
@@ -51,14 +51,16 @@ def pmc_traffic(count: int, modbits: int, mod) -> dict:
     measured (65,536 operands, 4096-bit modulus, 4x37 quad geometry); null
     otherwise. The algorithmic I/O is 1 KB per operand (base in, result out).
     Most FETCH bytes are window-table re-reads that miss the per-XCD L2
-    (DESIGN.md 5.4); they are served by the MALL, not by HBM."""
+    (DESIGN.md 5.4); the memory-side counters include Infinity-Cache hits, so
+    this is an upper bound on HBM bytes."""
     out = {"traffic": None, "traffic_unit": "bytes/launch", "algorithmic_io_bytes": count * 2 * modbits // 8}
     if count != 65536 or modbits != 4096 or (mod.P, mod.K) != (4, 37) or not os.path.exists(PMC_TRAFFIC):
         return out
     with open(PMC_TRAFFIC) as f:
         s = json.load(f)
     out["traffic"] = s["hbm_bytes_per_launch"]
-    out["traffic_source"] = os.path.relpath(PMC_TRAFFIC, ROOT) + " (FETCH_SIZE+WRITE_SIZE KB x 1024, uncorrected)"
+    out["traffic_source"] = (os.path.relpath(PMC_TRAFFIC, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE: the counters' "
+                             "calibration on this access width, tools/microbench/fetch_calib.hip)")
     return out
 
 # GPU clock / power / temperature sampler: a separate process (started before
