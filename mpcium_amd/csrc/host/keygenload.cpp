@@ -411,10 +411,15 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
 
   Engine::get().reset_busy();
   const double t0 = now();
-  {  // kWavesInFlight workers take the waves in order
+  {  // kWavesInFlight workers take the waves in order (MPCX_KEYGEN_WAVES: A/B runs)
+    static const size_t in_flight = [] {
+      const char* e = std::getenv("MPCX_KEYGEN_WAVES");
+      const int v = e ? std::atoi(e) : 0;
+      return v > 0 ? (size_t)v : kWavesInFlight;
+    }();
     std::atomic<size_t> next{0};
     std::vector<std::function<void()>> workers;
-    for (size_t k = 0; k < std::min(kWavesInFlight, n_waves); ++k)
+    for (size_t k = 0; k < std::min(in_flight, n_waves); ++k)
       workers.push_back([&] {
         for (;;) {
           const size_t w = next.fetch_add(1);
