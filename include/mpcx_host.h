@@ -296,11 +296,13 @@ int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t
  * wave wall times per kind), vss_checks, vss_failures.
  * trace_out: per wave the keygen trace words, then n*8 + 9 VSS words (per old
  * party the 8-word digest of its commitment, points and shares; the digest of
- * the new shares; the count of VSS checks that passed; zero on keygen waves). */
+ * the new shares; the count of VSS checks that passed; zero on keygen waves).
+ * tamper_session >= 0 (test hook; -1: none): in that resharing session old party
+ * 0 sends new party 1 a share off by one, so exactly one VSS check fails. */
 #define MPCXH_KEYGEN_RESHARE_STATS 19
 int mpcxh_bench_keygen_reshare(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
-                               uint64_t seed, uint32_t wave_sessions, int reshare_mix, double* stats_out,
-                               uint32_t* trace_out);
+                               uint64_t seed, uint32_t wave_sessions, int reshare_mix, int64_t tamper_session,
+                               double* stats_out, uint32_t* trace_out);
 
 /* Host-side helpers of the MtA path, exported as test hooks (no GPU needed):
  * common.SHA512_256i / SHA512_256i_TAGGED (tag == NULL: untagged) over count

@@ -789,7 +789,8 @@ int mpcxh_fac_verify_batch(uint32_t w, const uint8_t* sessions, uint32_t session
 
 namespace {
 keygenload::ProofStats bench_config5(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
-                                     uint64_t seed, uint32_t wave_sessions, int mix, uint32_t* trace_out) {
+                                     uint64_t seed, uint32_t wave_sessions, int mix, uint32_t* trace_out,
+                                     int64_t tamper = -1) {
   if (w < 64) throw std::invalid_argument("party integer width must be >= 64 words");
   if (!parties) throw std::invalid_argument("null argument");
   std::vector<keygenload::PartyKeys> ps(n_parties);
@@ -807,7 +808,7 @@ keygenload::ProofStats bench_config5(uint32_t w, const mpcxh_party_t* parties, u
     ps[i].q = Nat::from_words(a.q, w);
   }
   std::vector<uint32_t> tr;
-  const auto st = keygenload::RunKeygenProofs(ps, sessions, seed, wave_sessions, trace_out ? &tr : nullptr, mix);
+  const auto st = keygenload::RunKeygenProofs(ps, sessions, seed, wave_sessions, trace_out ? &tr : nullptr, mix, tamper);
   if (trace_out) std::memcpy(trace_out, tr.data(), tr.size() * sizeof(uint32_t));
   return st;
 }
@@ -833,12 +834,13 @@ int mpcxh_bench_keygen_proofs(uint32_t w, const mpcxh_party_t* parties, uint32_t
 }
 
 int mpcxh_bench_keygen_reshare(uint32_t w, const mpcxh_party_t* parties, uint32_t n_parties, uint32_t sessions,
-                               uint64_t seed, uint32_t wave_sessions, int reshare_mix, double* stats_out,
-                               uint32_t* trace_out) {
+                               uint64_t seed, uint32_t wave_sessions, int reshare_mix, int64_t tamper_session,
+                               double* stats_out, uint32_t* trace_out) {
   return guard([&] {
     if (!stats_out) throw std::invalid_argument("null argument");
     if (reshare_mix != 0 && reshare_mix != 1) throw std::invalid_argument("reshare_mix: 0 or 1");
-    const auto st = bench_config5(w, parties, n_parties, sessions, seed, wave_sessions, reshare_mix, trace_out);
+    const auto st =
+        bench_config5(w, parties, n_parties, sessions, seed, wave_sessions, reshare_mix, trace_out, tamper_session);
     keygen_stats(st, stats_out);
   });
 }

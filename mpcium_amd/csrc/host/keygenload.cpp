@@ -99,7 +99,7 @@ secp::Affine negate(const secp::Affine& P) {
 // the new committee's checks of it: two GPU EC batches (k_ec_combine) plus
 // host hashing. vt: the traced session's TraceVssWords(n) words (or null).
 void vss_wave(size_t lo, size_t hi, size_t n, uint64_t seed, size_t ts, uint32_t* vt, std::atomic<uint64_t>& checks,
-              std::atomic<uint64_t>& fails) {
+              std::atomic<uint64_t>& fails, int64_t tamper) {
   MPCX_PROF("keygen.vss");
   constexpr size_t T = kReshareThreshold;
   static_assert(T == 2, "the share check is one a*G + b*P + c*Q combination");
@@ -176,6 +176,10 @@ void vss_wave(size_t lo, size_t hi, size_t n, uint64_t seed, size_t ts, uint32_t
       o.C = SHA512_256i(in);  // commitments.NewHashCommitment(rand, flatVs...)
     }
   });
+  if (tamper >= (int64_t)lo && tamper < (int64_t)hi && n > 1) {  // old party 0 -> new party 1, off by one
+    Nat& sh = od[(size_t)tamper - lo][0].sh[1];
+    sh = (sh + Nat(1)) % q;
+  }
   // EC batch 2: new party j's share check of old party i:
   // (q - s_ij) G + j V_i1 + j^2 V_i2 == -V_i0
   std::vector<secp::Comb> c2(m * n * n);
@@ -254,7 +258,7 @@ void vss_wave(size_t lo, size_t hi, size_t n, uint64_t seed, size_t ts, uint32_t
 }  // namespace
 
 ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t sessions, uint64_t seed,
-                           size_t wave_sessions, std::vector<uint32_t>* trace, int reshare_mix) {
+                           size_t wave_sessions, std::vector<uint32_t>* trace, int reshare_mix, int64_t tamper_session) {
   const size_t n = parties.size();
   if (n < 2) throw std::invalid_argument("need at least two parties");
   const size_t W = wave_sessions ? wave_sessions : kDefaultWave;
@@ -371,7 +375,7 @@ ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t session
     if (reshare)  // the old committee's VSS beside the new committee's proof chains
       tasks.push_back([&, lo, hi] {
         vss_wave(lo, hi, n, seed, TracedSession(w, lo, hi), trace ? trace->data() + w * tw + tk : nullptr, vss_checks,
-                 vss_fails);
+                 vss_fails, tamper_session);
       });
     // every proof chain of the wave at once (35 for 5 parties): their small
     // per-pair batches meet in the coalescers; 8 at a time measured 5% slower

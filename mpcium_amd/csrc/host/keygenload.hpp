@@ -98,7 +98,10 @@ inline size_t TracedSession(size_t wave, size_t lo, size_t hi) { return lo + (wa
 // waves in flight are one of each kind (config 5: "reshare + keygen under
 // load"). Trace: TraceSessionWords(n) + (reshare_mix ? TraceVssWords(n) : 0)
 // words per wave (the VSS words zero on keygen waves).
+// tamper_session >= 0 (test hook): in that resharing session old party 0 sends
+// new party 1 a share off by one -- exactly one VSS check fails, nothing else.
 ProofStats RunKeygenProofs(const std::vector<PartyKeys>& parties, size_t sessions, uint64_t seed,
-                           size_t wave_sessions = 0, std::vector<uint32_t>* trace = nullptr, int reshare_mix = 0);
+                           size_t wave_sessions = 0, std::vector<uint32_t>* trace = nullptr, int reshare_mix = 0,
+                           int64_t tamper_session = -1);
 
 }  // namespace mpcx::host::keygenload

@@ -28,7 +28,7 @@ SIGNATURES = [
     ("mpcxh_fac_prove_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("mpcxh_fac_verify_batch", _i, [_u32, _vp, _u32, _vp, _vp, _vp, _vp, _u32, _vp, _vp, _vp]),
     ("mpcxh_bench_keygen_proofs", _i, [_u32, _vp, _u32, _u32, _u64, _u32, _vp, _vp]),
-    ("mpcxh_bench_keygen_reshare", _i, [_u32, _vp, _u32, _u32, _u64, _u32, _i, _vp, _vp]),
+    ("mpcxh_bench_keygen_reshare", _i, [_u32, _vp, _u32, _u32, _u64, _u32, _i, ctypes.c_int64, _vp, _vp]),
 ]
 _bound = False
 
@@ -160,7 +160,7 @@ RESHARE_STATS = KEYGEN_STATS + ["keygen_sessions", "reshare_sessions", "keygen_w
 
 
 def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B67, wave: int = 0,
-                        trace: bool = False, reshare: bool = False):
+                        trace: bool = False, reshare: bool = False, tamper_session: int = -1):
     """Config-5 driver (csrc/host/keygenload.hpp): the DLN / Mod / Fac proof
     work of `sessions` keygen sessions of len(parties) nodes, streamed in waves
     of `wave` sessions (0: the driver's default, 1024), two waves in flight;
@@ -192,7 +192,7 @@ def bench_keygen_proofs(parties: Sequence[dict], sessions: int, seed: int = 0x6B
     tw = tk + (n * 8 + 9 if reshare else 0)
     tr = np.zeros(max(1, n_waves * tw), dtype="<u4")
     if reshare:
-        rc = lib().mpcxh_bench_keygen_reshare(W, arr, n, sessions, seed, wave, 1, st.ctypes.data,
+        rc = lib().mpcxh_bench_keygen_reshare(W, arr, n, sessions, seed, wave, 1, tamper_session, st.ctypes.data,
                                               tr.ctypes.data if trace else None)
     else:
         rc = lib().mpcxh_bench_keygen_proofs(W, arr, n, sessions, seed, wave, st.ctypes.data,

@@ -202,3 +202,19 @@ def test_keygen_reshare_mix_matches_oracle(five_parties):
                 assert "vss" not in t
     finally:
         PR._pw = old
+
+
+def test_reshare_tampered_share_fails_only_its_check(five_parties):
+    """A resharing session where old party 0 sends new party 1 a share off by
+    one: exactly that one VSS check fails (s_01 G != sum_k V_0k 2^k), every
+    other check of every session and every proof still passes, and the traced
+    session of that wave reports one check fewer."""
+    from mpcium_amd import proofs as mproofs
+    n, sessions, wave, seed = 5, 64, 32, 0x6B6C
+    tr_session = 32 + (1 * 7919) % 32  # wave 1 (a resharing wave): its traced session
+    st, tr = mproofs.bench_keygen_proofs(five_parties, sessions, seed=seed, wave=wave, trace=True, reshare=True,
+                                         tamper_session=tr_session)
+    assert st["failures"] == 0
+    assert st["vss_failures"] == 1
+    assert st["vss_checks"] == st["reshare_sessions"] * (n * n + n)
+    assert tr[1]["session"] == tr_session and tr[1]["vss"]["passed"] == n * n + n - 1
