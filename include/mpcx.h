@@ -393,6 +393,9 @@ int mpcx_sync(void* stream);
  *                launch within 4 wavefronts per SIMD (round 5, three interleaved
  *                rounds vs 1: keygen/reshare 437.6 vs 419.7 sessions/s, signing
  *                7,110 vs 6,874 and 3,225 vs 3,039 sigs/s, profiles/r05/fbsplit).
+ *   "mx"         0 or 1: batches of the 4096-bit main geometry (>= "mx_min"
+ *                operands, default 2048) run k_modexp_mx, the Montgomery
+ *                reduction on the i8 matrix cores (environment: MPCX_MX).
  *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
  *                thread per candidate.
  *   "lanes"      1..8 (default 6, or MPCX_LANES): execution lanes (streams
@@ -415,6 +418,13 @@ int mpcx_sync(void* stream);
  * default 6: execution lanes per device), MPCX_GEOM_POLICY, MPCX_NARROW_ROUNDS,
  * MPCX_PRIME_COOP, MPCX_FB_WINDOW. */
 int mpcx_set_option(const char* key, int value);
+
+/* The constant tables of k_modexp_mx (the 4096-bit main geometry with its
+ * Montgomery reduction on the i8 matrix cores, mpcium_amd/csrc/mpcx_mx.hpp) for
+ * the odd modulus m (<= 4096 bits): the Toeplitz fragments of m'' = -m^-1 mod
+ * 2^4144, then of m, 37 + 41 KiB. Host-only (no device needed); for tests and
+ * tools. */
+int mpcx_mx_tables(const uint32_t* m_words, uint32_t m_len, uint8_t* out, size_t cap);
 
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):
  * digits L (radix 2^28), lanes per operand P, digits per lane K, operands per

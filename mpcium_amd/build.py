@@ -18,7 +18,7 @@ ARCH = "gfx950"
 
 NUM_GEOMS = 7  # kernel geometries (mpcx_internal.h), one translation unit each
 HIP_FLAGS = ["-O3", "-std=c++17", "-fPIC", "-Wall", "-Wno-unused-result"]
-KERNEL_HDRS = ["mpcx_device.hpp", "mpcx_internal.h"]
+KERNEL_HDRS = ["mpcx_device.hpp", "mpcx_mx.hpp", "mpcx_internal.h"]
 HOST_SRCS = ["host/bignum.cpp", "host/engine.cpp", "host/modint.cpp", "host/paillier.cpp", "host/safeprime.cpp",
              "host/tsscommon.cpp", "host/secp256k1.cpp", "host/mta.cpp", "host/proofs.cpp", "host/signing.cpp", "host/keygenload.cpp",
              "host/hostprof.cpp", "host/gorand.cpp", "host/capi.cpp"]

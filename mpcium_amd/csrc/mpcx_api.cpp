@@ -84,6 +84,9 @@ struct mpcx_modulus_s {
   std::vector<uint32_t> host_const;  // per geometry of the class: 3*L_g digits N, R mod N, R^2 mod N
   std::mutex mu;                     // guards the lazy per-device uploads
   uint32_t* d_const[kMaxDevices] = {};
+  // k_modexp_mx (4096-bit class): Toeplitz fragments of m'' and m, built on first use
+  std::vector<uint8_t> mx_host;
+  uint8_t* d_mx[kMaxDevices] = {};
 };
 
 struct mpcx_fixedbase_s {
@@ -121,6 +124,11 @@ int g_fb_split = MPCX_FB_SPLIT_DEFAULT;  // mpcx_set_option("fb_split", s): comb
 uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", n): operands per device slice
 bool g_prime_coop = true;                // mpcx_set_option("prime_coop", 0): thread-per-candidate prime kernels
 bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 1): test hook, see below
+#ifndef MPCX_MX_DEFAULT
+#define MPCX_MX_DEFAULT 0
+#endif
+int g_mx = MPCX_MX_DEFAULT;              // mpcx_set_option("mx", 1): geometry-2 batches reduce on the matrix cores
+uint32_t g_mx_min = 2048;                // mpcx_set_option("mx_min", n): smallest batch for k_modexp_mx
 struct Staging {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -444,6 +452,82 @@ std::vector<uint32_t> to_digits(const std::vector<uint32_t>& w, uint32_t L) {
     d[i] = (uint32_t)(v >> s) & kM28;
   }
   return d;
+}
+
+// ---- k_modexp_mx constants (mpcx_mx.hpp): m'' = -m^-1 mod R, R = 2^(28*148), and
+// the Toeplitz fragments of m'' and m for 16x16x64 i8 MFMAs: block j (delta = 16j)
+// is 64 lanes x 16 bytes, lane (i = lane & 15, h = lane >> 4) byte e = radix-2^7
+// digit 16j + i - 16h - e (0 outside [0, 592)).
+constexpr uint32_t kMxWords = 130;  // >= 4144 bits
+constexpr uint32_t kMxDigits7 = 592;
+
+// a * b mod 2^(32 n)
+static void mul_lo(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n) {
+  std::vector<uint64_t> acc(n, 0);
+  for (uint32_t i = 0; i < n; ++i) {
+    uint64_t carry = 0;
+    for (uint32_t j = 0; i + j < n; ++j) {
+      const uint64_t t = (uint64_t)a[i] * b[j] + (acc[i + j] & 0xFFFFFFFFu) + carry;
+      acc[i + j] = (acc[i + j] & ~0xFFFFFFFFull) | (t & 0xFFFFFFFFu);
+      carry = t >> 32;
+    }
+  }
+  for (uint32_t i = 0; i < n; ++i) out[i] = (uint32_t)acc[i];
+}
+
+static void mx_tables(const std::vector<uint32_t>& m, std::vector<uint8_t>& out) {
+  const uint32_t W = kMxWords;
+  std::vector<uint32_t> mm(W, 0), x(W, 0), t(W, 0), u(W, 0);
+  for (size_t i = 0; i < m.size() && i < W; ++i) mm[i] = m[i];
+  uint32_t inv = mm[0];
+  for (int i = 0; i < 5; ++i) inv *= 2u - mm[0] * inv;  // m^-1 mod 2^32
+  x[0] = inv;
+  // Newton: x <- x (2 - m x) doubles the correct low words
+  for (uint32_t prec = 1; prec < W;) {
+    const uint32_t np = std::min(2 * prec, W);
+    mul_lo(mm.data(), x.data(), t.data(), np);
+    uint64_t c = 3;  // t <- 2 - t mod 2^(32 np) = ~t + 1 + 2
+    for (uint32_t i = 0; i < np; ++i) {
+      const uint64_t v = (uint64_t)(uint32_t)~t[i] + c;
+      t[i] = (uint32_t)v;
+      c = v >> 32;
+    }
+    mul_lo(x.data(), t.data(), u.data(), np);
+    for (uint32_t i = 0; i < np; ++i) x[i] = u[i];
+    prec = np;
+  }
+  // m'' = -x mod 2^(32 W), radix-2^7 digits below 2^4144
+  uint64_t br = 1;
+  for (uint32_t i = 0; i < W; ++i) {
+    const uint64_t v = (uint64_t)(uint32_t)~x[i] + br;
+    x[i] = (uint32_t)v;
+    br = v >> 32;
+  }
+  auto d7 = [](const std::vector<uint32_t>& w, uint32_t d) -> uint8_t {
+    const uint32_t bit = 7 * d, wi = bit >> 5, sh = bit & 31;
+    uint64_t v = wi < w.size() ? w[wi] : 0;
+    if (wi + 1 < w.size()) v |= (uint64_t)w[wi + 1] << 32;
+    return (uint8_t)((v >> sh) & 0x7F);
+  };
+  std::vector<uint8_t> n2(kMxDigits7), n1(kMxDigits7);
+  std::vector<uint32_t> mv(m);
+  for (uint32_t d = 0; d < kMxDigits7; ++d) {
+    n2[d] = d7(x, d);
+    n1[d] = d7(mv, d);
+  }
+  out.assign((size_t)(MPCX_MX_NJ1 + MPCX_MX_NJ2) * 1024u, 0);
+  auto fill = [&](const std::vector<uint8_t>& v7, uint32_t nj, uint8_t* dst) {
+    for (uint32_t j = 0; j < nj; ++j)
+      for (int lane = 0; lane < 64; ++lane) {
+        const int i = lane & 15, h = lane >> 4;
+        for (int e = 0; e < 16; ++e) {
+          const int idx = 16 * (int)j + i - 16 * h - e;
+          if (idx >= 0 && idx < (int)kMxDigits7) dst[(j * 64 + lane) * 16 + e] = v7[idx];
+        }
+      }
+  };
+  fill(n2, MPCX_MX_NJ1, out.data());
+  fill(n1, MPCX_MX_NJ2, out.data() + (size_t)MPCX_MX_NJ1 * 1024u);
 }
 
 hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st) {
@@ -883,6 +967,23 @@ int mod_const(mpcx_mod_t mod, int di, const uint32_t** out) {
   return MPCX_OK;
 }
 
+int mx_const(mpcx_mod_t mod, int di, const uint8_t** out) {
+  std::lock_guard<std::mutex> lk(mod->mu);
+  if (!mod->d_mx[di]) {
+    if (mod->mx_host.empty()) mx_tables(mod->m, mod->mx_host);
+    uint8_t* p = nullptr;
+    hipError_t e = hipMalloc((void**)&p, mod->mx_host.size());
+    if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(mx tables): %s", hipGetErrorString(e));
+    if (int rc = copy_sync(p, mod->mx_host.data(), mod->mx_host.size(), hipMemcpyHostToDevice, nullptr)) {
+      (void)hipFree(p);
+      return rc;
+    }
+    mod->d_mx[di] = p;
+  }
+  *out = mod->d_mx[di];
+  return MPCX_OK;
+}
+
 int fb_table(mpcx_fb_t fb, int di, const uint32_t** out) {
   std::lock_guard<std::mutex> lk(fb->mu);
   if (!fb->d_table[di]) {
@@ -1054,6 +1155,13 @@ int mpcx_set_option(const char* key, int value) {
     // wavefronts sharing one comb operand's windows: 1, 2, 4; 0 picks by launch size
     if (value != 0 && value != 1 && value != 2 && value != 4) return fail(MPCX_EINVAL, "fb_split %d not 0/1/2/4", value);
     g_fb_split = value;
+  } else if (std::strcmp(key, "mx") == 0) {
+    // 1: batches of the 4096-bit main geometry reduce on the matrix cores (k_modexp_mx)
+    if (value != 0 && value != 1) return fail(MPCX_EINVAL, "mx %d not 0 or 1", value);
+    g_mx = value;
+  } else if (std::strcmp(key, "mx_min") == 0) {
+    if (value < 1) return fail(MPCX_EINVAL, "mx_min %d < 1", value);
+    g_mx_min = (uint32_t)value;
   } else if (std::strcmp(key, "fixed_window") == 0) {
     // widest fixed window of per-operand exponents: 4 (Go's) or 5 (above 320 bits)
     if (value != 4 && value != 5) return fail(MPCX_EINVAL, "fixed_window %d not 4 or 5", value);
@@ -1113,6 +1221,8 @@ static void read_env_options() {
   if (ln && g_ndev.load() == 0) g_lanes = std::max(1, std::min(kMaxLanes, std::atoi(ln)));
   const char* fw = std::getenv("MPCX_FB_WINDOW");  // fixed-base comb width of new tables
   if (fw) g_fb_window = std::max(4, std::min(MPCX_FB_MAX_WINDOW_BITS, std::atoi(fw)));
+  const char* mx = std::getenv("MPCX_MX");  // geometry-2 batches on k_modexp_mx
+  if (mx) g_mx = mx[0] != '0';
 }
 
 int mpcx_init(int device) {
@@ -1292,9 +1402,25 @@ int mpcx_modulus_register(const uint32_t* m_words, uint32_t m_len, mpcx_mod_t* o
 int mpcx_modulus_release(mpcx_mod_t mod) {
   if (!mod) return fail(MPCX_EINVAL, "null modulus");
   const int n = g_ndev.load();
-  for (int i = 0; i < n && i < kMaxDevices; ++i)
+  for (int i = 0; i < n && i < kMaxDevices; ++i) {
     if (mod->d_const[i] && bind(g_devs[i]) == MPCX_OK) (void)hipFree(mod->d_const[i]);
+    if (mod->d_mx[i] && bind(g_devs[i]) == MPCX_OK) (void)hipFree(mod->d_mx[i]);
+  }
   delete mod;
+  return MPCX_OK;
+}
+
+int mpcx_mx_tables(const uint32_t* m_words, uint32_t m_len, uint8_t* out, size_t cap) {
+  if (!m_words || !out || m_len == 0) return fail(MPCX_EINVAL, "null modulus or output");
+  const size_t need = (size_t)(MPCX_MX_NJ1 + MPCX_MX_NJ2) * 1024u;
+  if (cap < need) return fail(MPCX_EINVAL, "mx tables need %zu bytes", need);
+  std::vector<uint32_t> m(m_words, m_words + m_len);
+  while (m.size() > 1 && m.back() == 0) m.pop_back();
+  if ((m[0] & 1u) == 0 || bit_length(m) > (uint32_t)MPCX_CLASS_MAXBITS(2))
+    return fail(MPCX_EINVAL, "mx tables need an odd modulus of <= %d bits", MPCX_CLASS_MAXBITS(2));
+  std::vector<uint8_t> t;
+  mx_tables(m, t);
+  std::memcpy(out, t.data(), need);
   return MPCX_OK;
 }
 
@@ -1472,13 +1598,22 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     a.n0inv = mod->n0inv;
     a.exp_shared = exp_shared ? 1 : 0;
     a.sched = use_sched ? lane.ws + sched_off : nullptr;
+    // the 4096-bit main geometry with the reduction on the matrix cores
+    const bool mx = g_mx && pt.geom == MPCX_MAIN_GEOM(2) && pt.count >= g_mx_min;
+    if (mx) {
+      const uint8_t* t = nullptr;
+      if (int rc = mx_const(mod, di, &t)) return rc;
+      a.mx_f1 = t;
+      a.mx_f2 = t + (size_t)MPCX_MX_NJ1 * 1024u;
+    }
+    const char* kind = mx ? "modexp_mx" : "modexp";
     const int ks = kstat_begin(lane);
     hipError_t e = mpcx_launch_modexp(pt.geom, &a, waves, st);
     if (e != hipSuccess) return hip_fail(e, "launch k_modexp");
     g_devs[di].launches.fetch_add(1, std::memory_order_relaxed);
     const double alg = alg_macs >= 0 ? alg_macs * pt.count / count : go_macs(mod->bits, a.exp_bits) * pt.count;
-    kstat_end(lane, ks, g_devs[di], di, "modexp", pt.geom, pt.count, alg);
-    launch_log("modexp", pt.geom, pt.count, mod->bits, a.exp_bits, alg);
+    kstat_end(lane, ks, g_devs[di], di, kind, pt.geom, pt.count, alg);
+    launch_log(kind, pt.geom, pt.count, mod->bits, a.exp_bits, alg);
     ws_off += (size_t)waves * MPCX_TABLE_ENTRIES * K * 64u;
   }
   return MPCX_OK;

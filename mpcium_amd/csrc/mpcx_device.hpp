@@ -352,13 +352,23 @@ __device__ __forceinline__ void store_result(uint32_t (&A)[K], const uint32_t (&
   }
 }
 
+}  // namespace mpcx
+#include "mpcx_mx.hpp"
+namespace mpcx {
+
 // Batched x_i^e_i mod m for one registered odd modulus m: wavefront `blk` of
 // the batch described by a (k_modexp: one batch per launch; k_modexp_multi:
 // several batches, each its own segment of the launch's wavefronts).
-template <int P, int K, int G>
+// MX (geometry 2 only, a.mx_f1 set): every product but the final exit runs as
+// montmul_mx (reduction on the matrix cores, mpcx_mx.hpp); the multiplier row
+// lives in R1, which montmul_mx overwrites, so a row that the state machine
+// reuses across products is staged again before each (`restage`).
+template <int P, int K, int G, bool MX = false>
 __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t blk) {
   constexpr int L = P * K;
-  __shared__ uint32_t lds[(G + 1) * L + 2];  // +2: the b prefetch reads up to two past a row
+  static_assert(!MX || (P == MX_P && K == MX_K && G == MX_G), "montmul_mx serves geometry 2 only");
+  // +2: the b prefetch reads up to two past a row; MX: R0, R1 and m's digits
+  __shared__ __attribute__((aligned(16))) uint32_t lds[MX ? MX_LDS_WORDS : (G + 1) * L + 2];
   const int lane = threadIdx.x;
   const int g_raw = lane / P;
   const bool idle = g_raw >= G;  // lanes beyond G*P carry zeros
@@ -366,12 +376,28 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
   const int p = lane - g_raw * P;
   const uint32_t op = blk * G + (idle ? 0 : g_raw);
   const bool active = !idle && op < a.count;
-  uint32_t* bl = lds + g * L;
+  uint32_t* bl = MX ? lds + MX_G * MX_ROW + g * L : lds + g * L;
   const int m_src_addr = (idle ? lane : g_raw * P) * 4;
 
   uint32_t Nd[K], A[K];
+  // L digits of a constant (m, R^2 mod m) into registers; MX: through an opaque
+  // pointer and lane index, so the per-digit addresses are not hoisted out of
+  // the step loop and held live across every product (as load_digits)
+  auto load_const = [&] __attribute__((always_inline))(const uint32_t* src, uint32_t (&v)[K]) {
+    if constexpr (MX) asm volatile("" : "+s"(src));
+    int pp = p;
+    if constexpr (MX) asm volatile("" : "+v"(pp));
 #pragma unroll
-  for (int k = 0; k < K; ++k) Nd[k] = idle ? 0u : a.nd[p * K + k];
+    for (int k = 0; k < K; ++k) v[k] = idle ? 0u : src[pp * K + k];
+  };
+  auto load_nd = [&] __attribute__((always_inline))() { load_const(a.nd, Nd); };
+  if constexpr (!MX) load_nd();  // MX: only the exit product and store_result need m in registers
+  MxConsts mxc{};
+  if constexpr (MX) {
+    uint32_t* md = lds + 2 * MX_G * MX_ROW;
+    for (int i = lane; i < MX_L; i += 64) md[i] = a.nd[i];
+    mxc = mx_consts(a.mx_f1, a.mx_f2);
+  }
 
   // operand words -> radix-2^28 digits (inactive operands compute on zero)
   auto load_digits = [&] __attribute__((always_inline))(const uint32_t* src, uint32_t words) {
@@ -530,8 +556,30 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
     }
   };
 
+  int restage = -1;  // MX: table entry (or MX_RESTAGE_R2) to put back in the row before the next product
+  constexpr int MX_RESTAGE_R2 = -2;
   for (;;) {
-    if (MPCX_SQR_OPT && sqr) {
+    if constexpr (MX) {
+      if (restage != -1) {
+        if (restage == MX_RESTAGE_R2) {
+          uint32_t r2[K];
+          load_const(a.r2d, r2);
+          lds_store_digits<K>(bl, p, r2);
+        } else {
+          lds_from_table((uint32_t)restage);
+        }
+        restage = -1;
+        wave_lds_fence();
+      }
+      if (st == ST_FIN) {
+        load_nd();  // exit product mont(z R, 1) <= m by the CIOS loop: canonical as store_result needs
+        montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
+      } else if (sqr) {
+        montmul_mx<true, (bool)MPCX_SQR_B2>(A, lds, lds + MX_G * MX_ROW, lds + 2 * MX_G * MX_ROW, mxc, lane);
+      } else {
+        montmul_mx<false, false>(A, lds, lds + MX_G * MX_ROW, lds + 2 * MX_G * MX_ROW, mxc, lane);
+      }
+    } else if (MPCX_SQR_OPT && sqr) {
       montmul<P, K, true, (bool)MPCX_SQR_B2>(A, bl, Nd, a.n0inv, m_src_addr, p);
     } else {
       montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
@@ -542,6 +590,7 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
     if (st == ST_PRE) {
       tbl_store(MPCX_MUL_ENTRY, A);
       load_digits(a.base, a.base_words);  // LDS still holds R^2
+      if constexpr (MX) restage = MX_RESTAGE_R2;
       st = ST_TAB;
       idx = 1;
     } else if (st == ST_TAB) {
@@ -552,6 +601,8 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
         st = ST_TSQ;
       } else if (!sched && idx == 1) {
         lds_store_digits<K>(bl, p, A);  // B = p_1 for the remaining table steps
+      } else if (MX && !sched && idx < T) {
+        restage = 1;  // the next table step multiplies by p_1 again
       }
       if (!sched && idx < T) {
         ++idx;
@@ -560,11 +611,13 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
       }
     } else if (st == ST_TSQ) {
       lds_store_digits<K>(bl, p, A);  // B = x^2 R for the odd-power chain
+      if constexpr (MX) tbl_store(MPCX_SQ_ENTRY, A);
       tbl_load(0, A);
       st = ST_STAB;
       idx = 1;
     } else if (st == ST_STAB) {
       tbl_store(idx, A);
+      if (MX && idx < T) restage = MPCX_SQ_ENTRY;  // the next odd power multiplies by x^2 R again
       if (idx < T) {
         ++idx;
       } else {
@@ -595,6 +648,12 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
 template <int P, int K, int G, int WPE>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp(const ModexpArgs a) {
   modexp_wave<P, K, G>(a, blockIdx.x);
+}
+
+// geometry 2 with the reduction on the matrix cores (a.mx_f1 / a.mx_f2 set)
+template <int WPE>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp_mx(const ModexpArgs a) {
+  modexp_wave<MX_P, MX_K, MX_G, true>(a, blockIdx.x);
 }
 
 // Several batches of one modulus class in one launch (mpcx_modexp_multi_batch:

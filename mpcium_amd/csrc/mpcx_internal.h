@@ -57,8 +57,11 @@
 // table entries per wavefront in the workspace: powers p_0..p_15 (fixed
 // window) or the odd powers x, x^3, ..., x^63 (sliding window, table[0..31]),
 // + the Montgomery form of the optional multiplier (entry 32)
-#define MPCX_TABLE_ENTRIES 33
+#define MPCX_TABLE_ENTRIES 34
 #define MPCX_MUL_ENTRY 32
+// k_modexp_mx: x^2 R, the odd-power chain's multiplier, staged again before each
+// product (montmul_mx overwrites its LDS row)
+#define MPCX_SQ_ENTRY 33
 
 // Sliding-window schedule of a shared exponent (built by k_expsched on the
 // launch stream, read by k_modexp through scalar loads):
@@ -99,7 +102,14 @@ struct ModexpArgs {
   uint32_t n0inv;       // -m^-1 mod 2^28
   int exp_shared;
   const uint32_t* sched; // shared exponent: its window schedule (nullptr: fixed window)
+  // geometry 2 only: Toeplitz fragment tables of m'' = -m^-1 mod R and of m
+  // (mpcx_mx.hpp; MPCX_MX_NJ1 / MPCX_MX_NJ2 KiB): k_modexp_mx, the reduction on the
+  // matrix cores. nullptr: k_modexp
+  const void* mx_f1;
+  const void* mx_f2;
 };
+#define MPCX_MX_NJ1 37
+#define MPCX_MX_NJ2 41
 
 // Fixed-base tables (mpcx_fixedbase_register): w-bit windows (w chosen per
 // table, <= MPCX_FB_MAX_WINDOW_BITS); for window j < nwin and value v < 2^w,

@@ -38,6 +38,7 @@ SIGNATURES = [
     ("mpcx_modulus_release", ctypes.c_int, [_vp]),
     ("mpcx_modulus_info", ctypes.c_int, [_vp, _u32p, _u32p]),
     ("mpcx_modulus_geometry", ctypes.c_int, [_vp, _u32p, _u32p, _u32p, _u32p]),
+    ("mpcx_mx_tables", ctypes.c_int, [_u32p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     ("mpcx_modexp_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
                                          ctypes.c_int, _vp, ctypes.c_uint32]),
     ("mpcx_modexp_batch_device", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
@@ -172,6 +173,18 @@ def copy_stats() -> dict:
     v = [ctypes.c_uint64(0) for _ in range(3)]
     _check(lib().mpcx_copy_stats(*(ctypes.byref(x) for x in v)))
     return {"direct_bytes": v[0].value, "bounced_bytes": v[1].value, "bounce_allocs": v[2].value}
+
+
+MX_TABLE_BYTES = (37 + 41) * 1024
+
+
+def mx_tables(m: int) -> bytes:
+    """mpcx_mx_tables: k_modexp_mx's Toeplitz fragments of m'' = -m^-1 mod 2^4144
+    and of m (host-only, no device needed)."""
+    w = int_to_words(m, 128)
+    out = ctypes.create_string_buffer(MX_TABLE_BYTES)
+    _check(lib().mpcx_mx_tables(w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 128, out, MX_TABLE_BYTES))
+    return out.raw
 
 
 def select_device(index: int):

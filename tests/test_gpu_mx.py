@@ -1,0 +1,100 @@
+"""k_modexp_mx -- the 4096-bit main geometry with its Montgomery reduction on the
+i8 matrix cores (mpcium_amd/csrc/mpcx_mx.hpp) -- against Python's pow and against
+the CIOS kernel (k_modexp) on the same inputs: bit-exact.
+
+The shapes follow the reference's hot path: r^N mod N^2 with a shared 2048-bit N
+(config 2, up:crypto/paillier Encrypt), per-operand exponents (HomoMult c^m), a
+multiplier (Encrypt's Gamma^m * r^N), and the edge operands 0, 1, m - 1.
+"""
+import random
+
+import pytest
+
+from mpcium_amd import mpcx
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def dev():
+    mpcx.init(0)
+    mpcx.set_option("kernel_stats", 1)
+    mpcx.set_option("geom_policy", 2)  # the main geometry at every batch size
+    yield
+    mpcx.set_option("mx", 0)
+    mpcx.set_option("geom_policy", 1)
+    mpcx.set_option("kernel_stats", 0)
+
+
+def _modulus(rng, bits=4096):
+    # N^2 of a random odd 2048-bit N (top bit set): the Paillier modulus shape
+    n = rng.getrandbits(2048) | (1 << 2047) | 1
+    return n, n * n
+
+
+def _run(m, bases, exps, mx, muls=None):
+    mpcx.set_option("mx", mx)
+    mpcx.kernel_stats(reset=True)
+    mod = mpcx.Modulus(m)
+    try:
+        out = mod.exp_mul(bases, exps, muls) if muls is not None else mod.exp(bases, exps)
+    finally:
+        mod.release()
+    return out, mpcx.kernel_stats()
+
+
+def _mx_launched(stats):
+    return any(k.get("kind") == "modexp_mx" and k.get("launches", 0) > 0 for k in stats.get("kernels", []))
+
+
+def test_mx_shared_exponent_matches_pow_and_cios(dev):
+    rng = random.Random(5101)
+    n, m = _modulus(rng)
+    bases = [rng.randrange(m) for _ in range(4096)]
+    bases[0], bases[1], bases[2], bases[3] = 0, 1, m - 1, 2
+    got, st = _run(m, bases, n, 1)
+    assert _mx_launched(st), st
+    ref, st0 = _run(m, bases, n, 0)
+    assert not _mx_launched(st0)
+    assert got == ref
+    for i in list(range(8)) + rng.sample(range(8, len(bases)), 56):
+        assert got[i] == pow(bases[i], n, m), i
+
+
+def test_mx_per_operand_exponents(dev):
+    rng = random.Random(5102)
+    _, m = _modulus(rng)
+    bases = [rng.randrange(m) for _ in range(2048)]
+    exps = [rng.getrandbits(rng.choice([1, 2, 64, 256, 2048])) for _ in bases]
+    exps[0], exps[1] = 0, 1
+    got, st = _run(m, bases, exps, 1)
+    assert _mx_launched(st)
+    for i in list(range(4)) + rng.sample(range(4, len(bases)), 60):
+        assert got[i] == pow(bases[i], exps[i], m), i
+
+
+def test_mx_with_multiplier(dev):
+    rng = random.Random(5103)
+    n, m = _modulus(rng)
+    bases = [rng.randrange(m) for _ in range(2048)]
+    muls = [rng.randrange(m) for _ in bases]
+    got, st = _run(m, bases, n, 1, muls=muls)
+    assert _mx_launched(st)
+    ref, _ = _run(m, bases, n, 0, muls=muls)
+    assert got == ref
+    for i in rng.sample(range(len(bases)), 32):
+        assert got[i] == muls[i] * pow(bases[i], n, m) % m, i
+
+
+def test_mx_small_exponents_and_odd_moduli(dev):
+    # shared exponents of 1..7 bits (short schedules, the odd-power table's
+    # restaged rows) and moduli well below 2^4096
+    rng = random.Random(5104)
+    for bits in (4096, 3001, 2081):
+        m = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        bases = [rng.randrange(m) for _ in range(2048)]
+        for e in (1, 2, 3, 5, 127, (1 << 70) + 12345):
+            got, st = _run(m, bases, e, 1)
+            assert _mx_launched(st)
+            for i in rng.sample(range(len(bases)), 12):
+                assert got[i] == pow(bases[i], e, m), (bits, e, i)

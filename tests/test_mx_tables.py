@@ -1,0 +1,127 @@
+"""k_modexp_mx on the CPU: its constant tables (mpcx_mx_tables, host-only) against a
+Python restatement, and the digit-level arithmetic of montmul_mx
+(mpcium_amd/csrc/mpcx_mx.hpp) restated step by step in integers, so the bounds the
+kernel relies on are checked on edge operands as well as random ones:
+  - q (balanced radix-2^28 digits after ONE carry step) is a Montgomery quotient,
+    |q| <= R/2 (1 + 2^-10), and every radix-2^7 byte of it is a valid signed i8;
+  - every i8 column sum fits i32;
+  - the carry out of the low half, rounded from its top four column sums, is exact;
+  - U + m (the kernel's result) lies in (0, 2m) and is A B R^-1 mod m.
+"""
+import random
+
+import pytest
+
+from mpcium_amd import mpcx
+
+L, DB = 148, 28
+RBITS = L * DB
+R = 1 << RBITS
+M28 = (1 << 28) - 1
+
+
+def digits(v, n, bits):
+    return [(v >> (bits * i)) & ((1 << bits) - 1) for i in range(n)]
+
+
+def toeplitz(v7, nj):
+    out = bytearray(nj * 64 * 16)
+    for j in range(nj):
+        for lane in range(64):
+            i, h = lane & 15, lane >> 4
+            for e in range(16):
+                idx = 16 * j + i - 16 * h - e
+                if 0 <= idx < len(v7):
+                    out[(j * 64 + lane) * 16 + e] = v7[idx]
+    return bytes(out)
+
+
+def i32(x):
+    x &= 0xFFFFFFFF
+    return x - (1 << 32) if x >= 1 << 31 else x
+
+
+def split(c, add):
+    lo_sum = c[0] + ((c[1] & 0x1FFFFF) << 7) + ((c[2] & 0x3FFF) << 14) + ((c[3] & 0x7F) << 21) + add
+    assert -(1 << 31) <= lo_sum < (1 << 31)
+    return lo_sum, (c[1] >> 21) + (c[2] >> 14) + (c[3] >> 7)
+
+
+def spread_bytes(e):
+    x = e & 0xFFFFFFFF
+    for msk in (0xFFFFFF80, 0xFFFF8000, 0xFF800000):
+        x = (x + (x & msk)) & 0xFFFFFFFF
+    return [((x >> (8 * i)) & 0xFF) - (256 if (x >> (8 * i)) & 0x80 else 0) for i in range(4)]
+
+
+def conv(a, b, lo, hi):
+    out = []
+    for P in range(lo, hi):
+        k0, k1 = max(0, P - len(b) + 1), min(P, len(a) - 1)
+        out.append(sum(a[k] * b[P - k] for k in range(k0, k1 + 1)))
+    return out
+
+
+def montmul_mx_model(a, b, m):
+    m2 = (-pow(m, -1, R)) % R
+    T = a * b
+    tl, th = digits(T % R, L, DB), digits(T >> RBITS, L, DB)
+    c1 = conv(digits(T % R, 592, 7), digits(m2, 592, 7), 0, 592)
+    assert max(c1) < 1 << 31
+    e, hprev = [], 0
+    for d in range(L):
+        lo_sum, hi_sum = split(c1[4 * d:4 * d + 4], 1 << 27)
+        e.append((lo_sum & M28) - (1 << 27) + hprev)
+        hprev = hi_sum + (lo_sum >> 28)
+    q7 = [v for ed in e for v in spread_bytes(ed)]
+    assert all(-128 <= v <= 127 for v in q7)
+    q = sum(v << (7 * i) for i, v in enumerate(q7))
+    assert q == sum(v << (28 * i) for i, v in enumerate(e))
+    assert (T + q * m) % R == 0
+    assert abs(q) <= (R >> 1) + (R >> 11)
+    m7 = digits(m, 592, 7)
+    c2 = conv(q7, m7, 0, 1184)
+    assert max(abs(v) for v in c2) < 1 << 31
+    lo_sum, hi_sum = split(c2[588:592], tl[147] + (1 << 27))
+    carry = hi_sum + (lo_sum >> 28)
+    low = sum(c2[P] << (7 * P) for P in range(592)) + (T % R)
+    assert low % R == 0 and carry == low // R
+    md, u, cin = digits(m, L, DB), [], carry
+    for d in range(L):
+        lo_sum, hi_sum = split(c2[592 + 4 * d:596 + 4 * d], th[d] + md[d])
+        hi = hi_sum + (lo_sum >> 28)
+        u.append(i32(lo_sum + (hi_sum << 28)) + cin if d == L - 1 else (lo_sum & M28) + cin)
+        cin = hi
+    U = sum(v << (28 * i) for i, v in enumerate(u))
+    assert U == (T + q * m) // R + m
+    return U
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_mx_tables_match_restatement(seed):
+    rng = random.Random(seed)
+    for bits in (4096, 4095, 3001):
+        m = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        m2 = (-pow(m, -1, R)) % R
+        want = toeplitz(digits(m2, 592, 7), 37) + toeplitz(digits(m, 592, 7), 41)
+        assert mpcx.mx_tables(m) == want
+
+
+def test_mx_tables_reject_even_modulus():
+    with pytest.raises(mpcx.MpcxError):
+        mpcx.mx_tables(1 << 4000)
+
+
+def test_mx_reduction_arithmetic():
+    rng = random.Random(77)
+    cases = []
+    for t in range(12):
+        bits = (4096, 4096, 3001, 2081)[t % 4]
+        m = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        if t == 1:
+            m = (1 << 4096) - 1  # all-ones digits: the largest column sums
+        cases += [(rng.randrange(2 * m), rng.randrange(2 * m), m), (2 * m - 1, 2 * m - 1, m), (0, 0, m), (1, 1, m)]
+    for a, b, m in cases:
+        U = montmul_mx_model(a, b, m)
+        assert 0 < U < 2 * m
+        assert U % m == a * b * pow(R, -1, m) % m
