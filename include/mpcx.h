@@ -421,9 +421,9 @@ int mpcx_set_option(const char* key, int value);
 
 /* The constant tables of k_modexp_mx (the 4096-bit main geometry with its
  * Montgomery reduction on the i8 matrix cores, mpcium_amd/csrc/mpcx_mx.hpp) for
- * the odd modulus m (<= 4096 bits): the Toeplitz fragments of m'' = -m^-1 mod
- * 2^4144, then of m, 37 + 41 KiB. Host-only (no device needed); for tests and
- * tools. */
+ * the odd modulus m (<= 4096 bits): the LDS image of the Toeplitz tables of
+ * m'' = -m^-1 mod 2^4144 and of m, 2 x 16 row copies of 720 bytes (23,040
+ * bytes). Host-only (no device needed); for tests and tools. */
 int mpcx_mx_tables(const uint32_t* m_words, uint32_t m_len, uint8_t* out, size_t cap);
 
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):

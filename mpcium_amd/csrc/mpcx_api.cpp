@@ -515,19 +515,18 @@ static void mx_tables(const std::vector<uint32_t>& m, std::vector<uint8_t>& out)
     n2[d] = d7(x, d);
     n1[d] = d7(mv, d);
   }
-  out.assign((size_t)(MPCX_MX_NJ1 + MPCX_MX_NJ2) * 1024u, 0);
-  auto fill = [&](const std::vector<uint8_t>& v7, uint32_t nj, uint8_t* dst) {
-    for (uint32_t j = 0; j < nj; ++j)
-      for (int lane = 0; lane < 64; ++lane) {
-        const int i = lane & 15, h = lane >> 4;
-        for (int e = 0; e < 16; ++e) {
-          const int idx = 16 * (int)j + i - 16 * h - e;
-          if (idx >= 0 && idx < (int)kMxDigits7) dst[(j * 64 + lane) * 16 + e] = v7[idx];
-        }
+  // the LDS image k_modexp_mx copies (mpcx_mx.hpp): per table 16 row copies of the
+  // reversed digit string, copy_i[x] = v7[640 - x + i] (0 outside [0, 592))
+  out.assign(2u * MPCX_MX_TAB_BYTES, 0);
+  auto fill = [&](const std::vector<uint8_t>& v7, uint8_t* dst) {
+    for (int i = 0; i < 16; ++i)
+      for (int x = 0; x < MPCX_MX_TAB_STRIDE; ++x) {
+        const int idx = 640 - x + i;
+        if (idx >= 0 && idx < (int)kMxDigits7) dst[i * MPCX_MX_TAB_STRIDE + x] = v7[idx];
       }
   };
-  fill(n2, MPCX_MX_NJ1, out.data());
-  fill(n1, MPCX_MX_NJ2, out.data() + (size_t)MPCX_MX_NJ1 * 1024u);
+  fill(n2, out.data());
+  fill(n1, out.data() + MPCX_MX_TAB_BYTES);
 }
 
 hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st) {
@@ -1412,7 +1411,7 @@ int mpcx_modulus_release(mpcx_mod_t mod) {
 
 int mpcx_mx_tables(const uint32_t* m_words, uint32_t m_len, uint8_t* out, size_t cap) {
   if (!m_words || !out || m_len == 0) return fail(MPCX_EINVAL, "null modulus or output");
-  const size_t need = (size_t)(MPCX_MX_NJ1 + MPCX_MX_NJ2) * 1024u;
+  const size_t need = 2u * MPCX_MX_TAB_BYTES;
   if (cap < need) return fail(MPCX_EINVAL, "mx tables need %zu bytes", need);
   std::vector<uint32_t> m(m_words, m_words + m_len);
   while (m.size() > 1 && m.back() == 0) m.pop_back();
@@ -1600,11 +1599,11 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     a.sched = use_sched ? lane.ws + sched_off : nullptr;
     // the 4096-bit main geometry with the reduction on the matrix cores
     const bool mx = g_mx && pt.geom == MPCX_MAIN_GEOM(2) && pt.count >= g_mx_min;
+    a.nwaves = waves;
     if (mx) {
       const uint8_t* t = nullptr;
       if (int rc = mx_const(mod, di, &t)) return rc;
-      a.mx_f1 = t;
-      a.mx_f2 = t + (size_t)MPCX_MX_NJ1 * 1024u;
+      a.mx_img = t;
     }
     const char* kind = mx ? "modexp_mx" : "modexp";
     const int ks = kstat_begin(lane);

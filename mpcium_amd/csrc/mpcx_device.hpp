@@ -359,24 +359,35 @@ namespace mpcx {
 // Batched x_i^e_i mod m for one registered odd modulus m: wavefront `blk` of
 // the batch described by a (k_modexp: one batch per launch; k_modexp_multi:
 // several batches, each its own segment of the launch's wavefronts).
-// MX (geometry 2 only, a.mx_f1 set): every product but the final exit runs as
-// montmul_mx (reduction on the matrix cores, mpcx_mx.hpp); the multiplier row
-// lives in R1, which montmul_mx overwrites, so a row that the state machine
-// reuses across products is staged again before each (`restage`).
+// MX (geometry 2 only, a.mx_img set; MX_WG wavefronts per workgroup): every
+// product but the final exit runs as montmul_mx (reduction on the matrix cores,
+// mpcx_mx.hpp) with the workgroup's LDS copy of the Toeplitz tables; the
+// multiplier row is montmul_mx's scratch, so a row that the state machine reuses
+// across products is staged again before each (`restage`).
 template <int P, int K, int G, bool MX = false>
 __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t blk) {
   constexpr int L = P * K;
   static_assert(!MX || (P == MX_P && K == MX_K && G == MX_G), "montmul_mx serves geometry 2 only");
-  // +2: the b prefetch reads up to two past a row; MX: R0, R1 and m's digits
-  __shared__ __attribute__((aligned(16))) uint32_t lds[MX ? MX_LDS_WORDS : (G + 1) * L + 2];
-  const int lane = threadIdx.x;
+  // +2: the b prefetch reads up to two past a row; MX: tables, m's digits, rows
+  __shared__ __attribute__((aligned(16))) uint32_t lds_all[MX ? MX_LDS_WORDS_WG : (G + 1) * L + 2];
+  uint32_t* lds = lds_all;
+  if constexpr (MX) {
+    // the workgroup's tables and m's digits, then the wavefronts part
+    const uint32_t* img = static_cast<const uint32_t*>(a.mx_img);
+    for (int i = (int)threadIdx.x; i < MX_IMG_BYTES / 4; i += 64 * MX_WG) lds_all[i] = img[i];
+    for (int i = (int)threadIdx.x; i < MX_L; i += 64 * MX_WG) lds_all[MX_IMG_BYTES / 4 + i] = a.nd[i];
+    __syncthreads();
+    if (blk >= a.nwaves) return;  // the last workgroup's spare wavefronts
+    lds = lds_all + MX_IMG_BYTES / 4 + MX_L + 4 + (threadIdx.x >> 6) * MX_WAVE_WORDS;
+  }
+  const int lane = MX ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
   const int g_raw = lane / P;
   const bool idle = g_raw >= G;  // lanes beyond G*P carry zeros
   const int g = idle ? G : g_raw;
   const int p = lane - g_raw * P;
   const uint32_t op = blk * G + (idle ? 0 : g_raw);
   const bool active = !idle && op < a.count;
-  uint32_t* bl = MX ? lds + MX_G * MX_ROW + g * L : lds + g * L;
+  uint32_t* bl = lds + g * L;
   const int m_src_addr = (idle ? lane : g_raw * P) * 4;
 
   uint32_t Nd[K], A[K];
@@ -393,11 +404,8 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
   auto load_nd = [&] __attribute__((always_inline))() { load_const(a.nd, Nd); };
   if constexpr (!MX) load_nd();  // MX: only the exit product and store_result need m in registers
   MxConsts mxc{};
-  if constexpr (MX) {
-    uint32_t* md = lds + 2 * MX_G * MX_ROW;
-    for (int i = lane; i < MX_L; i += 64) md[i] = a.nd[i];
-    mxc = mx_consts(a.mx_f1, a.mx_f2);
-  }
+  const uint32_t* mx_md = lds_all + MX_IMG_BYTES / 4;  // MX: m's digits (LDS)
+  if constexpr (MX) mxc = mx_consts(reinterpret_cast<const uint8_t*>(lds_all), lane);
 
   // operand words -> radix-2^28 digits (inactive operands compute on zero)
   auto load_digits = [&] __attribute__((always_inline))(const uint32_t* src, uint32_t words) {
@@ -571,13 +579,11 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
         restage = -1;
         wave_lds_fence();
       }
-      if (st == ST_FIN) {
-        load_nd();  // exit product mont(z R, 1) <= m by the CIOS loop: canonical as store_result needs
-        montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
-      } else if (sqr) {
-        montmul_mx<true, (bool)MPCX_SQR_B2>(A, lds, lds + MX_G * MX_ROW, lds + 2 * MX_G * MX_ROW, mxc, lane);
+      if (st == ST_FIN) break;  // the exit product runs after the loop (m's digits live only there)
+      if (sqr) {
+        montmul_mx<true, (bool)MPCX_SQR_B2>(A, lds, mx_md, mxc, lane);
       } else {
-        montmul_mx<false, false>(A, lds, lds + MX_G * MX_ROW, lds + 2 * MX_G * MX_ROW, mxc, lane);
+        montmul_mx<false, false>(A, lds, mx_md, mxc, lane);
       }
     } else if (MPCX_SQR_OPT && sqr) {
       montmul<P, K, true, (bool)MPCX_SQR_B2>(A, bl, Nd, a.n0inv, m_src_addr, p);
@@ -642,6 +648,10 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
     wave_lds_fence();
   }
 
+  if constexpr (MX) {
+    load_nd();  // exit product mont(z R, 1) <= m by the CIOS loop: canonical as store_result needs
+    montmul<P, K, false>(A, bl, Nd, a.n0inv, m_src_addr, p);
+  }
   store_result<P, K>(A, Nd, bl, p, g_raw, idle, active, a.out + (size_t)op * a.out_words, a.out_words);
 }
 
@@ -650,10 +660,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   modexp_wave<P, K, G>(a, blockIdx.x);
 }
 
-// geometry 2 with the reduction on the matrix cores (a.mx_f1 / a.mx_f2 set)
+// geometry 2 with the reduction on the matrix cores (a.mx_img set): MX_WG
+// wavefronts per workgroup share the tables in LDS
 template <int WPE>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp_mx(const ModexpArgs a) {
-  modexp_wave<MX_P, MX_K, MX_G, true>(a, blockIdx.x);
+__global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp_mx(
+    const ModexpArgs a) {
+  modexp_wave<MX_P, MX_K, MX_G, true>(a, blockIdx.x * MX_WG + (threadIdx.x >> 6));
 }
 
 // Several batches of one modulus class in one launch (mpcx_modexp_multi_batch:

@@ -102,14 +102,14 @@ struct ModexpArgs {
   uint32_t n0inv;       // -m^-1 mod 2^28
   int exp_shared;
   const uint32_t* sched; // shared exponent: its window schedule (nullptr: fixed window)
-  // geometry 2 only: Toeplitz fragment tables of m'' = -m^-1 mod R and of m
-  // (mpcx_mx.hpp; MPCX_MX_NJ1 / MPCX_MX_NJ2 KiB): k_modexp_mx, the reduction on the
-  // matrix cores. nullptr: k_modexp
-  const void* mx_f1;
-  const void* mx_f2;
+  // geometry 2 only: the LDS image of the Toeplitz tables of m'' = -m^-1 mod R and
+  // of m (mpcx_mx.hpp, 2 x MPCX_MX_TAB_BYTES): k_modexp_mx, the reduction on the
+  // matrix cores, MX_WG wavefronts per workgroup. nullptr: k_modexp
+  const void* mx_img;
+  uint32_t nwaves;      // wavefronts with work (k_modexp_mx: the last workgroup's spare waves exit)
 };
-#define MPCX_MX_NJ1 37
-#define MPCX_MX_NJ2 41
+#define MPCX_MX_TAB_STRIDE 720
+#define MPCX_MX_TAB_BYTES (16 * MPCX_MX_TAB_STRIDE)
 
 // Fixed-base tables (mpcx_fixedbase_register): w-bit windows (w chosen per
 // table, <= MPCX_FB_MAX_WINDOW_BITS); for window j < nwin and value v < 2^w,

@@ -35,9 +35,9 @@
 //  * The carry out of the low half of T + q m (an exact multiple of R) is the
 //    rounded value of its top four column sums (the rest is < 2^-5 of a unit).
 //
-// Two LDS rows per operand: R1 = the multiplier row the product loop reads
-// (2A for squarings) and then q's bytes; R0 = T's low digits as the loop emits
-// them, then T's high digits + m, then U + m.
+// One LDS row per operand: the multiplier (2A for squarings), overwritten by T's
+// low digits as the product loop passes them, then T's high digits + m, then
+// U + m. q goes from the accumulator layout to B fragments by permlane swaps.
 // Included by mpcx_device.hpp (after montmul, before modexp_wave); not on its own.
 #pragma once
 
@@ -54,22 +54,36 @@ constexpr int MX_NJ2 = 41;   // Toeplitz blocks of m (delta = 16 j, j < 41)
 constexpr int MX_O2LO = 36, MX_O2HI = 74;  // output blocks of q m kept: positions 576..1183
 // output-block chunks (live accumulators: one chunk at a time)
 #ifndef MX_C1A
-#define MX_C1A 13
-#define MX_C1B 25
+#define MX_C1A 12  // phase-1 chunks end on 4-block boundaries (one B fragment of q per 4 blocks)
+#define MX_C1B 24
 #define MX_C2A 49
 #define MX_C2B 62
 #endif
-// LDS words per wavefront: R0, R1, m's radix-2^28 digits, +1 for the product
-// loop's read one past the last row
-constexpr int MX_LDS_WORDS = 2 * MX_G * MX_ROW + MX_L + 4;
+// LDS words per wavefront: the 16 operand rows, +4 for the product loop's read
+// one past the last row
+constexpr int MX_WAVE_WORDS = MX_G * MX_ROW + 4;
+// Toeplitz tables in LDS, shared by the workgroup: per table (m'' for q, m for
+// q m) 16 copies, one per fragment row i, of the digit string reversed and
+// shifted so that lane (i, h)'s 16 bytes of block j start 16-aligned at
+// i * MX_TAB_STRIDE + 16 (40 - j + h): copy_i[x] = v7[640 - x + i]. The stride
+// (45 x 16 B) puts the 16 rows of a ds_read_b128 lane group on distinct banks.
+constexpr int MX_TAB_STRIDE = 720;
+constexpr int MX_TAB_BYTES = 16 * MX_TAB_STRIDE;  // one table
+constexpr int MX_IMG_BYTES = 2 * MX_TAB_BYTES;    // the LDS image of both (the C-ABI uploads it)
+// workgroup: MX_WG wavefronts share the image and m's digits
+#ifndef MX_WG
+#define MX_WG 4
+#endif
+constexpr int MX_LDS_WORDS_WG = MX_IMG_BYTES / 4 + MX_L + 4 + MX_WG * MX_WAVE_WORDS;
 
 struct MxConsts {
-  __amdgpu_buffer_rsrc_t f1;  // [MX_NJ1][64] Toeplitz fragments of m'' = -m^-1 mod R
-  __amdgpu_buffer_rsrc_t f2;  // [MX_NJ2][64] Toeplitz fragments of m
+  const uint8_t* t1;  // LDS: table of m'' = -m^-1 mod R, pre-offset to this lane's row copy
+  const uint8_t* t2;  // LDS: table of m, likewise
 };
-__device__ __forceinline__ MxConsts mx_consts(const void* f1, const void* f2) {
-  return MxConsts{__builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(f1), (short)0, MX_NJ1 * 1024, 0x00020000),
-                  __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(f2), (short)0, MX_NJ2 * 1024, 0x00020000)};
+// lane (i = lane & 15, h = lane >> 4): fragment j at t + 16 (40 - j)
+__device__ __forceinline__ MxConsts mx_consts(const uint8_t* img, int lane) {
+  const int off = (lane & 15) * MX_TAB_STRIDE + 16 * (lane >> 4);
+  return MxConsts{img + off, img + MX_TAB_BYTES + off};
 }
 
 // radix-2^28 digit (two's complement, |x| < 2^28) -> 4 radix-2^7 digits, one per
@@ -150,12 +164,11 @@ __device__ __forceinline__ void mx_split(const mx_v4i c, int add, int& lo_sum, i
 // blocks O0 <= o < O1; Toeplitz block j (1 KB of fragments) is loaded once and
 // used for every kb it pairs with (one load ahead of its MFMAs)
 template <int NJ, int O0, int O1>
-__device__ __forceinline__ void mx_toeplitz(mx_v4i (&acc)[O1 - O0], __amdgpu_buffer_rsrc_t f,
+__device__ __forceinline__ void mx_toeplitz(mx_v4i (&acc)[O1 - O0], const uint8_t* f,
                                             const mx_v4i (&bf)[MX_KB], int lane) {
-  // buffer loads: lane offset in one VGPR, block offset a constant (no 64-bit
-  // per-block addresses held live across the exponentiation loop)
+  // one ds_read_b128 per block: lane base in a VGPR, block offset an immediate
   auto ld = [&](int j) __attribute__((always_inline)) {
-    return (mx_v4i)__builtin_amdgcn_raw_buffer_load_b128(f, lane * 16, j * 1024, 0);
+    return *reinterpret_cast<const mx_v4i*>(f + 16 * (40 - j));
   };
   static_for<0, O1 - O0>([&](auto oc) { acc[decltype(oc)::value] = mx_v4i{0, 0, 0, 0}; });
   // first and last Toeplitz block with an MFMA in this chunk
@@ -166,6 +179,9 @@ __device__ __forceinline__ void mx_toeplitz(mx_v4i (&acc)[O1 - O0], __amdgpu_buf
     constexpr int j = decltype(jc)::value;
     const mx_v4i fj = fnext;
     if constexpr (j + 1 <= JHI) fnext = ld(j + 1);
+    // the next block's read stays one block ahead: ALU and MFMA may move
+    // across, LDS reads may not (hoisting them all costs 4 VGPRs per block)
+    __builtin_amdgcn_sched_barrier(0x000F);
     static_for<0, MX_KB>([&](auto kc) {
       constexpr int kb = decltype(kc)::value;
       constexpr int o = j + 4 * kb;
@@ -174,43 +190,63 @@ __device__ __forceinline__ void mx_toeplitz(mx_v4i (&acc)[O1 - O0], __amdgpu_buf
   });
 }
 
-// A <- A * B * R^-1 + m (mod-m class preserved; result in (m/2, 3m/2) for A, B < 2m),
-// B's row (2B for squarings) at r1 + g * MX_ROW. r0 / r1: this wavefront's rows,
-// md: m's 148 radix-2^28 digits (LDS).
+// 4x4 transpose between the register index and the lane quarter (h): on return
+// y[i] in lane (n, h) is x[h] of lane (n, i). Two permlane32 and two permlane16
+// swaps (gfx950), no LDS.
+__device__ __forceinline__ mx_v4i mx_transpose4(uint32_t x0, uint32_t x1, uint32_t x2, uint32_t x3) {
+  auto r02 = __builtin_amdgcn_permlane32_swap(x0, x2, false, false);
+  auto r13 = __builtin_amdgcn_permlane32_swap(x1, x3, false, false);
+  auto r01 = __builtin_amdgcn_permlane16_swap(r02[0], r13[0], false, false);
+  auto r23 = __builtin_amdgcn_permlane16_swap(r02[1], r13[1], false, false);
+  return mx_v4i{(int)r01[0], (int)r01[1], (int)r23[0], (int)r23[1]};
+}
+
+// A <- A * B * R^-1 + m (mod-m class preserved; result in (m/2, 3m/2) for A, B < 2m).
+// rows: this wavefront's 16 operand rows (MX_ROW words each); operand g's row
+// holds B (2B for squarings) on entry and is the scratch of the whole product:
+// T's low digits overwrite B as the loop consumes it, then T's high digits + m,
+// then U + m. md: m's 148 radix-2^28 digits (LDS).
 template <bool SQR, bool B2IN>
-__device__ __forceinline__ void montmul_mx(uint32_t (&A)[MX_K], uint32_t* r0, uint32_t* r1, const uint32_t* md,
+__device__ __forceinline__ void montmul_mx(uint32_t (&A)[MX_K], uint32_t* rows, const uint32_t* md,
                                            const MxConsts& c, int lane) {
   const int g = lane >> 2, p = lane & 3;  // block layout
   const int n = lane & 15, h = lane >> 4;  // MFMA layout
-  // ---- T = A B on the VALU: low digits -> R0, high digits -> A
-  mx_product<MX_K, SQR, B2IN>(A, r1 + g * MX_ROW, r0 + g * MX_ROW, p);
+  uint32_t* rg = rows + g * MX_ROW;
+  uint32_t* rn = rows + n * MX_ROW;
+  // ---- T = A B on the VALU: low digits -> the row (behind the multiplier digits
+  // the loop has read), high digits -> A
+#ifndef MPCX_MX_TIMING
+#define MPCX_MX_TIMING 0  // microbench builds only: 1 = product loop alone, 2 = reduction alone
+#endif
+  if constexpr (MPCX_MX_TIMING != 2) mx_product<MX_K, SQR, B2IN>(A, rg, rg, p);
+  if constexpr (MPCX_MX_TIMING == 1) return;
   wave_lds_fence();
   // ---- T's low half as B fragments (radix-2^7 bytes)
   mx_v4i bf[MX_KB];
-  const uint32_t* rn0 = r0 + n * MX_ROW;
   static_for<0, MX_KB>([&](auto kc) {
     constexpr int kb = decltype(kc)::value;
     mx_v4i v = {0, 0, 0, 0};
-    if (kb < MX_KB - 1 || h == 0) v = *reinterpret_cast<const mx_v4i*>(rn0 + 16 * kb + 4 * h);
+    if (kb < MX_KB - 1 || h == 0) v = *reinterpret_cast<const mx_v4i*>(rn + 16 * kb + 4 * h);
     bf[kb] = v;
   });
-  const int t147 = (int)rn0[MX_L - 1];  // T's digit 147: positions 588..591 of the carry estimate
+  const int t147 = (int)rn[MX_L - 1];  // T's digit 147: positions 588..591 of the carry estimate
   static_for<0, MX_KB>([&](auto kc) {
     constexpr int kb = decltype(kc)::value;
 #pragma unroll
     for (int i = 0; i < 4; ++i) bf[kb][i] = (int)mx_spread7((uint32_t)bf[kb][i]);
   });
   wave_lds_fence();
-  // ---- R0 <- T's high digits + m (block layout)
+  // ---- the row <- T's high digits + m (block layout)
 #pragma unroll
-  for (int k = 0; k < MX_K; ++k) r0[g * MX_ROW + p * MX_K + k] = A[k] + md[p * MX_K + k];
-  // ---- q column sums (o = j + 4 kb; two chunks of output blocks bound the
-  // live accumulators), then balanced radix-2^28 digits with one carry step,
-  // as bytes -> R1 (MFMA layout)
+  for (int k = 0; k < MX_K; ++k) rg[p * MX_K + k] = A[k] + md[p * MX_K + k];
+  // ---- q column sums (o = j + 4 kb; chunks of output blocks bound the live
+  // accumulators), balanced radix-2^28 digits with one carry step, as bytes;
+  // every 4 blocks transposed in registers into one B fragment of phase 2
+  mx_v4i qf[MX_KB];
   {
-    uint32_t* rn1 = r1 + n * MX_ROW;
     int xprev = 0;
-    auto norm = [&](const mx_v4i& cs, int o) __attribute__((always_inline)) {
+    uint32_t X[4] = {0u, 0u, 0u, 0u};
+    auto norm = [&](const mx_v4i& cs) __attribute__((always_inline)) -> uint32_t {
       int lo_sum, hi_sum;
       mx_split(cs, 1 << 27, lo_sum, hi_sum);
       const int lo = (lo_sum & (int)M28) - (1 << 27);
@@ -218,33 +254,31 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[MX_K], uint32_t* r0, ui
       const int x = mx_from_prev_quarter(hi, lane);
       const int e = lo + (h == 0 ? xprev : x);
       xprev = x;
-      rn1[4 * o + h] = mx_spread7((uint32_t)e);
+      return mx_spread7((uint32_t)e);
     };
     auto chunk = [&](auto o0c, auto o1c) __attribute__((always_inline)) {
       constexpr int O0 = decltype(o0c)::value, O1 = decltype(o1c)::value;
       mx_v4i acc[O1 - O0];
-      mx_toeplitz<MX_NJ1, O0, O1>(acc, c.f1, bf, lane);
-      static_for<0, O1 - O0>([&](auto oc) { norm(acc[decltype(oc)::value], O0 + decltype(oc)::value); });
+      mx_toeplitz<MX_NJ1, O0, O1>(acc, c.t1, bf, lane);
+      static_for<0, O1 - O0>([&](auto oc) {
+        constexpr int o = O0 + decltype(oc)::value;
+        X[o & 3] = norm(acc[decltype(oc)::value]);
+        if constexpr ((o & 3) == 3) {
+          qf[o >> 2] = mx_transpose4(X[0], X[1], X[2], X[3]);
+        } else if constexpr (o == MX_O1 - 1) {
+          qf[o >> 2] = mx_transpose4(X[0], (o & 3) >= 1 ? X[1] : 0u, (o & 3) >= 2 ? X[2] : 0u, 0u);
+        }
+      });
       __builtin_amdgcn_sched_barrier(0);  // one chunk's accumulators live at a time
     };
     chunk(std::integral_constant<int, 0>{}, std::integral_constant<int, MX_C1A>{});
     chunk(std::integral_constant<int, MX_C1A>{}, std::integral_constant<int, MX_C1B>{});
     chunk(std::integral_constant<int, MX_C1B>{}, std::integral_constant<int, MX_O1>{});
   }
-  wave_lds_fence();
-  // ---- q's bytes as B fragments
-  const uint32_t* rn1c = r1 + n * MX_ROW;
-  static_for<0, MX_KB>([&](auto kc) {
-    constexpr int kb = decltype(kc)::value;
-    mx_v4i v = {0, 0, 0, 0};
-    if (kb < MX_KB - 1 || h == 0) v = *reinterpret_cast<const mx_v4i*>(rn1c + 16 * kb + 4 * h);
-    bf[kb] = v;
-  });
-  // ---- q m column sums for positions 576..1183, in two chunks; block 36 gives
-  // the carry out of the low half (lane h = 3), blocks 37.. the digits
-  // d = 4 (o - 37) + h of U + m, adding T's high digit + m from R0
+  // ---- q m column sums for positions 576..1183, in chunks; block 36 gives the
+  // carry out of the low half (lane h = 3), blocks 37.. the digits
+  // d = 4 (o - 37) + h of U + m, adding T's high digit + m from the row
   {
-    uint32_t* rn0w = r0 + n * MX_ROW;
     int xprev = 0;
     auto emit = [&](const mx_v4i& cs, int o) __attribute__((always_inline)) {
       int lo_sum, hi_sum;
@@ -255,7 +289,7 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[MX_K], uint32_t* r0, ui
         return;
       }
       const int d = 4 * (o - MX_O2LO - 1) + h;
-      mx_split(cs, (int)rn0w[d], lo_sum, hi_sum);
+      mx_split(cs, (int)rn[d], lo_sum, hi_sum);
       const int hi = hi_sum + (lo_sum >> 28);
       const int x = mx_from_prev_quarter(hi, lane);
       const int cin = h == 0 ? xprev : x;
@@ -263,12 +297,12 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[MX_K], uint32_t* r0, ui
       int u = (lo_sum & (int)M28) + cin;
       // the top digit keeps its carry (the value is < 2m < 2^4097)
       if (o == MX_O2HI - 1 && h == 3) u = (int)((uint32_t)lo_sum + ((uint32_t)hi_sum << 28)) + cin;
-      rn0w[d] = (uint32_t)u;
+      rn[d] = (uint32_t)u;
     };
     auto chunk = [&](auto o0c, auto o1c) __attribute__((always_inline)) {
       constexpr int O0 = decltype(o0c)::value, O1 = decltype(o1c)::value;
       mx_v4i acc[O1 - O0];
-      mx_toeplitz<MX_NJ2, O0, O1>(acc, c.f2, bf, lane);
+      mx_toeplitz<MX_NJ2, O0, O1>(acc, c.t2, qf, lane);
       static_for<0, O1 - O0>([&](auto oc) { emit(acc[decltype(oc)::value], O0 + decltype(oc)::value); });
       __builtin_amdgcn_sched_barrier(0);
     };
@@ -279,7 +313,7 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[MX_K], uint32_t* r0, ui
   wave_lds_fence();
   // ---- back to the block layout; signed carry passes until every digit is >= 0
 #pragma unroll
-  for (int k = 0; k < MX_K; ++k) A[k] = r0[g * MX_ROW + p * MX_K + k];
+  for (int k = 0; k < MX_K; ++k) A[k] = rg[p * MX_K + k];
   for (int it = 0; it < MX_L + 2; ++it) {
     const int top = (int)A[MX_K - 1];
     const int ctop = (p == MX_P - 1) ? 0 : (top >> DB);

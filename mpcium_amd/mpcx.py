@@ -175,12 +175,12 @@ def copy_stats() -> dict:
     return {"direct_bytes": v[0].value, "bounced_bytes": v[1].value, "bounce_allocs": v[2].value}
 
 
-MX_TABLE_BYTES = (37 + 41) * 1024
+MX_TABLE_BYTES = 2 * 16 * 720
 
 
 def mx_tables(m: int) -> bytes:
-    """mpcx_mx_tables: k_modexp_mx's Toeplitz fragments of m'' = -m^-1 mod 2^4144
-    and of m (host-only, no device needed)."""
+    """mpcx_mx_tables: the LDS image of k_modexp_mx's Toeplitz tables of
+    m'' = -m^-1 mod 2^4144 and of m (host-only, no device needed)."""
     w = int_to_words(m, 128)
     out = ctypes.create_string_buffer(MX_TABLE_BYTES)
     _check(lib().mpcx_mx_tables(w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 128, out, MX_TABLE_BYTES))

@@ -24,16 +24,25 @@ def digits(v, n, bits):
     return [(v >> (bits * i)) & ((1 << bits) - 1) for i in range(n)]
 
 
-def toeplitz(v7, nj):
-    out = bytearray(nj * 64 * 16)
-    for j in range(nj):
-        for lane in range(64):
-            i, h = lane & 15, lane >> 4
-            for e in range(16):
-                idx = 16 * j + i - 16 * h - e
-                if 0 <= idx < len(v7):
-                    out[(j * 64 + lane) * 16 + e] = v7[idx]
+STRIDE = 720
+
+
+def lds_table(v7):
+    """16 row copies of the reversed digit string: copy_i[x] = v7[640 - x + i]."""
+    out = bytearray(16 * STRIDE)
+    for i in range(16):
+        for x in range(STRIDE):
+            idx = 640 - x + i
+            if 0 <= idx < len(v7):
+                out[i * STRIDE + x] = v7[idx]
     return bytes(out)
+
+
+def fragment(tab, j, lane):
+    """The 16 bytes lane (i, h) reads for Toeplitz block j (mx_toeplitz)."""
+    i, h = lane & 15, lane >> 4
+    off = i * STRIDE + 16 * (40 - j + h)
+    return tab[off:off + 16]
 
 
 def i32(x):
@@ -103,8 +112,18 @@ def test_mx_tables_match_restatement(seed):
     for bits in (4096, 4095, 3001):
         m = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
         m2 = (-pow(m, -1, R)) % R
-        want = toeplitz(digits(m2, 592, 7), 37) + toeplitz(digits(m, 592, 7), 41)
-        assert mpcx.mx_tables(m) == want
+        v2, v1 = digits(m2, 592, 7), digits(m, 592, 7)
+        img = mpcx.mx_tables(m)
+        assert img == lds_table(v2) + lds_table(v1)
+        # each lane's read is the Toeplitz row it stands for: byte e of lane (i, h)
+        # in block j = v7[16 j + i - 16 h - e]
+        for tab, v7, nj in ((img[:16 * STRIDE], v2, 37), (img[16 * STRIDE:], v1, 41)):
+            for j in (0, 1, nj // 2, nj - 1):
+                for lane in (0, 5, 17, 33, 63):
+                    i, h = lane & 15, lane >> 4
+                    want = bytes(v7[16 * j + i - 16 * h - e] if 0 <= 16 * j + i - 16 * h - e < 592 else 0
+                                 for e in range(16))
+                    assert fragment(tab, j, lane) == want
 
 
 def test_mx_tables_reject_even_modulus():

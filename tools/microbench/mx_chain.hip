@@ -14,35 +14,40 @@ __global__ __launch_bounds__(64) void k_mfma_map(const mx_v4i* a, const mx_v4i* 
   c[l] = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[l], b[l], mx_v4i{0, 0, 0, 0}, 0, 0, 0);
 }
 
-// x: count x 148 radix-2^28 digits (< 2m); out: the same after S squarings
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_chain_mx(
-    const uint32_t* x, uint32_t* out, const mx_v4i* f1, const mx_v4i* f2, const uint32_t* md_g, uint32_t S,
-    uint32_t count, uint32_t* dbg) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[MX_LDS_WORDS];
-  uint32_t* r0 = lds;
-  uint32_t* r1 = lds + MX_G * MX_ROW;
-  uint32_t* md = lds + 2 * MX_G * MX_ROW;
-  const int lane = threadIdx.x;
+// x: count x 148 radix-2^28 digits (< 2m); out: the same after S squarings.
+// MX_WG wavefronts per workgroup share the LDS tables (img: mpcx_mx_tables).
+#ifndef MXB_WPE
+#define MXB_WPE 2
+#endif
+__global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(MXB_WPE))) void k_chain_mx(
+    const uint32_t* x, uint32_t* out, const uint32_t* img, const uint32_t* md_g, uint32_t S, uint32_t count,
+    uint32_t* dbg) {
+  __shared__ __attribute__((aligned(16))) uint32_t lds[MX_LDS_WORDS_WG];
+  for (int i = (int)threadIdx.x; i < MX_IMG_BYTES / 4; i += 64 * MX_WG) lds[i] = img[i];
+  for (int i = (int)threadIdx.x; i < MX_L; i += 64 * MX_WG) lds[MX_IMG_BYTES / 4 + i] = md_g[i];
+  __syncthreads();
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  uint32_t* rows = lds + MX_IMG_BYTES / 4 + MX_L + 4 + wave * MX_WAVE_WORDS;
+  const uint32_t* md = lds + MX_IMG_BYTES / 4;
   const int g = lane >> 2, p = lane & 3;
-  for (int i = lane; i < MX_L; i += 64) md[i] = md_g[i];
-  const uint32_t op = blockIdx.x * MX_G + g;
+  const uint32_t blk = blockIdx.x * MX_WG + wave;
+  const uint32_t op = blk * MX_G + g;
   uint32_t A[MX_K];
 #pragma unroll
   for (int k = 0; k < MX_K; ++k) A[k] = op < count ? x[(size_t)op * MX_L + p * MX_K + k] : 0u;
-  const MxConsts c = mx_consts(f1, f2);
-  wave_lds_fence();
+  const MxConsts c = mx_consts(reinterpret_cast<const uint8_t*>(lds), lane);
   for (uint32_t s = 0; s < S; ++s) {
-    lds_store_sqr<MX_K>(r1 + g * MX_ROW, p, A);
+    lds_store_sqr<MX_K>(rows + g * MX_ROW, p, A);
     wave_lds_fence();
-    montmul_mx<true, (bool)MPCX_SQR_B2>(A, r0, r1, md, c, lane);
+    montmul_mx<true, (bool)MPCX_SQR_B2>(A, rows, md, c, lane);
     wave_lds_fence();
   }
   if (op < count) {
 #pragma unroll
     for (int k = 0; k < MX_K; ++k) out[(size_t)op * MX_L + p * MX_K + k] = A[k];
   }
-  if (dbg) {  // the wavefront's rows after the last product (R0: U + m digits, R1: q's bytes)
-    for (int i = lane; i < 2 * MX_G * MX_ROW; i += 64) dbg[(size_t)blockIdx.x * 2 * MX_G * MX_ROW + i] = lds[i];
+  if (dbg && blk == 0) {  // wavefront 0's rows after the last product (U + m digits)
+    for (int i = lane; i < MX_G * MX_ROW; i += 64) dbg[i] = rows[i];
   }
 }
 
@@ -89,8 +94,7 @@ static float timed(hipStream_t s, void (*launch)(hipStream_t, void*), void* arg)
 struct MxArgs {
   const uint32_t* x;
   uint32_t* out;
-  const mx_v4i* f1;
-  const mx_v4i* f2;
+  const uint32_t* img;
   const uint32_t* md;
   uint32_t S, count;
   uint32_t* dbg;
@@ -110,16 +114,16 @@ int mxb_mfma_map(const void* a, const void* b, void* c) {
 }
 
 // returns milliseconds (< 0 on a launch error)
-float mxb_chain_mx(const void* x, void* out, const void* f1, const void* f2, const void* md, uint32_t S,
-                   uint32_t count, void* dbg) {
-  MxArgs a{(const uint32_t*)x, (uint32_t*)out,       (const mx_v4i*)f1, (const mx_v4i*)f2, (const uint32_t*)md, S, count,
-           (uint32_t*)dbg};
+float mxb_chain_mx(const void* x, void* out, const void* img, const void* md, uint32_t S, uint32_t count,
+                   void* dbg) {
+  MxArgs a{(const uint32_t*)x, (uint32_t*)out, (const uint32_t*)img, (const uint32_t*)md, S, count, (uint32_t*)dbg};
   const float ms = timed(
       nullptr,
       [](hipStream_t s, void* v) {
         const MxArgs& a = *(const MxArgs*)v;
-        hipLaunchKernelGGL(k_chain_mx, dim3((a.count + MX_G - 1) / MX_G), dim3(64), 0, s, a.x, a.out, a.f1, a.f2, a.md,
-                           a.S, a.count, a.dbg);
+        const uint32_t waves = (a.count + MX_G - 1) / MX_G;
+        hipLaunchKernelGGL(k_chain_mx, dim3((waves + MX_WG - 1) / MX_WG), dim3(64 * MX_WG), 0, s, a.x, a.out, a.img,
+                           a.md, a.S, a.count, a.dbg);
       },
       &a);
   return hipGetLastError() == hipSuccess ? ms : -1.f;

@@ -20,6 +20,9 @@ import sys
 
 import torch
 
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", ".."))
+from mpcium_amd import mpcx  # noqa: E402  (mpcx_mx_tables: host-only)
+
 HERE = os.path.dirname(os.path.abspath(__file__))
 L, DB = 148, 28
 RBITS = L * DB
@@ -94,17 +97,16 @@ def debug(lib, dev, rng):
     m = rng.getrandbits(4096) | (1 << 4095) | 1
     R = 1 << RBITS
     m2 = (-pow(m, -1, R)) % R
-    f1d = torch.frombuffer(bytearray(toeplitz(digits(m2, 592, 7), NJ1)), dtype=torch.uint8).to(dev)
-    f2d = torch.frombuffer(bytearray(toeplitz(digits(m, 592, 7), NJ2)), dtype=torch.uint8).to(dev)
+    imgd = torch.frombuffer(bytearray(mpcx.mx_tables(m)), dtype=torch.uint8).to(dev)
     md = torch.tensor(digits(m, L, DB), dtype=torch.int64).to(torch.int32).to(dev)
     xs = [rng.randrange(m) for _ in range(16)]
     xd = torch.tensor([digits(v, L, DB) for v in xs], dtype=torch.int64).to(torch.int32).to(dev)
     out = torch.zeros_like(xd)
-    dbg = torch.zeros(2 * 16 * L, dtype=torch.int32, device=dev)
+    dbg = torch.zeros(16 * L, dtype=torch.int32, device=dev)
     vp = lambda t: ctypes.c_void_p(t.data_ptr())
-    lib.mxb_chain_mx(vp(xd), vp(out), vp(f1d), vp(f2d), vp(md), 1, 16, vp(dbg))
+    lib.mxb_chain_mx(vp(xd), vp(out), vp(imgd), vp(md), 1, 16, vp(dbg))
     torch.cuda.synchronize()
-    rows = (dbg.cpu().to(torch.int64) & 0xFFFFFFFF).view(2, 16, L)
+    rows = (dbg.cpu().to(torch.int64) & 0xFFFFFFFF).view(1, 16, L)
     rep = []
     for n in range(4):
         e, u = model_step(xs[n], xs[n], m, m2)
@@ -114,7 +116,7 @@ def debug(lib, dev, rng):
             for msk in (0xFFFFFF80, 0xFFFF8000, 0xFF800000):
                 x = (x + (x & msk)) & 0xFFFFFFFF
             qw.append(x)
-        got_q = rows[1, n].tolist()
+        got_q = qw  # q stays in registers (permlane transposes)
         got_u = [v - (1 << 32) if v >= 1 << 31 else v for v in rows[0, n].tolist()]
         bq = [d for d in range(L) if got_q[d] != qw[d]]
         bu = [d for d in range(L) if got_u[d] != u[d]]
@@ -127,7 +129,7 @@ def debug(lib, dev, rng):
 def main():
     count = int(sys.argv[1]) if len(sys.argv) > 1 else 65536
     S = int(sys.argv[2]) if len(sys.argv) > 2 else 64
-    lib = ctypes.CDLL(os.path.join(HERE, "mx_chain.so"))
+    lib = ctypes.CDLL(os.path.join(HERE, os.environ.get("MX_CHAIN_SO", "mx_chain.so")))
     lib.mxb_chain_mx.restype = ctypes.c_float
     lib.mxb_chain_cios.restype = ctypes.c_float
     dev = torch.device("cuda:0")
@@ -159,10 +161,7 @@ def main():
     m = rng.getrandbits(4096) | (1 << 4095) | 1
     R = 1 << RBITS
     m2 = (-pow(m, -1, R)) % R
-    f1 = toeplitz(digits(m2, 592, 7), NJ1)
-    f2 = toeplitz(digits(m, 592, 7), NJ2)
-    f1d = torch.frombuffer(bytearray(f1), dtype=torch.uint8).to(dev)
-    f2d = torch.frombuffer(bytearray(f2), dtype=torch.uint8).to(dev)
+    imgd = torch.frombuffer(bytearray(mpcx.mx_tables(m)), dtype=torch.uint8).to(dev)
     md = torch.tensor(digits(m, L, DB), dtype=torch.int64).to(torch.int32).to(dev)
     n0inv = (-pow(m, -1, 1 << DB)) % (1 << DB)
 
@@ -175,9 +174,9 @@ def main():
     o_ci = torch.zeros_like(xd)
     vp = lambda t: ctypes.c_void_p(t.data_ptr())
     # warm-up, then timed
-    lib.mxb_chain_mx(vp(xd), vp(o_mx), vp(f1d), vp(f2d), vp(md), 2, count, None)
+    lib.mxb_chain_mx(vp(xd), vp(o_mx), vp(imgd), vp(md), 2, count, None)
     lib.mxb_chain_cios(vp(xd), vp(o_ci), vp(md), n0inv, 2, count)
-    t_mx = lib.mxb_chain_mx(vp(xd), vp(o_mx), vp(f1d), vp(f2d), vp(md), S, count, None)
+    t_mx = lib.mxb_chain_mx(vp(xd), vp(o_mx), vp(imgd), vp(md), S, count, None)
     t_ci = lib.mxb_chain_cios(vp(xd), vp(o_ci), vp(md), n0inv, S, count)
     torch.cuda.synchronize()
     omx, oci = o_mx.cpu().to(torch.int64) & 0xFFFFFFFF, o_ci.cpu().to(torch.int64) & 0xFFFFFFFF
