@@ -178,6 +178,58 @@ def gpu_index() -> int:
     import torch
     return int(os.environ.get("LOCAL_RANK", "0")) % max(1, torch.cuda.device_count())
 
+PEAK_I8_MFMA = 256 * 4 * 1024 * 2.4e9  # 2.5 P i8 MAC/s dense: 16x16x64 i8 = 16 cycles per SIMD
+
+
+def sliding_window_counts(e: int, width: int = 6):
+    """(squarings, table products, window products) of a left-to-right sliding
+    window over e with windows of up to `width` bits (k_expsched's schedule shape)."""
+    bits = bin(e)[2:]
+    i, sq, wins, top = 0, 0, 0, 0
+    first = True
+    while i < len(bits):
+        if bits[i] == "0":
+            sq += 0 if first else 1
+            i += 1
+            continue
+        j = min(len(bits), i + width)
+        while bits[j - 1] == "0":
+            j -= 1
+        v = int(bits[i:j], 2)
+        top = max(top, v)
+        if first:
+            first = False
+        else:
+            sq += j - i
+            wins += 1
+        i = j
+    return sq, (top - 1) // 2 + 1, wins
+
+
+def mx_floor(count: int, e: int, kernel_ms: float) -> dict:
+    """Resource floor of the work k_modexp_mx EXECUTES for count x x^e mod a 4096-bit
+    modulus: the product loop's v_mad_u64_u32 lane-MADs (148 iterations x 19 per lane
+    for a squaring, x 37 for a product, 4 lanes per operand) at the INT32 MAD peak,
+    and the reduction's i8 MACs (417 16x16x64 MFMAs per 16 operands per product) at
+    the dense i8 matrix peak. Everything else the kernel issues (carries, radix
+    conversions, normalisation, LDS traffic) is overhead over this floor."""
+    sq, tab, wins = sliding_window_counts(e)
+    sq += 1                      # x^2 R for the odd-power chain
+    prods = 1 + (tab - 1) + wins  # x R, the odd powers, the window multiplies (the exit runs on the CIOS loop)
+    valu = count * (sq * 148 * 19 * 4 + prods * 148 * 37 * 4)
+    i8 = count * (sq + prods) * 417 * 16384 / 16
+    t_valu, t_mfma = valu / PEAK_INT32_NOMINAL, i8 / PEAK_I8_MFMA
+    floor = max(t_valu, t_mfma)
+    return {"kernel": "k_modexp_mx (Montgomery reduction on v_mfma_i32_16x16x64_i8, mpcx_mx.hpp)",
+            "squarings": sq, "products": prods, "valu_lane_mads": valu, "mfma_i8_macs": i8,
+            "floor_ms_valu": t_valu * 1e3, "floor_ms_mfma": t_mfma * 1e3,
+            "frac_of_floor": floor / (kernel_ms * 1e-3),
+            "note": "frac_of_floor = the executed work's resource floor (its MADs at the INT32 MAD peak, "
+                    "its i8 MACs at the dense i8 MFMA peak, whichever is longer) over the launch time; the "
+                    "headline frac keeps the rounds' algorithmic definition (Go-equivalent 32-bit MACs at the "
+                    "INT32 MAD peak), which the matrix cores let exceed what a VALU-only kernel could reach"}
+
+
 def alg_macs(mod_bits: int, exp_bits: int) -> float:
     """W = (E + ceil(E/4)) * 2 L^2 32-bit MACs, L = 32-bit limbs."""
     L = math.ceil(mod_bits / 32)
@@ -1477,6 +1529,11 @@ def main():
         "cpu_baseline": None,
     }
     result["roofline"].update(pmc_traffic(count, args.modbits, mod))
+    mx_on = (args.modbits == 4096 and (mod.P, mod.K) == (4, 37) and mpcx.get_option("mx") == 1
+             and count >= mpcx.get_option("mx_min"))
+    result["roofline"]["kernel"] = "k_modexp_mx" if mx_on else "k_modexp<4, 37, 16, 2>"
+    if mx_on:
+        result["roofline"]["executed_floor"] = mx_floor(count, N, kernel_ms)
     if step_ms:
         srt = sorted(step_ms)
         q = max(1, len(step_ms) // 4)

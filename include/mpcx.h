@@ -418,6 +418,9 @@ int mpcx_sync(void* stream);
  * default 6: execution lanes per device), MPCX_GEOM_POLICY, MPCX_NARROW_ROUNDS,
  * MPCX_PRIME_COOP, MPCX_FB_WINDOW. */
 int mpcx_set_option(const char* key, int value);
+/* Current value of "mx", "mx_min", "geom_policy", "sched_width", "fixed_window",
+ * "fb_split" or "lanes" (benchmarks record which kernel path ran). */
+int mpcx_get_option(const char* key, int* value);
 
 /* The constant tables of k_modexp_mx (the 4096-bit main geometry with its
  * Montgomery reduction on the i8 matrix cores, mpcium_amd/csrc/mpcx_mx.hpp) for

@@ -125,7 +125,7 @@ uint32_t g_split_min = 4096;             // mpcx_set_option("device_split_min", 
 bool g_prime_coop = true;                // mpcx_set_option("prime_coop", 0): thread-per-candidate prime kernels
 bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 1): test hook, see below
 #ifndef MPCX_MX_DEFAULT
-#define MPCX_MX_DEFAULT 0
+#define MPCX_MX_DEFAULT 1
 #endif
 int g_mx = MPCX_MX_DEFAULT;              // mpcx_set_option("mx", 1): geometry-2 batches reduce on the matrix cores
 uint32_t g_mx_min = 2048;                // mpcx_set_option("mx_min", n): smallest batch for k_modexp_mx
@@ -1130,6 +1130,29 @@ uint32_t fb_split_for(const Device& dev, uint32_t blocks) {
 extern "C" {
 
 int mpcx_version(void) { return 200; }
+
+int mpcx_get_option(const char* key, int* value) {
+  if (!key || !value) return fail(MPCX_EINVAL, "null option or output");
+  std::lock_guard<std::mutex> lk(g_mu);
+  if (std::strcmp(key, "mx") == 0) {
+    *value = g_mx;
+  } else if (std::strcmp(key, "mx_min") == 0) {
+    *value = (int)g_mx_min;
+  } else if (std::strcmp(key, "geom_policy") == 0) {
+    *value = g_geom_policy;
+  } else if (std::strcmp(key, "sched_width") == 0) {
+    *value = g_sched_width;
+  } else if (std::strcmp(key, "fixed_window") == 0) {
+    *value = g_fixed_win;
+  } else if (std::strcmp(key, "fb_split") == 0) {
+    *value = g_fb_split;
+  } else if (std::strcmp(key, "lanes") == 0) {
+    *value = g_lanes.load();
+  } else {
+    return fail(MPCX_EINVAL, "option %s cannot be read", key);
+  }
+  return MPCX_OK;
+}
 
 int mpcx_set_option(const char* key, int value) {
   if (!key) return fail(MPCX_EINVAL, "null option");

@@ -106,6 +106,13 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
   uint32_t bnext = bl[0];
+#ifndef MPCX_MX_EMIT_REG
+#define MPCX_MX_EMIT_REG 0  // 1: T's low digits gathered in registers, stored once per block
+#endif
+#if MPCX_MX_EMIT_REG
+  uint32_t em[K];
+  const uint32_t shmask = p == 0 ? 0u : M28;
+#endif
 #pragma nounroll
   for (int o = 0; o < P; ++o) {
     const uint32_t* bo = bl + o * K;
@@ -132,12 +139,24 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
       });
       const uint64_t a0 = acc[u];
       acc[(u + 1) % K] += a0 >> DB;
-      const uint32_t lo = (uint32_t)a0 & M28;
       // lane 0's digit leaves the window as T's digit i (in CIOS it is zero);
       // it must not shift into the previous group's top slot
+#if MPCX_MX_EMIT_REG
+      em[u] = (uint32_t)a0;
+      acc[u] = from_next_lane((uint32_t)a0 & shmask);
+#else
+      const uint32_t lo = (uint32_t)a0 & M28;
       if (p == 0) to[u] = lo;
       acc[u] = from_next_lane(p == 0 ? 0u : lo);
+#endif
     });
+#if MPCX_MX_EMIT_REG
+    // the block's 37 digits of T, written once under one exec mask
+    if (p == 0) {
+#pragma unroll
+      for (int u = 0; u < K; ++u) to[u] = em[u] & M28;
+    }
+#endif
   }
   carry_pass64<P, K>(acc);
   const uint32_t ctop = (uint32_t)(acc[K - 1] >> DB);

@@ -24,6 +24,7 @@ _vp = ctypes.c_void_p
 SIGNATURES = [
     ("mpcx_version", ctypes.c_int, []),
     ("mpcx_set_option", ctypes.c_int, [ctypes.c_char_p, ctypes.c_int]),
+    ("mpcx_get_option", ctypes.c_int, [ctypes.c_char_p, ctypes.POINTER(ctypes.c_int)]),
     ("mpcx_last_error", ctypes.c_char_p, []),
     ("mpcx_device_count", ctypes.c_int, [ctypes.POINTER(ctypes.c_int)]),
     ("mpcx_init", ctypes.c_int, [ctypes.c_int]),
@@ -193,6 +194,12 @@ def select_device(index: int):
 
 def set_option(key: str, value: int):
     _check(lib().mpcx_set_option(key.encode(), int(value)))
+
+
+def get_option(key: str) -> int:
+    v = ctypes.c_int(0)
+    _check(lib().mpcx_get_option(key.encode(), ctypes.byref(v)))
+    return v.value
 
 
 def shutdown():

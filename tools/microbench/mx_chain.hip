@@ -36,6 +36,12 @@ __global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(MXB_
 #pragma unroll
   for (int k = 0; k < MX_K; ++k) A[k] = op < count ? x[(size_t)op * MX_L + p * MX_K + k] : 0u;
   const MxConsts c = mx_consts(reinterpret_cast<const uint8_t*>(lds), lane);
+#ifdef MXB_STAGGER
+  // the workgroup's second half (sharing SIMDs with the first) starts later, so
+  // one wave's matrix-core phase meets the other's VALU product loop
+  if (wave >= MX_WG / 2)
+    for (int i = 0; i < MXB_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
+#endif
   for (uint32_t s = 0; s < S; ++s) {
     lds_store_sqr<MX_K>(rows + g * MX_ROW, p, A);
     wave_lds_fence();
