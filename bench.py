@@ -40,10 +40,11 @@ PEAK_MAD_MEASURED = 33.8e12            # tools/microbench/valu_rates.hip, 8 wave
 
 
 
-PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc", "config2_traffic.json")
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc", "config2_traffic.json")        # k_modexp<4, 37, 16, 2>
+PMC_TRAFFIC_MX = os.path.join(ROOT, "profiles", "r05", "pmc_mx", "config2_traffic.json")  # k_modexp_mx
 
 
-def pmc_traffic(count: int, modbits: int, mod) -> dict:
+def pmc_traffic(count: int, modbits: int, mod, mx: bool = False) -> dict:
     """roofline.traffic: fabric bytes per launch of the bench kernel from the
     committed rocprofv3 FETCH_SIZE and WRITE_SIZE passes (separate --pmc runs of
     the bench command over the current kernel, tools/gpu.sh pmc). rocprofv3 cannot run
@@ -54,13 +55,14 @@ def pmc_traffic(count: int, modbits: int, mod) -> dict:
     (DESIGN.md 5.4); the memory-side counters include Infinity-Cache hits, so
     this is an upper bound on HBM bytes."""
     out = {"traffic": None, "traffic_unit": "bytes/launch", "algorithmic_io_bytes": count * 2 * modbits // 8}
-    if count != 65536 or modbits != 4096 or (mod.P, mod.K) != (4, 37) or not os.path.exists(PMC_TRAFFIC):
+    path = PMC_TRAFFIC_MX if mx else PMC_TRAFFIC
+    if count != 65536 or modbits != 4096 or (mod.P, mod.K) != (4, 37) or not os.path.exists(path):
         return out
-    with open(PMC_TRAFFIC) as f:
+    with open(path) as f:
         s = json.load(f)
     out["traffic"] = s["hbm_bytes_per_launch"]
-    out["traffic_source"] = (os.path.relpath(PMC_TRAFFIC, ROOT) + " (2 x FETCH_SIZE + WRITE_SIZE: the counters' "
-                             "calibration on this access width, tools/microbench/fetch_calib.hip)")
+    out["traffic_source"] = (os.path.relpath(path, ROOT) + f" ({s.get('kernel')}; 2 x FETCH_SIZE + WRITE_SIZE: the "
+                             "counters' calibration on this access width, tools/microbench/fetch_calib.hip)")
     return out
 
 # GPU clock / power / temperature sampler: a separate process (started before
@@ -1528,9 +1530,9 @@ def main():
                      "alg_ops_per_modexp": W, "kernel_ms": kernel_ms},
         "cpu_baseline": None,
     }
-    result["roofline"].update(pmc_traffic(count, args.modbits, mod))
     mx_on = (args.modbits == 4096 and (mod.P, mod.K) == (4, 37) and mpcx.get_option("mx") == 1
              and count >= mpcx.get_option("mx_min"))
+    result["roofline"].update(pmc_traffic(count, args.modbits, mod, mx_on))
     result["roofline"]["kernel"] = "k_modexp_mx" if mx_on else "k_modexp<4, 37, 16, 2>"
     if mx_on:
         result["roofline"]["executed_floor"] = mx_floor(count, N, kernel_ms)
