@@ -393,9 +393,13 @@ int mpcx_sync(void* stream);
  *                launch within 4 wavefronts per SIMD (round 5, three interleaved
  *                rounds vs 1: keygen/reshare 437.6 vs 419.7 sessions/s, signing
  *                7,110 vs 6,874 and 3,225 vs 3,039 sigs/s, profiles/r05/fbsplit).
- *   "mx"         0 or 1: batches of the 4096-bit main geometry (>= "mx_min"
- *                operands, default 2048) run k_modexp_mx, the Montgomery
- *                reduction on the i8 matrix cores (environment: MPCX_MX).
+ *   "mx"         1 (default), 0 or 2: batches of the 4096-bit main geometry
+ *                (>= "mx_min" operands, default 2048) run k_modexp_mx, the
+ *                Montgomery reduction on the i8 matrix cores (round 5: config 2
+ *                457K vs 378K modexp/s, profiles/r05/mx/); 2 adds the 2048-bit
+ *                lane-pair geometry, which measured slower (1.22M vs 1.40M
+ *                2048-bit modexp/s, keygen -7%: profiles/r05/mx/g5/).
+ *                Environment: MPCX_MX.
  *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
  *                thread per candidate.
  *   "lanes"      1..8 (default 6, or MPCX_LANES): execution lanes (streams
@@ -422,12 +426,14 @@ int mpcx_set_option(const char* key, int value);
  * "fb_split" or "lanes" (benchmarks record which kernel path ran). */
 int mpcx_get_option(const char* key, int* value);
 
-/* The constant tables of k_modexp_mx (the 4096-bit main geometry with its
- * Montgomery reduction on the i8 matrix cores, mpcium_amd/csrc/mpcx_mx.hpp) for
- * the odd modulus m (<= 4096 bits): the LDS image of the Toeplitz tables of
- * m'' = -m^-1 mod 2^4144 and of m, 2 x 16 row copies of 720 bytes (23,040
- * bytes). Host-only (no device needed); for tests and tools. */
-int mpcx_mx_tables(const uint32_t* m_words, uint32_t m_len, uint8_t* out, size_t cap);
+/* The constant tables of k_modexp_mx (the 4096- and 2048-bit main geometries
+ * with their Montgomery reduction on the i8 matrix cores,
+ * mpcium_amd/csrc/mpcx_mx.hpp) for the odd modulus m and the geometry's digit
+ * count L (148: R = 2^4144; 74: R = 2^2072; 4m < R): the LDS image of the
+ * Toeplitz tables of m'' = -m^-1 mod R and of m, 2 x 16 row copies of the
+ * reversed radix-2^7 digit strings (23,040 or 13,824 bytes). Host-only (no
+ * device needed); for tests and tools. */
+int mpcx_mx_tables(const uint32_t* m_words, uint32_t m_len, uint32_t L, uint8_t* out, size_t cap);
 
 /* Kernel-class geometry of a modulus (for benchmarks and roofline math):
  * digits L (radix 2^28), lanes per operand P, digits per lane K, operands per

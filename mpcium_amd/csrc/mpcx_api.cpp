@@ -454,13 +454,9 @@ std::vector<uint32_t> to_digits(const std::vector<uint32_t>& w, uint32_t L) {
   return d;
 }
 
-// ---- k_modexp_mx constants (mpcx_mx.hpp): m'' = -m^-1 mod R, R = 2^(28*148), and
-// the Toeplitz fragments of m'' and m for 16x16x64 i8 MFMAs: block j (delta = 16j)
-// is 64 lanes x 16 bytes, lane (i = lane & 15, h = lane >> 4) byte e = radix-2^7
-// digit 16j + i - 16h - e (0 outside [0, 592)).
-constexpr uint32_t kMxWords = 130;  // >= 4144 bits
-constexpr uint32_t kMxDigits7 = 592;
-
+// ---- k_modexp_mx constants (mpcx_mx.hpp): m'' = -m^-1 mod R, R = 2^(28 L), and
+// the LDS image of the Toeplitz tables of m'' and m (MxShape: per table 16 row
+// copies of the reversed radix-2^7 digit string, copy_i[x] = v7[D - x + i]).
 // a * b mod 2^(32 n)
 static void mul_lo(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t n) {
   std::vector<uint64_t> acc(n, 0);
@@ -475,8 +471,25 @@ static void mul_lo(const uint32_t* a, const uint32_t* b, uint32_t* out, uint32_t
   for (uint32_t i = 0; i < n; ++i) out[i] = (uint32_t)acc[i];
 }
 
-static void mx_tables(const std::vector<uint32_t>& m, std::vector<uint8_t>& out) {
-  const uint32_t W = kMxWords;
+// shape constants of the MX geometry with L digits (geometry 2: 148, geometry 5: 74)
+struct MxDims {
+  uint32_t n7, d, stride, img;
+};
+static bool mx_dims(uint32_t L, MxDims* o) {
+  if (L == mpcx::MxG2::L) {
+    *o = {mpcx::MxG2::N7, mpcx::MxG2::D, mpcx::MxG2::TAB_STRIDE, mpcx::MxG2::IMG_BYTES};
+  } else if (L == mpcx::MxG5::L) {
+    *o = {mpcx::MxG5::N7, mpcx::MxG5::D, mpcx::MxG5::TAB_STRIDE, mpcx::MxG5::IMG_BYTES};
+  } else {
+    return false;
+  }
+  return true;
+}
+
+static void mx_tables(const std::vector<uint32_t>& m, uint32_t L, std::vector<uint8_t>& out) {
+  MxDims dm{};
+  (void)mx_dims(L, &dm);
+  const uint32_t W = (kDigitBits * L + 31) / 32;  // words of R = 2^(28 L)
   std::vector<uint32_t> mm(W, 0), x(W, 0), t(W, 0), u(W, 0);
   for (size_t i = 0; i < m.size() && i < W; ++i) mm[i] = m[i];
   uint32_t inv = mm[0];
@@ -496,7 +509,7 @@ static void mx_tables(const std::vector<uint32_t>& m, std::vector<uint8_t>& out)
     for (uint32_t i = 0; i < np; ++i) x[i] = u[i];
     prec = np;
   }
-  // m'' = -x mod 2^(32 W), radix-2^7 digits below 2^4144
+  // m'' = -x mod 2^(32 W); its radix-2^7 digits below R
   uint64_t br = 1;
   for (uint32_t i = 0; i < W; ++i) {
     const uint64_t v = (uint64_t)(uint32_t)~x[i] + br;
@@ -509,24 +522,22 @@ static void mx_tables(const std::vector<uint32_t>& m, std::vector<uint8_t>& out)
     if (wi + 1 < w.size()) v |= (uint64_t)w[wi + 1] << 32;
     return (uint8_t)((v >> sh) & 0x7F);
   };
-  std::vector<uint8_t> n2(kMxDigits7), n1(kMxDigits7);
+  std::vector<uint8_t> n2(dm.n7), n1(dm.n7);
   std::vector<uint32_t> mv(m);
-  for (uint32_t d = 0; d < kMxDigits7; ++d) {
+  for (uint32_t d = 0; d < dm.n7; ++d) {
     n2[d] = d7(x, d);
     n1[d] = d7(mv, d);
   }
-  // the LDS image k_modexp_mx copies (mpcx_mx.hpp): per table 16 row copies of the
-  // reversed digit string, copy_i[x] = v7[640 - x + i] (0 outside [0, 592))
-  out.assign(2u * MPCX_MX_TAB_BYTES, 0);
+  out.assign(dm.img, 0);
   auto fill = [&](const std::vector<uint8_t>& v7, uint8_t* dst) {
     for (int i = 0; i < 16; ++i)
-      for (int x = 0; x < MPCX_MX_TAB_STRIDE; ++x) {
-        const int idx = 640 - x + i;
-        if (idx >= 0 && idx < (int)kMxDigits7) dst[i * MPCX_MX_TAB_STRIDE + x] = v7[idx];
+      for (int xx = 0; xx < (int)dm.stride; ++xx) {
+        const int idx = (int)dm.d - xx + i;
+        if (idx >= 0 && idx < (int)dm.n7) dst[i * dm.stride + xx] = v7[idx];
       }
   };
   fill(n2, out.data());
-  fill(n1, out.data() + MPCX_MX_TAB_BYTES);
+  fill(n1, out.data() + dm.img / 2);
 }
 
 hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st) {
@@ -969,7 +980,7 @@ int mod_const(mpcx_mod_t mod, int di, const uint32_t** out) {
 int mx_const(mpcx_mod_t mod, int di, const uint8_t** out) {
   std::lock_guard<std::mutex> lk(mod->mu);
   if (!mod->d_mx[di]) {
-    if (mod->mx_host.empty()) mx_tables(mod->m, mod->mx_host);
+    if (mod->mx_host.empty()) mx_tables(mod->m, (uint32_t)MPCX_GEOM_L(MPCX_MAIN_GEOM(mod->cls)), mod->mx_host);
     uint8_t* p = nullptr;
     hipError_t e = hipMalloc((void**)&p, mod->mx_host.size());
     if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipMalloc(mx tables): %s", hipGetErrorString(e));
@@ -1178,8 +1189,9 @@ int mpcx_set_option(const char* key, int value) {
     if (value != 0 && value != 1 && value != 2 && value != 4) return fail(MPCX_EINVAL, "fb_split %d not 0/1/2/4", value);
     g_fb_split = value;
   } else if (std::strcmp(key, "mx") == 0) {
-    // 1: batches of the 4096-bit main geometry reduce on the matrix cores (k_modexp_mx)
-    if (value != 0 && value != 1) return fail(MPCX_EINVAL, "mx %d not 0 or 1", value);
+    // 1: batches of the 4096-bit main geometry reduce on the matrix cores (k_modexp_mx);
+    // 2: the 2048-bit lane-pair geometry's as well
+    if (value < 0 || value > 2) return fail(MPCX_EINVAL, "mx %d not 0, 1 or 2", value);
     g_mx = value;
   } else if (std::strcmp(key, "mx_min") == 0) {
     if (value < 1) return fail(MPCX_EINVAL, "mx_min %d < 1", value);
@@ -1244,7 +1256,7 @@ static void read_env_options() {
   const char* fw = std::getenv("MPCX_FB_WINDOW");  // fixed-base comb width of new tables
   if (fw) g_fb_window = std::max(4, std::min(MPCX_FB_MAX_WINDOW_BITS, std::atoi(fw)));
   const char* mx = std::getenv("MPCX_MX");  // geometry-2 batches on k_modexp_mx
-  if (mx) g_mx = mx[0] != '0';
+  if (mx) g_mx = std::max(0, std::min(2, std::atoi(mx)));
 }
 
 int mpcx_init(int device) {
@@ -1432,17 +1444,19 @@ int mpcx_modulus_release(mpcx_mod_t mod) {
   return MPCX_OK;
 }
 
-int mpcx_mx_tables(const uint32_t* m_words, uint32_t m_len, uint8_t* out, size_t cap) {
+int mpcx_mx_tables(const uint32_t* m_words, uint32_t m_len, uint32_t L, uint8_t* out, size_t cap) {
   if (!m_words || !out || m_len == 0) return fail(MPCX_EINVAL, "null modulus or output");
-  const size_t need = 2u * MPCX_MX_TAB_BYTES;
-  if (cap < need) return fail(MPCX_EINVAL, "mx tables need %zu bytes", need);
+  MxDims dm{};
+  if (!mx_dims(L, &dm)) return fail(MPCX_EINVAL, "L %u is not an MX geometry's (148 or 74)", L);
+  if (cap < dm.img) return fail(MPCX_EINVAL, "mx tables need %u bytes", dm.img);
   std::vector<uint32_t> m(m_words, m_words + m_len);
   while (m.size() > 1 && m.back() == 0) m.pop_back();
-  if ((m[0] & 1u) == 0 || bit_length(m) > (uint32_t)MPCX_CLASS_MAXBITS(2))
-    return fail(MPCX_EINVAL, "mx tables need an odd modulus of <= %d bits", MPCX_CLASS_MAXBITS(2));
+  // R = 2^(28 L) > 4m
+  if ((m[0] & 1u) == 0 || bit_length(m) + 2 > kDigitBits * L)
+    return fail(MPCX_EINVAL, "mx tables need an odd modulus of < %u bits", kDigitBits * L - 2);
   std::vector<uint8_t> t;
-  mx_tables(m, t);
-  std::memcpy(out, t.data(), need);
+  mx_tables(m, L, t);
+  std::memcpy(out, t.data(), dm.img);
   return MPCX_OK;
 }
 
@@ -1620,8 +1634,11 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
     a.n0inv = mod->n0inv;
     a.exp_shared = exp_shared ? 1 : 0;
     a.sched = use_sched ? lane.ws + sched_off : nullptr;
-    // the 4096-bit main geometry with the reduction on the matrix cores
-    const bool mx = g_mx && pt.geom == MPCX_MAIN_GEOM(2) && pt.count >= g_mx_min;
+    // the main geometries with the reduction on the matrix cores: the 4096-bit one
+    // (mx >= 1), the 2048-bit lane pair only on request (mx = 2: it measured slower,
+    // profiles/r05/mx/g5/)
+    const bool mx = g_mx && pt.geom == MPCX_MAIN_GEOM(mod->cls) && (pt.geom == 2 || (pt.geom == 5 && g_mx >= 2)) &&
+                    pt.count >= g_mx_min;
     a.nwaves = waves;
     if (mx) {
       const uint8_t* t = nullptr;

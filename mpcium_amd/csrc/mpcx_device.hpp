@@ -367,18 +367,20 @@ namespace mpcx {
 template <int P, int K, int G, bool MX = false>
 __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t blk) {
   constexpr int L = P * K;
-  static_assert(!MX || (P == MX_P && K == MX_K && G == MX_G), "montmul_mx serves geometry 2 only");
+  using S = MxShape<P, K, G>;
+  static_assert(!MX || (P == 4 && K == 37 && G == 16) || (P == 2 && K == 37 && G == 32),
+                "montmul_mx serves geometries 2 and 5");
   // +2: the b prefetch reads up to two past a row; MX: tables, m's digits, rows
-  __shared__ __attribute__((aligned(16))) uint32_t lds_all[MX ? MX_LDS_WORDS_WG : (G + 1) * L + 2];
+  __shared__ __attribute__((aligned(16))) uint32_t lds_all[MX ? S::LDS_WORDS_WG : (G + 1) * L + 2];
   uint32_t* lds = lds_all;
   if constexpr (MX) {
     // the workgroup's tables and m's digits, then the wavefronts part
     const uint32_t* img = static_cast<const uint32_t*>(a.mx_img);
-    for (int i = (int)threadIdx.x; i < MX_IMG_BYTES / 4; i += 64 * MX_WG) lds_all[i] = img[i];
-    for (int i = (int)threadIdx.x; i < MX_L; i += 64 * MX_WG) lds_all[MX_IMG_BYTES / 4 + i] = a.nd[i];
+    for (int i = (int)threadIdx.x; i < S::IMG_BYTES / 4; i += 64 * MX_WG) lds_all[i] = img[i];
+    for (int i = (int)threadIdx.x; i < L; i += 64 * MX_WG) lds_all[S::IMG_BYTES / 4 + i] = a.nd[i];
     __syncthreads();
     if (blk >= a.nwaves) return;  // the last workgroup's spare wavefronts
-    lds = lds_all + MX_IMG_BYTES / 4 + MX_L + 4 + (threadIdx.x >> 6) * MX_WAVE_WORDS;
+    lds = lds_all + S::IMG_BYTES / 4 + L + 4 + (threadIdx.x >> 6) * S::WAVE_WORDS;
   }
   const int lane = MX ? (int)(threadIdx.x & 63u) : (int)threadIdx.x;
   const int g_raw = lane / P;
@@ -387,7 +389,7 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
   const int p = lane - g_raw * P;
   const uint32_t op = blk * G + (idle ? 0 : g_raw);
   const bool active = !idle && op < a.count;
-  uint32_t* bl = lds + g * L;
+  uint32_t* bl = lds + g * (MX ? S::ROW : L);
   const int m_src_addr = (idle ? lane : g_raw * P) * 4;
 
   uint32_t Nd[K], A[K];
@@ -404,8 +406,8 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
   auto load_nd = [&] __attribute__((always_inline))() { load_const(a.nd, Nd); };
   if constexpr (!MX) load_nd();  // MX: only the exit product and store_result need m in registers
   MxConsts mxc{};
-  const uint32_t* mx_md = lds_all + MX_IMG_BYTES / 4;  // MX: m's digits (LDS)
-  if constexpr (MX) mxc = mx_consts(reinterpret_cast<const uint8_t*>(lds_all), lane);
+  const uint32_t* mx_md = lds_all + S::IMG_BYTES / 4;  // MX: m's digits (LDS)
+  if constexpr (MX) mxc = mx_consts<S>(reinterpret_cast<const uint8_t*>(lds_all), lane);
 
   // operand words -> radix-2^28 digits (inactive operands compute on zero)
   auto load_digits = [&] __attribute__((always_inline))(const uint32_t* src, uint32_t words) {
@@ -581,9 +583,9 @@ __device__ __forceinline__ void modexp_wave(const ModexpArgs& a, const uint32_t 
       }
       if (st == ST_FIN) break;  // the exit product runs after the loop (m's digits live only there)
       if (sqr) {
-        montmul_mx<true, (bool)MPCX_SQR_B2>(A, lds, mx_md, mxc, lane);
+        montmul_mx<S, true, (bool)MPCX_SQR_B2>(A, lds, mx_md, mxc, lane);
       } else {
-        montmul_mx<false, false>(A, lds, mx_md, mxc, lane);
+        montmul_mx<S, false, false>(A, lds, mx_md, mxc, lane);
       }
     } else if (MPCX_SQR_OPT && sqr) {
       montmul<P, K, true, (bool)MPCX_SQR_B2>(A, bl, Nd, a.n0inv, m_src_addr, p);
@@ -662,10 +664,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
 
 // geometry 2 with the reduction on the matrix cores (a.mx_img set): MX_WG
 // wavefronts per workgroup share the tables in LDS
-template <int WPE>
+template <int P, int K, int G, int WPE>
 __global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp_mx(
     const ModexpArgs a) {
-  modexp_wave<MX_P, MX_K, MX_G, true>(a, blockIdx.x * MX_WG + (threadIdx.x >> 6));
+  modexp_wave<P, K, G, true>(a, blockIdx.x * MX_WG + (threadIdx.x >> 6));
 }
 
 // Several batches of one modulus class in one launch (mpcx_modexp_multi_batch:

@@ -53,9 +53,11 @@ extern "C" {
 
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_g, MPCX_GEOM_ID)(
     const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st) {
-#if MPCX_GEOM_ID == 2
+#if MPCX_GEOM_ID == 2 || MPCX_GEOM_ID == 5
   if (a->mx_img) {  // the reduction on the matrix cores (mpcx_mx.hpp), MX_WG wavefronts per workgroup
-    hipLaunchKernelGGL((mpcx::k_modexp_mx<2>), dim3((waves + MX_WG - 1) / MX_WG), dim3(64 * MX_WG), 0, st, *a);
+    hipLaunchKernelGGL((mpcx::k_modexp_mx<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
+                                          MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE_SINGLE>),
+                       dim3((waves + MX_WG - 1) / MX_WG), dim3(64 * MX_WG), 0, st, *a);
     return hipGetLastError();
   }
 #endif

@@ -108,8 +108,39 @@ struct ModexpArgs {
   const void* mx_img;
   uint32_t nwaves;      // wavefronts with work (k_modexp_mx: the last workgroup's spare waves exit)
 };
-#define MPCX_MX_TAB_STRIDE 720
-#define MPCX_MX_TAB_BYTES (16 * MPCX_MX_TAB_STRIDE)
+// workgroup: MX_WG wavefronts share the Toeplitz tables and m's digits in LDS
+#ifndef MX_WG
+#define MX_WG 4
+#endif
+
+// An MX geometry: P lanes x K radix-2^28 digits per operand, G operands per wave.
+template <int P_, int K_, int G_>
+struct MxShape {
+  static constexpr int P = P_, K = K_, G = G_, L = P * K;
+  static constexpr int HALVES = G / 16;  // 16 operands per MFMA column set
+  static constexpr int N7 = 4 * L;       // radix-2^7 digits of R
+  // dwords per operand row: 16-B aligned, an odd number of 16-B slots (ds_read_b128
+  // of 16 rows conflict-free)
+  static constexpr int ROW = (((L + 3) / 4) % 2 == 1 ? (L + 3) / 4 : (L + 3) / 4 + 1) * 4;
+  static constexpr int KB = (N7 + 63) / 64;          // K blocks of 64 digits
+  static constexpr int O1 = (N7 + 15) / 16;          // output blocks of q (digits >= L zeroed)
+  static constexpr int NJ1 = O1;                     // Toeplitz blocks of m'' (delta = 16 j)
+  static constexpr int NJ2 = (N7 + 62) / 16 + 1;     // Toeplitz blocks of m with a non-zero entry
+  static constexpr int JMAX = (NJ1 > NJ2 ? NJ1 : NJ2) - 1;
+  static constexpr int D = 16 * JMAX;                // table copy_i[x] = v7[D - x + i]
+  static constexpr int TAB_STRIDE = (((D + 64) / 16) % 2 == 1 ? (D + 64) / 16 : (D + 64) / 16 + 1) * 16;
+  static constexpr int TAB_BYTES = 16 * TAB_STRIDE;
+  static constexpr int IMG_BYTES = 2 * TAB_BYTES;    // the LDS image of both tables (the C-ABI uploads it)
+  static constexpr int O2LO = (N7 - 4) / 16;         // block of the low half's top 4 positions (the carry)
+  static constexpr int O2HI = (2 * N7 + 15) / 16;    // one past U's top block
+  static constexpr int CS1 = 13, CS2 = 13;           // output blocks per chunk (live accumulators)
+  static constexpr int WAVE_WORDS = G * ROW + 4;     // +4: the product loop reads one past the last row
+  static constexpr int LDS_WORDS_WG = IMG_BYTES / 4 + L + 4 + MX_WG * WAVE_WORDS;
+};
+// k_modexp_mx geometries (mpcx_mx.hpp)
+using MxG2 = MxShape<4, 37, 16>;  // geometry 2: R = 2^4144, 592 radix-2^7 digits
+using MxG5 = MxShape<2, 37, 32>;  // geometry 5: R = 2^2072, 296 radix-2^7 digits
+
 
 // Fixed-base tables (mpcx_fixedbase_register): w-bit windows (w chosen per
 // table, <= MPCX_FB_MAX_WINDOW_BITS); for window j < nwin and value v < 2^w,

@@ -39,7 +39,7 @@ SIGNATURES = [
     ("mpcx_modulus_release", ctypes.c_int, [_vp]),
     ("mpcx_modulus_info", ctypes.c_int, [_vp, _u32p, _u32p]),
     ("mpcx_modulus_geometry", ctypes.c_int, [_vp, _u32p, _u32p, _u32p, _u32p]),
-    ("mpcx_mx_tables", ctypes.c_int, [_u32p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    ("mpcx_mx_tables", ctypes.c_int, [_u32p, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     ("mpcx_modexp_batch", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
                                          ctypes.c_int, _vp, ctypes.c_uint32]),
     ("mpcx_modexp_batch_device", ctypes.c_int, [_vp, ctypes.c_uint32, _vp, ctypes.c_uint32, _vp, ctypes.c_uint32,
@@ -176,15 +176,16 @@ def copy_stats() -> dict:
     return {"direct_bytes": v[0].value, "bounced_bytes": v[1].value, "bounce_allocs": v[2].value}
 
 
-MX_TABLE_BYTES = 2 * 16 * 720
+MX_TABLE_BYTES = {148: 2 * 16 * 720, 74: 2 * 16 * 432}
 
 
-def mx_tables(m: int) -> bytes:
+def mx_tables(m: int, L: int = 148) -> bytes:
     """mpcx_mx_tables: the LDS image of k_modexp_mx's Toeplitz tables of
-    m'' = -m^-1 mod 2^4144 and of m (host-only, no device needed)."""
+    m'' = -m^-1 mod 2^(28 L) and of m (host-only, no device needed)."""
     w = int_to_words(m, 128)
-    out = ctypes.create_string_buffer(MX_TABLE_BYTES)
-    _check(lib().mpcx_mx_tables(w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 128, out, MX_TABLE_BYTES))
+    n = MX_TABLE_BYTES.get(L, 0)
+    out = ctypes.create_string_buffer(max(n, 1))
+    _check(lib().mpcx_mx_tables(w.ctypes.data_as(ctypes.POINTER(ctypes.c_uint32)), 128, L, out, n))
     return out.raw
 
 

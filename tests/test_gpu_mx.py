@@ -43,8 +43,9 @@ def _run(m, bases, exps, mx, muls=None):
     return out, mpcx.kernel_stats()
 
 
-def _mx_launched(stats):
-    return any(k.get("kind") == "modexp_mx" and k.get("launches", 0) > 0 for k in stats.get("kernels", []))
+def _mx_launched(stats, geom=2):
+    return any(k.get("kind") == "modexp_mx" and k.get("geom") == geom and k.get("launches", 0) > 0
+               for k in stats.get("kernels", []))
 
 
 def test_mx_shared_exponent_matches_pow_and_cios(dev):
@@ -98,3 +99,47 @@ def test_mx_small_exponents_and_odd_moduli(dev):
             assert _mx_launched(st)
             for i in rng.sample(range(len(bases)), 12):
                 assert got[i] == pow(bases[i], e, m), (bits, e, i)
+
+
+def test_mx_2048_geometry5(dev):
+    # the 2048-bit class's lane-pair geometry (32 operands per wave, two MFMA halves):
+    # ModProof's Z^N mod N shape (shared 2048-bit N), per-operand exponents, a multiplier
+    rng = random.Random(5105)
+    n = rng.getrandbits(2048) | (1 << 2047) | 1
+    bases = [rng.randrange(n) for _ in range(4096)]
+    bases[0], bases[1], bases[2] = 0, 1, n - 1
+    got, st = _run(n, bases, n, 2)  # mx = 2: the lane-pair geometry too (off by default)
+    assert _mx_launched(st, 5), st
+    ref, st0 = _run(n, bases, n, 0)
+    assert not _mx_launched(st0, 5)
+    assert got == ref
+    for i in list(range(3)) + rng.sample(range(3, len(bases)), 40):
+        assert got[i] == pow(bases[i], n, n), i
+    exps = [rng.getrandbits(rng.choice([1, 5, 300, 2048])) for _ in bases]
+    got, st = _run(n, bases, exps, 2)
+    assert _mx_launched(st, 5)
+    for i in rng.sample(range(len(bases)), 40):
+        assert got[i] == pow(bases[i], exps[i], n), i
+    muls = [rng.randrange(n) for _ in bases]
+    got, st = _run(n, bases, 65537, 2, muls=muls)
+    assert _mx_launched(st, 5)
+    for i in rng.sample(range(len(bases)), 24):
+        assert got[i] == muls[i] * pow(bases[i], 65537, n) % n, i
+    # moduli below the class maximum (N~ is a product of two 1024-bit safe primes: 2047-2048 bits)
+    for bits in (2047, 1800):
+        m = rng.getrandbits(bits) | (1 << (bits - 1)) | 1
+        b2 = [rng.randrange(m) for _ in range(2048)]
+        got, st = _run(m, b2, 3, 2)
+        assert _mx_launched(st, 5)
+        for i in rng.sample(range(len(b2)), 16):
+            assert got[i] == pow(b2[i], 3, m), (bits, i)
+
+
+def test_mx_default_leaves_the_lane_pair_geometry_on_cios(dev):
+    rng = random.Random(5106)
+    n = rng.getrandbits(2048) | (1 << 2047) | 1
+    bases = [rng.randrange(n) for _ in range(4096)]
+    got, st = _run(n, bases, n, 1)
+    assert not _mx_launched(st, 5)
+    for i in rng.sample(range(len(bases)), 8):
+        assert got[i] == pow(bases[i], n, n)

@@ -7,6 +7,7 @@
 #include "../../mpcium_amd/csrc/mpcx_device.hpp"
 
 using namespace mpcx;
+constexpr int MX_P = MxG2::P, MX_K = MxG2::K, MX_L = MxG2::L, MX_G = MxG2::G, MX_ROW = MxG2::ROW;
 
 // one MFMA: C = A B with per-lane fragments a[lane], b[lane] (16 bytes each)
 __global__ __launch_bounds__(64) void k_mfma_map(const mx_v4i* a, const mx_v4i* b, mx_v4i* c) {
@@ -22,20 +23,20 @@ __global__ __launch_bounds__(64) void k_mfma_map(const mx_v4i* a, const mx_v4i* 
 __global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(MXB_WPE))) void k_chain_mx(
     const uint32_t* x, uint32_t* out, const uint32_t* img, const uint32_t* md_g, uint32_t S, uint32_t count,
     uint32_t* dbg) {
-  __shared__ __attribute__((aligned(16))) uint32_t lds[MX_LDS_WORDS_WG];
-  for (int i = (int)threadIdx.x; i < MX_IMG_BYTES / 4; i += 64 * MX_WG) lds[i] = img[i];
-  for (int i = (int)threadIdx.x; i < MX_L; i += 64 * MX_WG) lds[MX_IMG_BYTES / 4 + i] = md_g[i];
+  __shared__ __attribute__((aligned(16))) uint32_t lds[MxG2::LDS_WORDS_WG];
+  for (int i = (int)threadIdx.x; i < MxG2::IMG_BYTES / 4; i += 64 * MX_WG) lds[i] = img[i];
+  for (int i = (int)threadIdx.x; i < MxG2::L; i += 64 * MX_WG) lds[MxG2::IMG_BYTES / 4 + i] = md_g[i];
   __syncthreads();
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  uint32_t* rows = lds + MX_IMG_BYTES / 4 + MX_L + 4 + wave * MX_WAVE_WORDS;
-  const uint32_t* md = lds + MX_IMG_BYTES / 4;
+  uint32_t* rows = lds + MxG2::IMG_BYTES / 4 + MxG2::L + 4 + wave * MxG2::WAVE_WORDS;
+  const uint32_t* md = lds + MxG2::IMG_BYTES / 4;
   const int g = lane >> 2, p = lane & 3;
   const uint32_t blk = blockIdx.x * MX_WG + wave;
   const uint32_t op = blk * MX_G + g;
   uint32_t A[MX_K];
 #pragma unroll
   for (int k = 0; k < MX_K; ++k) A[k] = op < count ? x[(size_t)op * MX_L + p * MX_K + k] : 0u;
-  const MxConsts c = mx_consts(reinterpret_cast<const uint8_t*>(lds), lane);
+  const MxConsts c = mx_consts<MxG2>(reinterpret_cast<const uint8_t*>(lds), lane);
 #ifdef MXB_STAGGER
   // the workgroup's second half (sharing SIMDs with the first) starts later, so
   // one wave's matrix-core phase meets the other's VALU product loop
@@ -43,9 +44,9 @@ __global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(MXB_
     for (int i = 0; i < MXB_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
   for (uint32_t s = 0; s < S; ++s) {
-    lds_store_sqr<MX_K>(rows + g * MX_ROW, p, A);
+    lds_store_sqr<MX_K>(rows + g * MxG2::ROW, p, A);
     wave_lds_fence();
-    montmul_mx<true, (bool)MPCX_SQR_B2>(A, rows, md, c, lane);
+    montmul_mx<MxG2, true, (bool)MPCX_SQR_B2>(A, rows, md, c, lane);
     wave_lds_fence();
   }
   if (op < count) {

@@ -97,7 +97,7 @@ def debug(lib, dev, rng):
     m = rng.getrandbits(4096) | (1 << 4095) | 1
     R = 1 << RBITS
     m2 = (-pow(m, -1, R)) % R
-    imgd = torch.frombuffer(bytearray(mpcx.mx_tables(m)), dtype=torch.uint8).to(dev)
+    imgd = torch.frombuffer(bytearray(mpcx.mx_tables(m, 148)), dtype=torch.uint8).to(dev)
     md = torch.tensor(digits(m, L, DB), dtype=torch.int64).to(torch.int32).to(dev)
     xs = [rng.randrange(m) for _ in range(16)]
     xd = torch.tensor([digits(v, L, DB) for v in xs], dtype=torch.int64).to(torch.int32).to(dev)
@@ -161,7 +161,7 @@ def main():
     m = rng.getrandbits(4096) | (1 << 4095) | 1
     R = 1 << RBITS
     m2 = (-pow(m, -1, R)) % R
-    imgd = torch.frombuffer(bytearray(mpcx.mx_tables(m)), dtype=torch.uint8).to(dev)
+    imgd = torch.frombuffer(bytearray(mpcx.mx_tables(m, 148)), dtype=torch.uint8).to(dev)
     md = torch.tensor(digits(m, L, DB), dtype=torch.int64).to(torch.int32).to(dev)
     n0inv = (-pow(m, -1, 1 << DB)) % (1 << DB)
 
