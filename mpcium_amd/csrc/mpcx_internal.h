@@ -133,7 +133,10 @@ struct MxShape {
   static constexpr int IMG_BYTES = 2 * TAB_BYTES;    // the LDS image of both tables (the C-ABI uploads it)
   static constexpr int O2LO = (N7 - 4) / 16;         // block of the low half's top 4 positions (the carry)
   static constexpr int O2HI = (2 * N7 + 15) / 16;    // one past U's top block
-  static constexpr int CS1 = 13, CS2 = 13;           // output blocks per chunk (live accumulators)
+#ifndef MX_CS
+#define MX_CS 13
+#endif
+  static constexpr int CS1 = MX_CS, CS2 = MX_CS;     // output blocks per chunk (live accumulators)
   static constexpr int WAVE_WORDS = G * ROW + 4;     // +4: the product loop reads one past the last row
   static constexpr int LDS_WORDS_WG = IMG_BYTES / 4 + L + 4 + MX_WG * WAVE_WORDS;
 };

@@ -154,7 +154,10 @@ __device__ __forceinline__ void mx_toeplitz(mx_v4i (&acc)[O1 - O0], const uint8_
     if constexpr (j + 1 <= JHI) fnext = ld(j + 1);
     // the next block's read stays one block ahead: ALU and MFMA may move
     // across, LDS reads may not (hoisting them all costs 4 VGPRs per block)
-    __builtin_amdgcn_sched_barrier(0x000F);
+#ifndef MX_READ_FENCE
+#define MX_READ_FENCE 1
+#endif
+    if constexpr (MX_READ_FENCE) __builtin_amdgcn_sched_barrier(0x000F);
     static_for<0, S::KB>([&](auto kc) {
       constexpr int kb = decltype(kc)::value;
       constexpr int o = j + 4 * kb;
@@ -219,6 +222,10 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
   // ---- the row <- T's high digits + m (block layout)
 #pragma unroll
   for (int k = 0; k < K; ++k) rg[p * K + k] = A[k] + md[p * K + k];
+#ifndef MX_PRIO
+#define MX_PRIO 0  // 1: raise the wave's issue priority over the matrix-core phases
+#endif
+  if constexpr (MX_PRIO) __builtin_amdgcn_s_setprio(1);
   static_for<0, S::HALVES>([&](auto sc) {
     constexpr int s = decltype(sc)::value;
     uint32_t* rn = rows + (16 * s + n) * ROW;
@@ -289,6 +296,7 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
       });
     }
   });
+  if constexpr (MX_PRIO) __builtin_amdgcn_s_setprio(0);
   wave_lds_fence();
   // ---- back to the block layout; signed carry passes until every digit is >= 0
 #pragma unroll
