@@ -106,3 +106,20 @@ def test_gpus_without_launcher_relaunches_under_torchrun(monkeypatch):
     assert cmd[1:3] == ["-m", "torch.distributed.run"]
     assert "--nproc-per-node=4" in cmd and "127.0.0.1" in cmd
     assert cmd[-4:] == ["--gpus", "4", "--steps", "3"]
+
+
+def test_mx_executed_floor_counts_the_schedule():
+    """bench.mx_floor: the executed-work floor of k_modexp_mx counts
+    the sliding-window schedule of the exponent and prices the product loops' MADs
+    and the reduction's i8 MACs at their peaks."""
+    import bench
+    # 0b1011 with width 6: one window (the top), no squarings after it
+    assert bench.sliding_window_counts(0b1011) == (0, 6, 0)
+    # 2^10 + 1: top window 1, then 10 squarings and one window multiply
+    sq, tab, wins = bench.sliding_window_counts((1 << 10) + 1)
+    assert (sq, wins) == (10, 1) and tab == 1
+    f = bench.mx_floor(65536, (1 << 2047) | 1, 100.0)
+    assert f["squarings"] == 2048 and f["products"] >= 2
+    assert abs(f["valu_lane_mads"] - 65536 * (2048 * 148 * 19 * 4 + f["products"] * 148 * 37 * 4)) < 1
+    assert f["floor_ms_valu"] > f["floor_ms_mfma"] > 0
+    assert abs(f["frac_of_floor"] - f["floor_ms_valu"] / 100.0) < 1e-9
