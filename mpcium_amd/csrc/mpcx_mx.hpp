@@ -109,8 +109,21 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
       // lane 0's digit leaves the window as T's digit i (in CIOS it is zero);
       // it must not shift into the previous group's top slot
       const uint32_t lo = (uint32_t)a0 & M28;
-      if (p == 0) to[u] = lo;
+#ifndef MX_EMIT_BCAST
+#define MX_EMIT_BCAST 0  // 1: every lane of the group stores lane 0's digit (spills the product loop: measured no gain)
+#endif
+      if constexpr (MX_EMIT_BCAST) {
+        // every lane of the group writes lane 0's digit to the same address: no
+        // exec-mask switch per iteration
+        to[u] = group_bcast<P>(lo, 0);
+      } else {
+        if (p == 0) to[u] = lo;
+      }
       acc[u] = from_next_lane(p == 0 ? 0u : lo);
+#ifndef MX_ITER_FENCE
+#define MX_ITER_FENCE 0
+#endif
+      if constexpr (MX_ITER_FENCE) __builtin_amdgcn_sched_barrier(0);
     });
   }
   carry_pass64<P, K>(acc);
