@@ -110,7 +110,7 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
       // it must not shift into the previous group's top slot
       const uint32_t lo = (uint32_t)a0 & M28;
 #ifndef MX_EMIT_BCAST
-#define MX_EMIT_BCAST 0  // 1: every lane of the group stores lane 0's digit (spills the product loop: measured no gain)
+#define MX_EMIT_BCAST 0  // 1: every lane of the group stores lane 0's digit (not used: it spills the product loop at 256 VGPRs)
 #endif
       if constexpr (MX_EMIT_BCAST) {
         // every lane of the group writes lane 0's digit to the same address: no
