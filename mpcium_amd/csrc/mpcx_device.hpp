@@ -30,7 +30,9 @@
 //    per-operand exponents use Go's fixed 4-bit window. Tables (<= 33 entries
 //    per operand) live in a global workspace, lane-coalesced; b operands are
 //    staged in LDS and read as group-broadcast ds_read_b32.
-//  * MFMA is not used: this is not a dense contraction.
+//  * The per-operand product is not a dense contraction. The REDUCTION of a
+//    batch that shares its modulus is (fixed Toeplitz matrices of m'' and m):
+//    geometry 2 runs it on the i8 matrix cores, k_modexp_mx (mpcx_mx.hpp).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
