@@ -43,7 +43,7 @@
 #define MPCX_GEOM_DECL(g)                                                                              \
   hipError_t mpcx_launch_modexp_g##g(const mpcx::ModexpArgs* a, uint32_t waves, hipStream_t st);     \
   hipError_t mpcx_launch_modexp_multi_g##g(const mpcx::ModexpArgs* segs, const uint32_t* first,      \
-                                           uint32_t nsegs, uint32_t waves, hipStream_t st);          \
+                                           uint32_t nsegs, uint32_t waves, int mx, hipStream_t st);  \
   hipError_t mpcx_modexp_occupancy_g##g(int* blocks_per_cu);
 #define MPCX_FOR_EACH_GEOM(X) X(0) X(1) X(2) X(3) X(4) X(5) X(6)
 static_assert(MPCX_NUM_GEOMS == 7, "update MPCX_FOR_EACH_GEOM and build.py GEOMS");
@@ -129,6 +129,7 @@ bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 
 #endif
 int g_mx = MPCX_MX_DEFAULT;              // mpcx_set_option("mx", 1): geometry-2 batches reduce on the matrix cores
 uint32_t g_mx_min = 2048;                // mpcx_set_option("mx_min", n): smallest batch for k_modexp_mx
+uint32_t g_mx_seg_min = 256;             // mpcx_set_option("mx_seg_min", n): smallest segment of a k_modexp_multi_mx launch
 struct Staging {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -552,12 +553,13 @@ hipError_t mpcx_launch_modexp(int geom, const mpcx::ModexpArgs* a, uint32_t wave
   }
 }
 
+// mx: segments laid out in MX_WG-wavefront workgroups (first[] counts workgroups), k_modexp_multi_mx
 hipError_t mpcx_launch_modexp_multi(int geom, const mpcx::ModexpArgs* segs, const uint32_t* first, uint32_t nsegs,
-                                    uint32_t waves, hipStream_t st) {
+                                    uint32_t waves, int mx, hipStream_t st) {
   switch (geom) {
 #define MPCX_CASE(g) \
   case g:            \
-    return mpcx_launch_modexp_multi_g##g(segs, first, nsegs, waves, st);
+    return mpcx_launch_modexp_multi_g##g(segs, first, nsegs, waves, mx, st);
     MPCX_FOR_EACH_GEOM(MPCX_CASE)
 #undef MPCX_CASE
     default:
@@ -1149,6 +1151,8 @@ int mpcx_get_option(const char* key, int* value) {
     *value = g_mx;
   } else if (std::strcmp(key, "mx_min") == 0) {
     *value = (int)g_mx_min;
+  } else if (std::strcmp(key, "mx_seg_min") == 0) {
+    *value = (int)g_mx_seg_min;
   } else if (std::strcmp(key, "geom_policy") == 0) {
     *value = g_geom_policy;
   } else if (std::strcmp(key, "sched_width") == 0) {
@@ -1196,6 +1200,9 @@ int mpcx_set_option(const char* key, int value) {
   } else if (std::strcmp(key, "mx_min") == 0) {
     if (value < 1) return fail(MPCX_EINVAL, "mx_min %d < 1", value);
     g_mx_min = (uint32_t)value;
+  } else if (std::strcmp(key, "mx_seg_min") == 0) {
+    if (value < 1) return fail(MPCX_EINVAL, "mx_seg_min %d < 1", value);
+    g_mx_seg_min = (uint32_t)value;
   } else if (std::strcmp(key, "fixed_window") == 0) {
     // widest fixed window of per-operand exponents: 4 (Go's) or 5 (above 320 bits)
     if (value != 4 && value != 5) return fail(MPCX_EINVAL, "fixed_window %d not 4 or 5", value);
@@ -1906,6 +1913,11 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
   }
   const int geom = choose_geom(dev, cls, (uint32_t)total, main_ok, forced_ok);
   const uint32_t G = (uint32_t)MPCX_GEOM_G(geom), K = (uint32_t)MPCX_GEOM_K(geom), L = (uint32_t)MPCX_GEOM_L(geom);
+  // the 4096-bit main geometry's segments on the matrix cores when the launch is
+  // large and every segment fills at least one workgroup's worth of its tables
+  bool mx = g_mx && geom == MPCX_MAIN_GEOM(2) && total >= g_mx_min;
+  for (uint32_t i = 0; i < n_groups && mx; ++i)
+    if (gs[i].count && gs[i].count < g_mx_seg_min) mx = false;
   // host-side layout of the packed inputs and outputs (words)
   struct Seg {
     uint32_t gi, waves, exp_bits;
@@ -2004,7 +2016,15 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
     a.n0inv = g.mod->n0inv;
     a.exp_shared = g.exp_shared ? 1 : 0;
     a.sched = sg.use_sched ? l.ws + sg.sched : nullptr;
-    first[k + 1] = first[k] + sg.waves;
+    if (mx) {
+      const uint8_t* t = nullptr;
+      if ((rc = mx_const(g.mod, di, &t))) return rc;
+      a.mx_img = t;
+      a.nwaves = sg.waves;
+      first[k + 1] = first[k] + (sg.waves + MX_WG - 1) / MX_WG;  // workgroups
+    } else {
+      first[k + 1] = first[k] + sg.waves;
+    }
   }
   if ((rc = h2d(l, l.stage[3].ptr, args.data(), seg_bytes)) ||
       (rc = h2d(l, (char*)l.stage[3].ptr + seg_bytes, first.data(), first_bytes)))
@@ -2012,7 +2032,7 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
   const int ks = kstat_begin(l);
   hipError_t e = mpcx_launch_modexp_multi(geom, (const mpcx::ModexpArgs*)l.stage[3].ptr,
                                           (const uint32_t*)((const char*)l.stage[3].ptr + seg_bytes),
-                                          (uint32_t)nseg, first[nseg], l.st);
+                                          (uint32_t)nseg, first[nseg], mx ? 1 : 0, l.st);
   if (e != hipSuccess) return hip_fail(e, "launch k_modexp_multi");
   dev.launches.fetch_add(1, std::memory_order_relaxed);
   {
@@ -2022,9 +2042,10 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
       alg += sg.alg;
       ops += gs[sg.gi].count;
     }
-    kstat_end(l, ks, dev, di, "modexp_multi", geom, ops, alg);
+    kstat_end(l, ks, dev, di, mx ? "modexp_multi_mx" : "modexp_multi", geom, ops, alg);
   }
-  for (const auto& sg : segs) launch_log("modexp_multi", geom, gs[sg.gi].count, gs[sg.gi].mod->bits, sg.exp_bits, sg.alg);
+  for (const auto& sg : segs)
+    launch_log(mx ? "modexp_multi_mx" : "modexp_multi", geom, gs[sg.gi].count, gs[sg.gi].mod->bits, sg.exp_bits, sg.alg);
   for (const auto& sg : segs) {  // results straight into each group's buffer
     const mpcx_modexp_group_t& g = gs[sg.gi];
     if ((rc = d2h(l, g.out, d_out + sg.out_o, (size_t)g.count * g.out_words * 4))) return rc;

@@ -664,6 +664,19 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(WPE))) void 
   modexp_wave<P, K, G>(a, blockIdx.x);
 }
 
+// k_modexp_multi with the reduction on the matrix cores: every segment starts on
+// a workgroup boundary (first[] counts MX_WG-wavefront workgroups), so the
+// workgroup's waves share the segment's tables
+template <int P, int K, int G, int WPE>
+__global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(WPE))) void k_modexp_multi_mx(
+    const ModexpArgs* __restrict__ segs, const uint32_t* __restrict__ first, uint32_t nsegs) {
+  const uint32_t b = blockIdx.x;
+  uint32_t s = 0;
+  while (s + 1u < nsegs && __builtin_amdgcn_readfirstlane(first[s + 1u]) <= b) ++s;
+  s = __builtin_amdgcn_readfirstlane(s);
+  modexp_wave<P, K, G, true>(segs[s], (b - __builtin_amdgcn_readfirstlane(first[s])) * MX_WG + (threadIdx.x >> 6));
+}
+
 // geometry 2 with the reduction on the matrix cores (a.mx_img set): MX_WG
 // wavefronts per workgroup share the tables in LDS
 template <int P, int K, int G, int WPE>

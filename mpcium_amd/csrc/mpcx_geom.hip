@@ -67,7 +67,17 @@ __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_g, 
 
 // several batches in one launch: segs / first are device arrays of nsegs entries
 __attribute__((visibility("hidden"))) hipError_t MPCX_CAT(mpcx_launch_modexp_multi_g, MPCX_GEOM_ID)(
-    const mpcx::ModexpArgs* segs, const uint32_t* first, uint32_t nsegs, uint32_t waves, hipStream_t st) {
+    const mpcx::ModexpArgs* segs, const uint32_t* first, uint32_t nsegs, uint32_t waves, int mx, hipStream_t st) {
+#if MPCX_GEOM_ID == 2
+  if (mx) {  // `waves` counts MX_WG-wavefront workgroups here
+    hipLaunchKernelGGL((mpcx::k_modexp_multi_mx<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
+                                                MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE_SINGLE>),
+                       dim3(waves), dim3(64 * MX_WG), 0, st, segs, first, nsegs);
+    return hipGetLastError();
+  }
+#else
+  if (mx) return hipErrorInvalidValue;
+#endif
   hipLaunchKernelGGL((mpcx::k_modexp_multi<MPCX_GEOM_P(MPCX_GEOM_ID), MPCX_GEOM_K(MPCX_GEOM_ID),
                                            MPCX_GEOM_G(MPCX_GEOM_ID), MPCX_WPE_MULTI>),
                      dim3(waves), dim3(64), 0, st, segs, first, nsegs);

@@ -143,3 +143,46 @@ def test_mx_default_leaves_the_lane_pair_geometry_on_cios(dev):
     assert not _mx_launched(st, 5)
     for i in rng.sample(range(len(bases)), 8):
         assert got[i] == pow(bases[i], n, n)
+
+
+def test_mx_multi_batch_segments(dev):
+    # k_modexp_multi_mx: several 4096-bit moduli in one launch, every segment on a
+    # workgroup boundary with its own tables (the shape of signing's and config 1's
+    # merged Paillier launches): bit-exact against pow and against k_modexp_multi
+    rng = random.Random(5107)
+    mods, groups = [], []
+    for t, cnt in enumerate((300, 1024, 257, 700)):
+        n, m = _modulus(rng)
+        mod = mpcx.Modulus(m)
+        mods.append(mod)
+        bases = [rng.randrange(m) for _ in range(cnt)]
+        if t == 0:
+            groups.append((mod, bases, n, None))  # shared exponent (Encrypt's r^N)
+        elif t == 1:
+            groups.append((mod, bases, [rng.getrandbits(256) for _ in bases], None))  # HomoMult c^b
+        elif t == 2:
+            groups.append((mod, bases, n, [rng.randrange(m) for _ in bases]))  # with a multiplier
+        else:
+            groups.append((mod, bases, 65537, None))
+    try:
+        mpcx.set_option("mx", 1)
+        mpcx.kernel_stats(reset=True)
+        got = mpcx.modexp_multi(groups)
+        st = mpcx.kernel_stats()
+        assert any(k.get("kind") == "modexp_multi_mx" and k.get("launches", 0) > 0 for k in st["kernels"]), st
+        mpcx.set_option("mx", 0)
+        ref = mpcx.modexp_multi(groups)
+        assert got == ref
+        for (mod, bases, exps, muls), out in zip(groups, got):
+            m = mod.m if hasattr(mod, "m") else None
+            for i in rng.sample(range(len(bases)), 6):
+                e = exps if isinstance(exps, int) else exps[i]
+                want = pow(bases[i], e, m) if m is not None else None
+                if want is not None:
+                    if muls is not None:
+                        want = want * muls[i] % m
+                    assert out[i] == want
+    finally:
+        mpcx.set_option("mx", 0)
+        for mod in mods:
+            mod.release()
