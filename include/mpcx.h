@@ -399,6 +399,9 @@ int mpcx_sync(void* stream);
  *                457K vs 378K modexp/s, profiles/r05/mx/); 2 adds the 2048-bit
  *                lane-pair geometry, which measured slower (1.22M vs 1.40M
  *                2048-bit modexp/s, keygen -7%: profiles/r05/mx/g5/).
+ *                Multi-batch launches of the 4096-bit main geometry use it too
+ *                (k_modexp_multi_mx) when every group has >= "mx_seg_min"
+ *                operands (default 256): signing +10%, profiles/r05/mx/multi/.
  *                Environment: MPCX_MX.
  *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
  *                thread per candidate.
@@ -422,8 +425,8 @@ int mpcx_sync(void* stream);
  * default 6: execution lanes per device), MPCX_GEOM_POLICY, MPCX_NARROW_ROUNDS,
  * MPCX_PRIME_COOP, MPCX_FB_WINDOW. */
 int mpcx_set_option(const char* key, int value);
-/* Current value of "mx", "mx_min", "geom_policy", "sched_width", "fixed_window",
- * "fb_split" or "lanes" (benchmarks record which kernel path ran). */
+/* Current value of "mx", "mx_min", "mx_seg_min", "geom_policy", "sched_width",
+ * "fixed_window", "fb_split" or "lanes" (benchmarks record which kernel path ran). */
 int mpcx_get_option(const char* key, int* value);
 
 /* The constant tables of k_modexp_mx (the 4096- and 2048-bit main geometries
