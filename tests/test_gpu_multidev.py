@@ -140,6 +140,20 @@ mpcx.set_option("device_split_min", 64)
 l0 = [mpcx.device_launches(i) for i in range(2)]
 out["split_ok"] = mod.exp(xs, N) == [pow(x, N, N2) for x in xs]
 out["split_launches"] = [mpcx.device_launches(i) - l0[i] for i in range(2)]
+# the matrix-core kernel on both logical devices: each builds and uploads its own tables
+mpcx.set_option("device_split_min", 2048)
+mpcx.set_option("geom_policy", 2)
+mpcx.set_option("kernel_stats", 1)
+mpcx.kernel_stats(reset=True)
+ys = [rng.randrange(N2) for _ in range(4160)]
+l0 = [mpcx.device_launches(i) for i in range(2)]
+got = mod.exp(ys, N)
+ks = mpcx.kernel_stats()
+out["mx_split_ok"] = all(got[i] == pow(ys[i], N, N2) for i in rng.sample(range(len(ys)), 24))
+out["mx_split_launches"] = [mpcx.device_launches(i) - l0[i] for i in range(2)]
+out["mx_operands"] = sum(k["operands"] for k in ks["kernels"] if k["kind"] == "modexp_mx")
+mpcx.set_option("kernel_stats", 0)
+mpcx.set_option("geom_policy", 1)
 mod.release()
 mpcx.set_option("device_split_min", 4096)
 d = load_golden("node_preparams.json")
@@ -168,6 +182,7 @@ def test_two_logical_devices(gpu):
     out = json.loads(r.stdout.strip().splitlines()[-1])
     assert out["devices"] == [0, 0]
     assert out["split_ok"] and all(n >= 1 for n in out["split_launches"])
+    assert out["mx_split_ok"] and all(n >= 1 for n in out["mx_split_launches"]) and out["mx_operands"] == 4160
     s = out["signing"]
     assert s["errors"] == 0 and s["relation_failures"] == 0 and s["verified"] == 300 and s["aborted"] == 0
     assert out["keygen"]["failures"] == 0 and out["keygen"]["waves"] == 2
