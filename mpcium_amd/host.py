@@ -158,6 +158,25 @@ class PublicKey:
                                                   c.ctypes.data, cw, err.ctypes.data))
         return words_to_ints(c), [int(e) for e in err]
 
+    def encrypt_words(self, Mw: np.ndarray, mn: np.ndarray, R: np.ndarray):
+        """encrypt on little-endian word arrays (count x words; mn: 1 where m < 0):
+        the same C-ABI call without the Python-int conversions -> (c words, err)."""
+        cw = 2 * len(self._Nw)
+        c, err = self._out(Mw.shape[0], cw)
+        _check(lib().mpcxh_paillier_encrypt_batch(self._Nw.ctypes.data, len(self._Nw), Mw.shape[0], Mw.ctypes.data,
+                                                  Mw.shape[1], mn.ctypes.data, R.ctypes.data, R.shape[1],
+                                                  c.ctypes.data, cw, err.ctypes.data))
+        return c, err
+
+    def homo_mult_words(self, Mw: np.ndarray, mn: np.ndarray, C: np.ndarray, cn: np.ndarray):
+        """homo_mult on word arrays (as encrypt_words) -> (words, err)."""
+        ow = 2 * len(self._Nw)
+        o, err = self._out(Mw.shape[0], ow)
+        _check(lib().mpcxh_paillier_homomult_batch(self._Nw.ctypes.data, len(self._Nw), Mw.shape[0], Mw.ctypes.data,
+                                                   Mw.shape[1], mn.ctypes.data, C.ctypes.data, C.shape[1],
+                                                   cn.ctypes.data, o.ctypes.data, ow, err.ctypes.data))
+        return o, err
+
     def homo_mult(self, ms: Sequence[int], c1s: Sequence[int]):
         Mw, mn = _signed(ms)
         C, cn = _signed(c1s)
