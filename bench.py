@@ -537,8 +537,8 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: i
             "batches_in_flight": {"batches": inflight, "value": batch * reps * inflight * world / el,
                                   "seconds": el, "kernel_roofline": flight_roof,
                                   "checked": "worker 0's last batch, 64 outputs vs oracle/gomath.py"},
-            "note": "host-buffer API end to end (word arrays -> PCIe -> GPU -> back; the Python-int conversions are outside the timed loops); Encrypt's Gamma^m "
-                    "is the bit-exact 1 + mN shortcut, r^N a shared-exponent GPU batch, c^b per-operand; value: one "
+            "note": "host-buffer API end to end (word arrays -> PCIe -> GPU -> back; the Python-int conversions "
+                    "are outside the timed loops); Encrypt's Gamma^m is the bit-exact 1 + mN shortcut, r^N a shared-exponent GPU batch, c^b per-operand; value: one "
                     "1,024-op batch at a time (BASELINE configs[0]); batches_in_flight: a different shape, "
                     f"{inflight} such batches concurrently from their own threads",
             "cpu_baseline": None}
@@ -548,7 +548,8 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: i
     alg = sum((2048 + 512) * L2 + (b.bit_length() + (b.bit_length() + 3) // 4) * L2 for b in bs) * reps
     line["roofline"] = seq_roof
     line["job_roofline"] = _job_roofline(alg, el_seq, world)
-    line["job_roofline"]["scope"] = "end to end (host buffers incl. PCIe; word arrays, no Python-int conversion in the timed loop); batch of 1,024 = latency-bound"
+    line["job_roofline"]["scope"] = ("end to end (host buffers incl. PCIe; word arrays, no Python-int conversion in "
+                                     "the timed loop); batch of 1,024 = latency-bound")
     line["alg_ops_per_op"] = alg / (batch * reps)
     if cpu:
         line["cpu_baseline"] = cpu_baseline_paillier(N, 12.0, info)
