@@ -539,7 +539,8 @@ def paillier_line(N: int, batch: int, reps: int, cpu: bool, info: dict, world: i
                                   "checked": "worker 0's last batch, 64 outputs vs oracle/gomath.py"},
             "note": "host-buffer API end to end (word arrays -> PCIe -> GPU -> back; the Python-int conversions "
                     "are outside the timed loops); Encrypt's Gamma^m is the bit-exact 1 + mN shortcut, r^N a "
-                    "shared-exponent GPU batch, c^b per-operand; value: one 1,024-op batch at a time (BASELINE configs[0]); batches_in_flight: a different shape, "
+                    "shared-exponent GPU batch, c^b per-operand; value: one 1,024-op batch at a time (BASELINE "
+                    "configs[0]); batches_in_flight: a different shape, "
                     f"{inflight} such batches concurrently from their own threads",
             "cpu_baseline": None}
     # Go-equivalent work per op (SURVEY.md 8(d) W = (E + E/4) 2 L^2, L = 128 words of N^2): r^N (E = 2048) + c^b
