@@ -1583,7 +1583,8 @@ def main():
         progress(f"config 4: signing, {args.signers} signers")
         result["signing"] = signing_line(args, world, rank, args.signers)
         result["signing"]["cpu_baseline"] = sign_cpu
-        if args.signers != 3 and not args.no_sign3:  # mpcium signs with every ready peer (/root/reference/pkg/mpc/node.go:148)
+        # mpcium signs with every ready peer (/root/reference/pkg/mpc/node.go:148)
+        if args.signers != 3 and not args.no_sign3:
             progress("config 4: signing, 3 signers")
             result["signing_3_signers"] = signing_line(args, world, rank, 3)
             result["signing_3_signers"]["cpu_baseline"] = sign3_cpu

@@ -8,8 +8,8 @@
 //     after a random delay (the real copies run while other callers queue);
 //   - a host range that starts inside an mpcx_host_alloc block must end inside
 //     it (the real library's registry check) or the process aborts;
-//   - mpcx_host_alloc fails at random (MOCK_PIN_FAIL per mille), forcing the
-//     Engine's pageable fallback;
+//   - mpcx_host_alloc fails at random (MOCK_PIN_FAIL per mille) and on each
+//     thread's first two calls, forcing the Engine's pageable fallback;
 //   - fixed-base tables are heap objects whose contents every launch reads
 //     (a launch on a released table is a use-after-free ASAN reports), and
 //     report 2 GB each so the Engine's 24 GB cache evicts under load.
@@ -103,7 +103,10 @@ int mpcx_host_alloc(size_t bytes, void** out) {
     const char* e = std::getenv("MOCK_PIN_FAIL");
     return e ? std::atoi(e) : 100;
   }();
-  if ((int)rnd(1000) < fail_pm) {
+  // each thread's first two calls are refused too: the Engine's release-and-retry
+  // then fails as well, so every run takes the pageable fallback at least once
+  thread_local int t_calls = 0;
+  if (++t_calls <= 2 || (int)rnd(1000) < fail_pm) {
     g_fallbacks++;
     return fail(MPCX_ENOMEM, "mock: pinned allocation refused");
   }
