@@ -174,15 +174,36 @@ def test_mx_multi_batch_segments(dev):
         ref = mpcx.modexp_multi(groups)
         assert got == ref
         for (mod, bases, exps, muls), out in zip(groups, got):
-            m = mod.m if hasattr(mod, "m") else None
+            m = mod.m
             for i in rng.sample(range(len(bases)), 6):
                 e = exps if isinstance(exps, int) else exps[i]
-                want = pow(bases[i], e, m) if m is not None else None
-                if want is not None:
-                    if muls is not None:
-                        want = want * muls[i] % m
-                    assert out[i] == want
+                want = pow(bases[i], e, m)
+                if muls is not None:
+                    want = want * muls[i] % m
+                assert out[i] == want
     finally:
         mpcx.set_option("mx", 0)
         for mod in mods:
             mod.release()
+
+
+def test_mx_structured_moduli(dev):
+    # moduli whose digit strings stress the reduction's bounds: all-ones (the
+    # largest i8 column sums of m and of m'' = 1), one sparse (m = 2^4095 + 1, m'' dense),
+    # 2^4096 - 2^2048 - 1 (a long run of ones over zeros), each with bases at the
+    # edges (0, 1, 2, m - 1, m - 2) and random ones; shared and per-operand exponents
+    rng = random.Random(5108)
+    mods = ((1 << 4096) - 1, (1 << 4095) + 1, (1 << 4096) - (1 << 2048) - 1)
+    for m in mods:
+        bases = [rng.randrange(m) for _ in range(2048)]
+        bases[:5] = [0, 1, 2, m - 1, m - 2]
+        for e in ((1 << 2048) - 1, rng.getrandbits(2048) | 1):
+            got, st = _run(m, bases, e, 1)
+            assert _mx_launched(st), st
+            for i in list(range(5)) + rng.sample(range(5, len(bases)), 11):
+                assert got[i] == pow(bases[i], e, m), (hex(m)[:12], i)
+        exps = [rng.getrandbits(rng.choice([1, 17, 256, 4096])) for _ in bases]
+        got, st = _run(m, bases, exps, 1)
+        assert _mx_launched(st)
+        for i in list(range(5)) + rng.sample(range(5, len(bases)), 11):
+            assert got[i] == pow(bases[i], exps[i], m), (hex(m)[:12], i)

@@ -157,3 +157,14 @@ def test_mx_reduction_arithmetic(L):
         U, R = montmul_mx_model(a, b, m, L)
         assert 0 < U < 2 * m
         assert U % m == a * b * pow(R, -1, m) % m
+
+
+def test_mx_reduction_arithmetic_structured_moduli():
+    # the moduli of tests/test_gpu_mx.py::test_mx_structured_moduli, with edge operands
+    rng = random.Random(79)
+    for m in ((1 << 4096) - 1, (1 << 4095) + 1, (1 << 4096) - (1 << 2048) - 1):
+        for a, b in ((2 * m - 1, 2 * m - 1), (m - 1, m - 1), (1, 2 * m - 1), (0, 5),
+                     (rng.randrange(2 * m), rng.randrange(2 * m))):
+            U, R = montmul_mx_model(a, b, m, 148)
+            assert 0 < U < 2 * m
+            assert U % m == a * b * pow(R, -1, m) % m
