@@ -18,11 +18,13 @@ pytestmark = pytest.mark.gpu
 @pytest.fixture(scope="module")
 def dev():
     mpcx.init(0)
+    keys = ("mx", "geom_policy")
+    saved = {k: mpcx.get_option(k) for k in keys}  # the later test modules see the defaults again
     mpcx.set_option("kernel_stats", 1)
     mpcx.set_option("geom_policy", 2)  # the main geometry at every batch size
     yield
-    mpcx.set_option("mx", 0)
-    mpcx.set_option("geom_policy", 1)
+    for k in keys:
+        mpcx.set_option(k, saved[k])
     mpcx.set_option("kernel_stats", 0)
 
 
@@ -182,7 +184,6 @@ def test_mx_multi_batch_segments(dev):
                     want = want * muls[i] % m
                 assert out[i] == want
     finally:
-        mpcx.set_option("mx", 0)
         for mod in mods:
             mod.release()
 
