@@ -1044,6 +1044,13 @@ def compact_line(result: dict, detail_path: str | None) -> dict:
                         "kernel_ms": _r(r.get("kernel_ms"), 5)}
     if r.get("frac_at_measured_clock") is not None:
         line["roofline"]["frac_at_clock"] = _r(r["frac_at_measured_clock"])
+    if r.get("kernel"):
+        line["roofline"]["kernel"] = r["kernel"]
+    ef = r.get("executed_floor") or {}
+    if ef.get("frac_of_floor") is not None:
+        # the matrix cores take the reduction, so the algorithmic frac (Go-equivalent
+        # MACs at the INT32 MAD peak) can pass 1; this is the executed work's floor
+        line["roofline"]["frac_of_executed_floor"] = _r(ef["frac_of_floor"])
     cb = result.get("cpu_baseline")
     line["cpu_baseline"] = None if not cb else {
         "value": _r(cb.get("value")), "unit": cb.get("unit"), "cores": cb.get("cores"), "kind": cb.get("kind"),
