@@ -232,6 +232,37 @@ def mx_floor(count: int, e: int, kernel_ms: float) -> dict:
                     "INT32 MAD peak), which the matrix cores let exceed what a VALU-only kernel could reach"}
 
 
+def two_pipe_roofline(r: dict) -> None:
+    """k_modexp_mx runs on two pipes (VALU product loop, i8 matrix-core reduction),
+    so the INT32-VALU ratio of the Go-equivalent work can pass 1 and is no
+    utilisation. In place: `frac` becomes the executed work's
+    floor over the launch (its VALU lane-MADs at the INT32 MAD peak or its i8 MACs
+    at the dense i8 peak, whichever binds; <= 1), `achieved`/`peak` the binding
+    pipe's executed rate and peak, `bound` "valu+mfma_i8"; the rounds' algorithmic
+    ratio moves to the go_equiv_* keys, the other pipe's rate beside it."""
+    ef = r["executed_floor"]
+    t = r["kernel_ms"] * 1e-3
+    valu_rate, i8_rate = ef["valu_lane_mads"] / t, ef["mfma_i8_macs"] / t
+    valu_binds = ef["floor_ms_valu"] >= ef["floor_ms_mfma"]
+    r["go_equiv_achieved"], r["go_equiv_peak"], r["go_equiv_frac"] = r["achieved"], r["peak"], r["frac"]
+    r["go_equiv_note"] = ("Go-equivalent 32-bit MACs (SURVEY 8(d): (E + E/4) 2 L^2 per modexp) per second against "
+                          "the INT32 MAD peak: the rounds' throughput ratio, not a utilisation once the matrix "
+                          "cores take the reduction")
+    if "frac_at_measured_clock" in r:
+        r["go_equiv_frac_at_clock"] = r.pop("frac_at_measured_clock")
+    r["bound"] = "valu+mfma_i8"
+    r["binding_pipe"] = "valu" if valu_binds else "mfma_i8"
+    r["achieved_valu"], r["peak_valu"] = valu_rate / 1e12, PEAK_INT32_NOMINAL / 1e12
+    r["achieved_i8"], r["peak_i8"] = i8_rate / 1e12, PEAK_I8_MFMA / 1e12
+    r["frac_valu"], r["frac_i8"] = valu_rate / PEAK_INT32_NOMINAL, i8_rate / PEAK_I8_MFMA
+    r["achieved"], r["peak"] = (r["achieved_valu"], r["peak_valu"]) if valu_binds else (r["achieved_i8"], r["peak_i8"])
+    r["frac"] = ef["frac_of_floor"]
+    r["unit"] = "TOP/s"
+    clk = r.get("gfxclk_mhz_measured")
+    if clk:
+        r["frac_at_clock"] = r["frac"] * 2400.0 / clk
+
+
 def alg_macs(mod_bits: int, exp_bits: int) -> float:
     """W = (E + ceil(E/4)) * 2 L^2 32-bit MACs, L = 32-bit limbs."""
     L = math.ceil(mod_bits / 32)
@@ -1044,13 +1075,15 @@ def compact_line(result: dict, detail_path: str | None) -> dict:
                         "kernel_ms": _r(r.get("kernel_ms"), 5)}
     if r.get("frac_at_measured_clock") is not None:
         line["roofline"]["frac_at_clock"] = _r(r["frac_at_measured_clock"])
+    if r.get("frac_at_clock") is not None:
+        line["roofline"]["frac_at_clock"] = _r(r["frac_at_clock"])
     if r.get("kernel"):
         line["roofline"]["kernel"] = r["kernel"]
-    ef = r.get("executed_floor") or {}
-    if ef.get("frac_of_floor") is not None:
-        # the matrix cores take the reduction, so the algorithmic frac (Go-equivalent
-        # MACs at the INT32 MAD peak) can pass 1; this is the executed work's floor
-        line["roofline"]["frac_of_executed_floor"] = _r(ef["frac_of_floor"])
+    if r.get("go_equiv_frac") is not None:
+        # two-pipe kernel (two_pipe_roofline): frac is the executed-work floor's; the
+        # Go-equivalent INT32 ratio and the matrix pipe's rate sit beside it
+        for k in ("binding_pipe", "peak_i8", "achieved_i8", "frac_i8", "go_equiv_frac", "go_equiv_achieved"):
+            line["roofline"][k] = _r(r[k]) if isinstance(r.get(k), float) else r.get(k)
     cb = result.get("cpu_baseline")
     line["cpu_baseline"] = None if not cb else {
         "value": _r(cb.get("value")), "unit": cb.get("unit"), "cores": cb.get("cores"), "kind": cb.get("kind"),
@@ -1579,6 +1612,8 @@ def main():
                 peak_clk = 256 * 64 * clk * 1e6
                 result["roofline"]["gfxclk_mhz_measured"] = clk
                 result["roofline"]["frac_at_measured_clock"] = achieved / peak_clk
+    if result["roofline"].get("executed_floor"):
+        two_pipe_roofline(result["roofline"])
     if digest:
         result["batch_digest"] = digest
     if sub_lines:

@@ -704,6 +704,7 @@ struct LaneDrain {
 // `bytes` of lane bounce buffer b. When it is full, the lane's queued work
 // is waited for first (copies may still read the in-buffer; bounced results
 // are delivered), then the buffer grows if one request needs more.
+void retire_pinned(char* p, size_t bytes);
 int bounce_reserve(Lane& l, Lane::Bounce& b, size_t bytes, char** out) {
   const size_t need = (bytes + 255) & ~(size_t)255;
   if (b.used + need > b.cap) {
@@ -715,7 +716,7 @@ int bounce_reserve(Lane& l, Lane::Bounce& b, size_t bytes, char** out) {
       l.hin.used = l.hout.used = 0;
     }
     if (need > b.cap) {
-      if (b.p) (void)hipHostFree(b.p);
+      if (b.p) retire_pinned(b.p, b.cap);
       b.p = nullptr;
       b.cap = 0;
       const size_t want = std::max<size_t>({need + need / 4, (size_t)1 << 20});
@@ -781,9 +782,74 @@ int d2h_sync(void* h, const void* d, size_t bytes, Lane& l) {
   return lane_wait(l);
 }
 
+// Pinned staging for copy_sync: persistent 16-MB chunks handed out under a
+// mutex. hipHostFree synchronises the whole device, so a chunk allocated and
+// freed per call stalled every lane's in-flight kernels on each modulus, mx
+// table or comb-table upload; chunks are now allocated once (one
+// per concurrent copier) and kept until mpcx_shutdown.
+constexpr size_t kStageChunk = (size_t)16 << 20;
+struct StageChunks {
+  std::mutex mu;
+  std::vector<char*> free_list;
+  size_t allocated = 0;
+  char* get() {
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!free_list.empty()) {
+        char* c = free_list.back();
+        free_list.pop_back();
+        return c;
+      }
+    }
+    char* c = nullptr;
+    if (hipHostMalloc((void**)&c, kStageChunk, hipHostMallocPortable) != hipSuccess) return nullptr;
+    std::lock_guard<std::mutex> lk(mu);
+    ++allocated;
+    return c;
+  }
+  void put(char* c) {
+    std::lock_guard<std::mutex> lk(mu);
+    free_list.push_back(c);
+  }
+  void release_all() {  // mpcx_shutdown: no copy in flight
+    std::lock_guard<std::mutex> lk(mu);
+    for (char* c : free_list) (void)hipHostFree(c);
+    free_list.clear();
+    allocated = 0;
+  }
+};
+StageChunks g_stage_chunks;
+
+// Pinned buffers retired by a bounce buffer's growth: freed in one batch (one
+// device-wide synchronisation) once they pass kRetireMax, or at shutdown,
+// rather than one hipHostFree under the lane lock per growth.
+constexpr size_t kRetireMax = (size_t)1 << 30;
+std::mutex g_retire_mu;
+std::vector<std::pair<char*, size_t>> g_retired;
+size_t g_retired_bytes = 0;
+void retire_pinned(char* p, size_t bytes) {
+  std::vector<std::pair<char*, size_t>> out;
+  {
+    std::lock_guard<std::mutex> lk(g_retire_mu);
+    g_retired.push_back({p, bytes});
+    g_retired_bytes += bytes;
+    if (g_retired_bytes > kRetireMax) {
+      out.swap(g_retired);
+      g_retired_bytes = 0;
+    }
+  }
+  for (auto& r : out) (void)hipHostFree(r.first);
+}
+void free_retired() {
+  std::lock_guard<std::mutex> lk(g_retire_mu);
+  for (auto& r : g_retired) (void)hipHostFree(r.first);
+  g_retired.clear();
+  g_retired_bytes = 0;
+}
+
 // Synchronous copy of a large or one-off host buffer (modulus constants, comb
 // tables and their build inputs, the public mpcx_memcpy_* helpers) on stream
-// st, through a temporary pinned chunk unless the range is registered pinned.
+// st, through a persistent pinned staging chunk unless the range is registered pinned.
 int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipStream_t st) {
   if (!bytes) return MPCX_OK;
   const void* hp = kind == hipMemcpyHostToDevice ? src : dst;
@@ -795,11 +861,10 @@ int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipS
     if (e == hipSuccess) e = hipStreamSynchronize(st);
     return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy");
   }
-  constexpr size_t kChunk = (size_t)16 << 20;
-  char* buf = nullptr;
-  const size_t cb = std::min(bytes, kChunk);
-  e = hipHostMalloc((void**)&buf, cb, hipHostMallocPortable);
-  if (e != hipSuccess) return fail(MPCX_ENOMEM, "hipHostMalloc(copy chunk %zu): %s", cb, hipGetErrorString(e));
+  char* buf = g_stage_chunks.get();
+  if (!buf) return fail(MPCX_ENOMEM, "hipHostMalloc(copy chunk %zu)", kStageChunk);
+  const size_t cb = std::min(bytes, kStageChunk);
+  e = hipSuccess;
   for (size_t off = 0; off < bytes && e == hipSuccess; off += cb) {
     const size_t n = std::min(cb, bytes - off);
     if (kind == hipMemcpyHostToDevice) {
@@ -812,7 +877,7 @@ int copy_sync(void* dst, const void* src, size_t bytes, hipMemcpyKind kind, hipS
       if (e == hipSuccess) std::memcpy((char*)dst + off, buf, n);
     }
   }
-  (void)hipHostFree(buf);
+  g_stage_chunks.put(buf);
   g_cp_bounced.fetch_add(bytes, std::memory_order_relaxed);
   return e == hipSuccess ? MPCX_OK : hip_fail(e, "copy");
 }
@@ -1393,6 +1458,8 @@ int mpcx_shutdown(void) {
     }
     d.ordinal = -1;
   }
+  g_stage_chunks.release_all();
+  free_retired();
   g_ndev.store(0);
   return MPCX_OK;
 }

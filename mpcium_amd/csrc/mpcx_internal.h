@@ -137,7 +137,10 @@ struct MxShape {
 #define MX_CS 13
 #endif
   static constexpr int CS1 = MX_CS, CS2 = MX_CS;     // output blocks per chunk (live accumulators)
-  static constexpr int WAVE_WORDS = G * ROW + 4;     // +4: the product loop reads one past the last row
+  // +4: the product loop reads one past the last row; then the product loop's
+  // trash slots (lanes p != 0 store there: lane + digit index < 64 + L)
+  static constexpr int TRASH_OFF = G * ROW + 4;
+  static constexpr int WAVE_WORDS = TRASH_OFF + ((64 + L + 3) / 4) * 4;
   static constexpr int LDS_WORDS_WG = IMG_BYTES / 4 + L + 4 + MX_WG * WAVE_WORDS;
 };
 // k_modexp_mx geometries (mpcx_mx.hpp)

@@ -73,8 +73,17 @@ __device__ __forceinline__ uint32_t mx_spread7(uint32_t x) {
 // T = A * B (B == A for SQR; B2IN: the row holds 2B) in montmul's row loop without
 // the m_i N half: T's low L digits are emitted to tl[] as the window passes them
 // (lane p == 0 of the group), the high L digits end in A (<= 2^28 + 2^10).
+//
+// Emission (MX_EMIT): 0 = lane p == 0 stores under an exec mask (two exec writes
+// per iteration, and the SALU mask ops serialise against the MADs' carry-out
+// SGPRs); 1 = every lane stores, lanes p != 0 into a per-lane trash slot of the
+// wave's LDS area (tr: that lane's slots, L words from lane + 0), so the loop
+// body has no exec changes.
+#ifndef MX_EMIT
+#define MX_EMIT 1
+#endif
 template <int P, int K, bool SQR, bool B2IN>
-__device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl, uint32_t* tl, int p) {
+__device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl, uint32_t* tl, uint32_t* tr, int p) {
   static_assert(!SQR || (K % 2) == 1, "squaring schedule needs an odd digit count per lane");
   uint64_t acc[K];
 #pragma unroll
@@ -83,7 +92,7 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
 #pragma nounroll
   for (int o = 0; o < P; ++o) {
     const uint32_t* bo = bl + o * K;
-    uint32_t* to = tl + o * K;
+    uint32_t* to = ((MX_EMIT == 0 || p == 0) ? tl : tr) + o * K;
     const uint32_t dsh = p > o ? 0u : (p == o ? 1u : 31u);
     static_for<0, K>([&](auto uc) {
       constexpr int u = decltype(uc)::value;
@@ -112,7 +121,9 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
 #ifndef MX_EMIT_BCAST
 #define MX_EMIT_BCAST 0  // 1: every lane of the group stores lane 0's digit (not used: it spills the product loop at 256 VGPRs)
 #endif
-      if constexpr (MX_EMIT_BCAST) {
+      if constexpr (MX_EMIT == 1) {
+        to[u] = lo;
+      } else if constexpr (MX_EMIT_BCAST) {
         // every lane of the group writes lane 0's digit to the same address: no
         // exec-mask switch per iteration
         to[u] = group_bcast<P>(lo, 0);
@@ -207,7 +218,7 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
 #ifndef MPCX_MX_TIMING
 #define MPCX_MX_TIMING 0  // microbench builds only: 1 = product loop alone, 2 = reduction alone
 #endif
-  if constexpr (MPCX_MX_TIMING != 2) mx_product<P, K, SQR, B2IN>(A, rg, rg, p);
+  if constexpr (MPCX_MX_TIMING != 2) mx_product<P, K, SQR, B2IN>(A, rg, rg, rows + S::TRASH_OFF + lane, p);
   if constexpr (MPCX_MX_TIMING == 1) return;
   wave_lds_fence();
   // ---- T's low half as B fragments (radix-2^7 bytes), every half of the wave
