@@ -491,7 +491,9 @@ std::vector<uint8_t> verify_bob_core(const std::vector<const Bytes*>& session, c
     const char* e = std::getenv("MPCX_VERIFY_CRT");
     return !(e && e[0] == '0');
   }();
-  const bool crt = crt_on && own && !own->P.is_zero() && !own->Q.is_zero();
+  // the factors must be the key's: otherwise mod N^2 for the
+  // verification and alice_decrypt's own fallback for the plaintexts
+  const bool crt = crt_on && own && !own->P.is_zero() && !own->Q.is_zero() && own->P * own->Q == pk.N;
   // With the key's factors every exponentiation of the verification -- and,
   // when asked (AliceEnd), the CRT decryption of c2 -- is independent of the
   // others: ONE launch step. c1^s1 runs without a multiplier and is multiplied

@@ -130,6 +130,8 @@ bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 
 int g_mx = MPCX_MX_DEFAULT;              // mpcx_set_option("mx", 1): geometry-2 batches reduce on the matrix cores
 uint32_t g_mx_min = 2048;                // mpcx_set_option("mx_min", n): smallest batch for k_modexp_mx
 uint32_t g_mx_seg_min = 256;             // mpcx_set_option("mx_seg_min", n): smallest segment of a k_modexp_multi_mx launch
+double g_mx_step = 0.81;                 // mpcx_set_option("mx_step", 100x): k_modexp_mx's wave-round time / k_modexp's (0: model ignores mx)
+double g_geom_tput = 0.0;                // mpcx_set_option("geom_tput", 100x): GPU-share weight of the launch-time model
 struct Staging {
   void* ptr = nullptr;
   size_t bytes = 0;
@@ -1218,6 +1220,10 @@ int mpcx_get_option(const char* key, int* value) {
     *value = (int)g_mx_min;
   } else if (std::strcmp(key, "mx_seg_min") == 0) {
     *value = (int)g_mx_seg_min;
+  } else if (std::strcmp(key, "mx_step") == 0) {
+    *value = (int)std::lround(g_mx_step * 100.0);
+  } else if (std::strcmp(key, "geom_tput") == 0) {
+    *value = (int)std::lround(g_geom_tput * 100.0);
   } else if (std::strcmp(key, "geom_policy") == 0) {
     *value = g_geom_policy;
   } else if (std::strcmp(key, "sched_width") == 0) {
@@ -1268,6 +1274,14 @@ int mpcx_set_option(const char* key, int value) {
   } else if (std::strcmp(key, "mx_seg_min") == 0) {
     if (value < 1) return fail(MPCX_EINVAL, "mx_seg_min %d < 1", value);
     g_mx_seg_min = (uint32_t)value;
+  } else if (std::strcmp(key, "mx_step") == 0) {
+    // the launch-time model's k_modexp_mx wave-round time relative to k_modexp, x100 (100: as CIOS)
+    if (value < 10 || value > 200) return fail(MPCX_EINVAL, "mx_step %d outside [10, 200]", value);
+    g_mx_step = value / 100.0;
+  } else if (std::strcmp(key, "geom_tput") == 0) {
+    // the launch-time model's weight on the launch's share of the GPU's SIMD time, x100
+    if (value < 0 || value > 1000) return fail(MPCX_EINVAL, "geom_tput %d outside [0, 1000]", value);
+    g_geom_tput = value / 100.0;
   } else if (std::strcmp(key, "fixed_window") == 0) {
     // widest fixed window of per-operand exponents: 4 (Go's) or 5 (above 320 bits)
     if (value != 4 && value != 5) return fail(MPCX_EINVAL, "fixed_window %d not 4 or 5", value);
@@ -1329,6 +1343,10 @@ static void read_env_options() {
   if (fw) g_fb_window = std::max(4, std::min(MPCX_FB_MAX_WINDOW_BITS, std::atoi(fw)));
   const char* mx = std::getenv("MPCX_MX");  // geometry-2 batches on k_modexp_mx
   if (mx) g_mx = std::max(0, std::min(2, std::atoi(mx)));
+  const char* ms = std::getenv("MPCX_MX_STEP");  // x100, the launch-time model's k_modexp_mx step (A/B runs)
+  if (ms) g_mx_step = std::max(10, std::min(200, std::atoi(ms))) / 100.0;
+  const char* gt = std::getenv("MPCX_GEOM_TPUT");  // x100, the launch-time model's GPU-share weight
+  if (gt) g_geom_tput = std::max(0, std::min(1000, std::atoi(gt))) / 100.0;
 }
 
 int mpcx_init(int device) {
@@ -1572,19 +1590,26 @@ int mpcx_modulus_geometry(mpcx_mod_t mod, uint32_t* L, uint32_t* P, uint32_t* K,
 // profiles/r04/geom_sweep_c1/: lane pair 25.4 ms per wavefront-per-SIMD step,
 // 4 x 19 at 0.556 and 16 x 5 at 0.226 of it) sent mid-size batches to 4 x 19 and
 // measured 7% slower on config 5's concurrent load (profiles/r04/c1model_ab/).
-static int fastest_geom(int cls, uint32_t count, int nsimd) {
+// mx_ok: the main geometry's launch would run on the matrix cores (k_modexp_mx /
+// k_modexp_multi_mx), whose wave-per-SIMD step is g_mx_step of the CIOS one
+// (config 2: 139.5 vs 172.5 ms, profiles/r06/libab1/ vs profiles/r05/s2/).
+// g_geom_tput > 0 adds that weight x the launch's share of the GPU's SIMD time
+// (s x waves / nsimd) to its latency: under concurrent launches (signing,
+// keygen) the SIMDs a geometry occupies are time the other lanes' kernels lose.
+static int fastest_geom(int cls, uint32_t count, int nsimd, bool mx_ok = false) {
   struct M {
     int g;
     double c0, s;
   };
-  const M ms[3] = {{MPCX_MAIN_GEOM(cls), 0.10, 1.0}, {MPCX_MID_GEOM(cls), 0.12, 0.585},
+  const M ms[3] = {{MPCX_MAIN_GEOM(cls), 0.10, mx_ok ? g_mx_step : 1.0}, {MPCX_MID_GEOM(cls), 0.12, 0.585},
                    {MPCX_NARROW_GEOM(cls), 0.20, 0.245}};
   int best = ms[0].g;
   double tb = 1e300;
   for (const M& m : ms) {
     const uint32_t G = (uint32_t)MPCX_GEOM_G(m.g);
     const double waves = (double)((count + G - 1) / G);
-    const double t = m.c0 + m.s * std::ceil(waves / (double)std::max(1, nsimd));
+    const double t = m.c0 + m.s * std::ceil(waves / (double)std::max(1, nsimd)) +
+                     g_geom_tput * m.s * waves / (double)std::max(1, nsimd);
     if (t < tb) {
       tb = t;
       best = m.g;
@@ -1597,13 +1622,14 @@ static int fastest_geom(int cls, uint32_t count, int nsimd) {
 // forced geometry, or policy 2's main, or policy 1's launch-time model, or
 // the thresholds) -- the multi-batch launch takes one geometry for all its
 // segments.
-static int choose_geom(const Device& dev, int cls, uint32_t count, bool main_serves, bool forced_serves) {
+static int choose_geom(const Device& dev, int cls, uint32_t count, bool main_serves, bool forced_serves,
+                       bool mx_ok = false) {
   const int gm = main_serves ? g_main_geom[cls] : MPCX_FULL_GEOM(cls);
   const int gn = MPCX_NARROW_GEOM(cls), gmid = MPCX_MID_GEOM(cls);
   if (g_force_geom >= 0 && MPCX_GEOM_CLASS(g_force_geom) == cls)
     return forced_serves ? g_force_geom : MPCX_FULL_GEOM(cls);
   if (g_geom_policy == 2) return gm;
-  if (g_geom_policy == 1 && gmid >= 0 && gn >= 0) return fastest_geom(cls, count, dev.num_cus * 4);
+  if (g_geom_policy == 1 && gmid >= 0 && gn >= 0) return fastest_geom(cls, count, dev.num_cus * 4, mx_ok && main_serves);
   const uint32_t G = (uint32_t)MPCX_GEOM_G(gm);
   const double rounds = (double)((count + G - 1) / G) / (double)std::max(1, dev.geom_slots[gm]);
   if (gn >= 0 && rounds < g_narrow_rounds) return gn;
@@ -1653,7 +1679,8 @@ static int modexp_enqueue(int di, Lane& lane, mpcx_mod_t mod, uint32_t count, co
       // other lanes fill the SIMDs a small batch leaves idle)
       parts[nparts++] = {gm, 0, count};
     } else if (g_geom_policy == 1 && gmid >= 0 && gn >= 0) {
-      parts[nparts++] = {fastest_geom(mod->cls, count, dev.num_cus * 4), 0, count};
+      const bool mx_ok = g_mx && gm == 2 && count >= g_mx_min;  // the main geometry would be k_modexp_mx
+      parts[nparts++] = {fastest_geom(mod->cls, count, dev.num_cus * 4, mx_ok), 0, count};
     } else if (gn >= 0 && rounds < g_narrow_rounds) {
       parts[nparts++] = {gn, 0, count};
     } else {
@@ -1978,7 +2005,10 @@ int mpcx_modexp_multi_batch(uint32_t n_groups, const mpcx_modexp_group_t* gs) {
       }
     }
   }
-  const int geom = choose_geom(dev, cls, (uint32_t)total, main_ok, forced_ok);
+  bool mx_ok = g_mx && cls == 2 && total >= g_mx_min;  // the main geometry would run k_modexp_multi_mx
+  for (uint32_t i = 0; i < n_groups && mx_ok; ++i)
+    if (gs[i].count && gs[i].count < g_mx_seg_min) mx_ok = false;
+  const int geom = choose_geom(dev, cls, (uint32_t)total, main_ok, forced_ok, mx_ok);
   const uint32_t G = (uint32_t)MPCX_GEOM_G(geom), K = (uint32_t)MPCX_GEOM_K(geom), L = (uint32_t)MPCX_GEOM_L(geom);
   // the 4096-bit main geometry's segments on the matrix cores when the launch is
   // large and every segment fills at least one workgroup's worth of its tables

@@ -208,3 +208,32 @@ def test_mx_structured_moduli(dev):
         assert _mx_launched(st)
         for i in list(range(5)) + rng.sample(range(5, len(bases)), 11):
             assert got[i] == pow(bases[i], exps[i], m), (hex(m)[:12], i)
+
+
+def test_mx_ragged_batch_unreduced_operands(dev):
+    """a single k_modexp_mx launch whose last workgroup has spare
+    wavefronts (2,100 operands: not a whole number of MX_WG-wave workgroups of 16
+    operands per wave) and bases / multipliers at or above m, up to the class's
+    word width (what the C-ABI accepts): bit-exact against pow and the CIOS kernel."""
+    rng = random.Random(5109)
+    n, m = _modulus(rng)
+    mod = mpcx.Modulus(m)
+    lim = 1 << (32 * mod.class_words)
+    mod.release()
+    count = 2100
+    bases = [rng.randrange(m, lim) if i % 3 == 0 else rng.randrange(m) for i in range(count)]
+    bases[1], bases[2] = lim - 1, m
+    muls = [rng.randrange(m, lim) if i % 2 else rng.randrange(m) for i in range(count)]
+    got, st = _run(m, bases, n, 1, muls=muls)
+    assert _mx_launched(st), st
+    ref, st0 = _run(m, bases, n, 0, muls=muls)
+    assert not _mx_launched(st0)
+    assert got == ref
+    for i in list(range(4)) + rng.sample(range(4, count), 28) + [count - 1]:
+        assert got[i] == muls[i] * pow(bases[i], n, m) % m, i
+    # per-operand exponents on the same ragged batch
+    exps = [rng.getrandbits(256) for _ in range(count)]
+    got, st = _run(m, bases, exps, 1)
+    assert _mx_launched(st)
+    for i in [0, 1, 2, count - 1] + rng.sample(range(3, count - 1), 20):
+        assert got[i] == pow(bases[i], exps[i], m), i

@@ -121,6 +121,23 @@ def test_fac_golden_and_rejections(pr, nodes, vec):
     assert ok == [True, True] + [False] * (len(cases) - 2)
     for c, o in zip(cases, ok):
         assert PR.fac_verify(PR.FacProof(**c), ss, *args) == o
+    # FacVerify folds R^e into s^(N0 e) t^(Sigma e), so a peer's Sigma
+    # sets the length of a per-operand exponent. Over-long Sigma (off the group
+    # order, and shifted by a multiple of it, which leaves R unchanged), V = -1,
+    # and an honest proof in the same batch: the same decisions as the oracle,
+    # and nothing else in the batch fails
+    odd = []
+    for dsig in (1 << 6000, order << 3000, -1):
+        c = dict(got[0])
+        c["Sigma"] += dsig
+        odd.append(c)
+    c = dict(got[0])
+    c["V"] = -1
+    odd += [c, got[0]]
+    ok2 = pr.fac_verify([ss] * len(odd), *args, odd)
+    want = [PR.fac_verify(PR.FacProof(**c), ss, *args) for c in odd]
+    assert ok2 == want
+    assert ok2[0] is False and ok2[-1] is True
     # the proof is bound to the verifier's N~
     n2 = nodes[2]
     assert pr.fac_verify([ss], n0["N"], n2["NTildei"], n2["H1i"], n2["H2i"], [got[0]]) == [False]

@@ -43,12 +43,30 @@ __global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(MXB_
   if (wave >= MX_WG / 2)
     for (int i = 0; i < MXB_STAGGER; ++i) __builtin_amdgcn_s_sleep(127);
 #endif
+#ifdef MXB_PRIO_HALF
+  if (wave >= MX_WG / 2) __builtin_amdgcn_s_setprio(1);
+#endif
+  mx_phase_offset(wave);
+#ifdef MX_PROF
+  MxProf prof{};
+#define PROF_ARG , &prof
+#else
+#define PROF_ARG
+#endif
   for (uint32_t s = 0; s < S; ++s) {
     lds_store_sqr<MX_K>(rows + g * MxG2::ROW, p, A);
     wave_lds_fence();
-    montmul_mx<MxG2, true, (bool)MPCX_SQR_B2>(A, rows, md, c, lane);
+    montmul_mx<MxG2, true, (bool)MPCX_SQR_B2>(A, rows, md, c, lane PROF_ARG);
     wave_lds_fence();
   }
+#ifdef MX_PROF
+  // per-wave phase cycles (s_memtime ticks) after the rows' debug copy
+  if (dbg && lane == 0) {
+#pragma unroll
+    for (int i = 0; i < 6; ++i) dbg[MX_G * MX_ROW + blk * 8 + i] = (uint32_t)(prof.t[i] >> 8);
+  }
+#endif
+  mx_phase_tail(wave);
   if (op < count) {
 #pragma unroll
     for (int k = 0; k < MX_K; ++k) out[(size_t)op * MX_L + p * MX_K + k] = A[k];

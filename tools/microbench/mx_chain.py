@@ -176,7 +176,10 @@ def main():
     # warm-up, then timed
     lib.mxb_chain_mx(vp(xd), vp(o_mx), vp(imgd), vp(md), 2, count, None)
     lib.mxb_chain_cios(vp(xd), vp(o_ci), vp(md), n0inv, 2, count)
-    t_mx = lib.mxb_chain_mx(vp(xd), vp(o_mx), vp(imgd), vp(md), S, count, None)
+    prof = None
+    if os.environ.get("MX_PROF"):  # a build with -DMX_PROF: per-wave phase cycles after the rows
+        prof = torch.zeros(16 * L + ((count + 15) // 16) * 8, dtype=torch.int32, device=dev)
+    t_mx = lib.mxb_chain_mx(vp(xd), vp(o_mx), vp(imgd), vp(md), S, count, vp(prof) if prof is not None else None)
     t_ci = lib.mxb_chain_cios(vp(xd), vp(o_ci), vp(md), n0inv, S, count)
     torch.cuda.synchronize()
     omx, oci = o_mx.cpu().to(torch.int64) & 0xFFFFFFFF, o_ci.cpu().to(torch.int64) & 0xFFFFFFFF
@@ -200,6 +203,11 @@ def main():
         "ns_per_squaring_mx": round(t_mx * 1e6 / sq, 4), "ns_per_squaring_cios": round(t_ci * 1e6 / sq, 4),
         "speedup": round(t_ci / t_mx, 3) if t_mx > 0 else None,
     })
+    if prof is not None:
+        pv = (prof.cpu().to(torch.int64) & 0xFFFFFFFF)[16 * L:].view(-1, 8)[:, :6].to(torch.float64) * 256 / S
+        names = ["product", "fence_bfrag", "q_phase", "qm_emit", "fence", "carry_loop"]
+        res["phase_cycles_per_squaring_mean_wave"] = {k: round(float(v), 1) for k, v in zip(names, pv.mean(0))}
+        res["phase_cycles_total"] = round(float(pv.sum(1).mean()), 1)
     print(json.dumps(res))
 
 
