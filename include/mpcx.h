@@ -403,6 +403,17 @@ int mpcx_sync(void* stream);
  *                (k_modexp_multi_mx) when every group has >= "mx_seg_min"
  *                operands (default 256): signing +10%, profiles/r05/mx/multi/.
  *                Environment: MPCX_MX.
+ *   "mx_step"    10..200 (default 81): the launch-time model's wave-round time
+ *                of a 4096-bit main-geometry launch that will run on the
+ *                matrix cores, in percent of the CIOS kernel's (config 2: 139.5
+ *                vs 172.5 ms); 100 ignores the matrix cores (round 5's model).
+ *                Round 6, three interleaved rounds against 100: 2 signers 7,418
+ *                vs 7,237 sigs/s, 3 signers 3,398 vs 3,296, keygen 424 vs 419
+ *                (profiles/r06/geomtput/). Environment: MPCX_MX_STEP.
+ *   "geom_tput"  0..1000 (default 0): weight, in percent, of a launch's share of
+ *                the GPU's SIMD time in the launch-time model (latency +
+ *                weight x share). 150 / 300 measured neutral to slower (same
+ *                A/B). Environment: MPCX_GEOM_TPUT.
  *   "prime_coop" 1 (default): cooperative per-candidate prime kernels; 0:
  *                thread per candidate.
  *   "lanes"      1..8 (default 6, or MPCX_LANES): execution lanes (streams
@@ -423,10 +434,11 @@ int mpcx_sync(void* stream);
  *                with an event pair for mpcx_kernel_stats.
  * Environment, read at mpcx_init / mpcx_init_devices: MPCX_LANES (1..8,
  * default 6: execution lanes per device), MPCX_GEOM_POLICY, MPCX_NARROW_ROUNDS,
- * MPCX_PRIME_COOP, MPCX_FB_WINDOW. */
+ * MPCX_PRIME_COOP, MPCX_FB_WINDOW, MPCX_MX, MPCX_MX_STEP, MPCX_GEOM_TPUT. */
 int mpcx_set_option(const char* key, int value);
-/* Current value of "mx", "mx_min", "mx_seg_min", "geom_policy", "sched_width",
- * "fixed_window", "fb_split" or "lanes" (benchmarks record which kernel path ran). */
+/* Current value of "mx", "mx_min", "mx_seg_min", "mx_step", "geom_tput",
+ * "geom_policy", "sched_width", "fixed_window", "fb_split" or "lanes"
+ * (benchmarks record which kernel path ran). */
 int mpcx_get_option(const char* key, int* value);
 
 /* The constant tables of k_modexp_mx (the 4096- and 2048-bit main geometries

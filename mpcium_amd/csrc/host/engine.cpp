@@ -3,6 +3,7 @@
 
 #include <condition_variable>
 #include <cstdio>
+#include <cstdlib>
 #include <deque>
 #include <malloc.h>
 #include <string>
@@ -126,14 +127,24 @@ namespace {
 // Pool of page-locked host buffers (mpcx_host_alloc) for the batches' inputs
 // and outputs: libmpcx DMAs them directly (anything else it bounces through
 // its lanes' own pinned buffers with a CPU copy). Buffers are reused across
-// calls (size classes of powers of two); free buffers beyond kCacheMax bytes
+// calls (size classes of powers of two); free buffers beyond cache_max() bytes
 // are returned to the system. A failed pinned allocation first releases every
 // cached free buffer and retries; only then does the batch fall back to a
 // pageable buffer -- counted, and logged to stderr (the first 8 times, then
 // every 1000th), never silent.
 class PinnedPool {
  public:
-  static constexpr size_t kCacheMax = size_t(8) << 30;
+  // free pinned bytes kept for reuse: MPCX_PINNED_CACHE_MB, else 8 GB shared by
+  // the node's local ranks (LOCAL_WORLD_SIZE under torchrun), at least 1 GB
+  static size_t cache_max() {
+    static const size_t v = [] {
+      if (const char* e = std::getenv("MPCX_PINNED_CACHE_MB")) return (size_t)std::max(0L, std::atol(e)) << 20;
+      long ranks = 1;
+      if (const char* w = std::getenv("LOCAL_WORLD_SIZE")) ranks = std::max(1L, std::atol(w));
+      return std::max((size_t)1 << 30, ((size_t)8 << 30) / (size_t)ranks);
+    }();
+    return v;
+  }
   static PinnedPool& get() {
     static PinnedPool p;
     return p;
@@ -168,7 +179,7 @@ class PinnedPool {
     std::unique_lock<std::mutex> lk(mu_);
     const size_t cls = size_of_.at(p);
     in_use_bytes_ -= cls * 4;
-    if (cached_bytes_ + cls * 4 > kCacheMax) {
+    if (cached_bytes_ + cls * 4 > cache_max()) {
       size_of_.erase(p);
       held_bytes_ -= cls * 4;
       lk.unlock();

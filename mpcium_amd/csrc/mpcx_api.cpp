@@ -183,6 +183,8 @@ struct Lane {
   struct Bounce {
     char* p = nullptr;
     size_t cap = 0, used = 0;
+    size_t peak = 0;     // largest use since the last lane_wait
+    uint32_t quiet = 0;  // lane_waits in a row whose peak stayed under kBounceKeep
   };
   Bounce hin, hout;
   struct Post {
@@ -649,6 +651,28 @@ int lane_stream(Lane& l) {
 // few ms each: those spins were a third of the process's CPU time
 // (profiles/r03/sample1). The added latency is <= 100 us per launch.
 // MPCX_LANE_WAIT=event: hipEventSynchronize; =stream: hipStreamSynchronize.
+// A bounce buffer grown past kBounceKeep by a large request is released (to the
+// deferred-free list: hipHostFree synchronises the device) once kBounceQuiet
+// lane waits in a row stayed under kBounceKeep, so one large copy does not pin
+// its 1.25x for the life of the lane. Lane idle (used == 0).
+constexpr size_t kBounceKeep = (size_t)64 << 20;
+constexpr uint32_t kBounceQuiet = 256;
+void retire_pinned(char* p, size_t bytes);
+void bounce_trim(Lane& l) {
+  for (Lane::Bounce* b : {&l.hin, &l.hout}) {
+    if (b->cap <= kBounceKeep) {
+      b->peak = 0;
+      continue;
+    }
+    b->quiet = b->peak <= kBounceKeep ? b->quiet + 1 : 0;
+    b->peak = 0;
+    if (b->quiet >= kBounceQuiet) {
+      retire_pinned(b->p, b->cap);
+      *b = Lane::Bounce{};
+    }
+  }
+}
+
 int lane_wait(Lane& l) {
   static const int mode = [] {
     const char* e = std::getenv("MPCX_LANE_WAIT");
@@ -681,6 +705,7 @@ int lane_wait(Lane& l) {
   l.post.clear();
   l.hin.used = l.hout.used = 0;
   l.pending = false;
+  bounce_trim(l);
   if (!l.kpend.empty()) kstat_resolve(l);
   return MPCX_OK;
 }
@@ -733,6 +758,7 @@ int bounce_reserve(Lane& l, Lane::Bounce& b, size_t bytes, char** out) {
   }
   *out = b.p + b.used;
   b.used += need;
+  b.peak = std::max(b.peak, b.used);
   return MPCX_OK;
 }
 

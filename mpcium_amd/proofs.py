@@ -137,15 +137,23 @@ def fac_prove(sessions: Sequence[bytes], N0: int, NCap: int, s: int, t: int, N0p
 
 
 def fac_verify(sessions: Sequence[bytes], N0: int, NCap: int, s: int, t: int, pfs: Sequence[dict]) -> List[bool]:
+    """A proof with a field wider than the batch's W words (a peer's Sigma or V
+    has no length bound on the wire) cannot cross the C-ABI: it is rejected here,
+    as tss-lib rejects it (every field enters the challenge hash), and the rest
+    of the batch is verified."""
     n = len(pfs)
     ss, sl = _sessions(sessions)
     args = [_one(v) for v in (N0, NCap, s, t)]
+    lim = 1 << (32 * W)
+    wide = [any(abs(p[f]) >= lim for f in FAC_FIELDS) for p in pfs]
+    zero = dict.fromkeys(FAC_FIELDS, 0)
+    pfs = [zero if w else p for p, w in zip(pfs, wide)]  # all-zero fields fail the range checks
     pf = _col([abs(p[f]) for p in pfs for f in FAC_FIELDS])
     neg = np.array([1 if p["V"] < 0 else 0 for p in pfs], dtype=np.uint8)
     ok = np.zeros(n, dtype=np.uint8)
     _host._check(lib().mpcxh_fac_verify_batch(W, ss.ctypes.data, sl, *[a.ctypes.data for a in args], n,
                                               pf.ctypes.data, neg.ctypes.data, ok.ctypes.data))
-    return [bool(x) for x in ok]
+    return [bool(x) and not w for x, w in zip(ok, wide)]
 
 
 class _Party(ctypes.Structure):

@@ -125,7 +125,8 @@ def test_fac_golden_and_rejections(pr, nodes, vec):
     # sets the length of a per-operand exponent. Over-long Sigma (off the group
     # order, and shifted by a multiple of it, which leaves R unchanged), V = -1,
     # and an honest proof in the same batch: the same decisions as the oracle,
-    # and nothing else in the batch fails
+    # and nothing else in the batch fails (a field wider than the C-ABI's W words
+    # is rejected by the wrapper, proofs.fac_verify)
     odd = []
     for dsig in (1 << 6000, order << 3000, -1):
         c = dict(got[0])
