@@ -41,7 +41,7 @@ PEAK_MAD_MEASURED = 33.8e12            # tools/microbench/valu_rates.hip, 8 wave
 
 
 PMC_TRAFFIC = os.path.join(ROOT, "profiles", "r05", "pmc", "config2_traffic.json")        # k_modexp<4, 37, 16, 2>
-PMC_TRAFFIC_MX = os.path.join(ROOT, "profiles", "r05", "pmc_mx", "config2_traffic.json")  # k_modexp_mx
+PMC_TRAFFIC_MX = os.path.join(ROOT, "profiles", "r06", "pmc_mx", "config2_traffic.json")  # k_modexp_mx
 
 
 def pmc_traffic(count: int, modbits: int, mod, mx: bool = False) -> dict:
@@ -1227,6 +1227,12 @@ def node_main(args, progress) -> None:
                            "frac": W * count / (max(kms) * 1e-3) / PEAK_INT32_NOMINAL, "traffic": None,
                            "kernel_ms_per_device": kms},
               "device_launches": {"config2": launches}, "cpu_baseline": None}
+    if mpcx.get_option("mx") == 1 and count >= mpcx.get_option("mx_min"):
+        # the same two-pipe roofline as the per-rank line, per device
+        result["roofline"]["kernel_ms"] = max(kms)
+        result["roofline"]["kernel"] = "k_modexp_mx"
+        result["roofline"]["executed_floor"] = mx_floor(count, N, max(kms))
+        two_pipe_roofline(result["roofline"])
     if digest:
         result["batch_digest"] = digest
     nodes = load_nodes()
@@ -1278,7 +1284,7 @@ def node_main(args, progress) -> None:
     line = {k: result[k] for k in ("metric", "mode", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step",
                                    "higher_is_better", "scaling", "vs_baseline", "dtype", "data", "config")}
     line["roofline"] = {k: _r(v) if isinstance(v, float) else v for k, v in result["roofline"].items()
-                        if k != "kernel_ms_per_device"}
+                        if k not in ("kernel_ms_per_device", "executed_floor", "go_equiv_note")}
     line["cpu_baseline"] = None
     line["device_launches"] = result["device_launches"]["config2"]
     if digest:
