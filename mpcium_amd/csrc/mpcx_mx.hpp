@@ -184,6 +184,27 @@ __device__ __forceinline__ void mx_split(const mx_v4i c, int add, int& lo_sum, i
   hi_sum = (c[1] >> 21) + (c[2] >> 14) + (c[3] >> 7);
 }
 
+// MX_SPLIT_MAD: the same digit sum as one 64-bit value V = c0 + add + c1 2^7 +
+// c2 2^14 + c3 2^21 built by three v_mad_i64_i32 (the MAD pipe idles during the
+// reduction) instead of masks, shifts and adds on the VALU; lo = V mod 2^28 and
+// the carry V >> 28 (arithmetic) follow from V directly. Multipliers in SGPRs
+// (VOP3 takes no literal), so the compiler cannot turn them back into shifts.
+#ifndef MX_SPLIT_MAD
+#define MX_SPLIT_MAD 1
+#endif
+__device__ __forceinline__ int64_t mx_sum64(const mx_v4i c, int add) {
+  int64_t v = (int64_t)(c[0] + add);
+  uint64_t cy;
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(c[1]), "s"(1 << 7));
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(c[2]), "s"(1 << 14));
+  asm("v_mad_i64_i32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(c[3]), "s"(1 << 21));
+  return v;
+}
+// V >> 28 as a 32-bit int (|V| < 2^59): one v_alignbit_b32 of the two halves
+__device__ __forceinline__ int mx_hi28(int64_t v) {
+  return (int)__builtin_amdgcn_alignbit((uint32_t)((uint64_t)v >> 32), (uint32_t)v, 28);
+}
+
 // acc[o - O0] += sum over K blocks kb of F_j (j = o - 4 kb) x bf[kb], for output
 // blocks O0 <= o < O1; Toeplitz block j is read once and used for every kb it
 // pairs with (one block ahead of its MFMAs)
@@ -375,10 +396,17 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
       int xprev = 0;
       uint32_t X[4] = {0u, 0u, 0u, 0u};
       auto norm = [&](const mx_v4i& cs, int o) __attribute__((always_inline)) -> uint32_t {
-        int lo_sum, hi_sum;
-        mx_split(cs, 1 << 27, lo_sum, hi_sum);
-        const int lo = (lo_sum & (int)M28) - (1 << 27);
-        const int hi = hi_sum + (lo_sum >> 28);
+        int lo, hi;
+        if constexpr (MX_SPLIT_MAD) {
+          const int64_t v = mx_sum64(cs, 1 << 27);
+          lo = ((int)(uint32_t)v & (int)M28) - (1 << 27);
+          hi = mx_hi28(v);
+        } else {
+          int lo_sum, hi_sum;
+          mx_split(cs, 1 << 27, lo_sum, hi_sum);
+          lo = (lo_sum & (int)M28) - (1 << 27);
+          hi = hi_sum + (lo_sum >> 28);
+        }
         const int x = mx_from_prev_quarter(hi, lane);
         int e = lo + (h == 0 ? xprev : x);
         xprev = x;
@@ -444,14 +472,24 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
         const int d = (pos - S::N7) >> 2;  // U's digit (< 0: the low half)
         const int dc = d < 0 ? 0 : d;
         const int add = carry_lane ? ttop[s] + (1 << 27) : (int)rn[dc];
-        int lo_sum, hi_sum;
-        mx_split(cs, add, lo_sum, hi_sum);
-        const int hi = hi_sum + (lo_sum >> 28);  // on the carry lane: round(low half / R)
+        int hi, dig, top;  // dig: the sum's bits 0..27; top: the sum mod 2^32
+        if constexpr (MX_SPLIT_MAD) {
+          const int64_t v = mx_sum64(cs, add);
+          hi = mx_hi28(v);  // on the carry lane: round(low half / R)
+          top = (int)(uint32_t)v;
+          dig = top & (int)M28;
+        } else {
+          int lo_sum, hi_sum;
+          mx_split(cs, add, lo_sum, hi_sum);
+          hi = hi_sum + (lo_sum >> 28);
+          top = (int)((uint32_t)lo_sum + ((uint32_t)hi_sum << 28));
+          dig = lo_sum & (int)M28;
+        }
         const int x = mx_from_prev_quarter(hi, lane);
         const int cin = h == 0 ? xprev : x;
         xprev = x;
         // the top digit keeps its carry (the value is < 2m < 2^(28 L - 47))
-        const int u = d == L - 1 ? (int)((uint32_t)lo_sum + ((uint32_t)hi_sum << 28)) + cin : (lo_sum & (int)M28) + cin;
+        const int u = d == L - 1 ? top + cin : dig + cin;
         if (d >= 0) rn[dc] = (uint32_t)u;
       };
       constexpr int NC = (S::O2HI - S::O2LO + S::CS2 - 1) / S::CS2;
