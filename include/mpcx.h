@@ -401,7 +401,11 @@ int mpcx_sync(void* stream);
  *                2048-bit modexp/s, keygen -7%: profiles/r05/mx/g5/).
  *                Multi-batch launches of the 4096-bit main geometry use it too
  *                (k_modexp_multi_mx) when every group has >= "mx_seg_min"
- *                operands (default 256): signing +10%, profiles/r05/mx/multi/.
+ *                operands (default 64 since round 6: six interleaved rounds
+ *                against 256, 2 signers 7,454 vs 7,022 sigs/s, 3 signers 3,435
+ *                vs 3,318, keygen 417 vs 425 sessions/s, profiles/r06/segmin*;
+ *                round 5: the multi-batch kernel itself, signing +10%,
+ *                profiles/r05/mx/multi/).
  *                Environment: MPCX_MX.
  *   "mx_step"    10..200 (default 81): the launch-time model's wave-round time
  *                of a 4096-bit main-geometry launch that will run on the

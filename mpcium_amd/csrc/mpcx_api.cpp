@@ -129,7 +129,7 @@ bool g_dup_device = false;               // mpcx_set_option("duplicate_device", 
 #endif
 int g_mx = MPCX_MX_DEFAULT;              // mpcx_set_option("mx", 1): geometry-2 batches reduce on the matrix cores
 uint32_t g_mx_min = 2048;                // mpcx_set_option("mx_min", n): smallest batch for k_modexp_mx
-uint32_t g_mx_seg_min = 256;             // mpcx_set_option("mx_seg_min", n): smallest segment of a k_modexp_multi_mx launch
+uint32_t g_mx_seg_min = 64;              // mpcx_set_option("mx_seg_min", n): smallest segment of a k_modexp_multi_mx launch (round 6: 64 vs 256, profiles/r06/segmin*)
 double g_mx_step = 0.81;                 // mpcx_set_option("mx_step", 100x): k_modexp_mx's wave-round time / k_modexp's (0: model ignores mx)
 double g_geom_tput = 0.0;                // mpcx_set_option("geom_tput", 100x): GPU-share weight of the launch-time model
 struct Staging {
