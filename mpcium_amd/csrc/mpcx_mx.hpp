@@ -63,11 +63,40 @@ __device__ __forceinline__ MxConsts mx_consts(const uint8_t* img, int lane) {
 
 // radix-2^28 digit (two's complement, |x| < 2^28) -> 4 radix-2^7 digits, one per
 // byte (the top one signed): open a 1-bit gap above bits 6, 13 and 20
+// MX_SPREAD_MAD (A/B): the same bytes from the closed form
+// x + 2^7 (x >> 7) + 2^15 (x >> 14) + 2^23 (x >> 21) (mod 2^32, logical shifts),
+// 1: three VALU shifts and three v_mad_u64_u32; 2: the shifts as the high halves
+// of x * 2^25, 2^18, 2^11 (six MADs, no VALU shift)
+#ifndef MX_SPREAD_MAD
+#define MX_SPREAD_MAD 0
+#endif
 __device__ __forceinline__ uint32_t mx_spread7(uint32_t x) {
-  x += x & 0xFFFFFF80u;
-  x += x & 0xFFFF8000u;
-  x += x & 0xFF800000u;
-  return x;
+  if constexpr (MX_SPREAD_MAD == 0) {
+    x += x & 0xFFFFFF80u;
+    x += x & 0xFFFF8000u;
+    x += x & 0xFF800000u;
+    return x;
+  } else {
+    uint64_t v = x, cy;
+    uint32_t s7, s14, s21;
+    if constexpr (MX_SPREAD_MAD == 1) {
+      s7 = x >> 7;
+      s14 = x >> 14;
+      s21 = x >> 21;
+    } else {
+      uint64_t t;
+      asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(t), "=s"(cy) : "v"(x), "s"(1u << 25));
+      s7 = (uint32_t)(t >> 32);
+      asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(t), "=s"(cy) : "v"(x), "s"(1u << 18));
+      s14 = (uint32_t)(t >> 32);
+      asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(t), "=s"(cy) : "v"(x), "s"(1u << 11));
+      s21 = (uint32_t)(t >> 32);
+    }
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(s7), "s"(1u << 7));
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(s14), "s"(1u << 15));
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(s21), "s"(1u << 23));
+    return (uint32_t)v;
+  }
 }
 
 // T = A * B (B == A for SQR; B2IN: the row holds 2B) in montmul's row loop without
