@@ -563,7 +563,21 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
 #pragma unroll
   for (int k = 0; k < K; ++k) A[k] = rg[p * K + k];
   MX_STAMP(5);
-  for (int it = 0; it < L + 2; ++it) {
+  // MX_CARRY_SKIP: the emitted digits lie in (-2^16, 2^28 + 2^16) (one carry step
+  // of |carry| < 2^16); the next product takes any non-negative digits of that
+  // size (its 64-bit accumulators have the room), so the passes run only when
+  // some digit of the wave is negative (~1 wave in 4)
+#ifndef MX_CARRY_SKIP
+#define MX_CARRY_SKIP 0
+#endif
+  bool need = true;
+  if constexpr (MX_CARRY_SKIP) {
+    uint32_t sg = 0;
+#pragma unroll
+    for (int k = 0; k < K; ++k) sg |= A[k];
+    need = __any((int)sg < 0);
+  }
+  for (int it = 0; need && it < L + 2; ++it) {
     const int top = (int)A[K - 1];
     const int ctop = (p == P - 1) ? 0 : (top >> DB);
 #pragma unroll
