@@ -568,7 +568,7 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
   // size (its 64-bit accumulators have the room), so the passes run only when
   // some digit of the wave is negative (~1 wave in 4)
 #ifndef MX_CARRY_SKIP
-#define MX_CARRY_SKIP 0
+#define MX_CARRY_SKIP 1
 #endif
   bool need = true;
   if constexpr (MX_CARRY_SKIP) {
