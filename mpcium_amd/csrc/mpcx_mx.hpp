@@ -63,40 +63,13 @@ __device__ __forceinline__ MxConsts mx_consts(const uint8_t* img, int lane) {
 
 // radix-2^28 digit (two's complement, |x| < 2^28) -> 4 radix-2^7 digits, one per
 // byte (the top one signed): open a 1-bit gap above bits 6, 13 and 20
-// MX_SPREAD_MAD (A/B): the same bytes from the closed form
-// x + 2^7 (x >> 7) + 2^15 (x >> 14) + 2^23 (x >> 21) (mod 2^32, logical shifts),
-// 1: three VALU shifts and three v_mad_u64_u32; 2: the shifts as the high halves
-// of x * 2^25, 2^18, 2^11 (six MADs, no VALU shift)
-#ifndef MX_SPREAD_MAD
-#define MX_SPREAD_MAD 0
-#endif
+// (round 6: the closed form x + 2^7 (x >> 7) + 2^15 (x >> 14) + 2^23 (x >> 21) on the
+// MAD pipe measured slower, profiles/r06/spab/)
 __device__ __forceinline__ uint32_t mx_spread7(uint32_t x) {
-  if constexpr (MX_SPREAD_MAD == 0) {
-    x += x & 0xFFFFFF80u;
-    x += x & 0xFFFF8000u;
-    x += x & 0xFF800000u;
-    return x;
-  } else {
-    uint64_t v = x, cy;
-    uint32_t s7, s14, s21;
-    if constexpr (MX_SPREAD_MAD == 1) {
-      s7 = x >> 7;
-      s14 = x >> 14;
-      s21 = x >> 21;
-    } else {
-      uint64_t t;
-      asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(t), "=s"(cy) : "v"(x), "s"(1u << 25));
-      s7 = (uint32_t)(t >> 32);
-      asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(t), "=s"(cy) : "v"(x), "s"(1u << 18));
-      s14 = (uint32_t)(t >> 32);
-      asm("v_mad_u64_u32 %0, %1, %2, %3, 0" : "=v"(t), "=s"(cy) : "v"(x), "s"(1u << 11));
-      s21 = (uint32_t)(t >> 32);
-    }
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(s7), "s"(1u << 7));
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(s14), "s"(1u << 15));
-    asm("v_mad_u64_u32 %0, %1, %2, %3, %0" : "+v"(v), "=s"(cy) : "v"(s21), "s"(1u << 23));
-    return (uint32_t)v;
-  }
+  x += x & 0xFFFFFF80u;
+  x += x & 0xFFFF8000u;
+  x += x & 0xFF800000u;
+  return x;
 }
 
 // T = A * B (B == A for SQR; B2IN: the row holds 2B) in montmul's row loop without
@@ -118,14 +91,6 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
 #pragma unroll
   for (int k = 0; k < K; ++k) acc[k] = 0;
   uint32_t bnext = bl[0];
-#if defined(MX_DUMMY_MFMA) || defined(MX_DUMMY_VALU)
-  // microbench only (tools/microbench/mx_chain.hip): independent work issued from
-  // the product loop, to measure what it costs beside the MADs
-  mx_v4i dacc[4] = {{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}};
-  const mx_v4i dfa = {(int)A[0], (int)A[1], (int)A[2], (int)A[3]};
-  const mx_v4i dfb = {(int)A[4], (int)A[5], (int)A[6], (int)A[7]};
-  uint32_t dv[4] = {A[8], A[9], A[10], A[11]};
-#endif
 #pragma nounroll
   for (int o = 0; o < P; ++o) {
     const uint32_t* bo = bl + o * K;
@@ -150,32 +115,13 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
           }
         }
       });
-#ifdef MX_DUMMY_MFMA
-      static_for<0, MX_DUMMY_MFMA>([&](auto dc) {
-        constexpr int d = (decltype(dc)::value + u) & 3;
-        dacc[d] = __builtin_amdgcn_mfma_i32_16x16x64_i8(dfa, dfb, dacc[d], 0, 0, 0);
-      });
-#endif
-#ifdef MX_DUMMY_VALU
-      static_for<0, MX_DUMMY_VALU>([&](auto dc) {
-        constexpr int d = decltype(dc)::value & 3;
-        dv[d] = (dv[d] & 0x0FFFFFFFu) + (dv[(d + 1) & 3] >> 3);
-      });
-#endif
       const uint64_t a0 = acc[u];
       acc[(u + 1) % K] += a0 >> DB;
       // lane 0's digit leaves the window as T's digit i (in CIOS it is zero);
       // it must not shift into the previous group's top slot
       const uint32_t lo = (uint32_t)a0 & M28;
-#ifndef MX_EMIT_BCAST
-#define MX_EMIT_BCAST 0  // 1: every lane of the group stores lane 0's digit (not used: it spills the product loop at 256 VGPRs)
-#endif
       if constexpr (MX_EMIT == 1) {
         to[u] = lo;
-      } else if constexpr (MX_EMIT_BCAST) {
-        // every lane of the group writes lane 0's digit to the same address: no
-        // exec-mask switch per iteration
-        to[u] = group_bcast<P>(lo, 0);
       } else {
         if (p == 0) to[u] = lo;
       }
@@ -186,12 +132,6 @@ __device__ __forceinline__ void mx_product(uint32_t (&A)[K], const uint32_t* bl,
       if constexpr (MX_ITER_FENCE) __builtin_amdgcn_sched_barrier(0);
     });
   }
-#ifdef MX_DUMMY_MFMA
-  acc[1] += (uint32_t)(dacc[0][0] ^ dacc[1][1] ^ dacc[2][2] ^ dacc[3][3]);
-#endif
-#ifdef MX_DUMMY_VALU
-  acc[2] += dv[0] ^ dv[1] ^ dv[2] ^ dv[3];
-#endif
   carry_pass64<P, K>(acc);
   const uint32_t ctop = (uint32_t)(acc[K - 1] >> DB);
 #pragma unroll
@@ -266,37 +206,6 @@ __device__ __forceinline__ void mx_toeplitz(mx_v4i (&acc)[O1 - O0], const uint8_
   });
 }
 
-// mx_toeplitz with independent VALU work interleaved: fill(i) for i = 0..NFILL-1
-// is issued spread over the chunk's Toeplitz blocks (after block t's MFMAs, the
-// fills t NFILL / NJC .. (t + 1) NFILL / NJC - 1), so one chunk's normalisation
-// runs under the next chunk's MFMAs instead of after them (MX_PIPE)
-template <class S, int NJ, int O0, int O1, int NFILL, int NA, class Fill>
-__device__ __forceinline__ void mx_toeplitz_fill(mx_v4i (&acc)[NA], const uint8_t* f,
-                                                 const mx_v4i (&bf)[S::KB], Fill&& fill) {
-  static_assert(O1 - O0 <= NA, "chunk larger than its accumulators");
-  auto ld = [&](int j) __attribute__((always_inline)) {
-    return *reinterpret_cast<const mx_v4i*>(f + 16 * (S::JMAX - j));
-  };
-  static_for<0, O1 - O0>([&](auto oc) { acc[decltype(oc)::value] = mx_v4i{0, 0, 0, 0}; });
-  constexpr int JLO = (O0 - 4 * (S::KB - 1)) > 0 ? (O0 - 4 * (S::KB - 1)) : 0;
-  constexpr int JHI = (O1 - 1) < (NJ - 1) ? (O1 - 1) : (NJ - 1);
-  constexpr int NJC = JHI - JLO + 1;
-  mx_v4i fnext = ld(JLO);
-  static_for<JLO, JHI + 1>([&](auto jc) {
-    constexpr int j = decltype(jc)::value;
-    const mx_v4i fj = fnext;
-    if constexpr (j + 1 <= JHI) fnext = ld(j + 1);
-    if constexpr (MX_READ_FENCE) __builtin_amdgcn_sched_barrier(0x000F);
-    static_for<0, S::KB>([&](auto kc) {
-      constexpr int kb = decltype(kc)::value;
-      constexpr int o = j + 4 * kb;
-      if constexpr (o >= O0 && o < O1) acc[o - O0] = __builtin_amdgcn_mfma_i32_16x16x64_i8(fj, bf[kb], acc[o - O0], 0, 0, 0);
-    });
-    constexpr int t = j - JLO;
-    static_for<t * NFILL / NJC, (t + 1) * NFILL / NJC>([&](auto ic) { fill(ic); });
-  });
-}
-
 // 4x4 transpose between the register index and the lane quarter (h): on return
 // y[i] in lane (n, h) is x[h] of lane (n, i). Two permlane32 and two permlane16
 // swaps (gfx950), no LDS.
@@ -308,37 +217,9 @@ __device__ __forceinline__ mx_v4i mx_transpose4(uint32_t x0, uint32_t x1, uint32
   return mx_v4i{(int)r01[0], (int)r01[1], (int)r23[0], (int)r23[1]};
 }
 
-// MX_PIPE: 1 = each chunk's normalisation (q) / emission (U) runs interleaved with
-// the next chunk's MFMAs (mx_toeplitz_fill); 0 = MFMAs, then the chunk's VALU work
-#ifndef MX_PIPE
-#define MX_PIPE 0
-#endif
-
-// Phase pairing (MX_PHASE_BARRIER): a workgroup barrier after the product loop
-// and after the reduction, with the workgroup's second half one phase behind
-// (mx_phase_offset at the start), so the two wavefronts of a SIMD (w, w + MX_WG/2)
-// pair one's VALU product loop with the other's matrix-core reduction instead
-// of drifting into the same phase.
-#ifndef MX_PHASE_BARRIER
-#define MX_PHASE_BARRIER 0
-#endif
-__device__ __forceinline__ void mx_phase_barrier() {
-  if constexpr (MX_PHASE_BARRIER) __builtin_amdgcn_s_barrier();
-}
-// the second half of the workgroup starts one phase late
-__device__ __forceinline__ void mx_phase_offset(int wave) {
-  if constexpr (MX_PHASE_BARRIER) {
-    if (wave >= MX_WG / 2) __builtin_amdgcn_s_barrier();
-  }
-}
-
-// ... and the first half ends with one more, so every wave executes the same count
-__device__ __forceinline__ void mx_phase_tail(int wave) {
-  if constexpr (MX_PHASE_BARRIER) {
-    if (wave < MX_WG / 2) __builtin_amdgcn_s_barrier();
-  }
-}
-
+// Round 6 measured and removed: a workgroup barrier pairing one
+// wave's product loop with its SIMD partner's reduction (slower), and each chunk's
+// normalisation interleaved with the next chunk's MFMAs (equal).
 // A <- A * B * R^-1 + m (mod-m class preserved; result in (m/2, 3m/2) for A, B < 2m).
 // rows: this wavefront's G operand rows (S::ROW words each); operand g's row holds
 // B (2B for squarings) on entry and is the scratch of the whole product: T's low
@@ -383,7 +264,6 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
   MX_STAMP(1);
   if constexpr (MPCX_MX_TIMING == 1) return;
   wave_lds_fence();
-  mx_phase_barrier();
   // ---- T's low half as B fragments (radix-2^7 bytes), every half of the wave
   mx_v4i bf[S::HALVES][KB];
   int ttop[S::HALVES];  // T's digit L - 1: the top 4 positions of the carry estimate
@@ -452,41 +332,16 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
         }
       };
       constexpr int NC = (S::O1 + S::CS1 - 1) / S::CS1;
-      if constexpr (MX_PIPE) {
-        // chunk c's MFMAs with chunk c - 1's normalisation interleaved (two
-        // chunks of accumulators live, alternating by parity)
-        mx_v4i accE[S::CS1], accO[S::CS1];
-        static_for<0, NC + 1>([&](auto cc) {
-          constexpr int cI = decltype(cc)::value;
-          constexpr int P0 = S::CS1 * (cI - 1);  // the previous chunk's blocks
-          constexpr int P1 = cI == 0 ? 0 : (P0 + S::CS1 < S::O1 ? P0 + S::CS1 : S::O1);
-          auto& accP = *[&]() { if constexpr (cI % 2 == 1) return &accE; else return &accO; }();
-          auto& accC = *[&]() { if constexpr (cI % 2 == 0) return &accE; else return &accO; }();
-          auto fill = [&](auto ic) __attribute__((always_inline)) {
-            constexpr int i = decltype(ic)::value;
-            norm_block(accP[i], std::integral_constant<int, P0 + i>{});
-          };
-          if constexpr (cI < NC) {
-            constexpr int O0 = S::CS1 * cI;
-            constexpr int O1 = O0 + S::CS1 < S::O1 ? O0 + S::CS1 : S::O1;
-            mx_toeplitz_fill<S, S::NJ1, O0, O1, (cI == 0 ? 0 : P1 - P0)>(accC, c.t1, bf[s], fill);
-          } else {
-            static_for<0, P1 - P0>(fill);
-          }
-          __builtin_amdgcn_sched_barrier(0);
+      static_for<0, NC>([&](auto cc) {
+        constexpr int O0 = S::CS1 * decltype(cc)::value;
+        constexpr int O1 = O0 + S::CS1 < S::O1 ? O0 + S::CS1 : S::O1;
+        mx_v4i acc[O1 - O0];
+        mx_toeplitz<S, S::NJ1, O0, O1>(acc, c.t1, bf[s]);
+        static_for<0, O1 - O0>([&](auto oc) {
+          norm_block(acc[decltype(oc)::value], std::integral_constant<int, O0 + decltype(oc)::value>{});
         });
-      } else {
-        static_for<0, NC>([&](auto cc) {
-          constexpr int O0 = S::CS1 * decltype(cc)::value;
-          constexpr int O1 = O0 + S::CS1 < S::O1 ? O0 + S::CS1 : S::O1;
-          mx_v4i acc[O1 - O0];
-          mx_toeplitz<S, S::NJ1, O0, O1>(acc, c.t1, bf[s]);
-          static_for<0, O1 - O0>([&](auto oc) {
-            norm_block(acc[decltype(oc)::value], std::integral_constant<int, O0 + decltype(oc)::value>{});
-          });
-          __builtin_amdgcn_sched_barrier(0);  // one chunk's accumulators live at a time
-        });
-      }
+        __builtin_amdgcn_sched_barrier(0);  // one chunk's accumulators live at a time
+      });
     }
     MX_STAMP(3);
     // ---- q m column sums for blocks O2LO.. : the lane whose 4 positions are the
@@ -522,43 +377,19 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
         if (d >= 0) rn[dc] = (uint32_t)u;
       };
       constexpr int NC = (S::O2HI - S::O2LO + S::CS2 - 1) / S::CS2;
-      if constexpr (MX_PIPE) {
-        mx_v4i accE[S::CS2], accO[S::CS2];
-        static_for<0, NC + 1>([&](auto cc) {
-          constexpr int cI = decltype(cc)::value;
-          constexpr int P0 = S::O2LO + S::CS2 * (cI - 1);
-          constexpr int P1 = cI == 0 ? 0 : (P0 + S::CS2 < S::O2HI ? P0 + S::CS2 : S::O2HI);
-          auto& accP = *[&]() { if constexpr (cI % 2 == 1) return &accE; else return &accO; }();
-          auto& accC = *[&]() { if constexpr (cI % 2 == 0) return &accE; else return &accO; }();
-          auto fill = [&](auto ic) __attribute__((always_inline)) {
-            constexpr int i = decltype(ic)::value;
-            emit(accP[i], P0 + i);
-          };
-          if constexpr (cI < NC) {
-            constexpr int O0 = S::O2LO + S::CS2 * cI;
-            constexpr int O1 = O0 + S::CS2 < S::O2HI ? O0 + S::CS2 : S::O2HI;
-            mx_toeplitz_fill<S, S::NJ2, O0, O1, (cI == 0 ? 0 : P1 - P0)>(accC, c.t2, qf, fill);
-          } else {
-            static_for<0, P1 - P0>(fill);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        });
-      } else {
-        static_for<0, NC>([&](auto cc) {
-          constexpr int O0 = S::O2LO + S::CS2 * decltype(cc)::value;
-          constexpr int O1 = O0 + S::CS2 < S::O2HI ? O0 + S::CS2 : S::O2HI;
-          mx_v4i acc[O1 - O0];
-          mx_toeplitz<S, S::NJ2, O0, O1>(acc, c.t2, qf);
-          static_for<0, O1 - O0>([&](auto oc) { emit(acc[decltype(oc)::value], O0 + decltype(oc)::value); });
-          __builtin_amdgcn_sched_barrier(0);
-        });
-      }
+      static_for<0, NC>([&](auto cc) {
+        constexpr int O0 = S::O2LO + S::CS2 * decltype(cc)::value;
+        constexpr int O1 = O0 + S::CS2 < S::O2HI ? O0 + S::CS2 : S::O2HI;
+        mx_v4i acc[O1 - O0];
+        mx_toeplitz<S, S::NJ2, O0, O1>(acc, c.t2, qf);
+        static_for<0, O1 - O0>([&](auto oc) { emit(acc[decltype(oc)::value], O0 + decltype(oc)::value); });
+        __builtin_amdgcn_sched_barrier(0);
+      });
     }
   });
   if constexpr (MX_PRIO) __builtin_amdgcn_s_setprio(0);
   MX_STAMP(4);
   wave_lds_fence();
-  mx_phase_barrier();
   // ---- back to the block layout; signed carry passes until every digit is >= 0
 #pragma unroll
   for (int k = 0; k < K; ++k) A[k] = rg[p * K + k];

@@ -46,7 +46,6 @@ __global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(MXB_
 #ifdef MXB_PRIO_HALF
   if (wave >= MX_WG / 2) __builtin_amdgcn_s_setprio(1);
 #endif
-  mx_phase_offset(wave);
 #ifdef MX_PROF
   MxProf prof{};
 #define PROF_ARG , &prof
@@ -66,7 +65,6 @@ __global__ __launch_bounds__(64 * MX_WG) __attribute__((amdgpu_waves_per_eu(MXB_
     for (int i = 0; i < 6; ++i) dbg[MX_G * MX_ROW + blk * 8 + i] = (uint32_t)(prof.t[i] >> 8);
   }
 #endif
-  mx_phase_tail(wave);
   if (op < count) {
 #pragma unroll
     for (int k = 0; k < MX_K; ++k) out[(size_t)op * MX_L + p * MX_K + k] = A[k];
