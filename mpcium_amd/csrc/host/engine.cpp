@@ -282,19 +282,26 @@ class CoalescerT {
     int rc = MPCX_OK;
     std::string err;
   };
-  int run(Req& r, int max_inflight, uint64_t max_ops) {
+  // min_ops > 0: while another dispatch of this coalescer is in flight, a
+  // leader waits until the queue holds min_ops operands (a finishing dispatch
+  // or a new arrival wakes it; with nothing in flight it always launches)
+  int run(Req& r, int max_inflight, uint64_t max_ops, uint64_t min_ops = 0) {
     std::unique_lock<std::mutex> lk(mu_);
     q_.push_back(&r);
+    queued_ += r.g.count;
+    if (min_ops) cv_.notify_all();
     while (!r.done) {
-      if (!r.taken && inflight_ < max_inflight) {
+      if (!r.taken && inflight_ < max_inflight && (inflight_ == 0 || queued_ >= min_ops)) {
         std::vector<Req*> batch{&r};  // the leader's own group first, then arrival order
         r.taken = true;
         uint64_t ops = r.g.count;
+        queued_ -= r.g.count;
         for (auto it = q_.begin(); it != q_.end();) {
           if (*it == &r) {
             it = q_.erase(it);
           } else if (!(*it)->taken && ops + (*it)->g.count <= max_ops) {
             ops += (*it)->g.count;
+            queued_ -= (*it)->g.count;
             (*it)->taken = true;
             batch.push_back(*it);
             it = q_.erase(it);
@@ -341,6 +348,7 @@ class CoalescerT {
   std::mutex mu_;
   std::condition_variable cv_;
   std::deque<Req*> q_;
+  uint64_t queued_ = 0;  // operands of the groups in q_ not yet taken
   int inflight_ = 0;
 };
 
@@ -366,6 +374,18 @@ uint64_t coalesce_max_ops() {
     const char* e = std::getenv("MPCX_COALESCE_MAXOPS");
     const long long x = e ? std::atoll(e) : 0;
     return x > 0 ? (uint64_t)x : kCoalesceMaxOps;
+  }();
+  return v;
+}
+
+// MPCX_COALESCE_MIN_OPS: queued operands a modexp leader waits for while a
+// dispatch is in flight (0, the default: launch whenever the in-flight budget
+// allows)
+uint64_t coalesce_min_ops() {
+  static const uint64_t v = [] {
+    const char* e = std::getenv("MPCX_COALESCE_MIN_OPS");
+    const long long x = e ? std::atoll(e) : 0;
+    return x > 0 ? (uint64_t)x : (uint64_t)0;
   }();
   return v;
 }
@@ -493,7 +513,7 @@ void Engine::exp_into(const Nat& m, size_t n, const Nat* const* bases, const Nat
       r.g.mul_words = muls ? md.class_words : 0;
       r.g.out = out.p;
       r.g.out_words = md.words;
-      rc = coalescer(md.class_words).run(r, inflight, coalesce_max_ops());
+      rc = coalescer(md.class_words).run(r, inflight, coalesce_max_ops(), coalesce_min_ops());
       if (rc) {
         leave_call();
         throw EngineError(rc, "mpcx_modexp_multi_batch: " + r.err);
