@@ -259,8 +259,24 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
 #ifndef MPCX_MX_TIMING
 #define MPCX_MX_TIMING 0  // microbench builds only: 1 = product loop alone, 2 = reduction alone
 #endif
+  // MX_PRIO, the wave's issue priority by phase (s_setprio; the two waves of a
+  // SIMD are mostly in different phases): 0 none; 1 the matrix-core reduction
+  // raised (138.7 vs 139.6 ms, profiles/r06/libab1); 2 the product loop raised;
+  // 3 the product loop and the fragment build; 4 the product loop over the
+  // fragment build and reduction over the carry passes. Config 2, three
+  // interleaved rounds (profiles/r06/prioab2): 4 128.2, 2 129.1, 3 129.1,
+  // 1 133.5 ms. A product-loop wave issues a MAD every ~10 cycles on its own; with
+  // the arbiter's preference it gets each slot it can use and the partner's
+  // reduction fills the rest, instead of the reverse.
+#ifndef MX_PRIO
+#define MX_PRIO 4
+#endif
   MX_STAMP(0);
+  if constexpr (MX_PRIO == 2 || MX_PRIO == 3) __builtin_amdgcn_s_setprio(1);
+  if constexpr (MX_PRIO == 4) __builtin_amdgcn_s_setprio(2);
   if constexpr (MPCX_MX_TIMING != 2) mx_product<P, K, SQR, B2IN>(A, rg, rg, rows + S::TRASH_OFF + lane, p);
+  if constexpr (MX_PRIO == 2) __builtin_amdgcn_s_setprio(0);
+  if constexpr (MX_PRIO == 4) __builtin_amdgcn_s_setprio(1);
   MX_STAMP(1);
   if constexpr (MPCX_MX_TIMING == 1) return;
   wave_lds_fence();
@@ -290,10 +306,8 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
   // ---- the row <- T's high digits + m (block layout)
 #pragma unroll
   for (int k = 0; k < K; ++k) rg[p * K + k] = A[k] + md[p * K + k];
-#ifndef MX_PRIO
-#define MX_PRIO 1  // 1: raise the wave's issue priority over the matrix-core phases (round 6: 138.7 vs 139.6 ms, profiles/r06/libab1)
-#endif
-  if constexpr (MX_PRIO) __builtin_amdgcn_s_setprio(1);
+  if constexpr (MX_PRIO == 1) __builtin_amdgcn_s_setprio(1);
+  if constexpr (MX_PRIO == 3) __builtin_amdgcn_s_setprio(0);
   static_for<0, S::HALVES>([&](auto sc) {
     constexpr int s = decltype(sc)::value;
     uint32_t* rn = rows + (16 * s + n) * ROW;
@@ -387,7 +401,7 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
       });
     }
   });
-  if constexpr (MX_PRIO) __builtin_amdgcn_s_setprio(0);
+  if constexpr (MX_PRIO == 1 || MX_PRIO == 4) __builtin_amdgcn_s_setprio(0);
   MX_STAMP(4);
   wave_lds_fence();
   // ---- back to the block layout; signed carry passes until every digit is >= 0
