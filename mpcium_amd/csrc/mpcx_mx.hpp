@@ -259,24 +259,42 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
 #ifndef MPCX_MX_TIMING
 #define MPCX_MX_TIMING 0  // microbench builds only: 1 = product loop alone, 2 = reduction alone
 #endif
-  // MX_PRIO, the wave's issue priority by phase (s_setprio; the two waves of a
-  // SIMD are mostly in different phases): 0 none; 1 the matrix-core reduction
-  // raised (138.7 vs 139.6 ms, profiles/r06/libab1); 2 the product loop raised;
-  // 3 the product loop and the fragment build; 4 the product loop over the
-  // fragment build and reduction over the carry passes. Config 2, three
-  // interleaved rounds (profiles/r06/prioab2): 4 128.2, 2 129.1, 3 129.1,
-  // 1 133.5 ms. A product-loop wave issues a MAD every ~10 cycles on its own; with
-  // the arbiter's preference it gets each slot it can use and the partner's
-  // reduction fills the rest, instead of the reverse.
+  // MX_PRIO, the wave's issue priority by phase of the Montgomery product
+  // (s_setprio; the two waves of a SIMD are mostly in different phases):
+  // product loop P, fragment build F, q products R, q m products R2, carry
+  // passes C. Presets: 0 none; 1 R = 1 (138.7 vs 139.6 ms, profiles/r06/libab1);
+  // 2 P = 1; 3 P = F = 1; 4 P 2 > F = R = R2 1 > C 0; 5 (default) P 3 > F 2 >
+  // R 1 > R2 = C 0. Config 2, three interleaved rounds per A/B
+  // (profiles/r06/prioab2..4): 1 133.5 -> 4 128.2 (2, 3: 129.1) -> 5 123.3 ms.
+  // The levels must fall along the product: equal levels for P and F (126.5) or
+  // for R and R2 (124.9) lose. Whenever the two waves are in different phases,
+  // the one that is earlier in its product issues first; the other fills the
+  // slots it leaves (a product-loop wave alone issues a MAD only every ~10
+  // cycles).
 #ifndef MX_PRIO
-#define MX_PRIO 4
+#define MX_PRIO 5
 #endif
+  // -DMX_PRIO_P=.. etc. override one phase for an A/B
+#ifndef MX_PRIO_P
+#define MX_PRIO_P (MX_PRIO == 5 ? 3 : MX_PRIO == 4 ? 2 : (MX_PRIO == 2 || MX_PRIO == 3) ? 1 : 0)
+#endif
+#ifndef MX_PRIO_F
+#define MX_PRIO_F (MX_PRIO == 5 ? 2 : (MX_PRIO == 3 || MX_PRIO == 4) ? 1 : 0)
+#endif
+#ifndef MX_PRIO_R
+#define MX_PRIO_R ((MX_PRIO == 1 || MX_PRIO == 4 || MX_PRIO == 5) ? 1 : 0)
+#endif
+#ifndef MX_PRIO_R2
+#define MX_PRIO_R2 (MX_PRIO == 5 ? 0 : MX_PRIO_R)
+#endif
+#ifndef MX_PRIO_C
+#define MX_PRIO_C 0
+#endif
+  constexpr bool PRIO_ON = (MX_PRIO_P | MX_PRIO_F | MX_PRIO_R | MX_PRIO_R2 | MX_PRIO_C) != 0;
   MX_STAMP(0);
-  if constexpr (MX_PRIO == 2 || MX_PRIO == 3) __builtin_amdgcn_s_setprio(1);
-  if constexpr (MX_PRIO == 4) __builtin_amdgcn_s_setprio(2);
+  if constexpr (PRIO_ON) __builtin_amdgcn_s_setprio(MX_PRIO_P);
   if constexpr (MPCX_MX_TIMING != 2) mx_product<P, K, SQR, B2IN>(A, rg, rg, rows + S::TRASH_OFF + lane, p);
-  if constexpr (MX_PRIO == 2) __builtin_amdgcn_s_setprio(0);
-  if constexpr (MX_PRIO == 4) __builtin_amdgcn_s_setprio(1);
+  if constexpr (PRIO_ON) __builtin_amdgcn_s_setprio(MX_PRIO_F);
   MX_STAMP(1);
   if constexpr (MPCX_MX_TIMING == 1) return;
   wave_lds_fence();
@@ -306,11 +324,11 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
   // ---- the row <- T's high digits + m (block layout)
 #pragma unroll
   for (int k = 0; k < K; ++k) rg[p * K + k] = A[k] + md[p * K + k];
-  if constexpr (MX_PRIO == 1) __builtin_amdgcn_s_setprio(1);
-  if constexpr (MX_PRIO == 3) __builtin_amdgcn_s_setprio(0);
+  if constexpr (PRIO_ON && MX_PRIO_R != MX_PRIO_F) __builtin_amdgcn_s_setprio(MX_PRIO_R);
   static_for<0, S::HALVES>([&](auto sc) {
     constexpr int s = decltype(sc)::value;
     uint32_t* rn = rows + (16 * s + n) * ROW;
+    if constexpr (PRIO_ON && MX_PRIO_R2 != MX_PRIO_R && s > 0) __builtin_amdgcn_s_setprio(MX_PRIO_R);
     // ---- q column sums (o = j + 4 kb; chunks of output blocks bound the live
     // accumulators), balanced radix-2^28 digits with one carry step, as bytes;
     // every 4 blocks transposed in registers into one B fragment of phase 2
@@ -358,6 +376,7 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
       });
     }
     MX_STAMP(3);
+    if constexpr (PRIO_ON && MX_PRIO_R2 != MX_PRIO_R) __builtin_amdgcn_s_setprio(MX_PRIO_R2);
     // ---- q m column sums for blocks O2LO.. : the lane whose 4 positions are the
     // low half's top (N7 - 4 .. N7 - 1) gives the carry out of the low half, the
     // lanes at positions N7 + 4d the digits d of U + m, adding T's high digit + m
@@ -401,7 +420,7 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
       });
     }
   });
-  if constexpr (MX_PRIO == 1 || MX_PRIO == 4) __builtin_amdgcn_s_setprio(0);
+  if constexpr (PRIO_ON) __builtin_amdgcn_s_setprio(MX_PRIO_C);
   MX_STAMP(4);
   wave_lds_fence();
   // ---- back to the block layout; signed carry passes until every digit is >= 0
