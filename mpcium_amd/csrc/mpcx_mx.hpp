@@ -267,10 +267,11 @@ __device__ __forceinline__ void montmul_mx(uint32_t (&A)[S::K], uint32_t* rows, 
   // R 1 > R2 = C 0. Config 2, three interleaved rounds per A/B
   // (profiles/r06/prioab2..4): 1 133.5 -> 4 128.2 (2, 3: 129.1) -> 5 123.3 ms.
   // The levels must fall along the product: equal levels for P and F (126.5) or
-  // for R and R2 (124.9) lose. Whenever the two waves are in different phases,
-  // the one that is earlier in its product issues first; the other fills the
-  // slots it leaves (a product-loop wave alone issues a MAD only every ~10
-  // cycles).
+  // for R and R2 (124.9) lose, and so does the product loop's second half one
+  // level down (126.0-126.6 vs 125.2, prioab5). Whenever the two waves are in
+  // different phases, the one that is earlier in its product issues first; the
+  // other fills the slots it leaves (a product-loop wave alone issues a MAD only
+  // every ~10 cycles).
 #ifndef MX_PRIO
 #define MX_PRIO 5
 #endif
