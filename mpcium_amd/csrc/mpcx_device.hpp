@@ -754,7 +754,8 @@ __device__ __forceinline__ void fixedbase_wave(const FixedBaseArgs& a, const uin
   // loaded after the current product: loading it during the product into
   // registers measured 6% slower on config 5 (profiles/r03/fb_prefetch), and
   // staging it into a second LDS row set by LDS DMA (global_load_lds) 5-15%
-  // slower in isolation (profiles/r04/fb_dma_ab/isolated).
+  // slower in isolation (profiles/r04/fb_dma_ab/isolated). Issue priority for
+  // the fetch or for the products: no change (profiles/r06/fbab).
   uint32_t t = 0, j = wv;  // next window: base t, window j
   uint32_t part = 1;  // wave 0: next partial to multiply in
   bool own = true, fin = false;
